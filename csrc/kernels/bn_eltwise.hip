@@ -1,0 +1,486 @@
+// Training-mode BatchNorm3d + ReLU + residual + pooling kernels for NDHWC bf16 activations (gfx950).
+//
+// The conv epilogue already produced per-tile (sum, sumsq) partial slabs of each raw conv output y;
+// bn_finalize turns them into batch statistics, updates running stats (momentum, unbiased var) and
+// emits the per-channel affine (scale, shift) that consumers apply on load.  Everything elementwise
+// is 16-B vectorised (8 channels per lane, cdna_hip_programming.md Guideline 13) and works on strided
+// channel views (ld = row stride) so concatenated tensors are never copied.
+//
+// Backward: bn_bwd_reduce computes deterministic per-block partial sums of dz = g*mask, dz*xhat for
+// up to two BN inputs sharing one dz (conv_c and branch1 of a residual unit), bn_bwd_finalize turns
+// them into dgamma/dbeta (into the fp32 master-gradient buffer) and the coefficients of
+//   dy = A*dz + B*y + C            (A = g*r, B = -g*r^2*dgamma/M, C = g*r*(mean*r*dgamma - dbeta)/M)
+// and bn_bwd_apply materialises dy (bf16) for the dgrad/wgrad of the producing conv.
+#include "common.h"
+
+namespace {
+
+constexpr int NT = 256;
+
+// ------------------------------------------------------------------------------------------
+// finalize forward statistics
+// ------------------------------------------------------------------------------------------
+__global__ void bn_finalize_kernel(const float* __restrict__ part, int tiles, int C, int64_t count,
+                                   const float* __restrict__ gamma, const float* __restrict__ beta,
+                                   float* __restrict__ run_mean, float* __restrict__ run_var,
+                                   int64_t* __restrict__ nbt, float momentum, float eps,
+                                   float* __restrict__ save_mean, float* __restrict__ save_rstd,
+                                   float* __restrict__ scale, float* __restrict__ shift) {
+  const int c = blockIdx.x;
+  double s = 0.0, q = 0.0;
+  for (int t = threadIdx.x; t < tiles; t += NT) {
+    s += part[(int64_t)t * 2 * C + c];
+    q += part[(int64_t)t * 2 * C + C + c];
+  }
+  __shared__ double rs[NT], rq[NT];
+  rs[threadIdx.x] = s; rq[threadIdx.x] = q;
+  __syncthreads();
+  for (int o = NT / 2; o > 0; o >>= 1) {
+    if (threadIdx.x < o) { rs[threadIdx.x] += rs[threadIdx.x + o]; rq[threadIdx.x] += rq[threadIdx.x + o]; }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const double mean = rs[0] / (double)count;
+    double var = rq[0] / (double)count - mean * mean;
+    if (var < 0) var = 0;
+    const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+    save_mean[c] = (float)mean;
+    save_rstd[c] = rstd;
+    const float g = gamma[c], b = beta[c];
+    scale[c] = g * rstd;
+    shift[c] = b - (float)mean * g * rstd;
+    if (run_mean) {
+      const double unb = count > 1 ? var * (double)count / (double)(count - 1) : var;
+      run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * (float)mean;
+      run_var[c] = (1.f - momentum) * run_var[c] + momentum * (float)unb;
+    }
+    if (c == 0 && nbt) nbt[0] += 1;
+  }
+}
+
+// eval-mode affine from running statistics
+__global__ void bn_eval_affine_kernel(int C, const float* gamma, const float* beta, const float* rm, const float* rv,
+                                      float eps, float* scale, float* shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float r = rsqrtf(rv[c] + eps);
+  scale[c] = gamma[c] * r;
+  shift[c] = beta[c] - rm[c] * gamma[c] * r;
+}
+
+// ------------------------------------------------------------------------------------------
+// elementwise: out = act(y*scale + shift)       (strided channel views)
+// ------------------------------------------------------------------------------------------
+__global__ void bn_act_kernel(const uint16_t* __restrict__ y, int ldy, uint16_t* __restrict__ out, int ldo,
+                              const float* __restrict__ scale, const float* __restrict__ shift, int relu,
+                              int64_t M, int C) {
+  const int vecs = C >> 3;
+  const int64_t total = M * vecs;
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < total; i += (int64_t)gridDim.x * NT) {
+    const int64_t m = i / vecs;
+    const int c = (int)(i - m * vecs) << 3;
+    float f[8];
+    unpack8(*reinterpret_cast<const uint4*>(y + m * ldy + c), f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float z = f[e] * scale[c + e] + shift[c + e];
+      f[e] = relu ? fmaxf(z, 0.f) : z;
+    }
+    *reinterpret_cast<uint4*>(out + m * ldo + c) = pack8(f);
+  }
+}
+
+// residual unit output: out = relu(yc*sc + hc + (has_b1 ? y1*s1 + h1 : x))
+__global__ void res_out_kernel(const uint16_t* __restrict__ yc, const float* __restrict__ sc, const float* __restrict__ hc,
+                               const uint16_t* __restrict__ y1, const float* __restrict__ s1, const float* __restrict__ h1,
+                               const uint16_t* __restrict__ x, int ldx, uint16_t* __restrict__ out, int ldo,
+                               int64_t M, int C) {
+  const int vecs = C >> 3;
+  const int64_t total = M * vecs;
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < total; i += (int64_t)gridDim.x * NT) {
+    const int64_t m = i / vecs;
+    const int c = (int)(i - m * vecs) << 3;
+    float a[8], b[8];
+    unpack8(*reinterpret_cast<const uint4*>(yc + m * C + c), a);
+    if (y1) {
+      unpack8(*reinterpret_cast<const uint4*>(y1 + m * C + c), b);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) b[e] = b[e] * s1[c + e] + h1[c + e];
+    } else {
+      unpack8(*reinterpret_cast<const uint4*>(x + m * ldx + c), b);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) a[e] = fmaxf(a[e] * sc[c + e] + hc[c + e] + b[e], 0.f);
+    *reinterpret_cast<uint4*>(out + m * ldo + c) = pack8(a);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// backward reductions
+//   mask_mode 0: dz = g ; 1: dz = g * (mo > 0) ; 2: dz = g * (y0*ms + mh > 0)
+// ------------------------------------------------------------------------------------------
+__global__ void bn_bwd_reduce_kernel(const uint16_t* __restrict__ g, int ldg, int mask_mode,
+                                     const uint16_t* __restrict__ mo, int ldm,
+                                     const float* __restrict__ ms, const float* __restrict__ mh,
+                                     const uint16_t* __restrict__ y0, const float* __restrict__ mean0,
+                                     const float* __restrict__ rstd0,
+                                     const uint16_t* __restrict__ y1, const float* __restrict__ mean1,
+                                     const float* __restrict__ rstd1,
+                                     int64_t M, int C, int rows_per_block, float* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [3][C]
+  for (int i = threadIdx.x; i < 3 * C; i += NT) red[i] = 0.f;
+  __syncthreads();
+  const int vecs = C >> 3;
+  const int rpi = NT / vecs;  // rows per iteration
+  const int lv = threadIdx.x % vecs, lr = threadIdx.x / vecs;
+  const int c = lv << 3;
+  float sdz[8], s0[8], s1[8], m0[8], r0[8], m1[8], r1[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { sdz[e] = 0.f; s0[e] = 0.f; s1[e] = 0.f; }
+  if (lr < rpi) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      m0[e] = mean0[c + e]; r0[e] = rstd0[c + e];
+      if (y1) { m1[e] = mean1[c + e]; r1[e] = rstd1[c + e]; }
+    }
+    const int64_t mbeg = (int64_t)blockIdx.x * rows_per_block;
+    const int64_t mend = min<int64_t>(M, mbeg + rows_per_block);
+    for (int64_t m = mbeg + lr; m < mend; m += rpi) {
+      float dz[8], a[8];
+      unpack8(*reinterpret_cast<const uint4*>(g + m * ldg + c), dz);
+      unpack8(*reinterpret_cast<const uint4*>(y0 + m * C + c), a);
+      if (mask_mode == 1) {
+        float o[8];
+        unpack8(*reinterpret_cast<const uint4*>(mo + m * ldm + c), o);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dz[e] = o[e] > 0.f ? dz[e] : 0.f;
+      } else if (mask_mode == 2) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dz[e] = (a[e] * ms[c + e] + mh[c + e]) > 0.f ? dz[e] : 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { sdz[e] += dz[e]; s0[e] += dz[e] * (a[e] - m0[e]) * r0[e]; }
+      if (y1) {
+        float b[8];
+        unpack8(*reinterpret_cast<const uint4*>(y1 + m * C + c), b);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s1[e] += dz[e] * (b[e] - m1[e]) * r1[e];
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      atomicAdd(&red[c + e], sdz[e]);
+      atomicAdd(&red[C + c + e], s0[e]);
+      if (y1) atomicAdd(&red[2 * C + c + e], s1[e]);
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 3 * C; i += NT) part[(int64_t)blockIdx.x * 3 * C + i] = red[i];
+}
+
+// per channel: sums over blocks -> dgamma/dbeta (grad buffers, accumulate with beta_acc) + apply coeffs
+__global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int blocks, int C, int64_t count, int which,
+                                       const float* __restrict__ gamma, const float* __restrict__ mean,
+                                       const float* __restrict__ rstd, float* __restrict__ dgamma,
+                                       float* __restrict__ dbeta, float beta_acc, float* __restrict__ coef) {
+  const int c = blockIdx.x;
+  double sdz = 0.0, sx = 0.0;
+  for (int t = threadIdx.x; t < blocks; t += NT) {
+    sdz += part[(int64_t)t * 3 * C + c];
+    sx += part[(int64_t)t * 3 * C + (1 + which) * C + c];
+  }
+  __shared__ double ra[NT], rb[NT];
+  ra[threadIdx.x] = sdz; rb[threadIdx.x] = sx;
+  __syncthreads();
+  for (int o = NT / 2; o > 0; o >>= 1) {
+    if (threadIdx.x < o) { ra[threadIdx.x] += ra[threadIdx.x + o]; rb[threadIdx.x] += rb[threadIdx.x + o]; }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float db = (float)ra[0], dg = (float)rb[0];
+    if (dgamma) {
+      dgamma[c] = (beta_acc == 0.f ? 0.f : beta_acc * dgamma[c]) + dg;
+      dbeta[c] = (beta_acc == 0.f ? 0.f : beta_acc * dbeta[c]) + db;
+    }
+    const float gm = gamma[c], r = rstd[c], mu = mean[c];
+    const float inv = 1.f / (float)count;
+    coef[c] = gm * r;                                   // A
+    coef[C + c] = -gm * r * r * dg * inv;               // B
+    coef[2 * C + c] = gm * r * (mu * r * dg - db) * inv;  // C
+  }
+}
+
+// dy_k = A_k*dz + B_k*y_k + C_k  (k = 0, 1) ; optionally dz itself (identity shortcut gradient)
+__global__ void bn_bwd_apply_kernel(const uint16_t* __restrict__ g, int ldg, int mask_mode,
+                                    const uint16_t* __restrict__ mo, int ldm,
+                                    const float* __restrict__ ms, const float* __restrict__ mh,
+                                    const uint16_t* __restrict__ y0, const float* __restrict__ coef0,
+                                    uint16_t* __restrict__ dy0,
+                                    const uint16_t* __restrict__ y1, const float* __restrict__ coef1,
+                                    uint16_t* __restrict__ dy1,
+                                    uint16_t* __restrict__ dzout, int lddz, int dz_accum,
+                                    int64_t M, int C) {
+  const int vecs = C >> 3;
+  const int64_t total = M * vecs;
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < total; i += (int64_t)gridDim.x * NT) {
+    const int64_t m = i / vecs;
+    const int c = (int)(i - m * vecs) << 3;
+    float dz[8], a[8];
+    unpack8(*reinterpret_cast<const uint4*>(g + m * ldg + c), dz);
+    unpack8(*reinterpret_cast<const uint4*>(y0 + m * C + c), a);
+    if (mask_mode == 1) {
+      float o[8];
+      unpack8(*reinterpret_cast<const uint4*>(mo + m * ldm + c), o);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dz[e] = o[e] > 0.f ? dz[e] : 0.f;
+    } else if (mask_mode == 2) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dz[e] = (a[e] * ms[c + e] + mh[c + e]) > 0.f ? dz[e] : 0.f;
+    }
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = coef0[c + e] * dz[e] + coef0[C + c + e] * a[e] + coef0[2 * C + c + e];
+    *reinterpret_cast<uint4*>(dy0 + m * C + c) = pack8(o);
+    if (y1) {
+      unpack8(*reinterpret_cast<const uint4*>(y1 + m * C + c), a);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = coef1[c + e] * dz[e] + coef1[C + c + e] * a[e] + coef1[2 * C + c + e];
+      *reinterpret_cast<uint4*>(dy1 + m * C + c) = pack8(o);
+    }
+    if (dzout) {
+      uint16_t* d = dzout + m * lddz + c;
+      if (dz_accum) {
+        float p[8];
+        unpack8(*reinterpret_cast<const uint4*>(d), p);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dz[e] += p[e];
+      }
+      *reinterpret_cast<uint4*>(d) = pack8(dz);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// stem: out = maxpool_{1x3x3, s(1,2,2), p(0,1,1)}(relu(y*scale+shift)) ; argmax as 0..8 (uint8)
+// ------------------------------------------------------------------------------------------
+__global__ void stem_pool_fwd_kernel(const uint16_t* __restrict__ y, const float* __restrict__ scale,
+                                     const float* __restrict__ shift, uint16_t* __restrict__ out,
+                                     uint8_t* __restrict__ arg, int NT_, int H, int W, int Ho, int Wo, int C) {
+  const int vecs = C >> 3;
+  const int64_t total = (int64_t)NT_ * Ho * Wo * vecs;
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < total; i += (int64_t)gridDim.x * NT) {
+    int64_t r = i;
+    const int cv = r % vecs; r /= vecs;
+    const int wo = r % Wo; r /= Wo;
+    const int ho = r % Ho; r /= Ho;
+    const int64_t nt = r;
+    const int c = cv << 3;
+    float best[8];
+    uint8_t bi[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { best[e] = -INFINITY; bi[e] = 0; }
+    float sc[8], sh[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { sc[e] = scale[c + e]; sh[e] = shift[c + e]; }
+    for (int dh = 0; dh < 3; ++dh) {
+      const int h = ho * 2 - 1 + dh;
+      if ((unsigned)h >= (unsigned)H) continue;
+      for (int dw = 0; dw < 3; ++dw) {
+        const int w = wo * 2 - 1 + dw;
+        if ((unsigned)w >= (unsigned)W) continue;
+        float f[8];
+        unpack8(*reinterpret_cast<const uint4*>(y + ((nt * H + h) * W + w) * C + c), f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float a = fmaxf(f[e] * sc[e] + sh[e], 0.f);
+          if (a > best[e]) { best[e] = a; bi[e] = (uint8_t)(dh * 3 + dw); }
+        }
+      }
+    }
+    const int64_t o = ((nt * Ho + ho) * Wo + wo) * C + c;
+    *reinterpret_cast<uint4*>(out + o) = pack8(best);
+    uint2 pk;
+    pk.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((uint32_t)bi[3] << 24);
+    pk.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | ((uint32_t)bi[7] << 24);
+    *reinterpret_cast<uint2*>(arg + o) = pk;
+  }
+}
+
+// gather form of the max-pool backward: each input position sums the (<=4) windows whose argmax it is
+__global__ void stem_pool_bwd_kernel(const uint16_t* __restrict__ dout, int ldd, const uint8_t* __restrict__ arg,
+                                     uint16_t* __restrict__ dact, int NT_, int H, int W, int Ho, int Wo, int C) {
+  const int vecs = C >> 3;
+  const int64_t total = (int64_t)NT_ * H * W * vecs;
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < total; i += (int64_t)gridDim.x * NT) {
+    int64_t r = i;
+    const int cv = r % vecs; r /= vecs;
+    const int w = r % W; r /= W;
+    const int h = r % H; r /= H;
+    const int64_t nt = r;
+    const int c = cv << 3;
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+    // windows ho with ho*2-1 <= h <= ho*2+1
+    const int ho_lo = (h) / 2, ho_hi = min(Ho - 1, (h + 1) / 2);
+    const int wo_lo = (w) / 2, wo_hi = min(Wo - 1, (w + 1) / 2);
+    for (int ho = ho_lo; ho <= ho_hi; ++ho) {
+      const int dh = h - (ho * 2 - 1);
+      if (dh < 0 || dh > 2) continue;
+      for (int wo = wo_lo; wo <= wo_hi; ++wo) {
+        const int dw = w - (wo * 2 - 1);
+        if (dw < 0 || dw > 2) continue;
+        const int64_t o = (nt * Ho + ho) * Wo + wo;
+        const uint2 pk = *reinterpret_cast<const uint2*>(arg + o * C + c);
+        float g[8];
+        unpack8(*reinterpret_cast<const uint4*>(dout + o * ldd + c), g);
+        const uint8_t want = (uint8_t)(dh * 3 + dw);
+        uint8_t bi[8] = {(uint8_t)(pk.x), (uint8_t)(pk.x >> 8), (uint8_t)(pk.x >> 16), (uint8_t)(pk.x >> 24),
+                         (uint8_t)(pk.y), (uint8_t)(pk.y >> 8), (uint8_t)(pk.y >> 16), (uint8_t)(pk.y >> 24)};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) if (bi[e] == want) acc[e] += g[e];
+      }
+    }
+    *reinterpret_cast<uint4*>(dact + ((nt * H + h) * W + w) * C + c) = pack8(acc);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// AvgPool3d(k, stride 1) over an NDHWC tensor -> fp32 [N][P][ldo] at channel offset coff
+// ------------------------------------------------------------------------------------------
+__global__ void avgpool_fwd_kernel(const uint16_t* __restrict__ x, int T, int H, int W, int C, int kt, int kh, int kw,
+                                   float* __restrict__ out, int ldo, int coff, int N) {
+  const int To = T - kt + 1, Ho = H - kh + 1, Wo = W - kw + 1;
+  const int64_t total = (int64_t)N * To * Ho * Wo * C;
+  const float inv = 1.f / (float)(kt * kh * kw);
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < total; i += (int64_t)gridDim.x * NT) {
+    int64_t r = i;
+    const int c = r % C; r /= C;
+    const int wo = r % Wo; r /= Wo;
+    const int ho = r % Ho; r /= Ho;
+    const int to = r % To; r /= To;
+    const int n = (int)r;
+    float s = 0.f;
+    for (int a = 0; a < kt; ++a)
+      for (int b = 0; b < kh; ++b)
+        for (int d = 0; d < kw; ++d)
+          s += bf2f(x[((((int64_t)n * T + to + a) * H + ho + b) * W + wo + d) * C + c]);
+    out[(((int64_t)n * To + to) * Ho + ho) * Wo * ldo + (int64_t)wo * ldo + coff + c] = s * inv;
+  }
+}
+
+__global__ void avgpool_bwd_kernel(const float* __restrict__ dout, int ldo, int coff, int T, int H, int W, int C,
+                                   int kt, int kh, int kw, uint16_t* __restrict__ dx, int N) {
+  const int To = T - kt + 1, Ho = H - kh + 1, Wo = W - kw + 1;
+  const int64_t total = (int64_t)N * T * H * W * C;
+  const float inv = 1.f / (float)(kt * kh * kw);
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < total; i += (int64_t)gridDim.x * NT) {
+    int64_t r = i;
+    const int c = r % C; r /= C;
+    const int w = r % W; r /= W;
+    const int h = r % H; r /= H;
+    const int t = r % T; r /= T;
+    const int n = (int)r;
+    float s = 0.f;
+    for (int to = max(0, t - kt + 1); to <= min(To - 1, t); ++to)
+      for (int ho = max(0, h - kh + 1); ho <= min(Ho - 1, h); ++ho)
+        for (int wo = max(0, w - kw + 1); wo <= min(Wo - 1, w); ++wo)
+          s += dout[(((int64_t)n * To + to) * Ho + ho) * Wo * ldo + (int64_t)wo * ldo + coff + c];
+    dx[i] = f2bf(s * inv);
+  }
+}
+
+int grid_for(int64_t work) {
+  int64_t b = (work + NT - 1) / NT;
+  if (b > 8192) b = 8192;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+}  // namespace
+
+void bn_finalize_launch(const float* part, int tiles, int C, int64_t count, const float* gamma, const float* beta,
+                        float* rm, float* rv, int64_t* nbt, float momentum, float eps, float* smean, float* srstd,
+                        float* scale, float* shift, hipStream_t s) {
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(NT), 0, s, part, tiles, C, count, gamma, beta, rm, rv, nbt,
+                     momentum, eps, smean, srstd, scale, shift);
+}
+
+void bn_eval_affine_launch(int C, const float* gamma, const float* beta, const float* rm, const float* rv, float eps,
+                           float* scale, float* shift, hipStream_t s) {
+  hipLaunchKernelGGL(bn_eval_affine_kernel, dim3((C + 255) / 256), dim3(256), 0, s, C, gamma, beta, rm, rv, eps,
+                     scale, shift);
+}
+
+void bn_act_launch(const uint16_t* y, int ldy, uint16_t* out, int ldo, const float* scale, const float* shift,
+                   int relu, int64_t M, int C, hipStream_t s) {
+  hipLaunchKernelGGL(bn_act_kernel, dim3(grid_for(M * (C / 8))), dim3(NT), 0, s, y, ldy, out, ldo, scale, shift, relu,
+                     M, C);
+}
+
+void res_out_launch(const uint16_t* yc, const float* sc, const float* hc, const uint16_t* y1, const float* s1,
+                    const float* h1, const uint16_t* x, int ldx, uint16_t* out, int ldo, int64_t M, int C,
+                    hipStream_t s) {
+  hipLaunchKernelGGL(res_out_kernel, dim3(grid_for(M * (C / 8))), dim3(NT), 0, s, yc, sc, hc, y1, s1, h1, x, ldx, out,
+                     ldo, M, C);
+}
+
+int bn_bwd_reduce_blocks(int64_t M, int C, int* rows_per_block) {
+  const int vecs = C / 8;
+  const int rpi = NT / vecs;
+  // aim for ~16 rows per thread-row and at most 2048 blocks
+  int64_t rpb = (int64_t)rpi * 16;
+  int64_t blocks = (M + rpb - 1) / rpb;
+  if (blocks > 2048) { blocks = 2048; rpb = (M + blocks - 1) / blocks; }
+  *rows_per_block = (int)rpb;
+  return (int)blocks;
+}
+
+void bn_bwd_reduce_launch(const uint16_t* g, int ldg, int mask_mode, const uint16_t* mo, int ldm, const float* ms,
+                          const float* mh, const uint16_t* y0, const float* mean0, const float* rstd0,
+                          const uint16_t* y1, const float* mean1, const float* rstd1, int64_t M, int C, int blocks,
+                          int rows_per_block, float* part, hipStream_t s) {
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(blocks), dim3(NT), 3 * C * sizeof(float), s, g, ldg, mask_mode, mo,
+                     ldm, ms, mh, y0, mean0, rstd0, y1, mean1, rstd1, M, C, rows_per_block, part);
+}
+
+void bn_bwd_finalize_launch(const float* part, int blocks, int C, int64_t count, int which, const float* gamma,
+                            const float* mean, const float* rstd, float* dgamma, float* dbeta, float beta_acc,
+                            float* coef, hipStream_t s) {
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(NT), 0, s, part, blocks, C, count, which, gamma, mean, rstd,
+                     dgamma, dbeta, beta_acc, coef);
+}
+
+void bn_bwd_apply_launch(const uint16_t* g, int ldg, int mask_mode, const uint16_t* mo, int ldm, const float* ms,
+                         const float* mh, const uint16_t* y0, const float* coef0, uint16_t* dy0, const uint16_t* y1,
+                         const float* coef1, uint16_t* dy1, uint16_t* dzout, int lddz, int dz_accum, int64_t M, int C,
+                         hipStream_t s) {
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(M * (C / 8))), dim3(NT), 0, s, g, ldg, mask_mode, mo, ldm, ms,
+                     mh, y0, coef0, dy0, y1, coef1, dy1, dzout, lddz, dz_accum, M, C);
+}
+
+void stem_pool_fwd_launch(const uint16_t* y, const float* scale, const float* shift, uint16_t* out, uint8_t* arg,
+                          int NT_, int H, int W, int Ho, int Wo, int C, hipStream_t s) {
+  hipLaunchKernelGGL(stem_pool_fwd_kernel, dim3(grid_for((int64_t)NT_ * Ho * Wo * (C / 8))), dim3(NT), 0, s, y, scale,
+                     shift, out, arg, NT_, H, W, Ho, Wo, C);
+}
+
+void stem_pool_bwd_launch(const uint16_t* dout, int ldd, const uint8_t* arg, uint16_t* dact, int NT_, int H, int W,
+                          int Ho, int Wo, int C, hipStream_t s) {
+  hipLaunchKernelGGL(stem_pool_bwd_kernel, dim3(grid_for((int64_t)NT_ * H * W * (C / 8))), dim3(NT), 0, s, dout, ldd,
+                     arg, dact, NT_, H, W, Ho, Wo, C);
+}
+
+void avgpool_fwd_launch(const uint16_t* x, int N, int T, int H, int W, int C, int kt, int kh, int kw, float* out,
+                        int ldo, int coff, hipStream_t s) {
+  const int64_t total = (int64_t)N * (T - kt + 1) * (H - kh + 1) * (W - kw + 1) * C;
+  hipLaunchKernelGGL(avgpool_fwd_kernel, dim3(grid_for(total)), dim3(NT), 0, s, x, T, H, W, C, kt, kh, kw, out, ldo,
+                     coff, N);
+}
+
+void avgpool_bwd_launch(const float* dout, int ldo, int coff, int N, int T, int H, int W, int C, int kt, int kh,
+                        int kw, uint16_t* dx, hipStream_t s) {
+  const int64_t total = (int64_t)N * T * H * W * C;
+  hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(grid_for(total)), dim3(NT), 0, s, dout, ldo, coff, T, H, W, C, kt, kh,
+                     kw, dx, N);
+}

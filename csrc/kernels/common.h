@@ -1,0 +1,79 @@
+// Shared device helpers for the gfx950 (CDNA4) kernels of pytorchvideo_accelerate_amd.
+// Everything here is written for 64-lane wavefronts and the MFMA 16x16x32 bf16 operand maps
+// (cdna_hip_programming.md §3: lane l holds A[l&15][8(l>>4)+j], B[8(l>>4)+j][l&15];
+//  D: col = l&15, row = 4(l>>4)+r).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef uint16_t bf16_t;  // storage type of a bf16 element
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+typedef __attribute__((ext_vector_type(4))) short s16x4_t;
+typedef __attribute__((ext_vector_type(8))) short s16x8_t;
+
+#define PVA_WAVE 64
+#define PVA_NXCD 8
+
+__device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+
+// Round-to-nearest-even with NaN preserved (hipcc lowers the __bf16 cast to v_cvt_pk_bf16_f32).
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(bf16_t, b);
+}
+
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+}
+
+__device__ __forceinline__ void unpack8(const uint4& v, float* f) {
+  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
+  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
+  f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xffff0000u);
+  f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xffff0000u);
+}
+
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  return make_uint4(pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7]));
+}
+
+__device__ __forceinline__ void unpack4(const uint2& v, float* f) {
+  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
+  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
+}
+
+__device__ __forceinline__ uint2 pack4(const float* f) {
+  return make_uint2(pack2(f[0], f[1]), pack2(f[2], f[3]));
+}
+
+// Bijective XCD-aware remap of a linear workgroup id (cdna_hip_programming.md §5, "XCD swizzle must
+// be bijective"): consecutive remapped ids land on the same XCD so neighbouring tiles share its L2.
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  if (nwg < PVA_NXCD * 2) return orig;
+  const int q = nwg / PVA_NXCD, r = nwg % PVA_NXCD;
+  const int xcd = orig % PVA_NXCD;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / PVA_NXCD;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Sum across the 16 lanes that share (lane >> 4).
+__device__ __forceinline__ float sum16(float v) {
+  v += __shfl_xor(v, 1, 64);
+  v += __shfl_xor(v, 2, 64);
+  v += __shfl_xor(v, 4, 64);
+  v += __shfl_xor(v, 8, 64);
+  return v;
+}
+
+// Sum across lanes l, l^16, l^32, l^48 (same lane & 15).
+__device__ __forceinline__ float sum_hi4(float v) {
+  v += __shfl_xor(v, 16, 64);
+  v += __shfl_xor(v, 32, 64);
+  return v;
+}

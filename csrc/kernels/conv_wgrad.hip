@@ -1,0 +1,310 @@
+// Weight gradient of the NDHWC 3-D convolution on MFMA (gfx950), split-K over positions.
+//
+//   dW[n = cout][k = (tap, cin)] = sum_p dY[p][n] * im2col(X)[p][k]
+//
+// Both operands are position-major in HBM (channels contiguous), so the reduction axis p is the
+// strided one.  Tiles are staged as [p][cols] row-major images (contiguous 16-B loads, the im2col
+// side is the same chunk gather as the forward kernel) and the MFMA fragments are read with the gfx950
+// hardware-transpose LDS read ds_read_b64_tr_b16 (cdna_hip_programming.md T10): one 16-lane group
+// reads a 4(p) x 16(col) block and each lane receives one column's 4 p-values.  32-byte column
+// segments are XOR-swizzled with row bits 1 and 3 so the 8 rows a 32-lane half touches land on
+// disjoint bank groups.  The p axis is split over gridDim.z slabs (fp32 partials, deterministic, no
+// atomics); wgrad_reduce sums the slabs and scatters into PyTorch's [Cout][Cin][kt][kh][kw] layout,
+// accumulating into the fp32 master-gradient buffer.
+#include "common.h"
+#include "conv_params.h"
+#include <type_traits>
+
+namespace {
+
+constexpr int BP = 32;  // positions per reduction step (one MFMA k-step)
+
+template <int COLS>
+__device__ __forceinline__ int img_off(int row, int colbyte) {
+  // [BP][COLS] bf16 image; 32-byte segments swizzled by row bits 1 and 3.
+  constexpr int NSEG = COLS * 2 / 32;
+  const int seg = colbyte >> 5;
+  const int h = (((row >> 1) & 1) | (((row >> 3) & 1) << 1)) & (NSEG - 1);
+  return row * COLS * 2 + (((seg ^ h) << 5) | (colbyte & 31));
+}
+
+__device__ __forceinline__ s16x4_t tr_read(const char* base) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s16x4_t*)(base));
+}
+
+template <int BMW, int BNW, int WMW, int WNW, int CH>
+__global__ __launch_bounds__((BMW / WMW) * (BNW / WNW) * 64)
+void conv_wgrad_kernel(const WgradParams p) {
+  constexpr int NWN = BNW / WNW;
+  constexpr int NT = (BMW / WMW) * NWN * 64;
+  constexpr int A_CPR = BMW / 8;            // 16-B chunks per dY row
+  constexpr int B_CPR = BNW / CH;           // chunks per im2col row
+  constexpr int A_CHUNKS = BP * A_CPR, B_CHUNKS = BP * B_CPR;
+  constexpr int A_SLOTS = (A_CHUNKS + NT - 1) / NT;
+  constexpr int B_SLOTS = (B_CHUNKS + NT - 1) / NT;
+  constexpr int TM = WMW / 16, TN = WNW / 16;
+  constexpr int A_BYTES = BP * BMW * 2, B_BYTES = BP * BNW * 2;
+  constexpr int TILE = A_BYTES + B_BYTES;
+  static_assert(NT % A_CPR == 0 && NT % B_CPR == 0, "slot mapping");
+  using VT = typename std::conditional<CH == 8, uint4, uint2>::type;
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* aff = reinterpret_cast<float*>(smem + 2 * TILE);
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / NWN, wn = wid % NWN;
+  const int n0 = blockIdx.x * BMW;           // cout tile
+  const int k0 = blockIdx.y * BNW;           // k tile
+  const int split = blockIdx.z;
+  const int p_begin = split * p.p_per_split;
+  const int p_end = min(p.P, p_begin + p.p_per_split);
+  const int affine = p.affine;
+  if (affine) {
+    for (int i = tid; i < p.Cin; i += NT) { aff[i] = p.in_scale[i]; aff[p.Cin + i] = p.in_shift[i]; }
+  }
+
+  // ---- A (dY) slots: fixed column, rows advance by BP ----
+  const int a_col = tid % A_CPR;
+  const int a_n = n0 + a_col * 8;
+  const bool a_col_ok = a_n < p.Cout;
+
+  // ---- B (im2col) slots: fixed (tap, cin) column, rows advance by BP ----
+  const int b_col = tid % B_CPR;
+  const int kb = k0 + b_col * CH;
+  const bool b_col_ok = kb < p.K;
+  int b_dt = 0, b_dh = 0, b_dw = 0, b_c = 0;
+  if (b_col_ok) {
+    const int tap = kb / p.Cin;
+    b_c = kb - tap * p.Cin;
+    b_dt = tap / (p.kh * p.kw);
+    const int r = tap - b_dt * p.kh * p.kw;
+    b_dh = r / p.kw;
+    b_dw = r - b_dh * p.kw;
+  }
+  // Position decomposition of each B slot's row (advanced incrementally).
+  const int OHW = p.Ho * p.Wo, OTHW = p.To * OHW;
+  const int IHW = p.Hi * p.Wi, ITHW = p.Ti * IHW;
+  int pb[B_SLOTS], pt_[B_SLOTS], ph_[B_SLOTS], pw_[B_SLOTS];
+#pragma unroll
+  for (int s = 0; s < B_SLOTS; ++s) {
+    const int row = (tid + s * NT) / B_CPR;
+    int q = p_begin + row;
+    const int b = q / OTHW; q -= b * OTHW;
+    const int t = q / OHW; q -= t * OHW;
+    const int h = q / p.Wo;
+    pb[s] = b; pt_[s] = t; ph_[s] = h; pw_[s] = q - h * p.Wo;
+  }
+  auto advance_pos = [&](int s) {
+    pw_[s] += BP;
+    while (pw_[s] >= p.Wo) {
+      pw_[s] -= p.Wo;
+      if (++ph_[s] == p.Ho) { ph_[s] = 0; if (++pt_[s] == p.To) { pt_[s] = 0; ++pb[s]; } }
+    }
+  };
+
+  uint4 ra[A_SLOTS];
+  VT rb[B_SLOTS];
+  unsigned rb_valid = 0;
+  int pcur = p_begin;
+
+  auto load = [&]() {
+#pragma unroll
+    for (int s = 0; s < A_SLOTS; ++s) {
+      const int idx = tid + s * NT;
+      const int q = pcur + idx / A_CPR;
+      if (idx < A_CHUNKS && a_col_ok && q < p_end)
+        ra[s] = *reinterpret_cast<const uint4*>(p.dy + (int64_t)q * p.ldd + a_n);
+      else
+        ra[s] = uint4{0, 0, 0, 0};
+    }
+    rb_valid = 0;
+#pragma unroll
+    for (int s = 0; s < B_SLOTS; ++s) {
+      const int idx = tid + s * NT;
+      const int q = pcur + idx / B_CPR;
+      bool v = idx < B_CHUNKS && b_col_ok && q < p_end;
+      if (v) {
+        const int ti = pt_[s] * p.st - p.pt + b_dt;
+        const int hi = ph_[s] * p.sh - p.ph + b_dh;
+        const int wi = pw_[s] * p.sw - p.pw + b_dw;
+        v = (unsigned)ti < (unsigned)p.Ti && (unsigned)hi < (unsigned)p.Hi && (unsigned)wi < (unsigned)p.Wi;
+        if (v) {
+          const int64_t off = (int64_t)(pb[s] * ITHW + (ti * p.Hi + hi) * p.Wi + wi) * p.ldx + b_c;
+          rb[s] = *reinterpret_cast<const VT*>(p.x + off);
+          rb_valid |= 1u << s;
+        }
+      }
+      if (!v) rb[s] = VT{};
+      advance_pos(s);
+    }
+    pcur += BP;
+  };
+
+  auto store_lds = [&](int buf) {
+    char* A = smem + buf * TILE;
+    char* B = A + A_BYTES;
+#pragma unroll
+    for (int s = 0; s < A_SLOTS; ++s) {
+      const int idx = tid + s * NT;
+      if (idx >= A_CHUNKS) break;
+      *reinterpret_cast<uint4*>(A + img_off<BMW>(idx / A_CPR, a_col * 16)) = ra[s];
+    }
+#pragma unroll
+    for (int s = 0; s < B_SLOTS; ++s) {
+      const int idx = tid + s * NT;
+      if (idx >= B_CHUNKS) break;
+      VT v = rb[s];
+      if (affine && (rb_valid >> s & 1)) {
+        float f[CH];
+        if constexpr (CH == 8) unpack8(v, f); else unpack4(v, f);
+#pragma unroll
+        for (int e = 0; e < CH; ++e) {
+          const float z = f[e] * aff[b_c + e] + aff[p.Cin + b_c + e];
+          f[e] = (affine == 2) ? fmaxf(z, 0.f) : z;
+        }
+        if constexpr (CH == 8) v = pack8(f); else v = pack4(f);
+      }
+      *reinterpret_cast<VT*>(B + img_off<BNW>(idx / B_CPR, b_col * CH * 2)) = v;
+    }
+  };
+
+  f32x4_t acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int nsteps = (p_end - p_begin + BP - 1) / BP;
+  __syncthreads();
+  if (nsteps > 0) {
+    load();
+    store_lds(0);
+  }
+  __syncthreads();
+
+  // tr-read addressing: group g = lane>>4 covers p rows 8g..8g+7; lane i = lane&15 supplies row
+  // (i>>2) of a 4-row block and columns 4*(i&3)..+3 of the 16-column block.
+  const int g = lane >> 4, li = lane & 15;
+  const int tr_row = 8 * g + (li >> 2);
+  const int tr_colb = (li & 3) * 8;  // byte offset inside the 16-column (32-B) block
+  for (int step = 0; step < nsteps; ++step) {
+    const int cur = step & 1;
+    const bool has_next = step + 1 < nsteps;
+    if (has_next) load();
+    const char* A = smem + cur * TILE;
+    const char* B = A + A_BYTES;
+    bf16x8_t af[TM], bfr[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int cb = (wm * WMW + i * 16) * 2 + tr_colb;
+      s16x4_t lo = tr_read(A + img_off<BMW>(tr_row, cb));
+      s16x4_t hi = tr_read(A + img_off<BMW>(tr_row + 4, cb));
+      s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      af[i] = __builtin_bit_cast(bf16x8_t, v);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int cb = (wn * WNW + j * 16) * 2 + tr_colb;
+      s16x4_t lo = tr_read(B + img_off<BNW>(tr_row, cb));
+      s16x4_t hi = tr_read(B + img_off<BNW>(tr_row + 4, cb));
+      s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      bfr[j] = __builtin_bit_cast(bf16x8_t, v);
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    if (has_next) store_lds(cur ^ 1);
+    __syncthreads();
+  }
+
+  // D[n][k]: lane holds k = col (lane&15), n = 4*(lane>>4) + r
+  float* out = p.partial + (int64_t)split * p.Cout * p.K;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int k = k0 + wn * WNW + j * 16 + li;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + wm * WMW + i * 16 + 4 * g + r;
+        if (n < p.Cout && k < p.K) out[(int64_t)n * p.K + k] = acc[i][j][r];
+      }
+    }
+}
+
+template <int BMW, int BNW, int WMW, int WNW, int CH>
+void launch_w(const WgradParams& p, hipStream_t stream) {
+  constexpr int NT = (BMW / WMW) * (BNW / WNW) * 64;
+  dim3 grid((p.Cout + BMW - 1) / BMW, (p.K + BNW - 1) / BNW, p.splits);
+  const size_t lds = 2 * BP * (BMW + BNW) * 2 + (p.affine ? 2 * p.Cin * 4 : 0);
+  hipLaunchKernelGGL((conv_wgrad_kernel<BMW, BNW, WMW, WNW, CH>), grid, dim3(NT), lds, stream, p);
+}
+
+// dW (fp32 partial slabs [splits][Cout][taps][Cin]) -> grad[Cout][Cin][taps] (PyTorch layout),
+// grad = beta * grad + scale * sum_s partial[s]
+__global__ void wgrad_reduce_kernel(const float* __restrict__ partial, float* __restrict__ grad, int splits,
+                                    int Cout, int taps, int Cin, int Cin_real, float scale, float beta) {
+  const int64_t total = (int64_t)Cout * taps * Cin;
+  const int64_t stride = (int64_t)Cout * taps * Cin;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int k = 0; k < splits; ++k) s += partial[k * stride + i];
+    const int c = i % Cin;
+    if (c >= Cin_real) continue;
+    const int64_t rest = i / Cin;
+    const int tap = rest % taps;
+    const int n = rest / taps;
+    const int64_t o = ((int64_t)n * Cin_real + c) * taps + tap;
+    grad[o] = (beta == 0.f ? 0.f : beta * grad[o]) + scale * s;
+  }
+}
+
+}  // namespace
+
+// Shape-based tile choice: (BMW over cout, BNW over k).
+static int wgrad_variant(int Cout, int K) {
+  if (Cout <= 16) return 0;   // 16 x 128
+  if (Cout <= 32) return 1;   // 32 x 128
+  if (Cout <= 64) return 2;   // 64 x 64
+  return 3;                   // 128 x 64
+}
+
+void conv_wgrad_tile(int Cout, int K, int* bmw, int* bnw) {
+  switch (wgrad_variant(Cout, K)) {
+    case 0: *bmw = 16; *bnw = 128; break;
+    case 1: *bmw = 32; *bnw = 128; break;
+    case 2: *bmw = 64; *bnw = 64; break;
+    default: *bmw = 128; *bnw = 64; break;
+  }
+}
+
+void conv_wgrad_launch(const WgradParams& p, int chunk, hipStream_t stream) {
+  const int v = wgrad_variant(p.Cout, p.K);
+  if (chunk == 8) {
+    switch (v) {
+      case 0: launch_w<16, 128, 16, 32, 8>(p, stream); break;
+      case 1: launch_w<32, 128, 32, 32, 8>(p, stream); break;
+      case 2: launch_w<64, 64, 32, 32, 8>(p, stream); break;
+      default: launch_w<128, 64, 64, 32, 8>(p, stream); break;
+    }
+  } else {
+    switch (v) {
+      case 0: launch_w<16, 128, 16, 32, 4>(p, stream); break;
+      case 1: launch_w<32, 128, 32, 32, 4>(p, stream); break;
+      case 2: launch_w<64, 64, 32, 32, 4>(p, stream); break;
+      default: launch_w<128, 64, 64, 32, 4>(p, stream); break;
+    }
+  }
+}
+
+void wgrad_reduce_launch(const float* partial, float* grad, int splits, int Cout, int taps, int Cin, int Cin_real,
+                         float scale, float beta, hipStream_t stream) {
+  const int64_t total = (int64_t)Cout * taps * Cin;
+  int blocks = (int)std::min<int64_t>((total + 255) / 256, 4096);
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, stream, partial, grad, splits, Cout, taps, Cin,
+                     Cin_real, scale, beta);
+}

@@ -1,0 +1,164 @@
+// Optimizer step, bf16 weight packing and on-device video preprocessing (gfx950).
+//
+// * sgd_momentum_kernel: one launch over the flat fp32 master buffer (all 330+ parameter tensors):
+//   g' = g*gscale + wd*p ; buf = first ? g' : m*buf + g' ; p -= lr*buf  (torch.optim.SGD semantics,
+//   dampening 0, no nesterov).  lr is read from device memory so a captured HIP graph
+//   replays with the live cosine schedule value.  Non-finite gradients raise a device flag (fp16 scaler).
+// * pack_weights_kernel: multi-tensor fp32 [Cout][Cin][kt][kh][kw] -> bf16 packed forward layout
+//   [Cout][taps][Cin_pad] and dgrad layout [Cin][taps][Cout] in one launch (gridDim.y = tensor).
+// * video_preprocess_kernel: uint8 THWC decoded frames -> normalised bf16 NDHWC RGB0 clip: temporal
+//   index gather (UniformTemporalSubsample / PackPathway), bilinear short-side resize (align_corners =
+//   False, PyTorch source-index rule), crop, horizontal flip, (x/255 - mean)/std, all in one pass
+//   (normalisation commutes with the bilinear resize since the weights sum to 1).
+#include "common.h"
+
+namespace {
+
+__global__ void sgd_momentum_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ buf,
+                                    int64_t n, const float* __restrict__ lr_ptr, float momentum, float wd,
+                                    float gscale, int first, int* __restrict__ found_inf) {
+  const float lr = *lr_ptr;
+  const int64_t n4 = n >> 2;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    float4 pv = reinterpret_cast<float4*>(p)[i];
+    float4 gv = reinterpret_cast<const float4*>(g)[i];
+    float4 bv = first ? float4{0, 0, 0, 0} : reinterpret_cast<float4*>(buf)[i];
+    float* pp = &pv.x; float* gg = &gv.x; float* bb = &bv.x;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float gr = gg[e] * gscale;
+      if (found_inf && !isfinite(gr)) *found_inf = 1;
+      gr += wd * pp[e];
+      bb[e] = first ? gr : momentum * bb[e] + gr;
+      pp[e] -= lr * bb[e];
+    }
+    reinterpret_cast<float4*>(p)[i] = pv;
+    reinterpret_cast<float4*>(buf)[i] = bv;
+  }
+  // tail
+  if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
+    const int64_t i = (n4 << 2) + threadIdx.x;
+    float gr = g[i] * gscale;
+    if (found_inf && !isfinite(gr)) *found_inf = 1;
+    gr += wd * p[i];
+    buf[i] = first ? gr : momentum * buf[i] + gr;
+    p[i] -= lr * buf[i];
+  }
+}
+
+struct PackDesc {
+  int64_t src;     // offset in fp32 master buffer
+  int64_t fwd;     // offset in bf16 forward-pack buffer
+  int64_t dgr;     // offset in bf16 dgrad-pack buffer (-1: none)
+  int cout, cin, cin_pad, taps;
+};
+
+__global__ void pack_weights_kernel(const float* __restrict__ master, uint16_t* __restrict__ fwd,
+                                    uint16_t* __restrict__ dgr, const PackDesc* __restrict__ descs) {
+  const PackDesc d = descs[blockIdx.y];
+  const float* src = master + d.src;
+  const int64_t nf = (int64_t)d.cout * d.taps * d.cin_pad;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nf; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = i % d.cin_pad;
+    const int64_t r = i / d.cin_pad;
+    const int tap = r % d.taps;
+    const int n = r / d.taps;
+    const float v = c < d.cin ? src[((int64_t)n * d.cin + c) * d.taps + tap] : 0.f;
+    fwd[d.fwd + i] = f2bf(v);
+  }
+  if (d.dgr >= 0) {
+    const int64_t nd = (int64_t)d.cin * d.taps * d.cout;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nd; i += (int64_t)gridDim.x * blockDim.x) {
+      const int n = i % d.cout;
+      const int64_t r = i / d.cout;
+      const int tap = r % d.taps;
+      const int c = r / d.taps;
+      dgr[d.dgr + i] = f2bf(src[((int64_t)n * d.cin + c) * d.taps + tap]);
+    }
+  }
+}
+
+// frames: [B][Ts][Hs][Ws][3] uint8 ; tidx: [B][T] source frame index ; box: [B][4] = (rh, rw, top, left) ;
+// flip: [B] ; out: [B][T][S][S][4] bf16 (channel 3 = 0)
+__global__ void video_preprocess_kernel(const uint8_t* __restrict__ frames, int Ts, int Hs, int Ws,
+                                        const int* __restrict__ tidx, const int* __restrict__ box,
+                                        const int* __restrict__ flip, int T, int S, float m0, float m1, float m2,
+                                        float is0, float is1, float is2, uint16_t* __restrict__ out, int B) {
+  const int64_t total = (int64_t)B * T * S * S;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t r = i;
+    const int x = r % S; r /= S;
+    const int y = r % S; r /= S;
+    const int t = r % T; r /= T;
+    const int b = (int)r;
+    const int rh = box[b * 4 + 0], rw = box[b * 4 + 1], top = box[b * 4 + 2], left = box[b * 4 + 3];
+    const int xr = (flip[b] ? (S - 1 - x) : x) + left;
+    const int yr = y + top;
+    const float sy = fmaxf(((float)yr + 0.5f) * ((float)Hs / (float)rh) - 0.5f, 0.f);
+    const float sx = fmaxf(((float)xr + 0.5f) * ((float)Ws / (float)rw) - 0.5f, 0.f);
+    const int y0 = min((int)sy, Hs - 1), x0 = min((int)sx, Ws - 1);
+    const int y1 = min(y0 + 1, Hs - 1), x1 = min(x0 + 1, Ws - 1);
+    const float ly = sy - (float)y0, lx = sx - (float)x0;
+    const uint8_t* f = frames + ((int64_t)b * Ts + tidx[b * T + t]) * Hs * Ws * 3;
+    const uint8_t* p00 = f + ((int64_t)y0 * Ws + x0) * 3;
+    const uint8_t* p01 = f + ((int64_t)y0 * Ws + x1) * 3;
+    const uint8_t* p10 = f + ((int64_t)y1 * Ws + x0) * 3;
+    const uint8_t* p11 = f + ((int64_t)y1 * Ws + x1) * 3;
+    float v[4];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const float top_ = (1.f - lx) * (float)p00[c] + lx * (float)p01[c];
+      const float bot_ = (1.f - lx) * (float)p10[c] + lx * (float)p11[c];
+      v[c] = (1.f - ly) * top_ + ly * bot_;
+    }
+    v[0] = (v[0] * (1.f / 255.f) - m0) * is0;
+    v[1] = (v[1] * (1.f / 255.f) - m1) * is1;
+    v[2] = (v[2] * (1.f / 255.f) - m2) * is2;
+    v[3] = 0.f;
+    *reinterpret_cast<uint2*>(out + i * 4) = pack4(v);
+  }
+}
+
+// synthetic decoded frames on device: deterministic hash -> uint8 (no zeros: DVFS, BASELINE.md protocol)
+__global__ void synth_frames_kernel(uint8_t* __restrict__ out, int64_t n, uint32_t seed) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t h = (uint32_t)i * 2654435761u ^ seed;
+    h ^= h >> 16; h *= 0x7feb352du; h ^= h >> 15; h *= 0x846ca68bu; h ^= h >> 16;
+    out[i] = (uint8_t)h;
+  }
+}
+
+}  // namespace
+
+void sgd_momentum_launch(float* p, const float* g, float* buf, int64_t n, const float* lr, float momentum, float wd,
+                         float gscale, int first, int* found_inf, hipStream_t s) {
+  int64_t blocks = ((n >> 2) + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(sgd_momentum_kernel, dim3((int)blocks), dim3(256), 0, s, p, g, buf, n, lr, momentum, wd, gscale,
+                     first, found_inf);
+}
+
+void pack_weights_launch(const float* master, uint16_t* fwd, uint16_t* dgr, const void* descs, int ntensors,
+                         hipStream_t s) {
+  hipLaunchKernelGGL(pack_weights_kernel, dim3(64, ntensors), dim3(256), 0, s, master, fwd, dgr,
+                     reinterpret_cast<const PackDesc*>(descs));
+}
+
+int pack_desc_size() { return (int)sizeof(PackDesc); }
+
+void video_preprocess_launch(const uint8_t* frames, int B, int Ts, int Hs, int Ws, const int* tidx, const int* box,
+                             const int* flip, int T, int S, const float* mean, const float* std_, uint16_t* out,
+                             hipStream_t s) {
+  const int64_t total = (int64_t)B * T * S * S;
+  int64_t blocks = (total + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(video_preprocess_kernel, dim3((int)blocks), dim3(256), 0, s, frames, Ts, Hs, Ws, tidx, box, flip,
+                     T, S, mean[0], mean[1], mean[2], 1.f / std_[0], 1.f / std_[1], 1.f / std_[2], out, B);
+}
+
+void synth_frames_launch(uint8_t* out, int64_t n, uint32_t seed, hipStream_t s) {
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(synth_frames_kernel, dim3((int)blocks), dim3(256), 0, s, out, n, seed);
+}
