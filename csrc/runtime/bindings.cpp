@@ -1,0 +1,275 @@
+// pybind11 bindings of the gfx950 kernels (module pytorchvideo_accelerate_amd._C).
+//
+// Thin, allocation-free launch shims: every output buffer is pre-allocated by the Python executor
+// (so a whole training step can be captured into a HIP graph), kernels run on PyTorch's current HIP
+// stream, and shapes arrive as plain ints from the executor's static plan.
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include <hip/hip_runtime.h>
+
+#include "../kernels/conv_params.h"
+
+// ---- kernel launchers (defined in csrc/kernels/*.hip) ----
+void conv_igemm_launch(const ConvParams& p, int chunk, bool dgrad, hipStream_t stream);
+int conv_igemm_m_tiles(int M, int N);
+void conv_wgrad_launch(const WgradParams& p, int chunk, hipStream_t stream);
+void conv_wgrad_tile(int Cout, int K, int* bmw, int* bnw);
+void wgrad_reduce_launch(const float* partial, float* grad, int splits, int Cout, int taps, int Cin, int Cin_real,
+                         float scale, float beta, hipStream_t stream);
+void bn_finalize_launch(const float* part, int tiles, int C, int64_t count, const float* gamma, const float* beta,
+                        float* rm, float* rv, int64_t* nbt, float momentum, float eps, float* smean, float* srstd,
+                        float* scale, float* shift, hipStream_t s);
+void bn_eval_affine_launch(int C, const float* gamma, const float* beta, const float* rm, const float* rv, float eps,
+                           float* scale, float* shift, hipStream_t s);
+void bn_act_launch(const uint16_t* y, int ldy, uint16_t* out, int ldo, const float* scale, const float* shift,
+                   int relu, int64_t M, int C, hipStream_t s);
+void res_out_launch(const uint16_t* yc, const float* sc, const float* hc, const uint16_t* y1, const float* s1,
+                    const float* h1, const uint16_t* x, int ldx, uint16_t* out, int ldo, int64_t M, int C,
+                    hipStream_t s);
+int bn_bwd_reduce_blocks(int64_t M, int C, int* rows_per_block);
+void bn_bwd_reduce_launch(const uint16_t* g, int ldg, int mask_mode, const uint16_t* mo, int ldm, const float* ms,
+                          const float* mh, const uint16_t* y0, const float* mean0, const float* rstd0,
+                          const uint16_t* y1, const float* mean1, const float* rstd1, int64_t M, int C, int blocks,
+                          int rows_per_block, float* part, hipStream_t s);
+void bn_bwd_finalize_launch(const float* part, int blocks, int C, int64_t count, int which, const float* gamma,
+                            const float* mean, const float* rstd, float* dgamma, float* dbeta, float beta_acc,
+                            float* coef, hipStream_t s);
+void bn_bwd_apply_launch(const uint16_t* g, int ldg, int mask_mode, const uint16_t* mo, int ldm, const float* ms,
+                         const float* mh, const uint16_t* y0, const float* coef0, uint16_t* dy0, const uint16_t* y1,
+                         const float* coef1, uint16_t* dy1, uint16_t* dzout, int lddz, int dz_accum, int64_t M, int C,
+                         hipStream_t s);
+void stem_pool_fwd_launch(const uint16_t* y, const float* scale, const float* shift, uint16_t* out, uint8_t* arg,
+                          int NT_, int H, int W, int Ho, int Wo, int C, hipStream_t s);
+void stem_pool_bwd_launch(const uint16_t* dout, int ldd, const uint8_t* arg, uint16_t* dact, int NT_, int H, int W,
+                          int Ho, int Wo, int C, hipStream_t s);
+void avgpool_fwd_launch(const uint16_t* x, int N, int T, int H, int W, int C, int kt, int kh, int kw, float* out,
+                        int ldo, int coff, hipStream_t s);
+void avgpool_bwd_launch(const float* dout, int ldo, int coff, int N, int T, int H, int W, int C, int kt, int kh,
+                        int kw, uint16_t* dx, hipStream_t s);
+void sgd_momentum_launch(float* p, const float* g, float* buf, int64_t n, const float* lr, float momentum, float wd,
+                         float gscale, int first, int* found_inf, hipStream_t s);
+void pack_weights_launch(const float* master, uint16_t* fwd, uint16_t* dgr, const void* descs, int ntensors,
+                         hipStream_t s);
+int pack_desc_size();
+void video_preprocess_launch(const uint8_t* frames, int B, int Ts, int Hs, int Ws, const int* tidx, const int* box,
+                             const int* flip, int T, int S, const float* mean, const float* std_, uint16_t* out,
+                             hipStream_t s);
+void synth_frames_launch(uint8_t* out, int64_t n, uint32_t seed, hipStream_t s);
+
+namespace {
+
+using OptT = c10::optional<at::Tensor>;
+
+inline hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
+
+inline void check_dev(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.is_contiguous() || t.dim() <= 2, name, " must be contiguous");
+}
+inline const uint16_t* bfp(const at::Tensor& t) {
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, "expected bf16 tensor");
+  return reinterpret_cast<const uint16_t*>(t.data_ptr());
+}
+inline uint16_t* bfpm(const at::Tensor& t) {
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, "expected bf16 tensor");
+  return reinterpret_cast<uint16_t*>(t.data_ptr());
+}
+inline const uint16_t* bfo(const OptT& t) { return t.has_value() ? bfp(*t) : nullptr; }
+inline uint16_t* bfom(const OptT& t) { return t.has_value() ? bfpm(*t) : nullptr; }
+inline float* f32(const at::Tensor& t) {
+  TORCH_CHECK(t.scalar_type() == at::kFloat, "expected fp32 tensor");
+  return t.data_ptr<float>();
+}
+inline float* f32o(const OptT& t) { return t.has_value() ? f32(*t) : nullptr; }
+
+// geometry vector: [M, Ngemm, K, Cg, ldx, ldy, Gt, Gh, Gw, Rt, Rh, Rw, kt, kh, kw, st, sh, sw, pt, ph, pw]
+void conv_igemm(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, const OptT& stats,
+                const OptT& scale, const OptT& shift, int64_t affine, int64_t accum, std::vector<int64_t> g,
+                int64_t chunk, bool dgrad) {
+  TORCH_CHECK(g.size() == 21, "conv geometry must have 21 entries");
+  ConvParams p{};
+  p.x = bfp(x); p.w = bfp(w); p.y = bfpm(y);
+  p.stats = f32o(stats);
+  p.in_scale = f32o(scale); p.in_shift = f32o(shift);
+  p.affine = (int)affine; p.accum = (int)accum;
+  p.M = g[0]; p.Ngemm = g[1]; p.K = g[2]; p.Cg = g[3]; p.ldx = g[4]; p.ldy = g[5];
+  p.Gt = g[6]; p.Gh = g[7]; p.Gw = g[8]; p.Rt = g[9]; p.Rh = g[10]; p.Rw = g[11];
+  p.kt = g[12]; p.kh = g[13]; p.kw = g[14]; p.st = g[15]; p.sh = g[16]; p.sw = g[17];
+  p.pt = g[18]; p.ph = g[19]; p.pw = g[20];
+  TORCH_CHECK(p.Cg % chunk == 0 && p.Cg > 0, "gathered channels must be a multiple of the chunk");
+  TORCH_CHECK(p.Ngemm % 4 == 0, "output channels must be a multiple of 4");
+  TORCH_CHECK(p.ldx % chunk == 0 && p.ldy % 4 == 0, "row strides must keep vector alignment");
+  TORCH_CHECK(!affine || (scale.has_value() && shift.has_value()), "affine needs scale/shift");
+  TORCH_CHECK(p.K == p.kt * p.kh * p.kw * p.Cg, "K must equal taps*Cg");
+  if (p.M == 0) return;
+  conv_igemm_launch(p, (int)chunk, dgrad, cur_stream());
+}
+
+int64_t conv_m_tiles(int64_t M, int64_t N) { return conv_igemm_m_tiles((int)M, (int)N); }
+
+std::vector<int64_t> wgrad_tile(int64_t Cout, int64_t K) {
+  int a, b;
+  conv_wgrad_tile((int)Cout, (int)K, &a, &b);
+  return {a, b};
+}
+
+// geometry: [P, Cout, K, Cin, ldd, ldx, Ti, Hi, Wi, To, Ho, Wo, kt, kh, kw, st, sh, sw, pt, ph, pw, splits, pps]
+void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& partial, const OptT& scale,
+                const OptT& shift, int64_t affine, std::vector<int64_t> g, int64_t chunk) {
+  TORCH_CHECK(g.size() == 23, "wgrad geometry must have 23 entries");
+  WgradParams p{};
+  p.dy = bfp(dy); p.x = bfp(x); p.partial = f32(partial);
+  p.in_scale = f32o(scale); p.in_shift = f32o(shift); p.affine = (int)affine;
+  p.P = g[0]; p.Cout = g[1]; p.K = g[2]; p.Cin = g[3]; p.ldd = g[4]; p.ldx = g[5];
+  p.Ti = g[6]; p.Hi = g[7]; p.Wi = g[8]; p.To = g[9]; p.Ho = g[10]; p.Wo = g[11];
+  p.kt = g[12]; p.kh = g[13]; p.kw = g[14]; p.st = g[15]; p.sh = g[16]; p.sw = g[17];
+  p.pt = g[18]; p.ph = g[19]; p.pw = g[20]; p.splits = g[21]; p.p_per_split = g[22];
+  TORCH_CHECK(p.Cin % chunk == 0 && p.Cout % 8 == 0, "wgrad channel alignment");
+  TORCH_CHECK(p.p_per_split % 32 == 0, "p_per_split must be a multiple of 32");
+  TORCH_CHECK(partial.numel() >= (int64_t)p.splits * p.Cout * p.K, "partial slab too small");
+  conv_wgrad_launch(p, (int)chunk, cur_stream());
+}
+
+void wgrad_reduce(const at::Tensor& partial, const at::Tensor& grad, int64_t splits, int64_t Cout, int64_t taps,
+                  int64_t Cin, int64_t Cin_real, double scale, double beta) {
+  wgrad_reduce_launch(f32(partial), f32(grad), (int)splits, (int)Cout, (int)taps, (int)Cin, (int)Cin_real,
+                      (float)scale, (float)beta, cur_stream());
+}
+
+void bn_finalize(const at::Tensor& part, int64_t tiles, int64_t C, int64_t count, const at::Tensor& gamma,
+                 const at::Tensor& beta, const OptT& rm, const OptT& rv, const OptT& nbt, double momentum, double eps,
+                 const at::Tensor& smean, const at::Tensor& srstd, const at::Tensor& scale, const at::Tensor& shift) {
+  int64_t* nb = nbt.has_value() ? nbt->data_ptr<int64_t>() : nullptr;
+  bn_finalize_launch(f32(part), (int)tiles, (int)C, count, f32(gamma), f32(beta), f32o(rm), f32o(rv), nb,
+                     (float)momentum, (float)eps, f32(smean), f32(srstd), f32(scale), f32(shift), cur_stream());
+}
+
+void bn_eval_affine(const at::Tensor& gamma, const at::Tensor& beta, const at::Tensor& rm, const at::Tensor& rv,
+                    double eps, const at::Tensor& scale, const at::Tensor& shift) {
+  bn_eval_affine_launch((int)gamma.numel(), f32(gamma), f32(beta), f32(rm), f32(rv), (float)eps, f32(scale),
+                        f32(shift), cur_stream());
+}
+
+void bn_act(const at::Tensor& y, int64_t ldy, const at::Tensor& out, int64_t ldo, const at::Tensor& scale,
+            const at::Tensor& shift, int64_t relu, int64_t M, int64_t C) {
+  TORCH_CHECK(C % 8 == 0 && ldy % 8 == 0 && ldo % 8 == 0, "bn_act alignment");
+  bn_act_launch(bfp(y), (int)ldy, bfpm(out), (int)ldo, f32(scale), f32(shift), (int)relu, M, (int)C, cur_stream());
+}
+
+void res_out(const at::Tensor& yc, const at::Tensor& sc, const at::Tensor& hc, const OptT& y1, const OptT& s1,
+             const OptT& h1, const OptT& x, int64_t ldx, const at::Tensor& out, int64_t ldo, int64_t M, int64_t C) {
+  TORCH_CHECK(y1.has_value() || x.has_value(), "res_out needs a shortcut");
+  res_out_launch(bfp(yc), f32(sc), f32(hc), bfo(y1), f32o(s1), f32o(h1), bfo(x), (int)ldx, bfpm(out), (int)ldo, M,
+                 (int)C, cur_stream());
+}
+
+std::vector<int64_t> bn_bwd_blocks(int64_t M, int64_t C) {
+  int rpb;
+  int b = bn_bwd_reduce_blocks(M, (int)C, &rpb);
+  return {b, rpb};
+}
+
+void bn_bwd_reduce(const at::Tensor& g, int64_t ldg, int64_t mask_mode, const OptT& mo, int64_t ldm, const OptT& ms,
+                   const OptT& mh, const at::Tensor& y0, const at::Tensor& mean0, const at::Tensor& rstd0,
+                   const OptT& y1, const OptT& mean1, const OptT& rstd1, int64_t M, int64_t C, int64_t blocks,
+                   int64_t rpb, const at::Tensor& part) {
+  TORCH_CHECK(C % 8 == 0 && C <= 2048, "bn_bwd_reduce channel constraint");
+  bn_bwd_reduce_launch(bfp(g), (int)ldg, (int)mask_mode, bfo(mo), (int)ldm, f32o(ms), f32o(mh), bfp(y0), f32(mean0),
+                       f32(rstd0), bfo(y1), f32o(mean1), f32o(rstd1), M, (int)C, (int)blocks, (int)rpb, f32(part),
+                       cur_stream());
+}
+
+void bn_bwd_finalize(const at::Tensor& part, int64_t blocks, int64_t C, int64_t count, int64_t which,
+                     const at::Tensor& gamma, const at::Tensor& mean, const at::Tensor& rstd, const OptT& dgamma,
+                     const OptT& dbeta, double beta_acc, const at::Tensor& coef) {
+  bn_bwd_finalize_launch(f32(part), (int)blocks, (int)C, count, (int)which, f32(gamma), f32(mean), f32(rstd),
+                         f32o(dgamma), f32o(dbeta), (float)beta_acc, f32(coef), cur_stream());
+}
+
+void bn_bwd_apply(const at::Tensor& g, int64_t ldg, int64_t mask_mode, const OptT& mo, int64_t ldm, const OptT& ms,
+                  const OptT& mh, const at::Tensor& y0, const at::Tensor& coef0, const at::Tensor& dy0,
+                  const OptT& y1, const OptT& coef1, const OptT& dy1, const OptT& dzout, int64_t lddz,
+                  int64_t dz_accum, int64_t M, int64_t C) {
+  bn_bwd_apply_launch(bfp(g), (int)ldg, (int)mask_mode, bfo(mo), (int)ldm, f32o(ms), f32o(mh), bfp(y0), f32(coef0),
+                      bfpm(dy0), bfo(y1), f32o(coef1), bfom(dy1), bfom(dzout), (int)lddz, (int)dz_accum, M, (int)C,
+                      cur_stream());
+}
+
+void stem_pool_fwd(const at::Tensor& y, const at::Tensor& scale, const at::Tensor& shift, const at::Tensor& out,
+                   const at::Tensor& arg, int64_t NT_, int64_t H, int64_t W, int64_t Ho, int64_t Wo, int64_t C) {
+  stem_pool_fwd_launch(bfp(y), f32(scale), f32(shift), bfpm(out), arg.data_ptr<uint8_t>(), (int)NT_, (int)H, (int)W,
+                       (int)Ho, (int)Wo, (int)C, cur_stream());
+}
+
+void stem_pool_bwd(const at::Tensor& dout, int64_t ldd, const at::Tensor& arg, const at::Tensor& dact, int64_t NT_,
+                   int64_t H, int64_t W, int64_t Ho, int64_t Wo, int64_t C) {
+  stem_pool_bwd_launch(bfp(dout), (int)ldd, arg.data_ptr<uint8_t>(), bfpm(dact), (int)NT_, (int)H, (int)W, (int)Ho,
+                       (int)Wo, (int)C, cur_stream());
+}
+
+void avgpool_fwd(const at::Tensor& x, std::vector<int64_t> dims, std::vector<int64_t> k, const at::Tensor& out,
+                 int64_t ldo, int64_t coff) {
+  avgpool_fwd_launch(bfp(x), (int)dims[0], (int)dims[1], (int)dims[2], (int)dims[3], (int)dims[4], (int)k[0],
+                     (int)k[1], (int)k[2], f32(out), (int)ldo, (int)coff, cur_stream());
+}
+
+void avgpool_bwd(const at::Tensor& dout, int64_t ldo, int64_t coff, std::vector<int64_t> dims, std::vector<int64_t> k,
+                 const at::Tensor& dx) {
+  avgpool_bwd_launch(f32(dout), (int)ldo, (int)coff, (int)dims[0], (int)dims[1], (int)dims[2], (int)dims[3],
+                     (int)dims[4], (int)k[0], (int)k[1], (int)k[2], bfpm(dx), cur_stream());
+}
+
+void sgd_momentum(const at::Tensor& p, const at::Tensor& g, const at::Tensor& buf, const at::Tensor& lr,
+                  double momentum, double wd, double gscale, int64_t first, const OptT& found_inf) {
+  TORCH_CHECK(p.numel() == g.numel() && p.numel() == buf.numel(), "sgd buffers must match");
+  int* fi = found_inf.has_value() ? found_inf->data_ptr<int>() : nullptr;
+  sgd_momentum_launch(f32(p), f32(g), f32(buf), p.numel(), f32(lr), (float)momentum, (float)wd, (float)gscale,
+                      (int)first, fi, cur_stream());
+}
+
+void pack_weights(const at::Tensor& master, const at::Tensor& fwd, const at::Tensor& dgr, const at::Tensor& descs,
+                  int64_t ntensors) {
+  pack_weights_launch(f32(master), bfpm(fwd), bfpm(dgr), descs.data_ptr(), (int)ntensors, cur_stream());
+}
+
+void video_preprocess(const at::Tensor& frames, const at::Tensor& tidx, const at::Tensor& box, const at::Tensor& flip,
+                      int64_t T, int64_t S, std::vector<double> mean, std::vector<double> std_, const at::Tensor& out) {
+  TORCH_CHECK(frames.dim() == 5 && frames.size(4) == 3 && frames.scalar_type() == at::kByte, "frames [B,T,H,W,3] u8");
+  const float m[3] = {(float)mean[0], (float)mean[1], (float)mean[2]};
+  const float s[3] = {(float)std_[0], (float)std_[1], (float)std_[2]};
+  video_preprocess_launch(frames.data_ptr<uint8_t>(), (int)frames.size(0), (int)frames.size(1), (int)frames.size(2),
+                          (int)frames.size(3), tidx.data_ptr<int>(), box.data_ptr<int>(), flip.data_ptr<int>(),
+                          (int)T, (int)S, m, s, bfpm(out), cur_stream());
+}
+
+void synth_frames(const at::Tensor& out, int64_t seed) {
+  synth_frames_launch(out.data_ptr<uint8_t>(), out.numel(), (uint32_t)seed, cur_stream());
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "gfx950 HIP kernels for pytorchvideo_accelerate_amd";
+  m.def("conv_igemm", &conv_igemm);
+  m.def("conv_m_tiles", &conv_m_tiles);
+  m.def("wgrad_tile", &wgrad_tile);
+  m.def("conv_wgrad", &conv_wgrad);
+  m.def("wgrad_reduce", &wgrad_reduce);
+  m.def("bn_finalize", &bn_finalize);
+  m.def("bn_eval_affine", &bn_eval_affine);
+  m.def("bn_act", &bn_act);
+  m.def("res_out", &res_out);
+  m.def("bn_bwd_blocks", &bn_bwd_blocks);
+  m.def("bn_bwd_reduce", &bn_bwd_reduce);
+  m.def("bn_bwd_finalize", &bn_bwd_finalize);
+  m.def("bn_bwd_apply", &bn_bwd_apply);
+  m.def("stem_pool_fwd", &stem_pool_fwd);
+  m.def("stem_pool_bwd", &stem_pool_bwd);
+  m.def("avgpool_fwd", &avgpool_fwd);
+  m.def("avgpool_bwd", &avgpool_bwd);
+  m.def("sgd_momentum", &sgd_momentum);
+  m.def("pack_weights", &pack_weights);
+  m.def("pack_desc_size", &pack_desc_size);
+  m.def("video_preprocess", &video_preprocess);
+  m.def("synth_frames", &synth_frames);
+}

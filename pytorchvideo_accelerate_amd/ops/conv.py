@@ -1,0 +1,179 @@
+"""3-D convolution ops on the gfx950 implicit-GEMM kernels (NDHWC bf16).
+
+An activation is an :class:`Act`: a 2-D ``[positions, channels]`` bf16 tensor (possibly a channel
+slice of a wider buffer — its row stride is the NDHWC channel pitch) plus the (N, T, H, W) extents.
+
+* :func:`conv_fwd`   — forward; optional per-input-channel affine(+ReLU) on load (the producer's BN),
+  optional BN partial statistics of the output.
+* :func:`conv_dgrad` — data gradient (optionally accumulated into an existing gradient buffer).
+* :func:`conv_wgrad` — weight gradient, split-K over positions, reduced straight into the fp32
+  master-gradient tensor in PyTorch's ``[Cout, Cin, kt, kh, kw]`` layout.
+
+Reference semantics: ``torch.nn.functional.conv3d`` with ``bias=False`` (pytorchvideo convs,
+SURVEY.md §2.3); numerics are pinned against it in ``tests/test_kernels_gpu.py``.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional, Tuple
+
+import torch
+
+from ._ext import require
+
+Triple = Tuple[int, int, int]
+
+
+@dataclass
+class Act:
+    t: torch.Tensor      # [M, C] view, row stride = channel pitch
+    N: int
+    T: int
+    H: int
+    W: int
+
+    @property
+    def C(self) -> int:
+        return self.t.shape[1]
+
+    @property
+    def ld(self) -> int:
+        return self.t.stride(0)
+
+    @property
+    def M(self) -> int:
+        return self.N * self.T * self.H * self.W
+
+    def narrow(self, c0: int, c: int) -> "Act":
+        return Act(self.t.narrow(1, c0, c), self.N, self.T, self.H, self.W)
+
+    def to_ncthw(self) -> torch.Tensor:
+        return self.t.reshape(self.N, self.T, self.H, self.W, self.C).permute(0, 4, 1, 2, 3)
+
+    @staticmethod
+    def from_ncthw(x: torch.Tensor, c_pad: Optional[int] = None) -> "Act":
+        N, C, T, H, W = x.shape
+        y = x.permute(0, 2, 3, 4, 1)
+        if c_pad is not None and c_pad > C:
+            y = torch.nn.functional.pad(y, (0, c_pad - C))
+        y = y.contiguous().to(torch.bfloat16)
+        return Act(y.reshape(N * T * H * W, y.shape[-1]), N, T, H, W)
+
+
+@dataclass
+class ConvSpec:
+    cin: int
+    cout: int
+    k: Triple
+    stride: Triple = (1, 1, 1)
+    pad: Triple = (0, 0, 0)
+    cin_pad: int = 0          # packed input channels (stems: 3 -> 4)
+
+    def __post_init__(self):
+        if not self.cin_pad:
+            self.cin_pad = self.cin
+
+    @property
+    def taps(self) -> int:
+        return self.k[0] * self.k[1] * self.k[2]
+
+    @property
+    def chunk(self) -> int:
+        return 8 if self.cin_pad % 8 == 0 else 4
+
+    def out_dims(self, T: int, H: int, W: int) -> Triple:
+        o = []
+        for i, n in enumerate((T, H, W)):
+            o.append((n + 2 * self.pad[i] - self.k[i]) // self.stride[i] + 1)
+        return tuple(o)
+
+    def flops(self, N: int, T: int, H: int, W: int) -> int:
+        To, Ho, Wo = self.out_dims(T, H, W)
+        return 2 * N * To * Ho * Wo * self.cout * self.cin * self.taps
+
+
+def pack_weight(w: torch.Tensor, spec: ConvSpec) -> Tuple[torch.Tensor, torch.Tensor]:
+    """fp32 [Cout, Cin, kt, kh, kw] -> (bf16 forward pack [Cout, taps, Cin_pad], dgrad pack [Cin, taps, Cout]).
+
+    Host-side (torch) version used by tests and one-off packs; the training loop uses the multi-tensor
+    ``pack_weights`` kernel (ops/optim.py).
+    """
+    co, ci = w.shape[:2]
+    wf = w.reshape(co, ci, -1).permute(0, 2, 1)  # [Cout, taps, Cin]
+    if spec.cin_pad > ci:
+        wf = torch.nn.functional.pad(wf, (0, spec.cin_pad - ci))
+    wd = w.reshape(co, ci, -1).permute(1, 2, 0)  # [Cin, taps, Cout]
+    return wf.contiguous().to(torch.bfloat16), wd.contiguous().to(torch.bfloat16)
+
+
+def conv_m_tiles(M: int, N: int) -> int:
+    return require().conv_m_tiles(M, N)
+
+
+def conv_fwd(x: Act, wpack: torch.Tensor, spec: ConvSpec, out: Optional[torch.Tensor] = None,
+             stats: Optional[torch.Tensor] = None, in_scale: Optional[torch.Tensor] = None,
+             in_shift: Optional[torch.Tensor] = None, in_relu: bool = True) -> Act:
+    C = require()
+    assert x.C == spec.cin_pad, (x.C, spec.cin_pad)
+    To, Ho, Wo = spec.out_dims(x.T, x.H, x.W)
+    M = x.N * To * Ho * Wo
+    if out is None:
+        out = torch.empty(M, spec.cout, device=x.t.device, dtype=torch.bfloat16)
+    affine = 0 if in_scale is None else (2 if in_relu else 1)
+    g = [M, spec.cout, spec.taps * spec.cin_pad, spec.cin_pad, x.ld, out.stride(0),
+         x.T, x.H, x.W, To, Ho, Wo, *spec.k, *spec.stride, *spec.pad]
+    C.conv_igemm(x.t, wpack, out, stats, in_scale, in_shift, affine, 0, g, spec.chunk, False)
+    return Act(out, x.N, To, Ho, Wo)
+
+
+def conv_dgrad(dy: Act, wt_pack: torch.Tensor, spec: ConvSpec, in_dims: Triple, out: Optional[torch.Tensor] = None,
+               accum: bool = False) -> Act:
+    """dX[N,Ti,Hi,Wi,Cin] = conv_transpose(dY, W); ``accum`` adds into ``out``."""
+    C = require()
+    Ti, Hi, Wi = in_dims
+    assert dy.C == spec.cout and spec.cin % 8 == 0 and spec.cout % 8 == 0
+    M = dy.N * Ti * Hi * Wi
+    if out is None:
+        out = torch.empty(M, spec.cin, device=dy.t.device, dtype=torch.bfloat16)
+    g = [M, spec.cin, spec.taps * spec.cout, spec.cout, dy.ld, out.stride(0),
+         dy.T, dy.H, dy.W, Ti, Hi, Wi, *spec.k, *spec.stride, *spec.pad]
+    C.conv_igemm(dy.t, wt_pack, out, None, None, None, 0, 1 if accum else 0, g, 8, True)
+    return Act(out, dy.N, Ti, Hi, Wi)
+
+
+def wgrad_splits(P: int, Cout: int, K: int, target_blocks: int = 1024, min_rows: int = 512) -> Tuple[int, int]:
+    C = require()
+    bmw, bnw = C.wgrad_tile(Cout, K)
+    tiles = ((Cout + bmw - 1) // bmw) * ((K + bnw - 1) // bnw)
+    splits = max(1, min(target_blocks // max(tiles, 1), (P + min_rows - 1) // min_rows))
+    pps = (P + splits - 1) // splits
+    pps = (pps + 31) // 32 * 32
+    splits = (P + pps - 1) // pps
+    return splits, pps
+
+
+def conv_wgrad(dy: Act, x: Act, spec: ConvSpec, grad: torch.Tensor, workspace: Optional[torch.Tensor] = None,
+               in_scale: Optional[torch.Tensor] = None, in_shift: Optional[torch.Tensor] = None,
+               in_relu: bool = True, scale: float = 1.0, beta: float = 0.0,
+               splits_pps: Optional[Tuple[int, int]] = None) -> torch.Tensor:
+    """grad (fp32, [Cout, Cin, kt, kh, kw]) = beta*grad + scale * dW."""
+    C = require()
+    P = dy.M
+    K = spec.taps * spec.cin_pad
+    splits, pps = splits_pps or wgrad_splits(P, spec.cout, K)
+    need = splits * spec.cout * K
+    if workspace is None or workspace.numel() < need:
+        workspace = torch.empty(need, device=dy.t.device, dtype=torch.float32)
+    affine = 0 if in_scale is None else (2 if in_relu else 1)
+    g = [P, spec.cout, K, spec.cin_pad, dy.ld, x.ld, x.T, x.H, x.W, dy.T, dy.H, dy.W,
+         *spec.k, *spec.stride, *spec.pad, splits, pps]
+    C.conv_wgrad(dy.t, x.t, workspace, in_scale, in_shift, affine, g, spec.chunk)
+    C.wgrad_reduce(workspace, grad, splits, spec.cout, spec.taps, spec.cin_pad, spec.cin, scale, beta)
+    return grad
+
+
+# --------------------------------------------------------------------------------------------
+# torch references (used by tests and by the CPU path)
+# --------------------------------------------------------------------------------------------
+def ref_conv(x_ncthw: torch.Tensor, w: torch.Tensor, spec: ConvSpec) -> torch.Tensor:
+    return torch.nn.functional.conv3d(x_ncthw, w, None, spec.stride, spec.pad)

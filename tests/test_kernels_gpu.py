@@ -1,0 +1,127 @@
+"""Numerics of the gfx950 HIP kernels against plain PyTorch fp32 references of the same op.
+
+Random (non-zero) data, every conv class of SlowFast-R50 at a reduced batch:
+pointwise / temporal / spatial / stride-2 / lateral fusion / both stems / tiny-channel fast pathway.
+"""
+import pytest
+import torch
+
+from pytorchvideo_accelerate_amd.ops.conv import Act, ConvSpec, conv_dgrad, conv_fwd, conv_wgrad, pack_weight
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+# (cin, cout, k, stride, pad, (N, T, H, W))
+CASES = [
+    (64, 256, (1, 1, 1), (1, 1, 1), (0, 0, 0), (2, 4, 14, 14)),      # slow pointwise
+    (256, 64, (3, 1, 1), (1, 1, 1), (1, 0, 0), (2, 8, 14, 14)),      # slow temporal
+    (64, 64, (1, 3, 3), (1, 1, 1), (0, 1, 1), (2, 4, 14, 14)),       # slow spatial
+    (128, 128, (1, 3, 3), (1, 2, 2), (0, 1, 1), (2, 4, 28, 28)),     # spatial stride 2
+    (320, 512, (1, 1, 1), (1, 2, 2), (0, 0, 0), (2, 4, 14, 14)),     # branch1 stride 2
+    (8, 16, (7, 1, 1), (4, 1, 1), (3, 0, 0), (2, 32, 14, 14)),       # lateral fusion
+    (8, 8, (3, 1, 1), (1, 1, 1), (1, 0, 0), (2, 16, 14, 14)),        # fast temporal, N=8
+    (16, 16, (1, 3, 3), (1, 2, 2), (0, 1, 1), (2, 8, 14, 14)),       # fast spatial s2
+    (32, 8, (3, 1, 1), (1, 1, 1), (1, 0, 0), (2, 16, 7, 7)),         # fast conv_a
+    (80, 64, (1, 1, 1), (1, 1, 1), (0, 0, 0), (2, 4, 14, 14)),       # concat input (80 ch)
+    (512, 2048, (1, 1, 1), (1, 1, 1), (0, 0, 0), (2, 2, 7, 7)),      # res5 conv_c
+]
+
+STEMS = [
+    (3, 64, (1, 7, 7), (1, 2, 2), (0, 3, 3), (2, 2, 32, 32)),
+    (3, 8, (5, 7, 7), (1, 2, 2), (2, 3, 3), (2, 6, 32, 32)),
+]
+
+
+def rel_err(a, b):
+    return ((a.float() - b.float()).abs().max() / b.float().abs().max().clamp_min(1e-6)).item()
+
+
+def _mk(case, seed=0):
+    cin, cout, k, s, p, (N, T, H, W) = case
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    x = torch.randn(N, cin, T, H, W, generator=g).to(DEV).to(torch.bfloat16).float()
+    w = (torch.randn(cout, cin, *k, generator=g) / (cin * k[0] * k[1] * k[2]) ** 0.5).to(DEV)
+    w = w.to(torch.bfloat16).float()
+    spec = ConvSpec(cin, cout, k, s, p, cin_pad=4 if cin == 3 else 0)
+    return x, w, spec
+
+
+@pytest.mark.parametrize("case", CASES + STEMS)
+def test_conv_fwd(case):
+    x, w, spec = _mk(case)
+    ref = torch.nn.functional.conv3d(x, w, None, spec.stride, spec.pad)
+    wf, _ = pack_weight(w, spec)
+    xa = Act.from_ncthw(x, spec.cin_pad)
+    y = conv_fwd(xa, wf, spec)
+    assert rel_err(y.to_ncthw(), ref) < 1e-2
+
+
+@pytest.mark.parametrize("case", CASES[:4])
+def test_conv_fwd_stats_and_affine(case):
+    x, w, spec = _mk(case, seed=1)
+    C = spec.cin
+    sc = torch.rand(C, device=DEV) + 0.5
+    sh = torch.randn(C, device=DEV) * 0.5
+    xa = Act.from_ncthw(x)
+    xt = torch.relu(x * sc.view(1, C, 1, 1, 1) + sh.view(1, C, 1, 1, 1))
+    ref = torch.nn.functional.conv3d(xt, w, None, spec.stride, spec.pad)
+    wf, _ = pack_weight(w, spec)
+    from pytorchvideo_accelerate_amd.ops.conv import conv_m_tiles
+    To, Ho, Wo = spec.out_dims(xa.T, xa.H, xa.W)
+    M = xa.N * To * Ho * Wo
+    tiles = conv_m_tiles(M, spec.cout)
+    stats = torch.empty(tiles, 2, spec.cout, device=DEV)
+    y = conv_fwd(xa, wf, spec, stats=stats, in_scale=sc, in_shift=sh, in_relu=True)
+    assert rel_err(y.to_ncthw(), ref) < 1.5e-2
+    yf = y.t.float()
+    s = stats.sum(0)
+    torch.testing.assert_close(s[0], yf.sum(0), rtol=1e-3, atol=1e-2 * yf.abs().sum(0).max().item() / M ** 0.5)
+    torch.testing.assert_close(s[1], (yf * yf).sum(0), rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("case", [c for c in CASES if c[0] % 8 == 0])
+def test_conv_dgrad(case):
+    x, w, spec = _mk(case, seed=2)
+    x.requires_grad_(True)
+    ref_y = torch.nn.functional.conv3d(x, w, None, spec.stride, spec.pad)
+    gy = torch.randn_like(ref_y).to(torch.bfloat16).float()
+    ref_y.backward(gy)
+    _, wd = pack_weight(w, spec)
+    dy = Act.from_ncthw(gy)
+    dx = conv_dgrad(dy, wd, spec, tuple(x.shape[2:]))
+    assert rel_err(dx.to_ncthw(), x.grad) < 1e-2
+    # accumulate mode
+    dx2 = conv_dgrad(dy, wd, spec, tuple(x.shape[2:]), out=dx.t.clone(), accum=True)
+    assert rel_err(dx2.to_ncthw(), 2 * x.grad) < 1.5e-2
+
+
+@pytest.mark.parametrize("case", CASES + STEMS)
+def test_conv_wgrad(case):
+    x, w, spec = _mk(case, seed=3)
+    w.requires_grad_(True)
+    ref_y = torch.nn.functional.conv3d(x, w, None, spec.stride, spec.pad)
+    gy = torch.randn_like(ref_y).to(torch.bfloat16).float()
+    ref_y.backward(gy)
+    grad = torch.zeros_like(w)
+    conv_wgrad(Act.from_ncthw(gy), Act.from_ncthw(x, spec.cin_pad), spec, grad)
+    assert rel_err(grad, w.grad) < 1e-2
+    # beta / scale accumulate
+    conv_wgrad(Act.from_ncthw(gy), Act.from_ncthw(x, spec.cin_pad), spec, grad, scale=0.5, beta=1.0)
+    assert rel_err(grad, 1.5 * w.grad) < 1e-2
+
+
+def test_conv_wgrad_affine():
+    case = CASES[2]
+    x, w, spec = _mk(case, seed=4)
+    C = spec.cin
+    sc = torch.rand(C, device=DEV) + 0.5
+    sh = torch.randn(C, device=DEV) * 0.5
+    xt = torch.relu(x * sc.view(1, C, 1, 1, 1) + sh.view(1, C, 1, 1, 1))
+    w.requires_grad_(True)
+    ref_y = torch.nn.functional.conv3d(xt, w, None, spec.stride, spec.pad)
+    gy = torch.randn_like(ref_y).to(torch.bfloat16).float()
+    ref_y.backward(gy)
+    grad = torch.zeros_like(w)
+    conv_wgrad(Act.from_ncthw(gy), Act.from_ncthw(x), spec, grad, in_scale=sc, in_shift=sh)
+    assert rel_err(grad, w.grad) < 1.5e-2
