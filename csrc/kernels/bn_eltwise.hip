@@ -265,7 +265,7 @@ __global__ void bn_bwd_apply_kernel(const uint16_t* __restrict__ g, int ldg, int
 // ------------------------------------------------------------------------------------------
 __global__ void stem_pool_fwd_kernel(const uint16_t* __restrict__ y, const float* __restrict__ scale,
                                      const float* __restrict__ shift, uint16_t* __restrict__ out,
-                                     uint8_t* __restrict__ arg, int NT_, int H, int W, int Ho, int Wo, int C) {
+                                     uint8_t* __restrict__ arg, int NT_, int H, int W, int Ho, int Wo, int C, int ldo) {
   const int vecs = C >> 3;
   const int64_t total = (int64_t)NT_ * Ho * Wo * vecs;
   for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < total; i += (int64_t)gridDim.x * NT) {
@@ -297,8 +297,9 @@ __global__ void stem_pool_fwd_kernel(const uint16_t* __restrict__ y, const float
         }
       }
     }
-    const int64_t o = ((nt * Ho + ho) * Wo + wo) * C + c;
-    *reinterpret_cast<uint4*>(out + o) = pack8(best);
+    const int64_t pos = (nt * Ho + ho) * Wo + wo;
+    const int64_t o = pos * C + c;
+    *reinterpret_cast<uint4*>(out + pos * ldo + c) = pack8(best);
     uint2 pk;
     pk.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((uint32_t)bi[3] << 24);
     pk.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | ((uint32_t)bi[7] << 24);
@@ -460,9 +461,9 @@ void bn_bwd_apply_launch(const uint16_t* g, int ldg, int mask_mode, const uint16
 }
 
 void stem_pool_fwd_launch(const uint16_t* y, const float* scale, const float* shift, uint16_t* out, uint8_t* arg,
-                          int NT_, int H, int W, int Ho, int Wo, int C, hipStream_t s) {
+                          int NT_, int H, int W, int Ho, int Wo, int C, int ldo, hipStream_t s) {
   hipLaunchKernelGGL(stem_pool_fwd_kernel, dim3(grid_for((int64_t)NT_ * Ho * Wo * (C / 8))), dim3(NT), 0, s, y, scale,
-                     shift, out, arg, NT_, H, W, Ho, Wo, C);
+                     shift, out, arg, NT_, H, W, Ho, Wo, C, ldo);
 }
 
 void stem_pool_bwd_launch(const uint16_t* dout, int ldd, const uint8_t* arg, uint16_t* dact, int NT_, int H, int W,

@@ -39,7 +39,7 @@ void bn_bwd_apply_launch(const uint16_t* g, int ldg, int mask_mode, const uint16
                          const float* coef1, uint16_t* dy1, uint16_t* dzout, int lddz, int dz_accum, int64_t M, int C,
                          hipStream_t s);
 void stem_pool_fwd_launch(const uint16_t* y, const float* scale, const float* shift, uint16_t* out, uint8_t* arg,
-                          int NT_, int H, int W, int Ho, int Wo, int C, hipStream_t s);
+                          int NT_, int H, int W, int Ho, int Wo, int C, int ldo, hipStream_t s);
 void stem_pool_bwd_launch(const uint16_t* dout, int ldd, const uint8_t* arg, uint16_t* dact, int NT_, int H, int W,
                           int Ho, int Wo, int C, hipStream_t s);
 void avgpool_fwd_launch(const uint16_t* x, int N, int T, int H, int W, int C, int kt, int kh, int kw, float* out,
@@ -196,9 +196,10 @@ void bn_bwd_apply(const at::Tensor& g, int64_t ldg, int64_t mask_mode, const Opt
 }
 
 void stem_pool_fwd(const at::Tensor& y, const at::Tensor& scale, const at::Tensor& shift, const at::Tensor& out,
-                   const at::Tensor& arg, int64_t NT_, int64_t H, int64_t W, int64_t Ho, int64_t Wo, int64_t C) {
+                   int64_t ldo, const at::Tensor& arg, int64_t NT_, int64_t H, int64_t W, int64_t Ho, int64_t Wo,
+                   int64_t C) {
   stem_pool_fwd_launch(bfp(y), f32(scale), f32(shift), bfpm(out), arg.data_ptr<uint8_t>(), (int)NT_, (int)H, (int)W,
-                       (int)Ho, (int)Wo, (int)C, cur_stream());
+                       (int)Ho, (int)Wo, (int)C, (int)ldo, cur_stream());
 }
 
 void stem_pool_bwd(const at::Tensor& dout, int64_t ldd, const at::Tensor& arg, const at::Tensor& dact, int64_t NT_,

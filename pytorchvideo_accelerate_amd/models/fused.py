@@ -1,0 +1,599 @@
+"""Fused MI355X training/eval executor for SlowFast and Slow ResNet3D.
+
+This replaces PyTorch autograd for the backbone with an explicit, static forward/backward plan over the
+gfx950 kernels (``ops/conv.py`` + ``csrc/kernels``).  Design:
+
+* Activations are NDHWC bf16 :class:`Act` views.  Each conv stores only its **raw** output ``y``; the
+  training-mode BatchNorm (+ReLU) of ``y`` is applied by the *consumer* conv while it stages its input
+  tile (per-channel affine in the MFMA prologue), so normalised activations inside a bottleneck are
+  never written to HBM.  The conv epilogue emits the BN partial sums; ``bn_finalize`` produces
+  mean/rstd, the running-stat update and the consumer affine.
+* Residual-unit outputs (consumed by two convs and the identity path) are materialised once by the
+  ``res_out`` kernel.  The slow pathway's output of a fused stage is written straight into the channel
+  slice of the concatenation buffer, and the lateral fusion's BN-ReLU writes the other slice: the
+  concat costs nothing.
+* Backward reuses the same kernels: BN backward = deterministic reduce → finalize (dγ, dβ into the flat
+  fp32 gradient buffer) → apply (dy); wgrad recomputes the consumer's input BN-ReLU on the fly; dgrad
+  accumulates into shared input gradients (identity shortcut, fast-pathway fan-out).
+* Parameters live in ONE flat fp32 buffer (module parameters become views, so ``state_dict`` keys and
+  optimizers are untouched); gradients likewise — that is what the bucketed RCCL all-reduce
+  (``parallel/ddp.py``) and the single-launch fused SGD (``ops/optim.py``) operate on.  bf16 packed
+  weights (forward ``[Cout][taps][Cin]`` and dgrad ``[Cin][taps][Cout]`` layouts) are refreshed by one
+  multi-tensor kernel after each optimizer step.
+* The tiny classification head (dropout → linear → position mean → CE) runs in PyTorch fp32 on the
+  pooled features (≈0.01 % of FLOPs).
+
+Semantics follow the pytorchvideo modules in ``models/reference.py`` (reference ``run.py:105-118``);
+``tests/test_fused_gpu.py`` pins loss / gradient / running-stat parity against that oracle.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..ops._ext import require
+from ..ops.conv import Act, ConvSpec
+from . import reference as R
+
+
+class _Xf:
+    """Consumer-side input transform: y -> act(y*scale + shift)."""
+    __slots__ = ("scale", "shift", "relu")
+
+    def __init__(self, scale, shift, relu=True):
+        self.scale, self.shift, self.relu = scale, shift, relu
+
+
+class FlatParams:
+    """All parameters of a module in one flat fp32 buffer (plus a same-shaped gradient buffer).
+
+    Order = reverse of forward execution so that gradient buckets complete front-to-back during the
+    backward pass (first bucket = head, last = stems).
+    """
+
+    def __init__(self, params: Sequence[Tuple[str, nn.Parameter]], device):
+        self.names = [n for n, _ in params]
+        self.params = [p for _, p in params]
+        self.offsets = []
+        off = 0
+        for p in self.params:
+            self.offsets.append(off)
+            off += (p.numel() + 3) // 4 * 4  # 16-B alignment of every tensor
+        self.numel = off
+        self.data = torch.zeros(off, device=device, dtype=torch.float32)
+        self.grad = torch.zeros(off, device=device, dtype=torch.float32)
+        for p, o in zip(self.params, self.offsets):
+            n = p.numel()
+            self.data[o:o + n].copy_(p.data.reshape(-1).to(device))
+            p.data = self.data[o:o + n].view(p.shape)
+            p.grad = self.grad[o:o + n].view(p.shape)
+        self.index = {id(p): i for i, p in enumerate(self.params)}
+        self.zeroed = True  # gradient buffer logically zero: next backward overwrites it
+
+    def view(self, p: nn.Parameter) -> torch.Tensor:
+        i = self.index[id(p)]
+        return self.data[self.offsets[i]:self.offsets[i] + p.numel()].view(p.shape)
+
+    def gview(self, p: nn.Parameter) -> torch.Tensor:
+        i = self.index[id(p)]
+        return self.grad[self.offsets[i]:self.offsets[i] + p.numel()].view(p.shape)
+
+    def span(self, p: nn.Parameter) -> Tuple[int, int]:
+        i = self.index[id(p)]
+        return self.offsets[i], self.offsets[i] + p.numel()
+
+    def rebind(self):
+        """Re-point module parameters at the flat storage (after e.g. ``load_state_dict`` replaced data)."""
+        for p, o in zip(self.params, self.offsets):
+            n = p.numel()
+            if p.data.data_ptr() != self.data[o:o + n].data_ptr():
+                self.data[o:o + n].copy_(p.data.reshape(-1))
+                p.data = self.data[o:o + n].view(p.shape)
+            if p.grad is None or p.grad.data_ptr() != self.grad[o:o + n].data_ptr():
+                p.grad = self.grad[o:o + n].view(p.shape)
+
+
+class _ConvBN:
+    """One conv (bias-free) + its BatchNorm3d."""
+
+    def __init__(self, eng: "FusedNet", conv: nn.Conv3d, bn: nn.BatchNorm3d, name: str, cin_pad: int = 0):
+        self.eng, self.conv, self.bn, self.name = eng, conv, bn, name
+        self.spec = ConvSpec(conv.in_channels, conv.out_channels, tuple(conv.kernel_size), tuple(conv.stride),
+                             tuple(conv.padding), cin_pad)
+        C, dev = conv.out_channels, eng.device
+        self.mean = torch.zeros(C, device=dev)
+        self.rstd = torch.ones(C, device=dev)
+        self.scale = torch.ones(C, device=dev)
+        self.shift = torch.zeros(C, device=dev)
+        self.coef = torch.zeros(3 * C, device=dev)
+        self.wf = None  # bf16 forward pack view [Cout, taps*Cin_pad]
+        self.wd = None  # bf16 dgrad pack view [Cin, taps*Cout]
+
+    @property
+    def C(self):
+        return self.spec.cout
+
+    def xf(self, relu=True) -> _Xf:
+        return _Xf(self.scale, self.shift, relu)
+
+    # ---- forward ----
+    def fwd(self, x: Act, xf: Optional[_Xf], train: bool, tag: str) -> Act:
+        C = self.eng.C
+        s = self.spec
+        To, Ho, Wo = s.out_dims(x.T, x.H, x.W)
+        M = x.N * To * Ho * Wo
+        y = self.eng.ws((self.name, "y", tag), (M, s.cout), torch.bfloat16)
+        stats = None
+        if train:
+            tiles = C.conv_m_tiles(M, s.cout)
+            stats = self.eng.ws((self.name, "stats"), (tiles, 2, s.cout), torch.float32)
+        aff = 0 if xf is None else (2 if xf.relu else 1)
+        g = [M, s.cout, s.taps * s.cin_pad, s.cin_pad, x.ld, s.cout, x.T, x.H, x.W, To, Ho, Wo,
+             *s.k, *s.stride, *s.pad]
+        C.conv_igemm(x.t, self.wf, y, stats, None if xf is None else xf.scale, None if xf is None else xf.shift,
+                     aff, 0, g, s.chunk, False)
+        bn = self.bn
+        if train:
+            C.bn_finalize(stats, stats.shape[0], s.cout, M, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                          bn.num_batches_tracked, bn.momentum if bn.momentum is not None else 0.1, bn.eps,
+                          self.mean, self.rstd, self.scale, self.shift)
+        else:
+            C.bn_eval_affine(bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, self.scale, self.shift)
+        return Act(y, x.N, To, Ho, Wo)
+
+    # ---- backward pieces ----
+    def wgrad(self, dy: Act, x: Act, xf: Optional[_Xf]):
+        eng, s, C = self.eng, self.spec, self.eng.C
+        K = s.taps * s.cin_pad
+        key = (self.name, "wsplit", dy.M)
+        sp = eng._splits.get(key)
+        if sp is None:
+            from ..ops.conv import wgrad_splits
+            sp = eng._splits[key] = wgrad_splits(dy.M, s.cout, K)
+        splits, pps = sp
+        part = eng.scratch("wgrad_ws", splits * s.cout * K)
+        aff = 0 if xf is None else (2 if xf.relu else 1)
+        g = [dy.M, s.cout, K, s.cin_pad, dy.ld, x.ld, x.T, x.H, x.W, dy.T, dy.H, dy.W,
+             *s.k, *s.stride, *s.pad, splits, pps]
+        C.conv_wgrad(dy.t, x.t, part, None if xf is None else xf.scale, None if xf is None else xf.shift, aff, g,
+                     s.chunk)
+        C.wgrad_reduce(part, eng.flat.gview(self.conv.weight), splits, s.cout, s.taps, s.cin_pad, s.cin, 1.0,
+                       eng.grad_beta)
+
+    def dgrad(self, dy: Act, in_dims, out: torch.Tensor, accum: bool) -> Act:
+        s, C = self.spec, self.eng.C
+        Ti, Hi, Wi = in_dims
+        M = dy.N * Ti * Hi * Wi
+        g = [M, s.cin, s.taps * s.cout, s.cout, dy.ld, out.stride(0), dy.T, dy.H, dy.W, Ti, Hi, Wi,
+             *s.k, *s.stride, *s.pad]
+        C.conv_igemm(dy.t, self.wd, out, None, None, None, 0, 1 if accum else 0, g, 8, True)
+        return Act(out, dy.N, Ti, Hi, Wi)
+
+    def bn_backward(self, g: Act, y: Act, mask_mode: int, mo: Optional[Act], mxf: Optional[_Xf],
+                    dz_out: Optional[Act] = None, dz_accum: bool = False, other: Optional["_ConvBN"] = None,
+                    other_y: Optional[Act] = None) -> Tuple[Act, Optional[Act]]:
+        """dz = g*mask ; returns (dy_self, dy_other) for one or two BNs sharing dz."""
+        eng, C = self.eng, self.eng.C
+        M, Cc = y.M, self.C
+        blocks, rpb = eng._bn_blocks(M, Cc)
+        part = eng.scratch("bnpart", blocks * 3 * Cc)
+        C.bn_bwd_reduce(g.t, g.ld, mask_mode, None if mo is None else mo.t, 0 if mo is None else mo.ld,
+                        None if mxf is None else mxf.scale, None if mxf is None else mxf.shift,
+                        y.t, self.mean, self.rstd,
+                        None if other is None else other_y.t, None if other is None else other.mean,
+                        None if other is None else other.rstd, M, Cc, blocks, rpb, part)
+        fg = eng.flat
+        C.bn_bwd_finalize(part, blocks, Cc, M, 0, self.bn.weight, self.mean, self.rstd,
+                          fg.gview(self.bn.weight), fg.gview(self.bn.bias), eng.grad_beta, self.coef)
+        if other is not None:
+            C.bn_bwd_finalize(part, blocks, Cc, M, 1, other.bn.weight, other.mean, other.rstd,
+                              fg.gview(other.bn.weight), fg.gview(other.bn.bias), eng.grad_beta, other.coef)
+        dy = eng.ws((self.name, "dy"), (M, Cc), torch.bfloat16)
+        dy1 = eng.ws((other.name, "dy"), (M, Cc), torch.bfloat16) if other is not None else None
+        C.bn_bwd_apply(g.t, g.ld, mask_mode, None if mo is None else mo.t, 0 if mo is None else mo.ld,
+                       None if mxf is None else mxf.scale, None if mxf is None else mxf.shift,
+                       y.t, self.coef, dy, None if other is None else other_y.t,
+                       None if other is None else other.coef, dy1,
+                       None if dz_out is None else dz_out.t, 0 if dz_out is None else dz_out.ld,
+                       1 if dz_accum else 0, M, Cc)
+        a = Act(dy, y.N, y.T, y.H, y.W)
+        b = Act(dy1, y.N, y.T, y.H, y.W) if other is not None else None
+        return a, b
+
+
+class _Stem:
+    def __init__(self, eng, stem: R.ResNetBasicStem, name: str):
+        self.u = _ConvBN(eng, stem.conv, stem.norm, name + ".conv", cin_pad=4)
+        self.eng, self.name = eng, name
+        self.units = [self.u]
+
+    def out_channels(self):
+        return self.u.C
+
+    def out_dims(self, T, H, W):
+        To, Ho, Wo = self.u.spec.out_dims(T, H, W)
+        return To, (Ho - 1) // 2 + 1, (Wo - 1) // 2 + 1
+
+    def fwd(self, x: Act, out: torch.Tensor, train: bool, tag: str) -> Act:
+        C = self.eng.C
+        y = self.u.fwd(x, None, train, tag)
+        Ho, Wo = (y.H - 1) // 2 + 1, (y.W - 1) // 2 + 1
+        arg = self.eng.ws((self.name, "arg"), (y.N * y.T * Ho * Wo, self.u.C), torch.uint8)
+        C.stem_pool_fwd(y.t, self.u.scale, self.u.shift, out, out.stride(0), arg, y.N * y.T, y.H, y.W, Ho, Wo,
+                        self.u.C)
+        self.x, self.y, self.arg = x, y, arg
+        return Act(out, y.N, y.T, Ho, Wo)
+
+    def bwd(self, dout: Act):
+        C = self.eng.C
+        y = self.y
+        dact = self.eng.ws((self.name, "dact"), (y.M, self.u.C), torch.bfloat16)
+        C.stem_pool_bwd(dout.t, dout.ld, self.arg, dact, y.N * y.T, y.H, y.W, dout.H, dout.W, self.u.C)
+        dy, _ = self.u.bn_backward(Act(dact, y.N, y.T, y.H, y.W), y, 2, None, self.u.xf())
+        self.u.wgrad(dy, self.x, None)
+
+
+class _ResBlock:
+    def __init__(self, eng, blk: R.ResBlock, name: str):
+        b2 = blk.branch2
+        self.eng, self.name = eng, name
+        self.a = _ConvBN(eng, b2.conv_a, b2.norm_a, name + ".a")
+        self.b = _ConvBN(eng, b2.conv_b, b2.norm_b, name + ".b")
+        self.c = _ConvBN(eng, b2.conv_c, b2.norm_c, name + ".c")
+        self.one = _ConvBN(eng, blk.branch1_conv, blk.branch1_norm, name + ".1") if blk.branch1_conv is not None else None
+        self.units = [u for u in (self.a, self.b, self.c, self.one) if u is not None]
+
+    def out_channels(self):
+        return self.c.C
+
+    def out_dims(self, T, H, W):
+        return self.b.spec.out_dims(T, H, W)
+
+    def fwd(self, x: Act, out: torch.Tensor, train: bool, tag: str) -> Act:
+        C = self.eng.C
+        ya = self.a.fwd(x, None, train, tag)
+        yb = self.b.fwd(ya, self.a.xf(), train, tag)
+        yc = self.c.fwd(yb, self.b.xf(), train, tag)
+        y1 = self.one.fwd(x, None, train, tag) if self.one is not None else None
+        M = yc.M
+        C.res_out(yc.t, self.c.scale, self.c.shift,
+                  None if y1 is None else y1.t, None if y1 is None else self.one.scale,
+                  None if y1 is None else self.one.shift, None if y1 is not None else x.t, x.ld,
+                  out, out.stride(0), M, self.c.C)
+        o = Act(out, yc.N, yc.T, yc.H, yc.W)
+        self.x, self.ya, self.yb, self.yc, self.y1, self.out = x, ya, yb, yc, y1, o
+        return o
+
+    def bwd(self, dout: Act, dx: torch.Tensor, dx_accum: bool):
+        """dout: grad wrt block output; dx: [M_in, C_in] buffer receiving grad wrt block input."""
+        eng = self.eng
+        x, ya, yb, yc, y1 = self.x, self.ya, self.yb, self.yc, self.y1
+        dxa = Act(dx, x.N, x.T, x.H, x.W)
+        if self.one is None:
+            # identity shortcut: dz goes straight to dx
+            dyc, _ = self.c.bn_backward(dout, yc, 1, self.out, None, dz_out=dxa, dz_accum=dx_accum)
+            dy1 = None
+        else:
+            dyc, dy1 = self.c.bn_backward(dout, yc, 1, self.out, None, other=self.one, other_y=y1)
+        self.c.wgrad(dyc, yb, self.b.xf())
+        dab = eng.ws((self.name, "dab"), (yb.M, self.b.C), torch.bfloat16)
+        self.c.dgrad(dyc, (yb.T, yb.H, yb.W), dab, False)
+        dyb, _ = self.b.bn_backward(Act(dab, yb.N, yb.T, yb.H, yb.W), yb, 2, None, self.b.xf())
+        self.b.wgrad(dyb, ya, self.a.xf())
+        daa = eng.ws((self.name, "daa"), (ya.M, self.a.C), torch.bfloat16)
+        self.b.dgrad(dyb, (ya.T, ya.H, ya.W), daa, False)
+        dya, _ = self.a.bn_backward(Act(daa, ya.N, ya.T, ya.H, ya.W), ya, 2, None, self.a.xf())
+        self.a.wgrad(dya, x, None)
+        acc = True if self.one is None else dx_accum
+        if self.one is not None:
+            self.one.wgrad(dy1, x, None)
+            self.one.dgrad(dy1, (x.T, x.H, x.W), dx, dx_accum)
+            acc = True
+        self.a.dgrad(dya, (x.T, x.H, x.W), dx, acc)
+
+
+class _Stage:
+    def __init__(self, eng, stage: R.ResStage, name: str):
+        self.blocks = [_ResBlock(eng, b, f"{name}.{i}") for i, b in enumerate(stage.res_blocks)]
+        self.eng, self.name = eng, name
+        self.units = [u for b in self.blocks for u in b.units]
+
+    def out_channels(self):
+        return self.blocks[-1].out_channels()
+
+    def out_dims(self, T, H, W):
+        for b in self.blocks:
+            T, H, W = b.out_dims(T, H, W)
+        return T, H, W
+
+    def fwd(self, x: Act, out: torch.Tensor, train: bool, tag: str) -> Act:
+        eng = self.eng
+        for i, b in enumerate(self.blocks):
+            if i == len(self.blocks) - 1:
+                o = out
+            else:
+                T, H, W = b.out_dims(x.T, x.H, x.W)
+                o = eng.ws((b.name, "out", tag), (x.N * T * H * W, b.out_channels()), torch.bfloat16)
+            x = b.fwd(x, o, train, tag)
+        return x
+
+    def bwd(self, dout: Act, dx: torch.Tensor, dx_accum: bool):
+        eng = self.eng
+        for i in range(len(self.blocks) - 1, -1, -1):
+            b = self.blocks[i]
+            if i == 0:
+                tgt, acc = dx, dx_accum
+            else:
+                xin = b.x
+                tgt, acc = eng.ws((b.name, "dx"), (xin.M, xin.C), torch.bfloat16), False
+            b.bwd(dout, tgt, acc)
+            if i > 0:
+                xin = b.x
+                dout = Act(tgt, xin.N, xin.T, xin.H, xin.W)
+
+
+class _Fuse:
+    def __init__(self, eng, f: R.FuseFastToSlow, name: str):
+        self.u = _ConvBN(eng, f.conv_fast_to_slow, f.norm, name)
+        self.eng, self.name = eng, name
+        self.units = [self.u]
+
+    def fwd(self, xf: Act, cat_slice: torch.Tensor, train: bool, tag: str):
+        y = self.u.fwd(xf, None, train, tag)
+        self.eng.C.bn_act(y.t, y.ld, cat_slice, cat_slice.stride(0), self.u.scale, self.u.shift, 1, y.M, self.u.C)
+        self.xf_in, self.y = xf, y
+
+    def bwd(self, dcat_slice: Act, dfast: torch.Tensor):
+        """dcat_slice: grad wrt the fusion output slice; accumulates into dfast (grad wrt fast input)."""
+        y = self.y
+        dy, _ = self.u.bn_backward(dcat_slice, y, 2, None, self.u.xf())
+        self.u.wgrad(dy, self.xf_in, None)
+        x = self.xf_in
+        self.u.dgrad(dy, (x.T, x.H, x.W), dfast, True)
+
+
+class FusedNet:
+    """Executor bound to a reference ``Net`` (SlowFast or Slow ResNet3D) whose parameters it shares."""
+
+    def __init__(self, model: R.Net, device: torch.device):
+        self.C = require()
+        self.model = model
+        self.device = torch.device(device)
+        model.to(self.device)
+        self._ws: Dict = {}
+        self._splits: Dict = {}
+        self._bnb: Dict = {}
+        self._scratch: Dict[str, torch.Tensor] = {}
+        self.grad_beta = 0.0
+        blocks = list(model.blocks)
+        self.slowfast = isinstance(blocks[0], R.MultiPathWayWithFuse)
+        self.stages: List[Tuple[List, Optional[_Fuse]]] = []
+        if self.slowfast:
+            for i, b in enumerate(blocks):
+                if not isinstance(b, R.MultiPathWayWithFuse):
+                    break
+                paths = []
+                for p, m in enumerate(b.multipathway_blocks):
+                    nm = f"b{i}.p{p}"
+                    paths.append(_Stem(self, m, nm) if isinstance(m, R.ResNetBasicStem) else _Stage(self, m, nm))
+                fuse = _Fuse(self, b.multipathway_fusion, f"b{i}.fuse") if b.multipathway_fusion is not None else None
+                self.stages.append((paths, fuse))
+            pool = blocks[-2]
+            assert isinstance(pool, R.PoolConcatPathway)
+            self.head_pools = [tuple(p.kernel_size) for p in pool.pool]
+            self.head = blocks[-1]
+        else:
+            for i, b in enumerate(blocks[:-1]):
+                nm = f"b{i}.p0"
+                self.stages.append(([_Stem(self, b, nm) if isinstance(b, R.ResNetBasicStem) else _Stage(self, b, nm)],
+                                    None))
+            self.head = blocks[-1]
+            self.head_pools = [tuple(self.head.pool.kernel_size)] if self.head.pool is not None else [None]
+        self.npath = len(self.stages[0][0])
+        self.units: List[_ConvBN] = []
+        for paths, fuse in self.stages:
+            for p in paths:
+                self.units += p.units
+            if fuse is not None:
+                self.units += fuse.units
+        # flat parameters in reverse execution order (head first)
+        order = list(self.head.named_parameters(prefix="head"))
+        for u in reversed(self.units):
+            order += [(u.name + ".bn.w", u.bn.weight), (u.name + ".bn.b", u.bn.bias), (u.name + ".w", u.conv.weight)]
+        seen = set()
+        named = []
+        for n, p in order:
+            if id(p) not in seen:
+                seen.add(id(p))
+                named.append((n, p))
+        assert len(named) == len(list(model.parameters())), "executor does not cover every parameter"
+        self.flat = FlatParams(named, self.device)
+        self._build_packs()
+        self.pack()
+
+    # ------------------------------------------------------------------ buffers
+    def ws(self, key, shape, dtype) -> torch.Tensor:
+        t = self._ws.get(key)
+        if t is None or tuple(t.shape) != tuple(shape) or t.dtype != dtype:
+            t = torch.empty(shape, device=self.device, dtype=dtype)
+            self._ws[key] = t
+        return t
+
+    def scratch(self, key: str, numel: int) -> torch.Tensor:
+        """Grow-only fp32 scratch shared by sequential (stream-ordered) users."""
+        t = self._scratch.get(key)
+        if t is None or t.numel() < numel:
+            t = torch.empty(max(numel, 1 << 20), device=self.device, dtype=torch.float32)
+            self._scratch[key] = t
+        return t[:numel]
+
+    def _bn_blocks(self, M, C):
+        k = (M, C)
+        v = self._bnb.get(k)
+        if v is None:
+            v = self._bnb[k] = tuple(self.C.bn_bwd_blocks(M, C))
+        return v
+
+    def _build_packs(self):
+        fwd_n, dgr_n = 0, 0
+        offs = []
+        for u in self.units:
+            s = u.spec
+            nf = s.cout * s.taps * s.cin_pad
+            nd = s.cin * s.taps * s.cout if s.cin % 8 == 0 else 0
+            offs.append((fwd_n, dgr_n if nd else -1))
+            fwd_n += (nf + 7) // 8 * 8
+            dgr_n += (nd + 7) // 8 * 8
+        self.pack_fwd = torch.zeros(fwd_n, device=self.device, dtype=torch.bfloat16)
+        self.pack_dgr = torch.zeros(max(dgr_n, 8), device=self.device, dtype=torch.bfloat16)
+        import numpy as np
+        dsz = self.C.pack_desc_size()
+        assert dsz == 40
+        rec = np.zeros(len(self.units), dtype=np.dtype([("src", "<i8"), ("fwd", "<i8"), ("dgr", "<i8"),
+                                                        ("cout", "<i4"), ("cin", "<i4"), ("cin_pad", "<i4"),
+                                                        ("taps", "<i4")]))
+        for i, (u, (fo, do)) in enumerate(zip(self.units, offs)):
+            s = u.spec
+            a, _ = self.flat.span(u.conv.weight)
+            rec[i] = (a, fo, do, s.cout, s.cin, s.cin_pad, s.taps)
+            u.wf = self.pack_fwd[fo:fo + s.cout * s.taps * s.cin_pad].view(s.cout, s.taps * s.cin_pad)
+            if do >= 0:
+                u.wd = self.pack_dgr[do:do + s.cin * s.taps * s.cout].view(s.cin, s.taps * s.cout)
+        self.pack_desc = torch.from_numpy(rec.view(np.uint8).copy()).to(self.device)
+
+    def pack(self):
+        """Refresh bf16 packed weights from the fp32 master buffer (one launch)."""
+        self.C.pack_weights(self.flat.data, self.pack_fwd, self.pack_dgr, self.pack_desc, len(self.units))
+
+    # ------------------------------------------------------------------ forward
+    def _forward_backbone(self, xs: List[Act], train: bool) -> List[Act]:
+        tag = "t" if train else "e"
+        cur = list(xs)
+        self._cats = []
+        for si, (paths, fuse) in enumerate(self.stages):
+            outs = []
+            cat = None
+            for p, mod in enumerate(paths):
+                x = cur[p]
+                T, H, W = mod.out_dims(x.T, x.H, x.W)
+                M = x.N * T * H * W
+                co = mod.out_channels()
+                if p == 0 and fuse is not None:
+                    fT, fH, fW = paths[1].out_dims(cur[1].T, cur[1].H, cur[1].W)
+                    cat = self.ws(("cat", si, tag), (M, co + fuse.u.C), torch.bfloat16)
+                    out = cat[:, :co]
+                else:
+                    out = self.ws(("pout", si, p, tag), (M, co), torch.bfloat16)
+                outs.append(mod.fwd(x, out, train, tag))
+            if fuse is not None:
+                co = outs[0].C
+                fuse.fwd(outs[1], cat[:, co:], train, tag)
+                outs[0] = Act(cat, outs[0].N, outs[0].T, outs[0].H, outs[0].W)
+            self._cats.append(cat)
+            cur = outs
+        return cur
+
+    def _pool_features(self, outs: List[Act], tag: str) -> Tuple[torch.Tensor, List]:
+        shapes = []
+        for o, k in zip(outs, self.head_pools):
+            k = (o.T, o.H, o.W) if k is None else k
+            shapes.append(tuple(max(d - kk + 1, 0) for d, kk in zip((o.T, o.H, o.W), k)))
+        if not (all(s == shapes[0] for s in shapes) and all(v > 0 for v in shapes[0])):
+            # documented fallback (64-frame SlowFast): global average per pathway
+            ks = [(o.T, o.H, o.W) for o in outs]
+            P = 1
+        else:
+            ks = [((o.T, o.H, o.W) if k is None else k) for o, k in zip(outs, self.head_pools)]
+            P = shapes[0][0] * shapes[0][1] * shapes[0][2]
+        Ctot = sum(o.C for o in outs)
+        N = outs[0].N
+        feat = self.ws(("feat", tag), (N, P, Ctot), torch.float32)
+        coff = 0
+        for o, k in zip(outs, ks):
+            assert o.t.is_contiguous()
+            self.C.avgpool_fwd(o.t, [o.N, o.T, o.H, o.W, o.C], list(k), feat, Ctot, coff)
+            coff += o.C
+        return feat, ks
+
+    def _head(self, feat: torch.Tensor, train: bool) -> torch.Tensor:
+        h = self.head
+        x = feat
+        if train and h.dropout is not None:
+            x = F.dropout(x, h.dropout.p, training=True)
+        logits = F.linear(x, h.proj.weight, h.proj.bias)  # [N, P, K]
+        return logits.mean(1)
+
+    @torch.no_grad()
+    def forward_eval(self, xs: List[Act]) -> torch.Tensor:
+        outs = self._forward_backbone(xs, train=False)
+        feat, _ = self._pool_features(outs, "e")
+        return self._head(feat, train=False)
+
+    def forward_backward(self, xs: List[Act], labels: torch.Tensor, loss_scale: float = 1.0,
+                         accumulate: Optional[bool] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+        """One training micro-step.  Gradients of ``loss * loss_scale`` are written (``accumulate=False``)
+        or added (``accumulate=True``) into the flat fp32 gradient buffer; by default they accumulate
+        unless the optimizer's ``zero_grad`` marked the buffer zero.  Returns (loss, logits)."""
+        if accumulate is None:
+            accumulate = not self.flat.zeroed
+        self.flat.zeroed = False
+        self.grad_beta = 1.0 if accumulate else 0.0
+        with torch.no_grad():
+            outs = self._forward_backbone(xs, train=True)
+            feat, ks = self._pool_features(outs, "t")
+        h = self.head
+        feat_t = feat.detach().requires_grad_(True)
+        with torch.enable_grad():
+            logits = self._head(feat_t, train=True)
+            loss = F.cross_entropy(logits.float(), labels)
+            params = [h.proj.weight, h.proj.bias]
+            gfeat, gw, gb = torch.autograd.grad(loss * loss_scale, [feat_t] + params)
+        with torch.no_grad():
+            for p, g in ((h.proj.weight, gw), (h.proj.bias, gb)):
+                gv = self.flat.gview(p)
+                if accumulate:
+                    gv.add_(g)
+                else:
+                    gv.copy_(g)
+            self._backward_backbone(outs, gfeat.contiguous(), ks)
+        return loss.detach(), logits.detach()
+
+    def _backward_backbone(self, outs: List[Act], gfeat: torch.Tensor, ks):
+        C = self.C
+        Ctot = gfeat.shape[-1]
+        # head pools -> grads of the last stage outputs
+        douts = []
+        coff = 0
+        for p, (o, k) in enumerate(zip(outs, ks)):
+            d = self.ws(("dlast", p), (o.M, o.C), torch.bfloat16)
+            C.avgpool_bwd(gfeat, Ctot, coff, [o.N, o.T, o.H, o.W, o.C], list(k), d)
+            douts.append(Act(d, o.N, o.T, o.H, o.W))
+            coff += o.C
+        for si in range(len(self.stages) - 1, -1, -1):
+            paths, fuse = self.stages[si]
+            # grads for this stage's pathway outputs: douts (slow may be the full concat grad)
+            if fuse is not None:
+                dcat = douts[0]
+                co = paths[0].out_channels()
+                fuse.bwd(dcat.narrow(co, fuse.u.C), douts[1].t)
+                douts[0] = dcat.narrow(0, co)
+            new = []
+            for p, mod in enumerate(paths):
+                if isinstance(mod, _Stem):
+                    mod.bwd(douts[p])
+                    new.append(None)
+                else:
+                    xin = mod.blocks[0].x
+                    dx = self.ws(("dstage_in", si, p), (xin.M, xin.C), torch.bfloat16)
+                    mod.bwd(douts[p], dx, False)
+                    new.append(Act(dx, xin.N, xin.T, xin.H, xin.W))
+            douts = new
+
+    # ------------------------------------------------------------------ misc
+    def prepare_inputs(self, xs_ncthw: Sequence[torch.Tensor]) -> List[Act]:
+        """NCTHW float clips (already normalised) -> NDHWC bf16 RGB0 Acts."""
+        return [Act.from_ncthw(x.to(self.device), c_pad=4) for x in xs_ncthw]

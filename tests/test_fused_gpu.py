@@ -1,0 +1,140 @@
+"""Fused HIP executor vs the pure-PyTorch oracle (same weights, same bf16-rounded clip).
+
+Checks one training micro-step of SlowFast-R50 and Slow-R50 at reduced resolution: loss, logits, every
+parameter gradient (relative L2), BN running statistics, and that a few fused-SGD steps decrease the
+loss on a fixed batch.
+"""
+import copy
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from pytorchvideo_accelerate_amd.models import reference as R
+from pytorchvideo_accelerate_amd.models.fused import FusedNet
+from pytorchvideo_accelerate_amd.ops.optim import FusedSGD
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda")
+
+
+def _inputs(slowfast, N=2, T=8, S=64, alpha=4, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    fast = torch.randn(N, 3, T, S, S, generator=g).to(torch.bfloat16).float()
+    if not slowfast:
+        return [fast]
+    idx = torch.linspace(0, T - 1, T // alpha).long()
+    return [fast[:, :, idx].contiguous(), fast]
+
+
+def _build(slowfast, classes=10):
+    torch.manual_seed(0)
+    if slowfast:
+        return R.create_slowfast(50, classes, head_pool_kernel_sizes=((2, 2, 2), (8, 2, 2)), dropout_rate=0.0)
+    return R.create_resnet(50, classes, head_pool_kernel_size=(1, 2, 2), dropout_rate=0.0)
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12)).item()
+
+
+@pytest.mark.parametrize("slowfast", [True, False])
+def test_fused_step_matches_oracle(slowfast):
+    model = _build(slowfast)
+    oracle_init = copy.deepcopy(model)
+    oracle = copy.deepcopy(model).to(DEV).train()
+    xs = _inputs(slowfast)
+    labels = torch.tensor([1, 7], device=DEV)
+    # oracle fp32
+    out_ref = oracle([x.to(DEV) for x in xs] if slowfast else xs[0].to(DEV))
+    loss_ref = F.cross_entropy(out_ref, labels)
+    loss_ref.backward()
+    # fused
+    eng = FusedNet(model, DEV)
+    acts = eng.prepare_inputs(xs)
+    loss, logits = eng.forward_backward(acts, labels)
+    torch.cuda.synchronize()
+    # Stock PyTorch bf16 autocast on the same weights/inputs = the bf16 noise floor of a 50-layer net
+    # with batch statistics over tiny tensors (errors compound through every BN).
+    ac = copy.deepcopy(oracle_init).to(DEV).train()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        out_ac = ac([x.to(DEV) for x in xs] if slowfast else xs[0].to(DEV))
+    loss_ac = F.cross_entropy(out_ac.float(), labels)
+    loss_ac.backward()
+    tol = max(2e-2, 2 * abs(loss_ac.item() - loss_ref.item()))
+    assert abs(loss.item() - loss_ref.item()) < tol * max(1.0, abs(loss_ref.item()))
+    ref_params = dict(oracle.named_parameters())
+    ac_params = dict(ac.named_parameters())
+    fe = sorted(_rel(p.grad, ref_params[n].grad) for n, p in model.named_parameters())
+    ae = sorted(_rel(ac_params[n].grad, ref_params[n].grad) for n, _ in model.named_parameters())
+    assert fe[len(fe) // 2] <= 1.5 * ae[len(ae) // 2] + 0.02, (fe[len(fe) // 2], ae[len(ae) // 2])
+    ref_bufs = dict(oracle.named_buffers())
+    ac_bufs = dict(ac.named_buffers())
+    for n, b in model.named_buffers():
+        if n.endswith("running_var"):
+            assert _rel(b, ref_bufs[n]) <= 2 * _rel(ac_bufs[n], ref_bufs[n]) + 0.02, n
+        if n.endswith("num_batches_tracked"):
+            assert int(b) == int(ref_bufs[n]), n
+
+
+@pytest.mark.parametrize("slowfast", [True, False])
+def test_fused_eval_matches_oracle(slowfast):
+    model = _build(slowfast)
+    # make running stats non-trivial
+    for m in model.modules():
+        if isinstance(m, torch.nn.BatchNorm3d):
+            m.running_mean.uniform_(-0.1, 0.1)
+            m.running_var.uniform_(0.5, 1.5)
+    oracle = copy.deepcopy(model).to(DEV).eval()
+    xs = _inputs(slowfast, seed=1)
+    with torch.no_grad():
+        ref = oracle([x.to(DEV) for x in xs] if slowfast else xs[0].to(DEV))
+    eng = FusedNet(model, DEV)
+    out = eng.forward_eval(eng.prepare_inputs(xs))
+    assert _rel(out, ref) < 5e-2
+
+
+def test_fused_sgd_tracks_torch_training():
+    model = _build(True)
+    oracle = copy.deepcopy(model).to(DEV).train()
+    eng = FusedNet(model, DEV)
+    opt = FusedSGD(eng.flat, lr=0.01, momentum=0.9, weight_decay=1e-4, after_step=eng.pack)
+    ropt = torch.optim.SGD(oracle.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+    xs = _inputs(True, N=4, seed=3)
+    acts = eng.prepare_inputs(xs)
+    labels = torch.tensor([3, 4, 5, 6], device=DEV)
+    losses, ref_losses = [], []
+    for _ in range(6):
+        opt.zero_grad()
+        loss, _ = eng.forward_backward(acts, labels)
+        opt.step()
+        losses.append(loss.item())
+        ropt.zero_grad()
+        rl = F.cross_entropy(oracle([x.to(DEV) for x in xs]), labels)
+        rl.backward()
+        ropt.step()
+        ref_losses.append(rl.item())
+    # fused bf16 SGD tracks fp32 torch SGD over the first steps and decreases the loss
+    assert losses[1] < losses[0], (losses, ref_losses)
+    for a, b in zip(losses[:3], ref_losses[:3]):
+        assert abs(a - b) < 0.2 * abs(b) + 0.05, (losses, ref_losses)
+
+
+def test_fused_sgd_matches_torch_sgd():
+    model = _build(False)
+    ref = copy.deepcopy(model).to(DEV)
+    eng = FusedNet(model, DEV)
+    opt = FusedSGD(eng.flat, lr=0.1, momentum=0.9, weight_decay=1e-4)
+    ropt = torch.optim.SGD(ref.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+    g = torch.Generator(device="cpu").manual_seed(0)
+    for _ in range(3):
+        for (n, p), (_, q) in zip(model.named_parameters(), ref.named_parameters()):
+            gr = torch.randn(p.shape, generator=g).to(DEV)
+            eng.flat.gview(p).copy_(gr)
+            q.grad = gr.clone()
+        opt.step()
+        ropt.step()
+    for (n, p), (_, q) in zip(model.named_parameters(), ref.named_parameters()):
+        torch.testing.assert_close(p.data, q.data, rtol=1e-5, atol=1e-6)
+    sd = opt.state_dict()
+    assert "momentum_buffer" in sd["state"][0]
