@@ -1,0 +1,138 @@
+"""Headline benchmark: SlowFast-R50 32x2x224 bf16 training throughput (clips/s, whole job).
+
+    python bench.py --gpus N --steps K --warmup W          # N>1: launched by torch.distributed.run
+
+One training step = on-device video preprocessing of synthetic decoded uint8 clips (temporal subsample,
+random short-side scale, random crop, flip, normalise, PackPathway) → fused SlowFast forward/backward
+on the gfx950 kernels → bucketed RCCL gradient all-reduce overlapped with backward → fused SGD +
+weight re-pack.  Weights are random-init (no network); data is synthetic uint8 frames of the Kinetics
+clip shape (64 source frames = 2.13 s at 30 fps, 256x340).  Timing: W untimed warmup steps, then K
+steps bracketed by barrier + device synchronize, max over ranks; rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+METRIC = "clips/sec (whole node) SlowFast-R50 32x2x224 at 1/2/4/8 MI355X; step-time p50"
+# Stock PyTorch-ROCm eager (MIOpen conv3d + ATen BN + DDP) measured on one MI355X with the same
+# model/config/synthetic data (scripts/baseline_torch.py; profiles/baseline_torch/bench.jsonl).
+STOCK_CLIPS_PER_S_1GPU = 73.1
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("PVA_BENCH_BATCH", 16)),
+                    help="per-GPU clips per step")
+    ap.add_argument("--frames", type=int, default=32)
+    ap.add_argument("--alpha", type=int, default=4)
+    ap.add_argument("--crop", type=int, default=224)
+    ap.add_argument("--classes", type=int, default=400)
+    ap.add_argument("--depth", type=int, default=50)
+    ap.add_argument("--src-frames", type=int, default=64)
+    ap.add_argument("--src-h", type=int, default=256)
+    ap.add_argument("--src-w", type=int, default=340)
+    ap.add_argument("--bucket-mb", type=float, default=32.0)
+    ap.add_argument("--lr", type=float, default=0.1)
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    from pytorchvideo_accelerate_amd.parallel.dist import DistState
+    from pytorchvideo_accelerate_amd.parallel.ddp import GradSync
+    from pytorchvideo_accelerate_amd.models import reference as R
+    from pytorchvideo_accelerate_amd.models.fused import FusedNet
+    from pytorchvideo_accelerate_amd.ops.optim import FusedSGD
+    from pytorchvideo_accelerate_amd.data.transforms import GpuClipBatch, sample_params
+
+    st = DistState.from_env()
+    dev = st.device
+    assert dev.type == "cuda", "bench.py needs a GPU"
+    torch.manual_seed(1234)
+    model = R.create_slowfast(a.depth, a.classes)
+    eng = FusedNet(model, dev)
+    st.broadcast_tensors([eng.flat.data] + [b for b in model.buffers()])
+    eng.pack()
+    opt = FusedSGD(eng.flat, lr=a.lr, momentum=0.9, weight_decay=1e-4, after_step=eng.pack)
+    bounds = sorted(set(eng.flat.span(p)[1] for p in eng.flat.params))
+    sync = GradSync(eng.flat.grad, st, a.bucket_mb, boundaries=bounds)
+    eng.grad_hook = sync.progress
+
+    B = a.batch
+    gen = torch.Generator().manual_seed(1000 + st.rank)
+    frames = torch.empty(B, a.src_frames, a.src_h, a.src_w, 3, dtype=torch.uint8, device=dev)
+    eng.C.synth_frames(frames, 7 + st.rank)
+    prep = GpuClipBatch(dev, a.frames, a.crop, a.alpha)
+    labels_all = torch.randint(0, a.classes, (64, B), generator=gen).to(dev)
+
+    def step(i):
+        params = [sample_params(a.src_frames, a.src_h, a.src_w, a.frames, a.crop, True, generator=gen)
+                  for _ in range(B)]
+        xs = prep(frames, params)
+        opt.zero_grad()
+        sync.begin(True)
+        loss, _ = eng.forward_backward(xs, labels_all[i % 64])
+        sync.finish()
+        opt.step()
+        return loss
+
+    for i in range(a.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    st.barrier()
+    torch.cuda.synchronize()
+    times = []
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record()
+        loss = step(a.warmup + i)
+        ev1.record()
+        times.append((ev0, ev1))
+    torch.cuda.synchronize()
+    st.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    step_ms = sorted(e0.elapsed_time(e1) for e0, e1 in times)
+    p50 = step_ms[len(step_ms) // 2]
+    el = torch.tensor([elapsed], device=dev)
+    st.all_reduce_(el, "max")
+    elapsed = float(el.item())
+    ms_per_step = elapsed * 1000.0 / a.steps
+    clips = B * st.world_size * a.steps / elapsed
+    if st.is_main_process:
+        print(json.dumps({
+            "metric": METRIC,
+            "value": round(clips, 2),
+            "unit": "clips/s",
+            "n_gpus": st.world_size,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "step_time_p50_ms": round(p50, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(clips / (STOCK_CLIPS_PER_S_1GPU * st.world_size), 3),
+            "dtype": "bf16",
+            "data": "synthetic uint8 decoded clips (64x256x340), on-device preprocessing; random-init weights",
+            "config": {"model": f"SlowFast-R{a.depth} {a.frames}x2x{a.crop}", "global_batch": B * st.world_size,
+                       "per_gpu_batch": B, "seq_len": a.frames, "parallelism": f"dp{st.world_size}",
+                       "classes": a.classes, "final_loss": round(float(loss), 4)},
+        }), flush=True)
+    st.destroy()
+
+
+if __name__ == "__main__":
+    main()

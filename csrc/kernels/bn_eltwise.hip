@@ -17,6 +17,16 @@ namespace {
 
 constexpr int NT = 256;
 
+// Thread -> (row lane lr, 8-channel vector c) mapping shared by the channel-vectorised kernels: the
+// channel slot of a thread is fixed, so per-channel parameters are hoisted out of the row loop and no
+// 64-bit division is needed per element.
+#define ROW_VEC_SETUP(CH)                                  \
+  const int vecs = (CH) >> 3;                              \
+  const int rpi = NT / vecs;                               \
+  const int lr = threadIdx.x / vecs;                       \
+  const int c = (threadIdx.x - lr * vecs) << 3;            \
+  if (lr >= rpi) return;
+
 // ------------------------------------------------------------------------------------------
 // finalize forward statistics
 // ------------------------------------------------------------------------------------------
@@ -74,16 +84,16 @@ __global__ void bn_eval_affine_kernel(int C, const float* gamma, const float* be
 __global__ void bn_act_kernel(const uint16_t* __restrict__ y, int ldy, uint16_t* __restrict__ out, int ldo,
                               const float* __restrict__ scale, const float* __restrict__ shift, int relu,
                               int64_t M, int C) {
-  const int vecs = C >> 3;
-  const int64_t total = M * vecs;
-  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < total; i += (int64_t)gridDim.x * NT) {
-    const int64_t m = i / vecs;
-    const int c = (int)(i - m * vecs) << 3;
+  ROW_VEC_SETUP(C);
+  float sc[8], sh[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { sc[e] = scale[c + e]; sh[e] = shift[c + e]; }
+  for (int64_t m = (int64_t)blockIdx.x * rpi + lr; m < M; m += (int64_t)gridDim.x * rpi) {
     float f[8];
     unpack8(*reinterpret_cast<const uint4*>(y + m * ldy + c), f);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const float z = f[e] * scale[c + e] + shift[c + e];
+      const float z = f[e] * sc[e] + sh[e];
       f[e] = relu ? fmaxf(z, 0.f) : z;
     }
     *reinterpret_cast<uint4*>(out + m * ldo + c) = pack8(f);
@@ -95,22 +105,21 @@ __global__ void res_out_kernel(const uint16_t* __restrict__ yc, const float* __r
                                const uint16_t* __restrict__ y1, const float* __restrict__ s1, const float* __restrict__ h1,
                                const uint16_t* __restrict__ x, int ldx, uint16_t* __restrict__ out, int ldo,
                                int64_t M, int C) {
-  const int vecs = C >> 3;
-  const int64_t total = M * vecs;
-  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < total; i += (int64_t)gridDim.x * NT) {
-    const int64_t m = i / vecs;
-    const int c = (int)(i - m * vecs) << 3;
+  ROW_VEC_SETUP(C);
+  float a0[8], a1[8], b0[8], b1[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    a0[e] = sc[c + e]; a1[e] = hc[c + e];
+    b0[e] = y1 ? s1[c + e] : 1.f; b1[e] = y1 ? h1[c + e] : 0.f;
+  }
+  const uint16_t* sp = y1 ? y1 : x;
+  const int lds = y1 ? C : ldx;
+  for (int64_t m = (int64_t)blockIdx.x * rpi + lr; m < M; m += (int64_t)gridDim.x * rpi) {
     float a[8], b[8];
     unpack8(*reinterpret_cast<const uint4*>(yc + m * C + c), a);
-    if (y1) {
-      unpack8(*reinterpret_cast<const uint4*>(y1 + m * C + c), b);
+    unpack8(*reinterpret_cast<const uint4*>(sp + m * lds + c), b);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) b[e] = b[e] * s1[c + e] + h1[c + e];
-    } else {
-      unpack8(*reinterpret_cast<const uint4*>(x + m * ldx + c), b);
-    }
-#pragma unroll
-    for (int e = 0; e < 8; ++e) a[e] = fmaxf(a[e] * sc[c + e] + hc[c + e] + b[e], 0.f);
+    for (int e = 0; e < 8; ++e) a[e] = fmaxf(a[e] * a0[e] + a1[e] + b[e] * b0[e] + b1[e], 0.f);
     *reinterpret_cast<uint4*>(out + m * ldo + c) = pack8(a);
   }
 }
@@ -134,14 +143,15 @@ __global__ void bn_bwd_reduce_kernel(const uint16_t* __restrict__ g, int ldg, in
   const int rpi = NT / vecs;  // rows per iteration
   const int lv = threadIdx.x % vecs, lr = threadIdx.x / vecs;
   const int c = lv << 3;
-  float sdz[8], s0[8], s1[8], m0[8], r0[8], m1[8], r1[8];
+  float sdz[8], s0[8], s1[8], m0[8], r0[8], m1[8], r1[8], MS[8], MH[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) { sdz[e] = 0.f; s0[e] = 0.f; s1[e] = 0.f; }
   if (lr < rpi) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       m0[e] = mean0[c + e]; r0[e] = rstd0[c + e];
-      if (y1) { m1[e] = mean1[c + e]; r1[e] = rstd1[c + e]; }
+      m1[e] = y1 ? mean1[c + e] : 0.f; r1[e] = y1 ? rstd1[c + e] : 0.f;
+      MS[e] = mask_mode == 2 ? ms[c + e] : 0.f; MH[e] = mask_mode == 2 ? mh[c + e] : 0.f;
     }
     const int64_t mbeg = (int64_t)blockIdx.x * rows_per_block;
     const int64_t mend = min<int64_t>(M, mbeg + rows_per_block);
@@ -156,7 +166,7 @@ __global__ void bn_bwd_reduce_kernel(const uint16_t* __restrict__ g, int ldg, in
         for (int e = 0; e < 8; ++e) dz[e] = o[e] > 0.f ? dz[e] : 0.f;
       } else if (mask_mode == 2) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) dz[e] = (a[e] * ms[c + e] + mh[c + e]) > 0.f ? dz[e] : 0.f;
+        for (int e = 0; e < 8; ++e) dz[e] = (a[e] * MS[e] + MH[e]) > 0.f ? dz[e] : 0.f;
       }
 #pragma unroll
       for (int e = 0; e < 8; ++e) { sdz[e] += dz[e]; s0[e] += dz[e] * (a[e] - m0[e]) * r0[e]; }
@@ -220,11 +230,15 @@ __global__ void bn_bwd_apply_kernel(const uint16_t* __restrict__ g, int ldg, int
                                     uint16_t* __restrict__ dy1,
                                     uint16_t* __restrict__ dzout, int lddz, int dz_accum,
                                     int64_t M, int C) {
-  const int vecs = C >> 3;
-  const int64_t total = M * vecs;
-  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < total; i += (int64_t)gridDim.x * NT) {
-    const int64_t m = i / vecs;
-    const int c = (int)(i - m * vecs) << 3;
+  ROW_VEC_SETUP(C);
+  float A0[8], B0[8], C0[8], A1[8], B1[8], C1[8], MS[8], MH[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    A0[e] = coef0[c + e]; B0[e] = coef0[C + c + e]; C0[e] = coef0[2 * C + c + e];
+    A1[e] = y1 ? coef1[c + e] : 0.f; B1[e] = y1 ? coef1[C + c + e] : 0.f; C1[e] = y1 ? coef1[2 * C + c + e] : 0.f;
+    MS[e] = mask_mode == 2 ? ms[c + e] : 0.f; MH[e] = mask_mode == 2 ? mh[c + e] : 0.f;
+  }
+  for (int64_t m = (int64_t)blockIdx.x * rpi + lr; m < M; m += (int64_t)gridDim.x * rpi) {
     float dz[8], a[8];
     unpack8(*reinterpret_cast<const uint4*>(g + m * ldg + c), dz);
     unpack8(*reinterpret_cast<const uint4*>(y0 + m * C + c), a);
@@ -235,25 +249,25 @@ __global__ void bn_bwd_apply_kernel(const uint16_t* __restrict__ g, int ldg, int
       for (int e = 0; e < 8; ++e) dz[e] = o[e] > 0.f ? dz[e] : 0.f;
     } else if (mask_mode == 2) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) dz[e] = (a[e] * ms[c + e] + mh[c + e]) > 0.f ? dz[e] : 0.f;
+      for (int e = 0; e < 8; ++e) dz[e] = (a[e] * MS[e] + MH[e]) > 0.f ? dz[e] : 0.f;
     }
     float o[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) o[e] = coef0[c + e] * dz[e] + coef0[C + c + e] * a[e] + coef0[2 * C + c + e];
+    for (int e = 0; e < 8; ++e) o[e] = A0[e] * dz[e] + B0[e] * a[e] + C0[e];
     *reinterpret_cast<uint4*>(dy0 + m * C + c) = pack8(o);
     if (y1) {
       unpack8(*reinterpret_cast<const uint4*>(y1 + m * C + c), a);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = coef1[c + e] * dz[e] + coef1[C + c + e] * a[e] + coef1[2 * C + c + e];
+      for (int e = 0; e < 8; ++e) o[e] = A1[e] * dz[e] + B1[e] * a[e] + C1[e];
       *reinterpret_cast<uint4*>(dy1 + m * C + c) = pack8(o);
     }
     if (dzout) {
       uint16_t* d = dzout + m * lddz + c;
       if (dz_accum) {
-        float p[8];
-        unpack8(*reinterpret_cast<const uint4*>(d), p);
+        float q[8];
+        unpack8(*reinterpret_cast<const uint4*>(d), q);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) dz[e] += p[e];
+        for (int e = 0; e < 8; ++e) dz[e] += q[e];
       }
       *reinterpret_cast<uint4*>(d) = pack8(dz);
     }
@@ -349,24 +363,33 @@ __global__ void stem_pool_bwd_kernel(const uint16_t* __restrict__ dout, int ldd,
 // ------------------------------------------------------------------------------------------
 // AvgPool3d(k, stride 1) over an NDHWC tensor -> fp32 [N][P][ldo] at channel offset coff
 // ------------------------------------------------------------------------------------------
+// block = (n, output position, 64-channel group); 4 waves split the window, lane = channel
 __global__ void avgpool_fwd_kernel(const uint16_t* __restrict__ x, int T, int H, int W, int C, int kt, int kh, int kw,
                                    float* __restrict__ out, int ldo, int coff, int N) {
   const int To = T - kt + 1, Ho = H - kh + 1, Wo = W - kw + 1;
-  const int64_t total = (int64_t)N * To * Ho * Wo * C;
-  const float inv = 1.f / (float)(kt * kh * kw);
-  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < total; i += (int64_t)gridDim.x * NT) {
-    int64_t r = i;
-    const int c = r % C; r /= C;
-    const int wo = r % Wo; r /= Wo;
-    const int ho = r % Ho; r /= Ho;
-    const int to = r % To; r /= To;
-    const int n = (int)r;
-    float s = 0.f;
-    for (int a = 0; a < kt; ++a)
-      for (int b = 0; b < kh; ++b)
-        for (int d = 0; d < kw; ++d)
-          s += bf2f(x[((((int64_t)n * T + to + a) * H + ho + b) * W + wo + d) * C + c]);
-    out[(((int64_t)n * To + to) * Ho + ho) * Wo * ldo + (int64_t)wo * ldo + coff + c] = s * inv;
+  const int P = To * Ho * Wo;
+  const int cg = (C + 63) / 64;
+  int b = blockIdx.x;
+  const int g = b % cg; b /= cg;
+  const int pos = b % P;
+  const int n = b / P;
+  const int to = pos / (Ho * Wo), ho = (pos / Wo) % Ho, wo = pos % Wo;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = g * 64 + lane;
+  const int vol = kt * kh * kw;
+  float s = 0.f;
+  if (c < C) {
+    for (int i = w; i < vol; i += 4) {
+      const int a = i / (kh * kw), r = i % (kh * kw), bb = r / kw, d = r % kw;
+      s += bf2f(x[((((int64_t)n * T + to + a) * H + ho + bb) * W + wo + d) * C + c]);
+    }
+  }
+  __shared__ float red[4][64];
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && c < C) {
+    const float t = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+    out[((int64_t)n * P + pos) * ldo + coff + c] = t / (float)vol;
   }
 }
 
@@ -398,6 +421,15 @@ int grid_for(int64_t work) {
   return (int)b;
 }
 
+// grid for ROW_VEC_SETUP kernels: ~4 rows per thread-row, capped
+int grid_rows(int64_t M, int C) {
+  const int rpi = NT / (C / 8);
+  int64_t b = (M + (int64_t)rpi * 4 - 1) / ((int64_t)rpi * 4);
+  if (b > 16384) b = 16384;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
 }  // namespace
 
 void bn_finalize_launch(const float* part, int tiles, int C, int64_t count, const float* gamma, const float* beta,
@@ -415,14 +447,14 @@ void bn_eval_affine_launch(int C, const float* gamma, const float* beta, const f
 
 void bn_act_launch(const uint16_t* y, int ldy, uint16_t* out, int ldo, const float* scale, const float* shift,
                    int relu, int64_t M, int C, hipStream_t s) {
-  hipLaunchKernelGGL(bn_act_kernel, dim3(grid_for(M * (C / 8))), dim3(NT), 0, s, y, ldy, out, ldo, scale, shift, relu,
+  hipLaunchKernelGGL(bn_act_kernel, dim3(grid_rows(M, C)), dim3(NT), 0, s, y, ldy, out, ldo, scale, shift, relu,
                      M, C);
 }
 
 void res_out_launch(const uint16_t* yc, const float* sc, const float* hc, const uint16_t* y1, const float* s1,
                     const float* h1, const uint16_t* x, int ldx, uint16_t* out, int ldo, int64_t M, int C,
                     hipStream_t s) {
-  hipLaunchKernelGGL(res_out_kernel, dim3(grid_for(M * (C / 8))), dim3(NT), 0, s, yc, sc, hc, y1, s1, h1, x, ldx, out,
+  hipLaunchKernelGGL(res_out_kernel, dim3(grid_rows(M, C)), dim3(NT), 0, s, yc, sc, hc, y1, s1, h1, x, ldx, out,
                      ldo, M, C);
 }
 
@@ -456,7 +488,7 @@ void bn_bwd_apply_launch(const uint16_t* g, int ldg, int mask_mode, const uint16
                          const float* mh, const uint16_t* y0, const float* coef0, uint16_t* dy0, const uint16_t* y1,
                          const float* coef1, uint16_t* dy1, uint16_t* dzout, int lddz, int dz_accum, int64_t M, int C,
                          hipStream_t s) {
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(M * (C / 8))), dim3(NT), 0, s, g, ldg, mask_mode, mo, ldm, ms,
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_rows(M, C)), dim3(NT), 0, s, g, ldg, mask_mode, mo, ldm, ms,
                      mh, y0, coef0, dy0, y1, coef1, dy1, dzout, lddz, dz_accum, M, C);
 }
 
@@ -474,9 +506,9 @@ void stem_pool_bwd_launch(const uint16_t* dout, int ldd, const uint8_t* arg, uin
 
 void avgpool_fwd_launch(const uint16_t* x, int N, int T, int H, int W, int C, int kt, int kh, int kw, float* out,
                         int ldo, int coff, hipStream_t s) {
-  const int64_t total = (int64_t)N * (T - kt + 1) * (H - kh + 1) * (W - kw + 1) * C;
-  hipLaunchKernelGGL(avgpool_fwd_kernel, dim3(grid_for(total)), dim3(NT), 0, s, x, T, H, W, C, kt, kh, kw, out, ldo,
-                     coff, N);
+  const int P = (T - kt + 1) * (H - kh + 1) * (W - kw + 1);
+  const int blocks = N * P * ((C + 63) / 64);
+  hipLaunchKernelGGL(avgpool_fwd_kernel, dim3(blocks), dim3(NT), 0, s, x, T, H, W, C, kt, kh, kw, out, ldo, coff, N);
 }
 
 void avgpool_bwd_launch(const float* dout, int ldo, int coff, int N, int T, int H, int W, int C, int kt, int kh,

@@ -25,7 +25,8 @@ struct ConvParams {
 };
 
 // Weight gradient: dW[n = cout][k = (tap, cin)] = sum_p dY[p][cout] * im2col(X)[p][k]
-// Split over p in `splits` slabs of fp32 partials [splits][Cout][K], reduced by wgrad_reduce.
+// Split over p in `splits` slices whose fp32 results are atomically added into one zero-initialised
+// accumulator [Cout][K] (plain stores when splits == 1); wgrad_reduce converts it to PyTorch layout.
 struct WgradParams {
   const uint16_t* dy;       // [P][ldd]
   const uint16_t* x;        // gathered input activations [N,Ti,Hi,Wi][ldx]

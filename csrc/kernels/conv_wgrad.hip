@@ -8,9 +8,10 @@
 // hardware-transpose LDS read ds_read_b64_tr_b16 (cdna_hip_programming.md T10): one 16-lane group
 // reads a 4(p) x 16(col) block and each lane receives one column's 4 p-values.  32-byte column
 // segments are XOR-swizzled with row bits 1 and 3 so the 8 rows a 32-lane half touches land on
-// disjoint bank groups.  The p axis is split over gridDim.z slabs (fp32 partials, deterministic, no
-// atomics); wgrad_reduce sums the slabs and scatters into PyTorch's [Cout][Cin][kt][kh][kw] layout,
-// accumulating into the fp32 master-gradient buffer.
+// disjoint bank groups.  The p axis is split over gridDim.z slices whose fp32 tiles are added into one
+// accumulator with no-return float atomics (≈1.3 TB/s chip-wide; a serial slab reduce was 17 % of the
+// step); wgrad_reduce then scatters it into PyTorch's [Cout][Cin][kt][kh][kw] layout, accumulating into
+// the fp32 master-gradient buffer, and re-zeroes the accumulator.
 #include "common.h"
 #include "conv_params.h"
 #include <type_traits>
@@ -220,8 +221,11 @@ void conv_wgrad_kernel(const WgradParams p) {
     __syncthreads();
   }
 
-  // D[n][k]: lane holds k = col (lane&15), n = 4*(lane>>4) + r
-  float* out = p.partial + (int64_t)split * p.Cout * p.K;
+  // D[n][k]: lane holds k = col (lane&15), n = 4*(lane>>4) + r.  With one slab the tile is stored;
+  // with several, slabs accumulate into one zero-initialised fp32 buffer with no-return
+  // global_atomic_add_f32 (each wave-instruction = 4 rows x 64 contiguous bytes).
+  float* out = p.partial;
+  const bool atomic = p.splits > 1;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -230,7 +234,10 @@ void conv_wgrad_kernel(const WgradParams p) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int n = n0 + wm * WMW + i * 16 + 4 * g + r;
-        if (n < p.Cout && k < p.K) out[(int64_t)n * p.K + k] = acc[i][j][r];
+        if (n < p.Cout && k < p.K) {
+          if (atomic) atomicAdd(out + (int64_t)n * p.K + k, acc[i][j][r]);
+          else out[(int64_t)n * p.K + k] = acc[i][j][r];
+        }
       }
     }
 }
@@ -243,22 +250,20 @@ void launch_w(const WgradParams& p, hipStream_t stream) {
   hipLaunchKernelGGL((conv_wgrad_kernel<BMW, BNW, WMW, WNW, CH>), grid, dim3(NT), lds, stream, p);
 }
 
-// dW (fp32 partial slabs [splits][Cout][taps][Cin]) -> grad[Cout][Cin][taps] (PyTorch layout),
-// grad = beta * grad + scale * sum_s partial[s]
-__global__ void wgrad_reduce_kernel(const float* __restrict__ partial, float* __restrict__ grad, int splits,
-                                    int Cout, int taps, int Cin, int Cin_real, float scale, float beta) {
-  const int64_t total = (int64_t)Cout * taps * Cin;
-  const int64_t stride = (int64_t)Cout * taps * Cin;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    float s = 0.f;
-    for (int k = 0; k < splits; ++k) s += partial[k * stride + i];
-    const int c = i % Cin;
-    if (c >= Cin_real) continue;
-    const int64_t rest = i / Cin;
-    const int tap = rest % taps;
-    const int n = rest / taps;
-    const int64_t o = ((int64_t)n * Cin_real + c) * taps + tap;
-    grad[o] = (beta == 0.f ? 0.f : beta * grad[o]) + scale * s;
+// dW accumulator [Cout][taps][Cin_pad] -> grad[Cout][Cin][taps] (PyTorch layout),
+// grad = beta * grad + scale * acc ; the accumulator is re-zeroed for the next layer (atomic mode).
+__global__ void wgrad_convert_kernel(float* __restrict__ accbuf, float* __restrict__ grad, int total,
+                                     int taps, int Cin, int Cin_real, float scale, float beta, int rezero) {
+  const int per_n = Cin_real * taps;
+  for (int o = blockIdx.x * blockDim.x + threadIdx.x; o < total; o += gridDim.x * blockDim.x) {
+    const int n = o / per_n;
+    const int rem = o - n * per_n;
+    const int c = rem / taps;
+    const int tap = rem - c * taps;
+    const int a = (n * taps + tap) * Cin + c;
+    const float v = accbuf[a];
+    if (rezero) accbuf[a] = 0.f;
+    grad[o] = (beta == 0.f ? 0.f : beta * grad[o]) + scale * v;
   }
 }
 
@@ -300,11 +305,11 @@ void conv_wgrad_launch(const WgradParams& p, int chunk, hipStream_t stream) {
   }
 }
 
-void wgrad_reduce_launch(const float* partial, float* grad, int splits, int Cout, int taps, int Cin, int Cin_real,
+void wgrad_reduce_launch(float* accbuf, float* grad, int splits, int Cout, int taps, int Cin, int Cin_real,
                          float scale, float beta, hipStream_t stream) {
-  const int64_t total = (int64_t)Cout * taps * Cin;
-  int blocks = (int)std::min<int64_t>((total + 255) / 256, 4096);
+  const int total = Cout * taps * Cin_real;
+  int blocks = std::min((total + 255) / 256, 4096);
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, stream, partial, grad, splits, Cout, taps, Cin,
-                     Cin_real, scale, beta);
+  hipLaunchKernelGGL(wgrad_convert_kernel, dim3(blocks), dim3(256), 0, stream, accbuf, grad, total, taps, Cin,
+                     Cin_real, scale, beta, 1);
 }

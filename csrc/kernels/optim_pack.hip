@@ -55,26 +55,21 @@ struct PackDesc {
 
 __global__ void pack_weights_kernel(const float* __restrict__ master, uint16_t* __restrict__ fwd,
                                     uint16_t* __restrict__ dgr, const PackDesc* __restrict__ descs) {
+  // 32-bit index math (largest conv weight is 2.4 M elements); one source element per thread, written
+  // to both packed layouts, so the fp32 read is coalesced and happens once.
   const PackDesc d = descs[blockIdx.y];
   const float* src = master + d.src;
-  const int64_t nf = (int64_t)d.cout * d.taps * d.cin_pad;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nf; i += (int64_t)gridDim.x * blockDim.x) {
-    const int c = i % d.cin_pad;
-    const int64_t r = i / d.cin_pad;
-    const int tap = r % d.taps;
-    const int n = r / d.taps;
-    const float v = c < d.cin ? src[((int64_t)n * d.cin + c) * d.taps + tap] : 0.f;
-    fwd[d.fwd + i] = f2bf(v);
-  }
-  if (d.dgr >= 0) {
-    const int64_t nd = (int64_t)d.cin * d.taps * d.cout;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nd; i += (int64_t)gridDim.x * blockDim.x) {
-      const int n = i % d.cout;
-      const int64_t r = i / d.cout;
-      const int tap = r % d.taps;
-      const int c = r / d.taps;
-      dgr[d.dgr + i] = f2bf(src[((int64_t)n * d.cin + c) * d.taps + tap]);
-    }
+  uint16_t* fo = fwd + d.fwd;
+  uint16_t* dg = d.dgr >= 0 ? dgr + d.dgr : nullptr;
+  const int n_src = d.cout * d.cin * d.taps;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n_src; i += gridDim.x * blockDim.x) {
+    const int tap = i % d.taps;
+    const int r = i / d.taps;
+    const int c = r % d.cin;
+    const int n = r / d.cin;
+    const uint16_t v = f2bf(src[i]);
+    fo[(n * d.taps + tap) * d.cin_pad + c] = v;
+    if (dg) dg[(c * d.taps + tap) * d.cout + n] = v;
   }
 }
 

@@ -14,7 +14,7 @@ void conv_igemm_launch(const ConvParams& p, int chunk, bool dgrad, hipStream_t s
 int conv_igemm_m_tiles(int M, int N);
 void conv_wgrad_launch(const WgradParams& p, int chunk, hipStream_t stream);
 void conv_wgrad_tile(int Cout, int K, int* bmw, int* bnw);
-void wgrad_reduce_launch(const float* partial, float* grad, int splits, int Cout, int taps, int Cin, int Cin_real,
+void wgrad_reduce_launch(float* accbuf, float* grad, int splits, int Cout, int taps, int Cin, int Cin_real,
                          float scale, float beta, hipStream_t stream);
 void bn_finalize_launch(const float* part, int tiles, int C, int64_t count, const float* gamma, const float* beta,
                         float* rm, float* rv, int64_t* nbt, float momentum, float eps, float* smean, float* srstd,
@@ -126,7 +126,7 @@ void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& par
   p.pt = g[18]; p.ph = g[19]; p.pw = g[20]; p.splits = g[21]; p.p_per_split = g[22];
   TORCH_CHECK(p.Cin % chunk == 0 && p.Cout % 8 == 0, "wgrad channel alignment");
   TORCH_CHECK(p.p_per_split % 32 == 0, "p_per_split must be a multiple of 32");
-  TORCH_CHECK(partial.numel() >= (int64_t)p.splits * p.Cout * p.K, "partial slab too small");
+  TORCH_CHECK(partial.numel() >= (int64_t)p.Cout * p.K, "wgrad accumulator too small");
   conv_wgrad_launch(p, (int)chunk, cur_stream());
 }
 

@@ -155,7 +155,7 @@ class _ConvBN:
             from ..ops.conv import wgrad_splits
             sp = eng._splits[key] = wgrad_splits(dy.M, s.cout, K)
         splits, pps = sp
-        part = eng.scratch("wgrad_ws", splits * s.cout * K)
+        part = eng.scratch("wgrad_acc", s.cout * K, zero=True)
         aff = 0 if xf is None else (2 if xf.relu else 1)
         g = [dy.M, s.cout, K, s.cin_pad, dy.ld, x.ld, x.T, x.H, x.W, dy.T, dy.H, dy.W,
              *s.k, *s.stride, *s.pad, splits, pps]
@@ -331,6 +331,7 @@ class _Stage:
                 xin = b.x
                 tgt, acc = eng.ws((b.name, "dx"), (xin.M, xin.C), torch.bfloat16), False
             b.bwd(dout, tgt, acc)
+            b.eng_progress(b.flat_hi)
             if i > 0:
                 xin = b.x
                 dout = Act(tgt, xin.N, xin.T, xin.H, xin.W)
@@ -414,6 +415,21 @@ class FusedNet:
         self.flat = FlatParams(named, self.device)
         self._build_packs()
         self.pack()
+        # backward progress reporting for overlapped gradient all-reduce (parallel/ddp.GradSync)
+        self.grad_hook = None
+        self._head_hi = max(self.flat.span(p)[1] for p in self.head.parameters())
+        for paths, fuse in self.stages:
+            mods = list(paths) + ([fuse] if fuse is not None else [])
+            for m in mods:
+                subs = m.blocks if isinstance(m, _Stage) else [m]
+                for sub in subs:
+                    sub.flat_hi = max(self.flat.span(w)[1] for u in sub.units
+                                      for w in (u.conv.weight, u.bn.weight, u.bn.bias))
+                    sub.eng_progress = self._progress
+
+    def _progress(self, hi: int):
+        if self.grad_hook is not None:
+            self.grad_hook(hi)
 
     # ------------------------------------------------------------------ buffers
     def ws(self, key, shape, dtype) -> torch.Tensor:
@@ -423,11 +439,13 @@ class FusedNet:
             self._ws[key] = t
         return t
 
-    def scratch(self, key: str, numel: int) -> torch.Tensor:
-        """Grow-only fp32 scratch shared by sequential (stream-ordered) users."""
+    def scratch(self, key: str, numel: int, zero: bool = False) -> torch.Tensor:
+        """Grow-only fp32 scratch shared by sequential (stream-ordered) users.  ``zero``: allocated zeroed
+        (the wgrad accumulator is kept zero by its consumer, wgrad_reduce)."""
         t = self._scratch.get(key)
         if t is None or t.numel() < numel:
-            t = torch.empty(max(numel, 1 << 20), device=self.device, dtype=torch.float32)
+            alloc = torch.zeros if zero else torch.empty
+            t = alloc(max(numel, 1 << 20), device=self.device, dtype=torch.float32)
             self._scratch[key] = t
         return t[:numel]
 
@@ -559,6 +577,7 @@ class FusedNet:
                     gv.add_(g)
                 else:
                     gv.copy_(g)
+            self._progress(self._head_hi)
             self._backward_backbone(outs, gfeat.contiguous(), ks)
         return loss.detach(), logits.detach()
 
@@ -580,17 +599,20 @@ class FusedNet:
                 dcat = douts[0]
                 co = paths[0].out_channels()
                 fuse.bwd(dcat.narrow(co, fuse.u.C), douts[1].t)
+                self._progress(fuse.flat_hi)
                 douts[0] = dcat.narrow(0, co)
-            new = []
-            for p, mod in enumerate(paths):
+            new = [None] * len(paths)
+            # pathways in reverse order: matches the flat (reverse-execution) gradient layout
+            for p in range(len(paths) - 1, -1, -1):
+                mod = paths[p]
                 if isinstance(mod, _Stem):
                     mod.bwd(douts[p])
-                    new.append(None)
+                    self._progress(mod.flat_hi)
                 else:
                     xin = mod.blocks[0].x
                     dx = self.ws(("dstage_in", si, p), (xin.M, xin.C), torch.bfloat16)
                     mod.bwd(douts[p], dx, False)
-                    new.append(Act(dx, xin.N, xin.T, xin.H, xin.W))
+                    new[p] = Act(dx, xin.N, xin.T, xin.H, xin.W)
             douts = new
 
     # ------------------------------------------------------------------ misc

@@ -141,7 +141,7 @@ def conv_dgrad(dy: Act, wt_pack: torch.Tensor, spec: ConvSpec, in_dims: Triple, 
     return Act(out, dy.N, Ti, Hi, Wi)
 
 
-def wgrad_splits(P: int, Cout: int, K: int, target_blocks: int = 1024, min_rows: int = 512) -> Tuple[int, int]:
+def wgrad_splits(P: int, Cout: int, K: int, target_blocks: int = 1024, min_rows: int = 1024) -> Tuple[int, int]:
     C = require()
     bmw, bnw = C.wgrad_tile(Cout, K)
     tiles = ((Cout + bmw - 1) // bmw) * ((K + bnw - 1) // bnw)
@@ -161,9 +161,9 @@ def conv_wgrad(dy: Act, x: Act, spec: ConvSpec, grad: torch.Tensor, workspace: O
     P = dy.M
     K = spec.taps * spec.cin_pad
     splits, pps = splits_pps or wgrad_splits(P, spec.cout, K)
-    need = splits * spec.cout * K
+    need = spec.cout * K
     if workspace is None or workspace.numel() < need:
-        workspace = torch.empty(need, device=dy.t.device, dtype=torch.float32)
+        workspace = torch.zeros(need, device=dy.t.device, dtype=torch.float32)  # kept zero by wgrad_reduce
     affine = 0 if in_scale is None else (2 if in_relu else 1)
     g = [P, spec.cout, K, spec.cin_pad, dy.ld, x.ld, x.T, x.H, x.W, dy.T, dy.H, dy.W,
          *spec.k, *spec.stride, *spec.pad, splits, pps]

@@ -1,0 +1,88 @@
+"""Bucketed gradient all-reduce over RCCL, overlapped with the backward pass.
+
+The flat fp32 gradient buffer (``models/fused.FlatParams``) is laid out in reverse execution order, so
+the backward pass finalises it front to back.  ``GradSync`` cuts it into contiguous buckets; whenever
+the executor reports that everything below offset ``x`` is final (``progress(x)``), every bucket that
+ends at or below ``x`` is all-reduced immediately with ``async_op=True``.  ProcessGroupNCCL enqueues the
+collective on its own stream *after* the work already queued on the compute stream, so bucket k's
+RCCL ring runs concurrently with the dgrad/wgrad kernels of the remaining layers; ``finish()`` makes
+the compute stream wait for the outstanding collectives before the optimizer step.
+
+Differences to ``torch.nn.parallel.DistributedDataParallel`` as the reference uses it,
+all math-identical:
+* no per-parameter autograd hooks and no bucket copies (gradients *are* the buckets — the analogue of
+  ``gradient_as_bucket_view=True``), averaging via ``ReduceOp.AVG`` inside RCCL;
+* ``sync=False`` micro-steps under gradient accumulation skip the all-reduce (``no_sync``) — the
+  reference all-reduces every micro-step;
+* bucket size defaults to 32 MiB: large enough that each ring step is bandwidth- not latency-bound on
+  a single xGMI link (≈153 GB/s), small enough to give ≥4 buckets for SlowFast-R50's 135 MiB.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Tuple
+
+import torch
+
+from .dist import DistState
+
+
+class GradSync:
+    def __init__(self, grad: torch.Tensor, state: DistState, bucket_mb: float = 32.0,
+                 boundaries: Optional[List[int]] = None):
+        self.grad = grad
+        self.state = state
+        self.enabled = state.world_size > 1 and state.initialized
+        n = grad.numel()
+        cap = max(1, int(bucket_mb * (1 << 20) / grad.element_size()))
+        # cut at the given parameter boundaries (so a bucket never splits a tensor) near the cap
+        cuts = [0]
+        if boundaries:
+            last = 0
+            for b in boundaries:
+                if b - last >= cap:
+                    cuts.append(b)
+                    last = b
+        else:
+            cuts += list(range(cap, n, cap))
+        if cuts[-1] != n:
+            cuts.append(n)
+        self.buckets: List[Tuple[int, int]] = [(cuts[i], cuts[i + 1]) for i in range(len(cuts) - 1)]
+        self._next = 0
+        self._works = []
+        self.active = False
+
+    def begin(self, sync: bool = True):
+        """Start a backward pass; ``sync=False`` = no_sync micro-step (accumulate locally)."""
+        self._next = 0
+        self._works = []
+        self.active = self.enabled and sync
+
+    def _launch(self, b: int):
+        lo, hi = self.buckets[b]
+        t = self.grad[lo:hi]
+        import torch.distributed as dist
+        if self.state.backend == "nccl":
+            self._works.append((dist.all_reduce(t, op=dist.ReduceOp.AVG, async_op=True), None))
+        else:
+            self._works.append((dist.all_reduce(t, op=dist.ReduceOp.SUM, async_op=True), t))
+
+    def progress(self, offset: int):
+        """Everything in grad[:offset] is final."""
+        if not self.active:
+            return
+        while self._next < len(self.buckets) and self.buckets[self._next][1] <= offset:
+            self._launch(self._next)
+            self._next += 1
+
+    def finish(self):
+        if not self.active:
+            return
+        while self._next < len(self.buckets):
+            self._launch(self._next)
+            self._next += 1
+        for w, t in self._works:
+            w.wait()
+            if t is not None:
+                t.div_(self.state.world_size)
+        self._works = []
+        self.active = False

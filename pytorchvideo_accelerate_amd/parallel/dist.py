@@ -1,0 +1,132 @@
+"""Process-group bootstrap and small collectives (one process per GPU, RCCL over xGMI).
+
+Mirrors what the reference gets from ``accelerate``:
+
+* ``DistState.from_env()`` reads the torchrun / ``accelerate launch`` contract (``RANK``, ``LOCAL_RANK``,
+  ``WORLD_SIZE``, ``MASTER_ADDR``, ``MASTER_PORT``); with ``LOCAL_RANK`` set and a GPU present it
+  initialises the ``nccl`` backend (RCCL on ROCm) and binds ``cuda:LOCAL_RANK``; on CPU with
+  world > 1 it uses ``gloo``; otherwise it is single-process (``distributed_type == "NO"``).
+* ``broadcast_module`` (rank-0 params + buffers, coalesced into one flat buffer per dtype),
+  ``all_gather_cat`` (``accelerator.gather``), ``all_reduce_`` (AVG on RCCL, SUM/W on gloo), barrier.
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistState:
+    rank: int = 0
+    world_size: int = 1
+    local_rank: int = 0
+    backend: Optional[str] = None
+    device: torch.device = torch.device("cpu")
+    distributed_type: str = "NO"
+
+    @property
+    def is_main_process(self) -> bool:
+        return self.rank == 0
+
+    @property
+    def initialized(self) -> bool:
+        return dist.is_available() and dist.is_initialized()
+
+    @classmethod
+    def from_env(cls, cpu: bool = False, timeout_s: int = 1800) -> "DistState":
+        ws = int(os.environ.get("WORLD_SIZE", "1"))
+        rank = int(os.environ.get("RANK", "0"))
+        lr = int(os.environ.get("LOCAL_RANK", "0"))
+        use_gpu = (not cpu) and torch.cuda.is_available()
+        st = cls(rank=rank, world_size=ws, local_rank=lr)
+        if use_gpu:
+            ndev = torch.cuda.device_count()
+            st.device = torch.device("cuda", lr % max(ndev, 1))
+            torch.cuda.set_device(st.device)
+        if ws > 1:
+            st.backend = "nccl" if use_gpu else "gloo"
+            st.distributed_type = "MULTI_GPU" if use_gpu else "MULTI_CPU"
+            if not dist.is_initialized():
+                os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+                os.environ.setdefault("MASTER_PORT", "29500")
+                import datetime
+                kw = {}
+                if use_gpu:
+                    kw["device_id"] = st.device
+                dist.init_process_group(st.backend, rank=rank, world_size=ws,
+                                        timeout=datetime.timedelta(seconds=timeout_s), **kw)
+        return st
+
+    # -------------------------------------------------------------- collectives
+    def barrier(self):
+        if self.initialized and self.world_size > 1:
+            if self.backend == "nccl":
+                dist.barrier(device_ids=[self.device.index])
+            else:
+                dist.barrier()
+
+    def all_reduce_(self, t: torch.Tensor, op: str = "avg") -> torch.Tensor:
+        if not (self.initialized and self.world_size > 1):
+            return t
+        if op == "avg":
+            if self.backend == "nccl":
+                dist.all_reduce(t, op=dist.ReduceOp.AVG)
+            else:
+                dist.all_reduce(t, op=dist.ReduceOp.SUM)
+                t.div_(self.world_size)
+        elif op == "sum":
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        elif op == "max":
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        else:
+            raise ValueError(op)
+        return t
+
+    def all_gather_cat(self, t: torch.Tensor) -> torch.Tensor:
+        """``accelerator.gather``: concatenate every rank's tensor along dim 0 (equal shapes)."""
+        if not (self.initialized and self.world_size > 1):
+            return t
+        t = t.contiguous()
+        if self.backend == "nccl":
+            out = torch.empty((self.world_size * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+            dist.all_gather_into_tensor(out, t)
+            return out
+        parts = [torch.empty_like(t) for _ in range(self.world_size)]
+        dist.all_gather(parts, t)
+        return torch.cat(parts, 0)
+
+    def broadcast_tensors(self, tensors: List[torch.Tensor], src: int = 0):
+        """Coalesced broadcast (one flat buffer per dtype) of rank ``src``'s tensors, in place."""
+        if not (self.initialized and self.world_size > 1) or not tensors:
+            return
+        by_dtype = {}
+        for t in tensors:
+            by_dtype.setdefault(t.dtype, []).append(t)
+        for dt, ts in by_dtype.items():
+            flat = torch.cat([t.reshape(-1) for t in ts])
+            dist.broadcast(flat, src)
+            off = 0
+            for t in ts:
+                n = t.numel()
+                t.copy_(flat[off:off + n].view_as(t))
+                off += n
+
+    def broadcast_module(self, module: torch.nn.Module, src: int = 0, buffers_only: bool = False):
+        ts = [] if buffers_only else [p.data for p in module.parameters()]
+        ts += [b for b in module.buffers()]
+        self.broadcast_tensors(ts, src)
+
+    def broadcast_object(self, obj, src: int = 0):
+        if not (self.initialized and self.world_size > 1):
+            return obj
+        lst = [obj]
+        dist.broadcast_object_list(lst, src)
+        return lst[0]
+
+    def destroy(self):
+        if self.initialized:
+            dist.destroy_process_group()
