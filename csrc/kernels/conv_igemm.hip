@@ -29,22 +29,7 @@ __device__ __forceinline__ int lds_off(int row, int slot) {
   return row * 64 + ((slot ^ (((row >> 2) & 1) << 1)) << 4);
 }
 
-template <bool DGRAD>
-__device__ __forceinline__ bool gather_coord(int base_c, int d, int s, int G, int& g) {
-  if (!DGRAD) {
-    g = base_c + d;
-    return (unsigned)g < (unsigned)G;
-  } else {
-    int num = base_c - d;
-    if (num < 0) return false;
-    if (s == 1) { g = num; }
-    else if (s == 2) { if (num & 1) return false; g = num >> 1; }
-    else { int q = num / s; if (q * s != num) return false; g = q; }
-    return g < G;
-  }
-}
-
-template <int BM, int BN, int WM, int WN, int CH, bool DGRAD>
+template <int BM, int BN, int WM, int WN, int CH>
 __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64)
 void conv_igemm_kernel(const ConvParams p) {
   constexpr int NWN = BN / WN;
@@ -89,11 +74,10 @@ void conv_igemm_kernel(const ConvParams p) {
     if (idx < A_CHUNKS && m < p.M) {
       const int b = m / RTHW;
       int r = m - b * RTHW;
-      const int rt = r / RHW; r -= rt * RHW;
-      const int rh = r / p.Rw; const int rw = r - rh * p.Rw;
+      const int qt = r / RHW; r -= qt * RHW;
+      const int qh = r / p.Rw; const int qw = r - qh * p.Rw;
       a_base[s] = b * GTHW;
-      if (!DGRAD) { a_t[s] = rt * p.st - p.pt; a_h[s] = rh * p.sh - p.ph; a_w[s] = rw * p.sw - p.pw; }
-      else        { a_t[s] = rt + p.pt;        a_h[s] = rh + p.ph;        a_w[s] = rw + p.pw; }
+      a_t[s] = qt * p.ast + p.aot; a_h[s] = qh * p.ash + p.aoh; a_w[s] = qw * p.asw + p.aow;
     } else {
       a_base[s] = 0; a_t[s] = -(1 << 28); a_h[s] = 0; a_w[s] = 0;
     }
@@ -105,7 +89,7 @@ void conv_igemm_kernel(const ConvParams p) {
     kc += by;
     while (kc >= p.Cg) {
       kc -= p.Cg;
-      if (++kdw == p.kw) { kdw = 0; if (++kdh == p.kh) { kdh = 0; ++kdt; } }
+      if (++kdw == p.nw) { kdw = 0; if (++kdh == p.nh) { kdh = 0; ++kdt; } }
     }
   };
   kadvance(0);
@@ -113,17 +97,16 @@ void conv_igemm_kernel(const ConvParams p) {
   VT ra[A_SLOTS], rb[B_SLOTS];
   int ra_c = 0;            // channel offset of the staged A chunks
   unsigned ra_valid = 0;   // bit s: slot s loaded real data
-  int kglob = col * CH;    // k index of this thread's chunk in the current step
 
   auto load = [&]() {
-    const bool tap_ok = kdt < p.kt;
+    const bool tap_ok = kdt < p.nt;
+    const int dgt = p.dir * kdt, dgh = p.dir * kdh, dgw = p.dir * kdw;
     ra_c = kc; ra_valid = 0;
 #pragma unroll
     for (int s = 0; s < A_SLOTS; ++s) {
-      int gt, gh, gw;
-      bool v = tap_ok && gather_coord<DGRAD>(a_t[s], kdt, p.st, p.Gt, gt) &&
-               gather_coord<DGRAD>(a_h[s], kdh, p.sh, p.Gh, gh) &&
-               gather_coord<DGRAD>(a_w[s], kdw, p.sw, p.Gw, gw);
+      const int gt = a_t[s] + dgt, gh = a_h[s] + dgh, gw = a_w[s] + dgw;
+      const bool v = tap_ok && (unsigned)gt < (unsigned)p.Gt && (unsigned)gh < (unsigned)p.Gh &&
+                     (unsigned)gw < (unsigned)p.Gw;
       if (v) {
         const int64_t off = (int64_t)(a_base[s] + (gt * p.Gh + gh) * p.Gw + gw) * p.ldx + kc;
         ra[s] = *reinterpret_cast<const VT*>(p.x + off);
@@ -132,17 +115,18 @@ void conv_igemm_kernel(const ConvParams p) {
         ra[s] = VT{};
       }
     }
+    const int tapfull = ((p.bt0 + kdt * p.bts) * p.kh + (p.bh0 + kdh * p.bhs)) * p.kw + (p.bw0 + kdw * p.bws);
+    const int boff = tapfull * p.Cg + kc;
 #pragma unroll
     for (int s = 0; s < B_SLOTS; ++s) {
       const int idx = tid + s * NT;
       const int n = n0 + idx / CPR;
-      if (idx < B_CHUNKS && n < p.Ngemm && kglob < p.K)
-        rb[s] = *reinterpret_cast<const VT*>(p.w + (int64_t)n * p.K + kglob);
+      if (idx < B_CHUNKS && n < p.Ngemm && tap_ok)
+        rb[s] = *reinterpret_cast<const VT*>(p.w + (int64_t)n * p.Kfull + boff);
       else
         rb[s] = VT{};
     }
     kadvance(BK);
-    kglob += BK;
   };
 
   auto store_lds = [&](int buf) {
@@ -183,7 +167,7 @@ void conv_igemm_kernel(const ConvParams p) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  const int nsteps = (p.K + BK - 1) / BK;
+  const int nsteps = (p.nt * p.nh * p.nw * p.Cg + BK - 1) / BK;
   __syncthreads();  // affine table ready
   load();
   store_lds(0);
@@ -223,15 +207,24 @@ void conv_igemm_kernel(const ConvParams p) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) { cs[j][r] = 0.f; cq[j][r] = 0.f; }
 
+  const bool dense_rows = p.ost == 1 && p.osh == 1 && p.osw == 1 && p.Rt == p.Ot && p.Rh == p.Oh && p.Rw == p.Ow;
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int m = m0 + wm * WM + i * 16 + frow;
+    int64_t pos = m;
+    if (!dense_rows && m < p.M) {
+      const int b = m / RTHW;
+      int r = m - b * RTHW;
+      const int qt = r / RHW; r -= qt * RHW;
+      const int qh = r / p.Rw; const int qw = r - qh * p.Rw;
+      pos = (((int64_t)b * p.Ot + qt * p.ost + p.ort) * p.Oh + qh * p.osh + p.orh) * p.Ow + qw * p.osw + p.orw;
+    }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int n = n0 + wn * WN + j * 16 + 4 * fslot;
       float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
       if (m < p.M && n < p.Ngemm) {
-        uint16_t* dst = p.y + (int64_t)m * p.ldy + n;
+        uint16_t* dst = p.y + pos * p.ldy + n;
         if (p.accum) {
           float o[4];
           unpack4(*reinterpret_cast<const uint2*>(dst), o);
@@ -273,27 +266,15 @@ void conv_igemm_kernel(const ConvParams p) {
   }
 }
 
-struct TileCfg { int bm, bn; };
-
-template <int BM, int BN, int WM, int WN, int CH, bool DGRAD>
+template <int BM, int BN, int WM, int WN, int CH>
 void launch_cfg(const ConvParams& p, hipStream_t stream) {
   constexpr int NT = (BM / WM) * (BN / WN) * 64;
   const int m_tiles = (p.M + BM - 1) / BM, n_tiles = (p.Ngemm + BN - 1) / BN;
   const size_t lds = 2 * (BM + BN) * BK * 2 + 2 * BN * 4 + (p.affine ? 2 * p.Cg * 4 : 0);
-  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, DGRAD>), dim3(m_tiles * n_tiles), dim3(NT), lds,
-                     stream, p);
+  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH>), dim3(m_tiles * n_tiles), dim3(NT), lds, stream, p);
 }
 
 }  // namespace
-
-// Tile selection by GEMM shape. Returns the BM used (callers size the stats slab with it).
-int conv_igemm_pick_bm(int M, int N) {
-  if (N > 64) {
-    const long tiles = (long)((M + 127) / 128) * ((N + 127) / 128);
-    return tiles >= 160 ? 128 : 128;
-  }
-  return N > 32 ? 128 : 256;
-}
 
 static int pick_variant(int M, int N) {
   if (N > 64) return 0;       // 128 x 128
@@ -308,28 +289,21 @@ int conv_igemm_m_tiles(int M, int N) {
   return (M + bm - 1) / bm;
 }
 
-void conv_igemm_launch(const ConvParams& p, int chunk, bool dgrad, hipStream_t stream) {
+void conv_igemm_launch(const ConvParams& p, int chunk, hipStream_t stream) {
   const int v = pick_variant(p.M, p.Ngemm);
-  if (dgrad) {
+  if (chunk == 8) {
     switch (v) {
-      case 0: launch_cfg<128, 128, 64, 64, 8, true>(p, stream); break;
-      case 1: launch_cfg<128, 64, 64, 32, 8, true>(p, stream); break;
-      case 2: launch_cfg<256, 32, 64, 32, 8, true>(p, stream); break;
-      default: launch_cfg<256, 16, 64, 16, 8, true>(p, stream); break;
-    }
-  } else if (chunk == 8) {
-    switch (v) {
-      case 0: launch_cfg<128, 128, 64, 64, 8, false>(p, stream); break;
-      case 1: launch_cfg<128, 64, 64, 32, 8, false>(p, stream); break;
-      case 2: launch_cfg<256, 32, 64, 32, 8, false>(p, stream); break;
-      default: launch_cfg<256, 16, 64, 16, 8, false>(p, stream); break;
+      case 0: launch_cfg<128, 128, 64, 64, 8>(p, stream); break;
+      case 1: launch_cfg<128, 64, 64, 32, 8>(p, stream); break;
+      case 2: launch_cfg<256, 32, 64, 32, 8>(p, stream); break;
+      default: launch_cfg<256, 16, 64, 16, 8>(p, stream); break;
     }
   } else {
     switch (v) {
-      case 0: launch_cfg<128, 128, 64, 64, 4, false>(p, stream); break;
-      case 1: launch_cfg<128, 64, 64, 32, 4, false>(p, stream); break;
-      case 2: launch_cfg<256, 32, 64, 32, 4, false>(p, stream); break;
-      default: launch_cfg<256, 16, 64, 16, 4, false>(p, stream); break;
+      case 0: launch_cfg<128, 128, 64, 64, 4>(p, stream); break;
+      case 1: launch_cfg<128, 64, 64, 32, 4>(p, stream); break;
+      case 2: launch_cfg<256, 32, 64, 32, 4>(p, stream); break;
+      default: launch_cfg<256, 16, 64, 16, 4>(p, stream); break;
     }
   }
 }

@@ -3,25 +3,38 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-// Implicit-GEMM conv used for the forward pass and for dgrad.
-//   forward : rows m = output positions (N,To,Ho,Wo); gathered tensor = X (N,Ti,Hi,Wi,Cin);
-//             k = (tap, cin);  B = W  packed [Cout][taps][Cin]
-//   dgrad   : rows m = input positions (N,Ti,Hi,Wi);  gathered tensor = dY (N,To,Ho,Wo,Cout);
-//             k = (tap, cout); B = Wt packed [Cin][taps][Cout]; valid iff (i + pad - tap) % stride == 0
+// Implicit-GEMM conv used for the forward pass and for dgrad (one kernel, one addressing scheme).
+//
+// Rows of the GEMM are points q = (b, qt, qh, qw) of a row lattice (Rt, Rh, Rw).  For each spatial dim:
+//   output coordinate   o = q * os + or            (where the row is stored; output dims Ot, Oh, Ow)
+//   gather base         a = q * as + ao
+//   tap j (0 <= j < n)  reads gathered coordinate g = a + dir * j and weight tap d = b0 + j * bs
+//   forward : lattice = output grid, os=1 or=0, as=stride ao=-pad, dir=+1, n=k, b0=0 bs=1
+//   dgrad   : one launch per stride phase r (input coords i = q*s + r): os=s or=r, as=1,
+//             ao=(r + pad - d0)/s, dir=-1, b0=d0 = first tap with d = r + pad (mod s), bs=s,
+//             n = ceil((k - d0)/s).  Only contributing taps are visited: no divisibility tests and
+//             no MFMA work on structurally-zero operands (stride-2 dgrad does 1/4 of the naive work).
+// k is ordered (tap j, channel); the packed weight row has Kfull = taps_full * Cg elements.
 struct ConvParams {
   const uint16_t* x;        // gathered tensor (row stride ldx elements)
-  const uint16_t* w;        // packed weights [Ngemm][K]
-  uint16_t* y;              // output rows [M][ldy]
-  float* stats;             // optional BN partial sums [m_tiles][2][Ngemm]
+  const uint16_t* w;        // packed weights [Ngemm][taps_full][Cg]
+  uint16_t* y;              // output rows (row stride ldy)
+  float* stats;             // optional BN partial sums [m_tiles][2][Ngemm] (forward)
   const float* in_scale;    // optional per-gathered-channel affine (+ReLU) applied on load
   const float* in_shift;
   int affine;               // 0: none, 1: affine, 2: affine + relu
   int accum;                // 1: y += result (read-modify-write, bf16)
-  int M, Ngemm, K, Cg;      // GEMM dims; Cg = gathered channels (K = taps * Cg)
+  int M, Ngemm, Kfull, Cg;  // rows in this launch, output channels, packed row length, gathered channels
   int ldx, ldy;
   int Gt, Gh, Gw;           // gathered tensor spatial dims
-  int Rt, Rh, Rw;           // row-position spatial dims
-  int kt, kh, kw, st, sh, sw, pt, ph, pw;
+  int Rt, Rh, Rw;           // row lattice dims
+  int Ot, Oh, Ow;           // output tensor dims
+  int ost, osh, osw, ort, orh, orw;
+  int ast, ash, asw, aot, aoh, aow;
+  int dir;
+  int nt, nh, nw;           // taps visited per dim
+  int kh, kw;               // full kernel extents (weight tap index)
+  int bt0, bh0, bw0, bts, bhs, bws;
 };
 
 // Weight gradient: dW[n = cout][k = (tap, cin)] = sum_p dY[p][cout] * im2col(X)[p][k]

@@ -53,23 +53,43 @@ struct PackDesc {
   int cout, cin, cin_pad, taps;
 };
 
+// One 32(cout) x 32(cin) tile of one tap per block iteration, staged through LDS: the forward layout
+// [Cout][taps][Cin_pad] is written along cin, the dgrad layout [Cin][taps][Cout] along cout, so both
+// stores are contiguous (the dgrad pack is a transpose; scattered 2-B stores made it 10x slower).
 __global__ void pack_weights_kernel(const float* __restrict__ master, uint16_t* __restrict__ fwd,
                                     uint16_t* __restrict__ dgr, const PackDesc* __restrict__ descs) {
-  // 32-bit index math (largest conv weight is 2.4 M elements); one source element per thread, written
-  // to both packed layouts, so the fp32 read is coalesced and happens once.
   const PackDesc d = descs[blockIdx.y];
   const float* src = master + d.src;
   uint16_t* fo = fwd + d.fwd;
   uint16_t* dg = d.dgr >= 0 ? dgr + d.dgr : nullptr;
-  const int n_src = d.cout * d.cin * d.taps;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n_src; i += gridDim.x * blockDim.x) {
-    const int tap = i % d.taps;
-    const int r = i / d.taps;
-    const int c = r % d.cin;
-    const int n = r / d.cin;
-    const uint16_t v = f2bf(src[i]);
-    fo[(n * d.taps + tap) * d.cin_pad + c] = v;
-    if (dg) dg[(c * d.taps + tap) * d.cout + n] = v;
+  __shared__ uint16_t tile[32][33];
+  const int tn = (d.cout + 31) / 32, tc = (d.cin + 31) / 32;
+  const int ntiles = tn * tc * d.taps;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int tap = t % d.taps;
+    const int r = t / d.taps;
+    const int cb = (r % tc) * 32, nb = (r / tc) * 32;
+    // load rows n, columns c (source stride taps along c)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int n = nb + ty + 8 * k, c = cb + tx;
+      uint16_t v = 0;
+      if (n < d.cout && c < d.cin) {
+        v = f2bf(src[(n * d.cin + c) * d.taps + tap]);
+        fo[(n * d.taps + tap) * d.cin_pad + c] = v;
+      }
+      tile[ty + 8 * k][tx] = v;
+    }
+    if (dg) {
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int c = cb + ty + 8 * k, n = nb + tx;
+        if (n < d.cout && c < d.cin) dg[(c * d.taps + tap) * d.cout + n] = tile[tx][ty + 8 * k];
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -136,7 +156,7 @@ void sgd_momentum_launch(float* p, const float* g, float* buf, int64_t n, const 
 
 void pack_weights_launch(const float* master, uint16_t* fwd, uint16_t* dgr, const void* descs, int ntensors,
                          hipStream_t s) {
-  hipLaunchKernelGGL(pack_weights_kernel, dim3(64, ntensors), dim3(256), 0, s, master, fwd, dgr,
+  hipLaunchKernelGGL(pack_weights_kernel, dim3(128, ntensors), dim3(256), 0, s, master, fwd, dgr,
                      reinterpret_cast<const PackDesc*>(descs));
 }
 

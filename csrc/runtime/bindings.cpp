@@ -8,9 +8,13 @@
 #include <hip/hip_runtime.h>
 
 #include "../kernels/conv_params.h"
+#include <cstddef>
+
+static_assert(offsetof(ConvParams, bws) - offsetof(ConvParams, M) == 38 * sizeof(int),
+              "ConvParams integer block must be contiguous (filled from a 39-int geometry vector)");
 
 // ---- kernel launchers (defined in csrc/kernels/*.hip) ----
-void conv_igemm_launch(const ConvParams& p, int chunk, bool dgrad, hipStream_t stream);
+void conv_igemm_launch(const ConvParams& p, int chunk, hipStream_t stream);
 int conv_igemm_m_tiles(int M, int N);
 void conv_wgrad_launch(const WgradParams& p, int chunk, hipStream_t stream);
 void conv_wgrad_tile(int Cout, int K, int* bmw, int* bnw);
@@ -82,27 +86,27 @@ inline float* f32(const at::Tensor& t) {
 }
 inline float* f32o(const OptT& t) { return t.has_value() ? f32(*t) : nullptr; }
 
-// geometry vector: [M, Ngemm, K, Cg, ldx, ldy, Gt, Gh, Gw, Rt, Rh, Rw, kt, kh, kw, st, sh, sw, pt, ph, pw]
+// geometry vector (39): [M, Ngemm, Kfull, Cg, ldx, ldy, Gt, Gh, Gw, Rt, Rh, Rw, Ot, Oh, Ow,
+//   ost, osh, osw, ort, orh, orw, ast, ash, asw, aot, aoh, aow, dir, nt, nh, nw, kh, kw,
+//   bt0, bh0, bw0, bts, bhs, bws]   (see ConvParams; built by ops/conv.py)
 void conv_igemm(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, const OptT& stats,
                 const OptT& scale, const OptT& shift, int64_t affine, int64_t accum, std::vector<int64_t> g,
-                int64_t chunk, bool dgrad) {
-  TORCH_CHECK(g.size() == 21, "conv geometry must have 21 entries");
+                int64_t chunk) {
+  TORCH_CHECK(g.size() == 39, "conv geometry must have 39 entries");
   ConvParams p{};
   p.x = bfp(x); p.w = bfp(w); p.y = bfpm(y);
   p.stats = f32o(stats);
   p.in_scale = f32o(scale); p.in_shift = f32o(shift);
   p.affine = (int)affine; p.accum = (int)accum;
-  p.M = g[0]; p.Ngemm = g[1]; p.K = g[2]; p.Cg = g[3]; p.ldx = g[4]; p.ldy = g[5];
-  p.Gt = g[6]; p.Gh = g[7]; p.Gw = g[8]; p.Rt = g[9]; p.Rh = g[10]; p.Rw = g[11];
-  p.kt = g[12]; p.kh = g[13]; p.kw = g[14]; p.st = g[15]; p.sh = g[16]; p.sw = g[17];
-  p.pt = g[18]; p.ph = g[19]; p.pw = g[20];
+  int* f = &p.M;
+  for (int i = 0; i < 39; ++i) f[i] = (int)g[i];
   TORCH_CHECK(p.Cg % chunk == 0 && p.Cg > 0, "gathered channels must be a multiple of the chunk");
   TORCH_CHECK(p.Ngemm % 4 == 0, "output channels must be a multiple of 4");
   TORCH_CHECK(p.ldx % chunk == 0 && p.ldy % 4 == 0, "row strides must keep vector alignment");
   TORCH_CHECK(!affine || (scale.has_value() && shift.has_value()), "affine needs scale/shift");
-  TORCH_CHECK(p.K == p.kt * p.kh * p.kw * p.Cg, "K must equal taps*Cg");
+  TORCH_CHECK(w.numel() >= (int64_t)p.Ngemm * p.Kfull, "packed weight too small");
   if (p.M == 0) return;
-  conv_igemm_launch(p, (int)chunk, dgrad, cur_stream());
+  conv_igemm_launch(p, (int)chunk, cur_stream());
 }
 
 int64_t conv_m_tiles(int64_t M, int64_t N) { return conv_igemm_m_tiles((int)M, (int)N); }

@@ -36,7 +36,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops._ext import require
-from ..ops.conv import Act, ConvSpec
+from ..ops.conv import Act, ConvSpec, dgrad_phases, fwd_geometry
 from . import reference as R
 
 
@@ -110,6 +110,7 @@ class _ConvBN:
         self.scale = torch.ones(C, device=dev)
         self.shift = torch.zeros(C, device=dev)
         self.coef = torch.zeros(3 * C, device=dev)
+        self._geo = {}
         self.wf = None  # bf16 forward pack view [Cout, taps*Cin_pad]
         self.wd = None  # bf16 dgrad pack view [Cin, taps*Cout]
 
@@ -132,10 +133,12 @@ class _ConvBN:
             tiles = C.conv_m_tiles(M, s.cout)
             stats = self.eng.ws((self.name, "stats"), (tiles, 2, s.cout), torch.float32)
         aff = 0 if xf is None else (2 if xf.relu else 1)
-        g = [M, s.cout, s.taps * s.cin_pad, s.cin_pad, x.ld, s.cout, x.T, x.H, x.W, To, Ho, Wo,
-             *s.k, *s.stride, *s.pad]
+        key = ("fg", x.N, x.T, x.H, x.W, x.ld)
+        g = self._geo.get(key)
+        if g is None:
+            g = self._geo[key] = fwd_geometry(s, x.N, x.T, x.H, x.W, x.ld, s.cout)
         C.conv_igemm(x.t, self.wf, y, stats, None if xf is None else xf.scale, None if xf is None else xf.shift,
-                     aff, 0, g, s.chunk, False)
+                     aff, 0, g, s.chunk)
         bn = self.bn
         if train:
             C.bn_finalize(stats, stats.shape[0], s.cout, M, bn.weight, bn.bias, bn.running_mean, bn.running_var,
@@ -167,10 +170,14 @@ class _ConvBN:
     def dgrad(self, dy: Act, in_dims, out: torch.Tensor, accum: bool) -> Act:
         s, C = self.spec, self.eng.C
         Ti, Hi, Wi = in_dims
-        M = dy.N * Ti * Hi * Wi
-        g = [M, s.cin, s.taps * s.cout, s.cout, dy.ld, out.stride(0), dy.T, dy.H, dy.W, Ti, Hi, Wi,
-             *s.k, *s.stride, *s.pad]
-        C.conv_igemm(dy.t, self.wd, out, None, None, None, 0, 1 if accum else 0, g, 8, True)
+        key = ("dg", dy.N, tuple(in_dims), dy.ld, out.stride(0))
+        geo = self._geo.get(key)
+        if geo is None:
+            geo = self._geo[key] = dgrad_phases(s, dy.N, tuple(in_dims), (dy.T, dy.H, dy.W), dy.ld, out.stride(0))
+        for g in geo:
+            if accum and g[28] == 0:
+                continue
+            C.conv_igemm(dy.t, self.wd, out, None, None, None, 0, 1 if accum else 0, g, 8)
         return Act(out, dy.N, Ti, Hi, Wi)
 
     def bn_backward(self, g: Act, y: Act, mask_mode: int, mo: Optional[Act], mxf: Optional[_Xf],

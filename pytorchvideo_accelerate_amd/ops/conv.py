@@ -106,6 +106,50 @@ def pack_weight(w: torch.Tensor, spec: ConvSpec) -> Tuple[torch.Tensor, torch.Te
     return wf.contiguous().to(torch.bfloat16), wd.contiguous().to(torch.bfloat16)
 
 
+def fwd_geometry(spec: ConvSpec, N: int, T: int, H: int, W: int, ldx: int, ldy: int) -> list:
+    """Forward geometry vector (see ConvParams in csrc/kernels/conv_params.h)."""
+    To, Ho, Wo = spec.out_dims(T, H, W)
+    (kt, kh, kw), (st, sh, sw), (pt, ph, pw) = spec.k, spec.stride, spec.pad
+    M = N * To * Ho * Wo
+    return [M, spec.cout, spec.taps * spec.cin_pad, spec.cin_pad, ldx, ldy, T, H, W, To, Ho, Wo, To, Ho, Wo,
+            1, 1, 1, 0, 0, 0, st, sh, sw, -pt, -ph, -pw, 1, kt, kh, kw, kh, kw, 0, 0, 0, 1, 1, 1]
+
+
+def dgrad_phases(spec: ConvSpec, N: int, in_dims: Triple, out_dims: Triple, ldx: int, ldy: int) -> list:
+    """Per-stride-phase dgrad geometry vectors.
+
+    Input positions i = q*s + r (phase r) receive contributions only from taps d = d0 + j*s with
+    d0 = (r + pad) mod s, gathered at g = q + (r + pad - d0)/s - j: a dense stride-1 gather per phase.
+    A phase with no contributing tap (e.g. odd positions of a 1x1 stride-2 conv) has n = 0: the launch
+    just writes zeros.
+    """
+    geo = []
+    Ti, Hi, Wi = in_dims
+    To, Ho, Wo = out_dims
+    k, s, p = spec.k, spec.stride, spec.pad
+    for rt in range(s[0]):
+        for rh in range(s[1]):
+            for rw in range(s[2]):
+                R, ao, d0, n = [], [], [], []
+                for dim, r in enumerate((rt, rh, rw)):
+                    I = in_dims[dim]
+                    dd = (r + p[dim]) % s[dim]
+                    nn = (k[dim] - dd + s[dim] - 1) // s[dim] if dd < k[dim] else 0
+                    R.append((I - r + s[dim] - 1) // s[dim])
+                    ao.append((r + p[dim] - dd) // s[dim])
+                    d0.append(dd)
+                    n.append(nn)
+                if min(R) <= 0:
+                    continue
+                if min(n) == 0:
+                    n = [0, 0, 0]
+                M = N * R[0] * R[1] * R[2]
+                geo.append([M, spec.cin, spec.taps * spec.cout, spec.cout, ldx, ldy, To, Ho, Wo, R[0], R[1], R[2],
+                            Ti, Hi, Wi, s[0], s[1], s[2], rt, rh, rw, 1, 1, 1, ao[0], ao[1], ao[2], -1,
+                            n[0], n[1], n[2], k[1], k[2], d0[0], d0[1], d0[2], s[0], s[1], s[2]])
+    return geo
+
+
 def conv_m_tiles(M: int, N: int) -> int:
     return require().conv_m_tiles(M, N)
 
@@ -120,9 +164,8 @@ def conv_fwd(x: Act, wpack: torch.Tensor, spec: ConvSpec, out: Optional[torch.Te
     if out is None:
         out = torch.empty(M, spec.cout, device=x.t.device, dtype=torch.bfloat16)
     affine = 0 if in_scale is None else (2 if in_relu else 1)
-    g = [M, spec.cout, spec.taps * spec.cin_pad, spec.cin_pad, x.ld, out.stride(0),
-         x.T, x.H, x.W, To, Ho, Wo, *spec.k, *spec.stride, *spec.pad]
-    C.conv_igemm(x.t, wpack, out, stats, in_scale, in_shift, affine, 0, g, spec.chunk, False)
+    g = fwd_geometry(spec, x.N, x.T, x.H, x.W, x.ld, out.stride(0))
+    C.conv_igemm(x.t, wpack, out, stats, in_scale, in_shift, affine, 0, g, spec.chunk)
     return Act(out, x.N, To, Ho, Wo)
 
 
@@ -135,9 +178,10 @@ def conv_dgrad(dy: Act, wt_pack: torch.Tensor, spec: ConvSpec, in_dims: Triple, 
     M = dy.N * Ti * Hi * Wi
     if out is None:
         out = torch.empty(M, spec.cin, device=dy.t.device, dtype=torch.bfloat16)
-    g = [M, spec.cin, spec.taps * spec.cout, spec.cout, dy.ld, out.stride(0),
-         dy.T, dy.H, dy.W, Ti, Hi, Wi, *spec.k, *spec.stride, *spec.pad]
-    C.conv_igemm(dy.t, wt_pack, out, None, None, None, 0, 1 if accum else 0, g, 8, True)
+    for g in dgrad_phases(spec, dy.N, in_dims, (dy.T, dy.H, dy.W), dy.ld, out.stride(0)):
+        if accum and g[28] == 0:
+            continue
+        C.conv_igemm(dy.t, wt_pack, out, None, None, None, 0, 1 if accum else 0, g, 8)
     return Act(out, dy.N, Ti, Hi, Wi)
 
 

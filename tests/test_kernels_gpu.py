@@ -125,3 +125,15 @@ def test_conv_wgrad_affine():
     grad = torch.zeros_like(w)
     conv_wgrad(Act.from_ncthw(gy), Act.from_ncthw(x), spec, grad, in_scale=sc, in_shift=sh)
     assert rel_err(grad, w.grad) < 1.5e-2
+
+
+def test_pack_weights_kernel_matches_host_pack():
+    from pytorchvideo_accelerate_amd.models import reference as R
+    from pytorchvideo_accelerate_amd.models.fused import FusedNet
+    torch.manual_seed(0)
+    eng = FusedNet(R.create_slowfast(50, 10), torch.device(DEV))
+    for u in eng.units:
+        wf, wd = pack_weight(u.conv.weight.detach(), u.spec)
+        assert torch.equal(u.wf.view_as(wf), wf), u.name
+        if u.wd is not None:
+            assert torch.equal(u.wd.view_as(wd), wd), u.name
