@@ -22,14 +22,16 @@
 
 namespace {
 
-constexpr int BK = 32;
-
+// LDS tile rows are BK bf16 (64 or 128 bytes) of 16-byte slots, XOR-swizzled so that the 16-lane
+// groups of every ds_read_b128 fragment read hit 16 distinct slots of the 256-byte bank row
+// (brute-force checked against the gfx950 b128 lane groups for both row lengths).
+template <int BK>
 __device__ __forceinline__ int lds_off(int row, int slot) {
-  // 64-byte rows (BK = 32 bf16), 16-byte slots.
-  return row * 64 + ((slot ^ (((row >> 2) & 1) << 1)) << 4);
+  if constexpr (BK == 32) return row * 64 + ((slot ^ (((row >> 2) & 1) << 1)) << 4);
+  else return row * 128 + ((slot ^ (row & 6)) << 4);
 }
 
-template <int BM, int BN, int WM, int WN, int CH>
+template <int BM, int BN, int WM, int WN, int CH, int BK>
 __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64)
 void conv_igemm_kernel(const ConvParams p) {
   constexpr int NWN = BN / WN;
@@ -148,16 +150,16 @@ void conv_igemm_kernel(const ConvParams p) {
         if constexpr (CH == 8) v = pack8(f); else v = pack4(f);
       }
       const int row = idx / CPR;
-      if constexpr (CH == 8) *reinterpret_cast<VT*>(A + lds_off(row, col)) = v;
-      else *reinterpret_cast<VT*>(A + lds_off(row, col >> 1) + (col & 1) * 8) = v;
+      if constexpr (CH == 8) *reinterpret_cast<VT*>(A + lds_off<BK>(row, col)) = v;
+      else *reinterpret_cast<VT*>(A + lds_off<BK>(row, col >> 1) + (col & 1) * 8) = v;
     }
 #pragma unroll
     for (int s = 0; s < B_SLOTS; ++s) {
       const int idx = tid + s * NT;
       if (idx >= B_CHUNKS) break;
       const int row = idx / CPR;
-      if constexpr (CH == 8) *reinterpret_cast<VT*>(B + lds_off(row, col)) = rb[s];
-      else *reinterpret_cast<VT*>(B + lds_off(row, col >> 1) + (col & 1) * 8) = rb[s];
+      if constexpr (CH == 8) *reinterpret_cast<VT*>(B + lds_off<BK>(row, col)) = rb[s];
+      else *reinterpret_cast<VT*>(B + lds_off<BK>(row, col >> 1) + (col & 1) * 8) = rb[s];
     }
   };
 
@@ -180,22 +182,25 @@ void conv_igemm_kernel(const ConvParams p) {
     if (has_next) load();
     const char* A = smem + cur * TILE_BYTES;
     const char* B = A + BM * BK * 2;
-    bf16x8_t af[TM], bfr[TN];
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int row = wm * WM + i * 16 + frow;
-      af[i] = *reinterpret_cast<const bf16x8_t*>(A + lds_off(row, fslot));
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      bf16x8_t af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm * WM + i * 16 + frow;
+        af[i] = *reinterpret_cast<const bf16x8_t*>(A + lds_off<BK>(row, fslot + 4 * kk));
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = wn * WN + j * 16 + frow;
+        bfr[j] = *reinterpret_cast<const bf16x8_t*>(B + lds_off<BK>(row, fslot + 4 * kk));
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     }
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int row = wn * WN + j * 16 + frow;
-      bfr[j] = *reinterpret_cast<const bf16x8_t*>(B + lds_off(row, fslot));
-    }
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     if (has_next) store_lds(cur ^ 1);
     __syncthreads();
   }
@@ -266,12 +271,22 @@ void conv_igemm_kernel(const ConvParams p) {
   }
 }
 
-template <int BM, int BN, int WM, int WN, int CH>
+template <int BM, int BN, int WM, int WN, int CH, int BK>
 void launch_cfg(const ConvParams& p, hipStream_t stream) {
   constexpr int NT = (BM / WM) * (BN / WN) * 64;
   const int m_tiles = (p.M + BM - 1) / BM, n_tiles = (p.Ngemm + BN - 1) / BN;
   const size_t lds = 2 * (BM + BN) * BK * 2 + 2 * BN * 4 + (p.affine ? 2 * p.Cg * 4 : 0);
-  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH>), dim3(m_tiles * n_tiles), dim3(NT), lds, stream, p);
+  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK>), dim3(m_tiles * n_tiles), dim3(NT), lds, stream, p);
+}
+
+template <int CH, int BK>
+void launch_variant(int v, const ConvParams& p, hipStream_t stream) {
+  switch (v) {
+    case 0: launch_cfg<128, 128, 64, 64, CH, BK>(p, stream); break;
+    case 1: launch_cfg<128, 64, 64, 32, CH, BK>(p, stream); break;
+    case 2: launch_cfg<256, 32, 64, 32, CH, BK>(p, stream); break;
+    default: launch_cfg<256, 16, 64, 16, CH, BK>(p, stream); break;
+  }
 }
 
 }  // namespace
@@ -289,21 +304,16 @@ int conv_igemm_m_tiles(int M, int N) {
   return (M + bm - 1) / bm;
 }
 
+static int g_bk_override = -1;
+void conv_igemm_set_bk(int bk) { g_bk_override = bk; }
+
 void conv_igemm_launch(const ConvParams& p, int chunk, hipStream_t stream) {
   const int v = pick_variant(p.M, p.Ngemm);
+  const int K = p.nt * p.nh * p.nw * p.Cg;
+  int bk = g_bk_override > 0 ? g_bk_override : ((K >= 1024 && chunk == 8) ? 64 : 32);
   if (chunk == 8) {
-    switch (v) {
-      case 0: launch_cfg<128, 128, 64, 64, 8>(p, stream); break;
-      case 1: launch_cfg<128, 64, 64, 32, 8>(p, stream); break;
-      case 2: launch_cfg<256, 32, 64, 32, 8>(p, stream); break;
-      default: launch_cfg<256, 16, 64, 16, 8>(p, stream); break;
-    }
+    if (bk == 64) launch_variant<8, 64>(v, p, stream); else launch_variant<8, 32>(v, p, stream);
   } else {
-    switch (v) {
-      case 0: launch_cfg<128, 128, 64, 64, 4>(p, stream); break;
-      case 1: launch_cfg<128, 64, 64, 32, 4>(p, stream); break;
-      case 2: launch_cfg<256, 32, 64, 32, 4>(p, stream); break;
-      default: launch_cfg<256, 16, 64, 16, 4>(p, stream); break;
-    }
+    if (bk == 64) launch_variant<4, 64>(v, p, stream); else launch_variant<4, 32>(v, p, stream);
   }
 }

@@ -93,28 +93,32 @@ __global__ void pack_weights_kernel(const float* __restrict__ master, uint16_t* 
   }
 }
 
-// frames: [B][Ts][Hs][Ws][3] uint8 ; tidx: [B][T] source frame index ; box: [B][4] = (rh, rw, top, left) ;
-// flip: [B] ; out: [B][T][S][S][4] bf16 (channel 3 = 0)
-__global__ void video_preprocess_kernel(const uint8_t* __restrict__ frames, int Ts, int Hs, int Ws,
-                                        const int* __restrict__ tidx, const int* __restrict__ box,
-                                        const int* __restrict__ flip, int T, int S, float m0, float m1, float m2,
+// frames: packed uint8 clips, clip b = [Ts][Hs][Ws][3] at byte offset desc[b].off ;
+// desc: [B][10] int32 = (off_lo, off_hi, Ts, Hs, Ws, rh, rw, top, left, flip) ; tidx: [B][T] frame index
+// inside the clip ; out: [B][T][S][S][4] bf16 (channel 3 = 0).  One thread per output pixel; per-clip
+// geometry lets one launch serve a batch of differently sized source videos.
+__global__ void video_preprocess_kernel(const uint8_t* __restrict__ frames, const int* __restrict__ desc,
+                                        const int* __restrict__ tidx, int T, int S, float m0, float m1, float m2,
                                         float is0, float is1, float is2, uint16_t* __restrict__ out, int B) {
-  const int64_t total = (int64_t)B * T * S * S;
+  const int per_clip = T * S * S;
+  const int64_t total = (int64_t)B * per_clip;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    int64_t r = i;
+    const int b = (int)(i / per_clip);
+    int r = (int)(i - (int64_t)b * per_clip);
     const int x = r % S; r /= S;
-    const int y = r % S; r /= S;
-    const int t = r % T; r /= T;
-    const int b = (int)r;
-    const int rh = box[b * 4 + 0], rw = box[b * 4 + 1], top = box[b * 4 + 2], left = box[b * 4 + 3];
-    const int xr = (flip[b] ? (S - 1 - x) : x) + left;
+    const int y = r % S;
+    const int t = r / S;
+    const int* d = desc + b * 10;
+    const int64_t off = (int64_t)(uint32_t)d[0] | ((int64_t)d[1] << 31);
+    const int Hs = d[3], Ws = d[4], rh = d[5], rw = d[6], top = d[7], left = d[8], flip = d[9];
+    const int xr = (flip ? (S - 1 - x) : x) + left;
     const int yr = y + top;
     const float sy = fmaxf(((float)yr + 0.5f) * ((float)Hs / (float)rh) - 0.5f, 0.f);
     const float sx = fmaxf(((float)xr + 0.5f) * ((float)Ws / (float)rw) - 0.5f, 0.f);
     const int y0 = min((int)sy, Hs - 1), x0 = min((int)sx, Ws - 1);
     const int y1 = min(y0 + 1, Hs - 1), x1 = min(x0 + 1, Ws - 1);
     const float ly = sy - (float)y0, lx = sx - (float)x0;
-    const uint8_t* f = frames + ((int64_t)b * Ts + tidx[b * T + t]) * Hs * Ws * 3;
+    const uint8_t* f = frames + off + (int64_t)tidx[b * T + t] * Hs * Ws * 3;
     const uint8_t* p00 = f + ((int64_t)y0 * Ws + x0) * 3;
     const uint8_t* p01 = f + ((int64_t)y0 * Ws + x1) * 3;
     const uint8_t* p10 = f + ((int64_t)y1 * Ws + x0) * 3;
@@ -162,14 +166,13 @@ void pack_weights_launch(const float* master, uint16_t* fwd, uint16_t* dgr, cons
 
 int pack_desc_size() { return (int)sizeof(PackDesc); }
 
-void video_preprocess_launch(const uint8_t* frames, int B, int Ts, int Hs, int Ws, const int* tidx, const int* box,
-                             const int* flip, int T, int S, const float* mean, const float* std_, uint16_t* out,
-                             hipStream_t s) {
+void video_preprocess_launch(const uint8_t* frames, const int* desc, const int* tidx, int B, int T, int S,
+                             const float* mean, const float* std_, uint16_t* out, hipStream_t s) {
   const int64_t total = (int64_t)B * T * S * S;
   int64_t blocks = (total + 255) / 256;
   if (blocks > 16384) blocks = 16384;
-  hipLaunchKernelGGL(video_preprocess_kernel, dim3((int)blocks), dim3(256), 0, s, frames, Ts, Hs, Ws, tidx, box, flip,
-                     T, S, mean[0], mean[1], mean[2], 1.f / std_[0], 1.f / std_[1], 1.f / std_[2], out, B);
+  hipLaunchKernelGGL(video_preprocess_kernel, dim3((int)blocks), dim3(256), 0, s, frames, desc, tidx, T, S, mean[0],
+                     mean[1], mean[2], 1.f / std_[0], 1.f / std_[1], 1.f / std_[2], out, B);
 }
 
 void synth_frames_launch(uint8_t* out, int64_t n, uint32_t seed, hipStream_t s) {

@@ -16,6 +16,7 @@ static_assert(offsetof(ConvParams, bws) - offsetof(ConvParams, M) == 38 * sizeof
 // ---- kernel launchers (defined in csrc/kernels/*.hip) ----
 void conv_igemm_launch(const ConvParams& p, int chunk, hipStream_t stream);
 int conv_igemm_m_tiles(int M, int N);
+void conv_igemm_set_bk(int bk);
 void conv_wgrad_launch(const WgradParams& p, int chunk, hipStream_t stream);
 void conv_wgrad_tile(int Cout, int K, int* bmw, int* bnw);
 void wgrad_reduce_launch(float* accbuf, float* grad, int splits, int Cout, int taps, int Cin, int Cin_real,
@@ -55,10 +56,11 @@ void sgd_momentum_launch(float* p, const float* g, float* buf, int64_t n, const 
 void pack_weights_launch(const float* master, uint16_t* fwd, uint16_t* dgr, const void* descs, int ntensors,
                          hipStream_t s);
 int pack_desc_size();
-void video_preprocess_launch(const uint8_t* frames, int B, int Ts, int Hs, int Ws, const int* tidx, const int* box,
-                             const int* flip, int T, int S, const float* mean, const float* std_, uint16_t* out,
-                             hipStream_t s);
+void video_preprocess_launch(const uint8_t* frames, const int* desc, const int* tidx, int B, int T, int S,
+                             const float* mean, const float* std_, uint16_t* out, hipStream_t s);
 void synth_frames_launch(uint8_t* out, int64_t n, uint32_t seed, hipStream_t s);
+
+void register_clip_reader(pybind11::module& m);
 
 namespace {
 
@@ -237,13 +239,16 @@ void pack_weights(const at::Tensor& master, const at::Tensor& fwd, const at::Ten
   pack_weights_launch(f32(master), bfpm(fwd), bfpm(dgr), descs.data_ptr(), (int)ntensors, cur_stream());
 }
 
-void video_preprocess(const at::Tensor& frames, const at::Tensor& tidx, const at::Tensor& box, const at::Tensor& flip,
-                      int64_t T, int64_t S, std::vector<double> mean, std::vector<double> std_, const at::Tensor& out) {
-  TORCH_CHECK(frames.dim() == 5 && frames.size(4) == 3 && frames.scalar_type() == at::kByte, "frames [B,T,H,W,3] u8");
+// frames: packed uint8 ; desc [B,10] int32 ; tidx [B,T] int32 ; out [B*T*S*S, 4] bf16
+void video_preprocess(const at::Tensor& frames, const at::Tensor& desc, const at::Tensor& tidx, int64_t T, int64_t S,
+                      std::vector<double> mean, std::vector<double> std_, const at::Tensor& out) {
+  TORCH_CHECK(frames.scalar_type() == at::kByte, "frames must be uint8");
+  TORCH_CHECK(desc.dim() == 2 && desc.size(1) == 10 && desc.scalar_type() == at::kInt, "desc [B,10] int32");
+  TORCH_CHECK(tidx.dim() == 2 && tidx.size(1) == T && tidx.scalar_type() == at::kInt, "tidx [B,T] int32");
+  TORCH_CHECK(out.numel() >= desc.size(0) * T * S * S * 4, "output too small");
   const float m[3] = {(float)mean[0], (float)mean[1], (float)mean[2]};
   const float s[3] = {(float)std_[0], (float)std_[1], (float)std_[2]};
-  video_preprocess_launch(frames.data_ptr<uint8_t>(), (int)frames.size(0), (int)frames.size(1), (int)frames.size(2),
-                          (int)frames.size(3), tidx.data_ptr<int>(), box.data_ptr<int>(), flip.data_ptr<int>(),
+  video_preprocess_launch(frames.data_ptr<uint8_t>(), desc.data_ptr<int>(), tidx.data_ptr<int>(), (int)desc.size(0),
                           (int)T, (int)S, m, s, bfpm(out), cur_stream());
 }
 
@@ -257,6 +262,7 @@ PYBIND11_MODULE(_C, m) {
   m.doc() = "gfx950 HIP kernels for pytorchvideo_accelerate_amd";
   m.def("conv_igemm", &conv_igemm);
   m.def("conv_m_tiles", &conv_m_tiles);
+  m.def("conv_set_bk", [](int64_t bk) { conv_igemm_set_bk((int)bk); });
   m.def("wgrad_tile", &wgrad_tile);
   m.def("conv_wgrad", &conv_wgrad);
   m.def("wgrad_reduce", &wgrad_reduce);
@@ -277,4 +283,5 @@ PYBIND11_MODULE(_C, m) {
   m.def("pack_desc_size", &pack_desc_size);
   m.def("video_preprocess", &video_preprocess);
   m.def("synth_frames", &synth_frames);
+  register_clip_reader(m);
 }

@@ -115,31 +115,37 @@ class GpuClipBatch:
             self._out[key] = t
         return t
 
-    def params_tensors(self, params: Sequence[ClipParams]):
-        B = len(params)
-        tidx = torch.tensor([p.tidx for p in params], dtype=torch.int32)
-        box = torch.tensor([[p.rh, p.rw, p.top, p.left] for p in params], dtype=torch.int32)
-        flip = torch.tensor([int(p.flip) for p in params], dtype=torch.int32)
-        pin = torch.cuda.is_available()
-        if pin:
-            tidx, box, flip = tidx.pin_memory(), box.pin_memory(), flip.pin_memory()
-        d = self.device
-        return (tidx.to(d, non_blocking=True), box.to(d, non_blocking=True), flip.to(d, non_blocking=True))
-
-    def __call__(self, frames: torch.Tensor, params: Sequence[ClipParams]):
-        """frames: [B, T_src, H, W, 3] uint8 on device -> list of Acts ([slow, fast] or [clip])."""
+    def _run(self, frames: torch.Tensor, desc: torch.Tensor, tidx: torch.Tensor):
         from ..ops.conv import Act
-        B = frames.shape[0]
-        tidx, box, flip = self.params_tensors(params)
+        B = desc.shape[0]
         outs = []
-        fast = self._buf("fast", (B * self.T * self.S * self.S, 4))
         if self.alpha:
-            Ts = len(self.slow_sel)
-            slow = self._buf("slow", (B * Ts * self.S * self.S, 4))
-            sel = self.slow_sel.to(self.device)
+            sel = self.slow_sel.to(tidx.device)
             stidx = tidx.index_select(1, sel).contiguous()
-            self.C.video_preprocess(frames, stidx, box, flip, Ts, self.S, self.mean, self.std, slow)
+            Ts = stidx.shape[1]
+            slow = self._buf("slow", (B * Ts * self.S * self.S, 4))
+            self.C.video_preprocess(frames, desc, stidx, Ts, self.S, self.mean, self.std, slow)
             outs.append(Act(slow, B, Ts, self.S, self.S))
-        self.C.video_preprocess(frames, tidx, box, flip, self.T, self.S, self.mean, self.std, fast)
+        fast = self._buf("fast", (B * self.T * self.S * self.S, 4))
+        self.C.video_preprocess(frames, desc, tidx, self.T, self.S, self.mean, self.std, fast)
         outs.append(Act(fast, B, self.T, self.S, self.S))
         return outs
+
+    def __call__(self, frames: torch.Tensor, params: Sequence[ClipParams]):
+        """frames: [B, T_src, H, W, 3] uint8 on device (same source shape) -> [slow, fast] or [clip] Acts."""
+        B, Ts, H, W, _ = frames.shape
+        per = Ts * H * W * 3
+        desc = torch.tensor([[(b * per) & 0x7FFFFFFF, (b * per) >> 31, Ts, H, W, p.rh, p.rw, p.top, p.left,
+                              int(p.flip)] for b, p in enumerate(params)], dtype=torch.int32)
+        tidx = torch.tensor([p.tidx for p in params], dtype=torch.int32)
+        pin = self.device.type == "cuda"
+        if pin:
+            desc, tidx = desc.pin_memory(), tidx.pin_memory()
+        return self._run(frames, desc.to(self.device, non_blocking=pin), tidx.to(self.device, non_blocking=pin))
+
+    def from_packed(self, frames: torch.Tensor, desc: torch.Tensor, num_frames: int):
+        """Loader path: packed, already temporally-subsampled clips (tidx = identity)."""
+        B = desc.shape[0]
+        tidx = torch.arange(num_frames, dtype=torch.int32).repeat(B, 1)
+        return self._run(frames, desc.to(self.device, non_blocking=True),
+                         tidx.to(self.device, non_blocking=True))

@@ -1,0 +1,128 @@
+"""Execution back-ends behind one training-step interface.
+
+* :class:`FusedBackend` — the MI355X path: ``models/fused.FusedNet`` (gfx950 kernels, bf16) with the
+  bucketed RCCL gradient all-reduce of ``parallel/ddp.GradSync`` overlapped with the backward pass.
+* :class:`TorchBackend` — the reference PyTorch modules with autograd: CPU runs (``--cpu``, gloo DDP), fp32
+  (``--mixed_precision no``) or autocast fp16/bf16 on GPU.  Gradients land in the same flat buffer
+  (``FlatParams``), so the optimizer, gradient sync and checkpointing code are shared.
+
+Both expose ``train_step(batch, labels, loss_scale, sync) -> (loss, logits)``, ``eval_step``,
+``flat`` and ``model`` (the pytorchvideo-keyed ``nn.Module`` used for ``state_dict``).
+"""
+from __future__ import annotations
+
+import contextlib
+from typing import List, Optional
+
+import torch
+import torch.nn.functional as F
+
+from ..models.fused import FlatParams
+from ..parallel.ddp import GradSync
+from ..parallel.dist import DistState
+
+
+def _ordered_params(model):
+    return [(n, p) for n, p in reversed(list(model.named_parameters()))]
+
+
+class TorchBackend:
+    name = "torch"
+
+    def __init__(self, model: torch.nn.Module, state: DistState, mixed_precision: str = "no",
+                 bucket_mb: float = 32.0, trainable: Optional[List[torch.nn.Parameter]] = None):
+        self.model = model.to(state.device)
+        self.state = state
+        self.device = state.device
+        self.flat = FlatParams(_ordered_params(self.model), self.device)
+        self.sync = GradSync(self.flat.grad, state, bucket_mb)
+        self.mp = mixed_precision
+        self.amp_dtype = {"bf16": torch.bfloat16, "fp16": torch.float16}.get(mixed_precision)
+        self.scaler = None
+        if mixed_precision == "fp16" and self.device.type == "cuda":
+            self.scaler = torch.amp.GradScaler("cuda")
+
+    def _autocast(self):
+        if self.amp_dtype is None:
+            return contextlib.nullcontext()
+        return torch.autocast(self.device.type, dtype=self.amp_dtype)
+
+    def _input(self, video):
+        if isinstance(video, (list, tuple)):
+            return [v.to(self.device, non_blocking=True) for v in video]
+        return video.to(self.device, non_blocking=True)
+
+    def train(self):
+        self.model.train()
+
+    def eval(self):
+        self.model.eval()
+
+    def train_step(self, video, labels, loss_scale: float = 1.0, sync: bool = True):
+        if self.flat.zeroed:
+            self.flat.grad.zero_()
+            self.flat.zeroed = False
+        x = self._input(video)
+        labels = labels.to(self.device)
+        with self._autocast():
+            out = self.model(x)
+        loss = F.cross_entropy(out.float(), labels)
+        scaled = loss * loss_scale
+        if self.scaler is not None:
+            scaled = self.scaler.scale(scaled)
+        scaled.backward()
+        self.flat.rebind()
+        self.sync.begin(sync)
+        self.sync.finish()
+        return loss.detach(), out.detach().float()
+
+    @torch.no_grad()
+    def eval_step(self, video):
+        with self._autocast():
+            return self.model(self._input(video)).float()
+
+    def after_optimizer_step(self):
+        pass
+
+
+class FusedBackend:
+    name = "fused"
+
+    def __init__(self, model: torch.nn.Module, state: DistState, bucket_mb: float = 32.0):
+        from ..models.fused import FusedNet
+        self.state = state
+        self.device = state.device
+        self.net = FusedNet(model, self.device)
+        self.model = model
+        self.flat = self.net.flat
+        bounds = sorted(set(self.flat.span(p)[1] for p in self.flat.params))
+        self.sync = GradSync(self.flat.grad, state, bucket_mb, boundaries=bounds)
+        self.net.grad_hook = self.sync.progress
+        self.scaler = None
+        self._training = True
+
+    def train(self):
+        self._training = True
+        self.model.train()
+
+    def eval(self):
+        self._training = False
+        self.model.eval()
+
+    def train_step(self, video, labels, loss_scale: float = 1.0, sync: bool = True):
+        self.sync.begin(sync)
+        loss, logits = self.net.forward_backward(video, labels.to(self.device), loss_scale)
+        self.sync.finish()
+        return loss, logits
+
+    @torch.no_grad()
+    def eval_step(self, video):
+        return self.net.forward_eval(video)
+
+    def after_optimizer_step(self):
+        self.net.pack()
+
+    def reload_weights(self):
+        """After parameters were overwritten (checkpoint load): re-point views and re-pack bf16."""
+        self.flat.rebind()
+        self.net.pack()

@@ -93,8 +93,11 @@ class FlatParams:
             if p.data.data_ptr() != self.data[o:o + n].data_ptr():
                 self.data[o:o + n].copy_(p.data.reshape(-1))
                 p.data = self.data[o:o + n].view(p.shape)
-            if p.grad is None or p.grad.data_ptr() != self.grad[o:o + n].data_ptr():
-                p.grad = self.grad[o:o + n].view(p.shape)
+            gv = self.grad[o:o + n].view(p.shape)
+            if p.grad is None or p.grad.data_ptr() != gv.data_ptr():
+                if p.grad is not None:  # autograd replaced the view: keep its values
+                    gv.copy_(p.grad)
+                p.grad = gv
 
 
 class _ConvBN:
@@ -585,7 +588,8 @@ class FusedNet:
                 else:
                     gv.copy_(g)
             self._progress(self._head_hi)
-            self._backward_backbone(outs, gfeat.contiguous(), ks)
+            if any(p.requires_grad for p in self.units[0].conv.parameters()):  # else frozen backbone
+                self._backward_backbone(outs, gfeat.contiguous(), ks)
         return loss.detach(), logits.detach()
 
     def _backward_backbone(self, outs: List[Act], gfeat: torch.Tensor, ks):

@@ -31,6 +31,8 @@ class FusedSGD(torch.optim.SGD):
         self.found_inf = torch.zeros(1, device=flat.data.device, dtype=torch.int32)
         self._first = True
         self._C = require() if flat.data.is_cuda else None
+        self.span = None            # (lo, hi): only this slice of the flat buffer trains (frozen backbone)
+        self.step_was_skipped = False
 
     def _bind_state(self):
         for p in self.flat.params:
@@ -44,17 +46,19 @@ class FusedSGD(torch.optim.SGD):
     @torch.no_grad()
     def step(self, closure=None, grad_scale: float = 1.0):
         g = self.param_groups[0]
+        lo, hi = self.span if self.span is not None else (0, self.flat.numel)
+        data, grad, buf = self.flat.data[lo:hi], self.flat.grad[lo:hi], self.buf[lo:hi]
         if self._C is None:  # CPU path: plain torch math on the flat buffers
             lr, m, wd = g["lr"], g["momentum"], g["weight_decay"]
-            d = self.flat.grad * grad_scale + wd * self.flat.data
+            d = grad * grad_scale + wd * data
             if self._first:
-                self.buf.copy_(d)
+                buf.copy_(d)
             else:
-                self.buf.mul_(m).add_(d)
-            self.flat.data.add_(self.buf, alpha=-lr)
+                buf.mul_(m).add_(d)
+            data.add_(buf, alpha=-lr)
         else:
             self.set_lr_tensor()
-            self._C.sgd_momentum(self.flat.data, self.flat.grad, self.buf, self.lr_t, g["momentum"],
+            self._C.sgd_momentum(data, grad, buf, self.lr_t, g["momentum"],
                                  g["weight_decay"], grad_scale, 1 if self._first else 0, None)
         if self._first:
             self._bind_state()

@@ -51,6 +51,10 @@ class GradSync:
         self._works = []
         self.active = False
 
+    def restrict(self, lo: int, hi: int):
+        """Only all-reduce grad[lo:hi] (e.g. frozen backbone: just the head)."""
+        self.buckets = [(max(a, lo), min(b, hi)) for a, b in self.buckets if a < hi and b > lo]
+
     def begin(self, sync: bool = True):
         """Start a backward pass; ``sync=False`` = no_sync micro-step (accumulate locally)."""
         self._next = 0

@@ -53,7 +53,11 @@ def main():
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default="")
+    ap.add_argument("--bk", type=int, default=-1)
     a = ap.parse_args()
+    if a.bk > 0:
+        from pytorchvideo_accelerate_amd.ops._ext import require
+        require().conv_set_bk(a.bk)
     dev = "cuda"
     tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0}
     print(f"{'layer':18s} {'M':>8s} {'N':>5s} {'K':>5s} | {'fwd us':>8s} {'TF':>6s} | {'dgrad us':>8s} {'TF':>6s} | {'wgrad us':>8s} {'TF':>6s}")

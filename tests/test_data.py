@@ -1,0 +1,187 @@
+"""Data semantics: clip samplers, index math, Kinetics scan, sharding, decoders, native reader
+(pytorchvideo/torchvision are not importable, so expectations are hand-derived)."""
+import json
+import os
+from fractions import Fraction
+
+import numpy as np
+import pytest
+import torch
+
+from pytorchvideo_accelerate_amd.data.clip_sampling import (RandomClipSampler, UniformClipSampler,
+                                                            make_clip_sampler)
+from pytorchvideo_accelerate_amd.data.kinetics import (LabeledVideoPaths, SyntheticVideoPaths, VideoClipDataset,
+                                                       collate_gpu, distributed_video_indices)
+from pytorchvideo_accelerate_amd.data.transforms import (ClipParams, center_crop_box, pack_pathway_indices,
+                                                         reference_transform, sample_params,
+                                                         short_side_scale_size, uniform_temporal_indices)
+from pytorchvideo_accelerate_amd.data.video import RawFramesVideo, SyntheticVideo, frame_range
+
+
+def test_pack_pathway_indices_are_truncated_linspace():
+    assert pack_pathway_indices(32, 4).tolist() == [0, 4, 8, 13, 17, 22, 26, 31]
+    assert pack_pathway_indices(8, 4).tolist() == [0, 7]
+
+
+def test_uniform_temporal_subsample():
+    assert uniform_temporal_indices(64, 32).tolist() == torch.linspace(0, 63, 32).long().tolist()
+    assert uniform_temporal_indices(10, 4).tolist() == [0, 3, 6, 9]
+    assert uniform_temporal_indices(3, 5).tolist() == [0, 0, 1, 1, 2]  # repeats when too short
+
+
+def test_short_side_scale_and_crops():
+    assert short_side_scale_size(240, 320, 256) == (256, 341)
+    assert short_side_scale_size(320, 240, 256) == (341, 256)
+    assert short_side_scale_size(256, 256, 300) == (300, 300)
+    assert center_crop_box(256, 341, 256) == (0, 42)
+    assert center_crop_box(257, 257, 224) == (16, 16)   # round(16.5) banker's -> 16 like torchvision
+
+
+def test_random_clip_sampler():
+    import random
+    random.seed(0)
+    s = RandomClipSampler(Fraction(32, 15))
+    for _ in range(20):
+        c = s(None, Fraction(10))
+        assert 0 <= c.clip_start_sec <= 10 - Fraction(32, 15) and c.is_last_clip
+        assert c.clip_end_sec - c.clip_start_sec == Fraction(32, 15)
+    c = s(None, Fraction(1))  # shorter than the clip: start at 0
+    assert c.clip_start_sec == 0
+
+
+def test_uniform_clip_sampler_counts_and_bounds():
+    d = Fraction(64, 30)
+    s = UniformClipSampler(d)
+    clips, last = [], None
+    while True:
+        c = s(last, Fraction(10))
+        clips.append(c)
+        last = c.clip_end_sec
+        if c.is_last_clip:
+            break
+    assert len(clips) == 4 and clips[0].clip_start_sec == 0 and clips[1].clip_start_sec == d
+    assert [c.clip_index for c in clips] == [0, 1, 2, 3]
+    assert UniformClipSampler(d).num_clips(Fraction(10)) == 4
+    assert UniformClipSampler(d).num_clips(Fraction(1)) == 1
+    assert isinstance(make_clip_sampler("uniform", d), UniformClipSampler)
+    with pytest.raises(NotImplementedError):
+        make_clip_sampler("bogus", d)
+
+
+def test_frame_range():
+    assert frame_range(Fraction(0), Fraction(64, 30), 30, 300) == (0, 64)
+    assert frame_range(Fraction(1), Fraction(2), 30, 45) == (30, 45)
+
+
+def test_distributed_indices_match_torch_sampler():
+    from torch.utils.data import DistributedSampler
+    ds = list(range(11))
+    for world in (1, 2, 3, 4):
+        for rank in range(world):
+            ref = list(DistributedSampler(ds, num_replicas=world, rank=rank, shuffle=True, seed=0))
+            assert distributed_video_indices(11, rank, world, seed=0, epoch=0) == ref
+
+
+def _make_corpus(root, classes=("b_cls", "a_cls"), per=2, T=20, H=24, W=32, fps=10):
+    rng = np.random.default_rng(0)
+    for split in ("train", "val"):
+        for c in classes:
+            d = os.path.join(root, split, c)
+            os.makedirs(d)
+            for i in range(per):
+                np.save(os.path.join(d, f"v{i}.npy"), rng.integers(0, 255, (T, H, W, 3), dtype=np.uint8))
+                with open(os.path.join(d, f"v{i}.json"), "w") as fh:
+                    json.dump({"fps": fps}, fh)
+            open(os.path.join(d, "notes.txt"), "w").close()
+
+
+def test_kinetics_directory_scan(tmp_path):
+    _make_corpus(str(tmp_path))
+    p = LabeledVideoPaths.from_directory(str(tmp_path / "train"))
+    assert p.classes == ["a_cls", "b_cls"] and p.num_videos == 4 and p.num_labels == 2
+    assert p[0][1]["label"] == 0 and p[0][0].endswith("a_cls/v0.npy")
+    v = RawFramesVideo(p[0][0])
+    assert v.fps == 10 and v.num_frames == 20 and v.duration == 2
+
+
+def test_clip_dataset_train_and_full_val(tmp_path):
+    _make_corpus(str(tmp_path), T=50, fps=10)  # 5 s videos
+    vids = LabeledVideoPaths.from_directory(str(tmp_path / "train"))
+    tr = VideoClipDataset(vids, 1.6, True, num_frames=8, crop_size=16, slowfast_alpha=4, mode="cpu",
+                          min_scale=20, max_scale=24)
+    assert len(tr) == 4
+    s = tr[0]
+    slow, fast = s["video"]
+    assert fast.shape == (3, 8, 16, 16) and slow.shape == (3, 2, 16, 16)
+    va = VideoClipDataset(vids, 1.6, False, num_frames=8, crop_size=16, slowfast_alpha=None, mode="cpu",
+                          min_scale=20)
+    assert len(va) == 4 * 3  # every uniform clip: 0-1.6, 1.6-3.2, 3.2-4.8
+    assert va[0]["video"].shape == (3, 8, 16, 16)
+    # reference LimitDataset behaviour: one clip per video
+    va1 = VideoClipDataset(vids, 1.6, False, num_frames=8, crop_size=16, slowfast_alpha=None, mode="cpu",
+                           min_scale=20, full_val=False)
+    assert len(va1) == 4
+    # distributed shards partition the (padded) video list
+    a = VideoClipDataset(vids, 1.6, True, 8, 16, None, rank=0, world=3, distributed=True, mode="cpu")
+    b = VideoClipDataset(vids, 1.6, True, 8, 16, None, rank=1, world=3, distributed=True, mode="cpu")
+    assert len(a) == len(b) == 2
+
+
+def test_gpu_mode_items_and_collate(tmp_path):
+    _make_corpus(str(tmp_path), T=30, H=24, W=32, fps=10)
+    vids = LabeledVideoPaths.from_directory(str(tmp_path / "train"))
+    ds = VideoClipDataset(vids, 1.6, True, num_frames=8, crop_size=16, slowfast_alpha=4, mode="gpu",
+                          min_scale=20, max_scale=24)
+    items = [ds[i] for i in range(3)]
+    assert items[0]["frames"].shape == (8, 24, 32, 3) and items[0]["frames"].dtype == torch.uint8
+    b = collate_gpu(items)
+    assert b["desc"].shape == (3, 10) and b["frames"].numel() == 3 * 8 * 24 * 32 * 3
+    assert b["desc"][1, 0].item() == 8 * 24 * 32 * 3
+
+
+def test_reference_transform_shapes_and_flip():
+    fr = torch.randint(0, 255, (10, 30, 40, 3), dtype=torch.uint8)
+    p = ClipParams(list(range(0, 10, 2)), 30, 40, 2, 5, False)
+    x = reference_transform(fr, p, 16)
+    assert x.shape == (3, 5, 16, 16)
+    xf = reference_transform(fr, ClipParams(p.tidx, 30, 40, 2, 5, True), 16)
+    torch.testing.assert_close(xf, x.flip(-1))
+    # identity resize: normalised pixels exactly
+    ref = (fr[0, 2, 5:21].permute(1, 0).float() / 255 - 0.45) / 0.225
+    torch.testing.assert_close(x[:, 0, 0, :], ref)
+
+
+def test_sample_params_rng_stream_matches_reference_order():
+    g1 = torch.Generator().manual_seed(5)
+    p = sample_params(64, 240, 320, 32, 224, True, generator=g1)
+    g2 = torch.Generator().manual_seed(5)
+    size = int(torch.randint(256, 321, (1,), generator=g2).item())
+    rh, rw = short_side_scale_size(240, 320, size)
+    top = int(torch.randint(0, rh - 224 + 1, size=(1,), generator=g2).item())
+    left = int(torch.randint(0, rw - 224 + 1, size=(1,), generator=g2).item())
+    flip = bool(torch.rand(1, generator=g2).item() < 0.5)
+    assert (p.rh, p.rw, p.top, p.left, p.flip) == (rh, rw, top, left, flip)
+
+
+def test_synthetic_corpus_deterministic():
+    c = SyntheticVideoPaths(6, 3)
+    assert c.num_labels == 3 and c.num_videos == 6
+    a = c.open(2).get_clip(0, Fraction(1, 2))
+    b = c.open(2).get_clip(0, Fraction(1, 2))
+    assert a.shape == (15, 256, 340, 3) and np.array_equal(a, b) and a.min() >= 1
+
+
+def test_native_clip_reader(tmp_path):
+    from pytorchvideo_accelerate_amd.ops import _ext
+    C = _ext.load()
+    if C is None:
+        pytest.skip("extension not built")
+    arr = np.random.default_rng(1).integers(0, 255, (12, 5, 6, 3), dtype=np.uint8)
+    p = str(tmp_path / "v.npy")
+    np.save(p, arr)
+    v = RawFramesVideo(p)
+    fb = 5 * 6 * 3
+    dst = torch.zeros(2 * 3 * fb, dtype=torch.uint8)
+    C.read_clips(dst, [(p, v.data_offset, fb, [0, 5, 11], 0), (p, v.data_offset, fb, [2, 2, 3], 3 * fb)], 4)
+    out = dst.numpy().reshape(6, 5, 6, 3)
+    assert np.array_equal(out[:3], arr[[0, 5, 11]]) and np.array_equal(out[3:], arr[[2, 2, 3]])
