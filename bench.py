@@ -73,7 +73,7 @@ def main():
     gen = torch.Generator().manual_seed(1000 + st.rank)
     frames = torch.empty(B, a.src_frames, a.src_h, a.src_w, 3, dtype=torch.uint8, device=dev)
     eng.C.synth_frames(frames, 7 + st.rank)
-    prep = GpuClipBatch(dev, a.frames, a.crop, a.alpha)
+    prep = GpuClipBatch(dev, a.frames, a.crop, a.alpha, s2d=eng.input_s2d)
     labels_all = torch.randint(0, a.classes, (64, B), generator=gen).to(dev)
 
     def step(i):

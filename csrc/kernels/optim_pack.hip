@@ -99,7 +99,8 @@ __global__ void pack_weights_kernel(const float* __restrict__ master, uint16_t* 
 // geometry lets one launch serve a batch of differently sized source videos.
 __global__ void video_preprocess_kernel(const uint8_t* __restrict__ frames, const int* __restrict__ desc,
                                         const int* __restrict__ tidx, int T, int S, float m0, float m1, float m2,
-                                        float is0, float is1, float is2, uint16_t* __restrict__ out, int B) {
+                                        float is0, float is1, float is2, uint16_t* __restrict__ out, int B,
+                                        int s2d) {
   const int per_clip = T * S * S;
   const int64_t total = (int64_t)B * per_clip;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
@@ -134,7 +135,12 @@ __global__ void video_preprocess_kernel(const uint8_t* __restrict__ frames, cons
     v[1] = (v[1] * (1.f / 255.f) - m1) * is1;
     v[2] = (v[2] * (1.f / 255.f) - m2) * is2;
     v[3] = 0.f;
-    *reinterpret_cast<uint2*>(out + i * 4) = pack4(v);
+    int64_t o = i * 4;
+    if (s2d) {  // space-to-depth: 2x2 pixel block x RGB0 = 16 channels at s2d position (y/2, x/2)
+      const int S2 = S >> 1;
+      o = ((((int64_t)b * T + t) * S2 + (y >> 1)) * S2 + (x >> 1)) * 16 + ((y & 1) * 2 + (x & 1)) * 4;
+    }
+    *reinterpret_cast<uint2*>(out + o) = pack4(v);
   }
 }
 
@@ -167,12 +173,12 @@ void pack_weights_launch(const float* master, uint16_t* fwd, uint16_t* dgr, cons
 int pack_desc_size() { return (int)sizeof(PackDesc); }
 
 void video_preprocess_launch(const uint8_t* frames, const int* desc, const int* tidx, int B, int T, int S,
-                             const float* mean, const float* std_, uint16_t* out, hipStream_t s) {
+                             const float* mean, const float* std_, uint16_t* out, int s2d, hipStream_t s) {
   const int64_t total = (int64_t)B * T * S * S;
   int64_t blocks = (total + 255) / 256;
   if (blocks > 16384) blocks = 16384;
   hipLaunchKernelGGL(video_preprocess_kernel, dim3((int)blocks), dim3(256), 0, s, frames, desc, tidx, T, S, mean[0],
-                     mean[1], mean[2], 1.f / std_[0], 1.f / std_[1], 1.f / std_[2], out, B);
+                     mean[1], mean[2], 1.f / std_[0], 1.f / std_[1], 1.f / std_[2], out, B, s2d);
 }
 
 void synth_frames_launch(uint8_t* out, int64_t n, uint32_t seed, hipStream_t s) {

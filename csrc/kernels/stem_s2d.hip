@@ -1,0 +1,368 @@
+// Direct (halo-tiled) space-to-depth stem convolutions for SlowFast / Slow on gfx950.
+//
+// The stems are 7x7 stride-2 convs on 3-channel frames (slow: k(1,7,7), Cout 64; fast: k(5,7,7),
+// Cout 8).  As implicit GEMMs they are hopeless: Cout 8 leaves MFMA columns idle and each input pixel is
+// re-gathered ~60x through the cache hierarchy (the fast stem alone was 12 % of a training step).
+// Instead:
+//   * the preprocessing kernel writes stem inputs in space-to-depth layout: a 2x2 pixel block x RGB0 =
+//     16 bf16 channels, so the conv becomes k(kt,4,4) stride 1 with 32-byte positions (weights for
+//     the tap positions outside the 7x7 window are zero);
+//   * a workgroup owns an 8x16 output tile of one clip and walks its frames: input frames live in an
+//     LDS ring of kt+1 slots (each frame is read from HBM exactly once per tile, the next frame is
+//     prefetched into registers while the current one computes); one barrier per frame;
+//   * forward: all weight fragments sit in VGPRs (A operand), input fragments are one ds_read_b128
+//     each (B operand), BN partial sums are produced in the epilogue;
+//   * wgrad: dY tile of the frame is staged in LDS, both MFMA operands are read with the gfx950
+//     transpose read ds_read_b64_tr_b16 (positions are the reduction axis), each wave keeps a slice of
+//     the taps in accumulators across all frames, and adds it to the fp32 dW accumulator once.
+#include "common.h"
+
+namespace {
+
+constexpr int TH = 8, TW = 16;              // output tile (positions = 128 = 4 waves x 2 rows)
+constexpr int PH = TH + 3, PW = TW + 3;     // s2d patch (kernel 4)
+constexpr int POSB = 32;                    // bytes per s2d position (16 bf16)
+constexpr int FRAME_BYTES = PH * PW * POSB; // 6688
+
+struct StemParams {
+  const uint16_t* x;    // [N, T, Hs, Ws, 16] s2d input
+  const uint16_t* w;    // forward: [Cout_pad][taps*16] packed s2d weights
+  uint16_t* y;          // [N, To, Ho, Wo, Cout]
+  float* stats;         // [nblocks][2][Cout]
+  const uint16_t* dy;   // wgrad: [N, To, Ho, Wo, Cout]
+  float* dw;            // wgrad accumulator [Cout][taps*16] fp32
+  int N, T, Hs, Ws, Cout;
+  int To, Ho, Wo;
+  int pt;               // temporal padding (kt/2)
+  int tiles_h, tiles_w;
+};
+
+// load one input frame's patch (zero outside) into registers: 418 16-B chunks over 256 threads
+struct PatchRegs { uint4 v[2]; };
+
+__device__ __forceinline__ void load_patch(const StemParams& p, int n, int ti, int hs0, int ws0, PatchRegs& r) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int idx = tid + s * 256;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (idx < PH * PW * 2 && ti >= 0 && ti < p.T) {
+      const int pos = idx >> 1, half = idx & 1;
+      const int r_ = pos / PW, c_ = pos - r_ * PW;
+      const int hs = hs0 + r_ - 2, ws = ws0 + c_ - 2;
+      if ((unsigned)hs < (unsigned)p.Hs && (unsigned)ws < (unsigned)p.Ws)
+        v = *reinterpret_cast<const uint4*>(p.x + ((((int64_t)n * p.T + ti) * p.Hs + hs) * p.Ws + ws) * 16 + half * 8);
+    }
+    r.v[s] = v;
+  }
+}
+
+__device__ __forceinline__ void store_patch(char* slot, const PatchRegs& r) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int idx = tid + s * 256;
+    if (idx < PH * PW * 2) *reinterpret_cast<uint4*>(slot + idx * 16) = r.v[s];
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// forward
+// ------------------------------------------------------------------------------------------------
+template <int KT, int COT>
+__global__ __launch_bounds__(256) void stem_fwd_kernel(const StemParams p) {
+  constexpr int TAPS = KT * 16;
+  constexpr int KSTEPS = TAPS * 16 / 32;  // 2 taps per MFMA k-step
+  constexpr int SLOTS = KT + 1;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* red = reinterpret_cast<float*>(smem + SLOTS * FRAME_BYTES);  // [2][COT*16]
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  int b = blockIdx.x;
+  const int tw = b % p.tiles_w; b /= p.tiles_w;
+  const int th = b % p.tiles_h;
+  const int n = b / p.tiles_h;
+  const int ho0 = th * TH, wo0 = tw * TW;
+  for (int i = tid; i < 2 * COT * 16; i += 256) red[i] = 0.f;
+
+  // weight fragments (A operand: lane holds W[co = 16*c + li][k = 32*ks + 8*g .. +8])
+  bf16x8_t wa[COT][KSTEPS];
+#pragma unroll
+  for (int c = 0; c < COT; ++c)
+#pragma unroll
+    for (int ks = 0; ks < KSTEPS; ++ks)
+      wa[c][ks] = *reinterpret_cast<const bf16x8_t*>(p.w + (int64_t)(16 * c + li) * (TAPS * 16) + ks * 32 + 8 * g);
+
+  // prologue: frames -pt .. -pt+KT-1
+  PatchRegs pr;
+  for (int f = 0; f < KT; ++f) {
+    const int ti = f - p.pt;
+    load_patch(p, n, ti, ho0, wo0, pr);
+    store_patch(smem + ((ti + p.pt) % SLOTS) * FRAME_BYTES, pr);
+  }
+  __syncthreads();
+
+  float cs[COT][4], cq[COT][4];
+#pragma unroll
+  for (int c = 0; c < COT; ++c)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { cs[c][r] = 0.f; cq[c][r] = 0.f; }
+
+  const int ww = li;                 // position column inside the tile
+  const int half = g & 1;            // channel half of the lane's 8 k-values
+  for (int to = 0; to < p.To; ++to) {
+    const int tnext = to - p.pt + KT;  // frame needed first by the next output frame
+    const bool pf = to + 1 < p.To;
+    if (pf) load_patch(p, n, tnext, ho0, wo0, pr);
+    f32x4_t acc[2][COT];
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int c = 0; c < COT; ++c) acc[q][c] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KSTEPS; ++ks) {
+      const int tap = 2 * ks + (g >> 1);
+      const int dt = tap >> 4, bh = (tap >> 2) & 3, bw = tap & 3;
+      const char* slot = smem + ((to + dt) % SLOTS) * FRAME_BYTES;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int hh = 2 * w + q;
+        const bf16x8_t xb = *reinterpret_cast<const bf16x8_t*>(
+            slot + ((hh + bh) * PW + (ww + bw)) * POSB + half * 16);
+#pragma unroll
+        for (int c = 0; c < COT; ++c)
+          acc[q][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[c][ks], xb, acc[q][c], 0, 0, 0);
+      }
+    }
+    // epilogue: D[co][pos]: lane holds co = 16c + 4g + r for position (row 2w+q, col li)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int ho = ho0 + 2 * w + q, wo = wo0 + li;
+      const bool valid = ho < p.Ho && wo < p.Wo;
+      const int64_t pos = (((int64_t)n * p.To + to) * p.Ho + ho) * p.Wo + wo;
+#pragma unroll
+      for (int c = 0; c < COT; ++c) {
+        const int co = 16 * c + 4 * g;
+        if (valid && co < p.Cout) {
+          float v[4] = {acc[q][c][0], acc[q][c][1], acc[q][c][2], acc[q][c][3]};
+          const uint2 pk = pack4(v);
+          *reinterpret_cast<uint2*>(p.y + pos * p.Cout + co) = pk;
+          float f[4];
+          unpack4(pk, f);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) { cs[c][r] += f[r]; cq[c][r] += f[r] * f[r]; }
+        }
+      }
+    }
+    if (pf) {
+      __syncthreads();  // everyone is done reading the slot about to be overwritten
+      store_patch(smem + ((tnext + p.pt) % SLOTS) * FRAME_BYTES, pr);
+      __syncthreads();
+    }
+  }
+  // BN partial sums of this workgroup
+#pragma unroll
+  for (int c = 0; c < COT; ++c)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float s = sum16(cs[c][r]), q = sum16(cq[c][r]);
+      if (li == 0) {
+        atomicAdd(&red[16 * c + 4 * g + r], s);
+        atomicAdd(&red[COT * 16 + 16 * c + 4 * g + r], q);
+      }
+    }
+  __syncthreads();
+  for (int i = tid; i < p.Cout; i += 256) {
+    p.stats[(int64_t)blockIdx.x * 2 * p.Cout + i] = red[i];
+    p.stats[(int64_t)blockIdx.x * 2 * p.Cout + p.Cout + i] = red[COT * 16 + i];
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// weight gradient
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ s16x4_t trr(const char* a) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(a));
+}
+
+template <int KT, int COT>
+__global__ __launch_bounds__(256) void stem_wgrad_kernel(const StemParams p) {
+  constexpr int TAPS = KT * 16;
+  constexpr int TPW = TAPS / 4;              // taps per wave
+  constexpr int SLOTS = KT + 1;
+  constexpr int DYB = TH * TW * COT * 16 * 2;  // dY tile bytes [128 pos][COT*16 co]
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* dyt = smem + SLOTS * FRAME_BYTES;
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  int b = blockIdx.x;
+  const int tw = b % p.tiles_w; b /= p.tiles_w;
+  const int th = b % p.tiles_h;
+  const int n = b / p.tiles_h;
+  const int ho0 = th * TH, wo0 = tw * TW;
+  const int COP = COT * 16;
+
+  f32x4_t acc[COT][TPW];
+#pragma unroll
+  for (int c = 0; c < COT; ++c)
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) acc[c][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  PatchRegs pr;
+  for (int f = 0; f < KT; ++f) {
+    const int ti = f - p.pt;
+    load_patch(p, n, ti, ho0, wo0, pr);
+    store_patch(smem + ((ti + p.pt) % SLOTS) * FRAME_BYTES, pr);
+  }
+  // tr-read lane roles: group g covers positions 8g..8g+7 of a 32-position k-step (rows of 16 w);
+  // lane supplies row (li >> 2) of a 4-row block and 4 columns at 8*(li & 3) bytes.
+  const int rq = li >> 2, cb = (li & 3) * 8;
+  for (int to = 0; to < p.To; ++to) {
+    // stage the dY tile of this frame: [pos = hh*16 + ww][COP] (zero for co >= Cout / invalid pos)
+    for (int idx = tid; idx < TH * TW * COP / 8; idx += 256) {
+      const int pos = idx / (COP / 8), ch = (idx % (COP / 8)) * 8;
+      const int ho = ho0 + pos / TW, wo = wo0 + pos % TW;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (ho < p.Ho && wo < p.Wo && ch < p.Cout)
+        v = *reinterpret_cast<const uint4*>(p.dy + ((((int64_t)n * p.To + to) * p.Ho + ho) * p.Wo + wo) * p.Cout + ch);
+      *reinterpret_cast<uint4*>(dyt + pos * COP * 2 + ch * 2) = v;
+    }
+    const int tnext = to - p.pt + KT;
+    const bool pf = to + 1 < p.To;
+    if (pf) load_patch(p, n, tnext, ho0, wo0, pr);
+    __syncthreads();
+#pragma unroll
+    for (int kstep = 0; kstep < TH * TW / 32; ++kstep) {
+      // positions of this k-step: rows 2*kstep, 2*kstep+1; group g -> row 2*kstep + (g >> 1), w 8*(g&1)..+7
+      const int hh = 2 * kstep + (g >> 1);
+      const int wq = 8 * (g & 1) + rq;          // position column of the lane's tr-read row (first block)
+      bf16x8_t a[COT];
+#pragma unroll
+      for (int c = 0; c < COT; ++c) {
+        const char* base = dyt + (hh * TW + wq) * COP * 2 + c * 32 + cb;
+        s16x4_t lo = trr(base), hi = trr(base + 4 * COP * 2);
+        s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        a[c] = __builtin_bit_cast(bf16x8_t, v);
+      }
+#pragma unroll
+      for (int t = 0; t < TPW; ++t) {
+        const int tap = w * TPW + t;
+        const int dt = tap >> 4, bh = (tap >> 2) & 3, bw = tap & 3;
+        const char* slot = smem + ((to + dt) % SLOTS) * FRAME_BYTES;
+        const char* base = slot + ((hh + bh) * PW + (wq + bw)) * POSB + cb;
+        s16x4_t lo = trr(base), hi = trr(base + 4 * POSB);
+        s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        const bf16x8_t xb = __builtin_bit_cast(bf16x8_t, v);
+#pragma unroll
+        for (int c = 0; c < COT; ++c)
+          acc[c][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[c], xb, acc[c][t], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+    if (pf) {
+      store_patch(smem + ((tnext + p.pt) % SLOTS) * FRAME_BYTES, pr);
+    }
+  }
+  // D[co][k]: lane holds channel k = li of tap, co = 16c + 4g + r
+#pragma unroll
+  for (int c = 0; c < COT; ++c)
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+      const int tap = w * TPW + t;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = 16 * c + 4 * g + r;
+        if (co < p.Cout) atomicAdd(p.dw + (int64_t)co * TAPS * 16 + tap * 16 + li, acc[c][t][r]);
+      }
+    }
+}
+
+// dW (s2d accumulator [Cout][kt][4][4][sy][sx][c4]) -> grad [Cout][3][kt][7][7] ; re-zeroes the accumulator
+__global__ void stem_wgrad_convert_kernel(float* __restrict__ acc, float* __restrict__ grad, int Cout, int kt,
+                                          float beta) {
+  const int total = Cout * 3 * kt * 49;
+  for (int o = blockIdx.x * blockDim.x + threadIdx.x; o < total; o += gridDim.x * blockDim.x) {
+    int r = o;
+    const int kw = r % 7; r /= 7;
+    const int kh = r % 7; r /= 7;
+    const int dt = r % kt; r /= kt;
+    const int c = r % 3;
+    const int co = r / 3;
+    const int bh = (kh + 1) >> 1, sy = (kh + 1) & 1, bw = (kw + 1) >> 1, sx = (kw + 1) & 1;
+    const int a = co * kt * 256 + ((dt * 4 + bh) * 4 + bw) * 16 + (sy * 2 + sx) * 4 + c;
+    grad[o] = (beta == 0.f ? 0.f : beta * grad[o]) + acc[a];
+  }
+}
+
+__global__ void zero_kernel(float* p, int n) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) p[i] = 0.f;
+}
+
+// fp32 [Cout][3][kt][7][7] -> bf16 s2d packed [Cout_pad16][kt*16 taps][16]
+__global__ void stem_pack_kernel(const float* __restrict__ w, uint16_t* __restrict__ out, int Cout, int Cpad, int kt) {
+  const int K = kt * 256;
+  const int total = Cpad * K;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int co = i / K;
+    int k = i % K;
+    const int ch = k % 16, tap = k / 16;
+    const int c = ch % 4, sx = (ch / 4) & 1, sy = ch / 8;
+    const int bw = tap % 4, bh = (tap / 4) % 4, dt = tap / 16;
+    const int kh = 2 * bh + sy - 1, kw = 2 * bw + sx - 1;
+    float v = 0.f;
+    if (co < Cout && c < 3 && kh >= 0 && kh < 7 && kw >= 0 && kw < 7)
+      v = w[(((co * 3 + c) * kt + dt) * 7 + kh) * 7 + kw];
+    out[i] = f2bf(v);
+  }
+}
+
+template <int KT, int COT>
+void launch_fwd(const StemParams& p, hipStream_t s) {
+  const size_t lds = (KT + 1) * FRAME_BYTES + 2 * COT * 16 * 4;
+  hipLaunchKernelGGL((stem_fwd_kernel<KT, COT>), dim3(p.N * p.tiles_h * p.tiles_w), dim3(256), lds, s, p);
+}
+
+template <int KT, int COT>
+void launch_wgrad(const StemParams& p, hipStream_t s) {
+  const size_t lds = (KT + 1) * FRAME_BYTES + TH * TW * COT * 16 * 2;
+  hipLaunchKernelGGL((stem_wgrad_kernel<KT, COT>), dim3(p.N * p.tiles_h * p.tiles_w), dim3(256), lds, s, p);
+}
+
+}  // namespace
+
+int stem_tiles(int Ho, int Wo, int N) { return N * ((Ho + TH - 1) / TH) * ((Wo + TW - 1) / TW); }
+
+// mode 0: forward, 1: wgrad
+void stem_s2d_launch(int mode, const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, const uint16_t* dy,
+                     float* dw, int N, int T, int Hs, int Ws, int Cout, int kt, hipStream_t s) {
+  StemParams p{};
+  p.x = x; p.w = w; p.y = y; p.stats = stats; p.dy = dy; p.dw = dw;
+  p.N = N; p.T = T; p.Hs = Hs; p.Ws = Ws; p.Cout = Cout;
+  p.To = T; p.Ho = Hs; p.Wo = Ws; p.pt = kt / 2;
+  p.tiles_h = (Hs + TH - 1) / TH; p.tiles_w = (Ws + TW - 1) / TW;
+  if (mode == 0) {
+    if (kt == 5 && Cout <= 16) launch_fwd<5, 1>(p, s);
+    else if (kt == 1 && Cout <= 64) launch_fwd<1, 4>(p, s);
+    else if (kt == 1 && Cout <= 16) launch_fwd<1, 1>(p, s);
+  } else {
+    if (kt == 5 && Cout <= 16) launch_wgrad<5, 1>(p, s);
+    else if (kt == 1 && Cout <= 64) launch_wgrad<1, 4>(p, s);
+  }
+}
+
+bool stem_s2d_supported(int Cout, int kt) { return (kt == 5 && Cout <= 16) || (kt == 1 && Cout <= 64); }
+
+void stem_wgrad_convert_launch(float* acc, float* grad, int Cout, int kt, float beta, hipStream_t s) {
+  const int total = Cout * 3 * kt * 49;
+  hipLaunchKernelGGL(stem_wgrad_convert_kernel, dim3((total + 255) / 256), dim3(256), 0, s, acc, grad, Cout, kt, beta);
+  const int n = Cout * kt * 256;
+  hipLaunchKernelGGL(zero_kernel, dim3((n + 255) / 256), dim3(256), 0, s, acc, n);
+}
+
+void stem_pack_launch(const float* w, uint16_t* out, int Cout, int kt, hipStream_t s) {
+  const int Cpad = (Cout + 15) / 16 * 16;
+  const int total = Cpad * kt * 256;
+  hipLaunchKernelGGL(stem_pack_kernel, dim3((total + 255) / 256), dim3(256), 0, s, w, out, Cout, Cpad, kt);
+}

@@ -57,7 +57,13 @@ void pack_weights_launch(const float* master, uint16_t* fwd, uint16_t* dgr, cons
                          hipStream_t s);
 int pack_desc_size();
 void video_preprocess_launch(const uint8_t* frames, const int* desc, const int* tidx, int B, int T, int S,
-                             const float* mean, const float* std_, uint16_t* out, hipStream_t s);
+                             const float* mean, const float* std_, uint16_t* out, int s2d, hipStream_t s);
+int stem_tiles(int Ho, int Wo, int N);
+void stem_s2d_launch(int mode, const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, const uint16_t* dy,
+                     float* dw, int N, int T, int Hs, int Ws, int Cout, int kt, hipStream_t s);
+bool stem_s2d_supported(int Cout, int kt);
+void stem_wgrad_convert_launch(float* acc, float* grad, int Cout, int kt, float beta, hipStream_t s);
+void stem_pack_launch(const float* w, uint16_t* out, int Cout, int kt, hipStream_t s);
 void synth_frames_launch(uint8_t* out, int64_t n, uint32_t seed, hipStream_t s);
 
 void register_clip_reader(pybind11::module& m);
@@ -241,7 +247,8 @@ void pack_weights(const at::Tensor& master, const at::Tensor& fwd, const at::Ten
 
 // frames: packed uint8 ; desc [B,10] int32 ; tidx [B,T] int32 ; out [B*T*S*S, 4] bf16
 void video_preprocess(const at::Tensor& frames, const at::Tensor& desc, const at::Tensor& tidx, int64_t T, int64_t S,
-                      std::vector<double> mean, std::vector<double> std_, const at::Tensor& out) {
+                      std::vector<double> mean, std::vector<double> std_, const at::Tensor& out, bool s2d) {
+  TORCH_CHECK(!s2d || S % 2 == 0, "space-to-depth output needs an even crop");
   TORCH_CHECK(frames.scalar_type() == at::kByte, "frames must be uint8");
   TORCH_CHECK(desc.dim() == 2 && desc.size(1) == 10 && desc.scalar_type() == at::kInt, "desc [B,10] int32");
   TORCH_CHECK(tidx.dim() == 2 && tidx.size(1) == T && tidx.scalar_type() == at::kInt, "tidx [B,T] int32");
@@ -249,7 +256,27 @@ void video_preprocess(const at::Tensor& frames, const at::Tensor& desc, const at
   const float m[3] = {(float)mean[0], (float)mean[1], (float)mean[2]};
   const float s[3] = {(float)std_[0], (float)std_[1], (float)std_[2]};
   video_preprocess_launch(frames.data_ptr<uint8_t>(), desc.data_ptr<int>(), tidx.data_ptr<int>(), (int)desc.size(0),
-                          (int)T, (int)S, m, s, bfpm(out), cur_stream());
+                          (int)T, (int)S, m, s, bfpm(out), s2d ? 1 : 0, cur_stream());
+}
+
+// space-to-depth stems: x [N*T*Hs*Ws, 16] bf16 ; wpack [Cout_pad16, kt*256] bf16
+void stem_fwd(const at::Tensor& x, const at::Tensor& wpack, const at::Tensor& y, const at::Tensor& stats,
+              std::vector<int64_t> dims, int64_t Cout, int64_t kt) {
+  TORCH_CHECK(stem_s2d_supported((int)Cout, (int)kt), "unsupported stem");
+  TORCH_CHECK(x.size(1) == 16 && x.is_contiguous(), "stem input must be dense s2d [M,16]");
+  const int N = dims[0], T = dims[1], Hs = dims[2], Ws = dims[3];
+  TORCH_CHECK(stats.numel() >= (int64_t)stem_tiles(Hs, Ws, N) * 2 * Cout, "stats too small");
+  stem_s2d_launch(0, bfp(x), bfp(wpack), bfpm(y), f32(stats), nullptr, nullptr, N, T, Hs, Ws, (int)Cout, (int)kt,
+                  cur_stream());
+}
+
+void stem_wgrad(const at::Tensor& x, const at::Tensor& dy, const at::Tensor& acc, std::vector<int64_t> dims,
+                int64_t Cout, int64_t kt) {
+  TORCH_CHECK(stem_s2d_supported((int)Cout, (int)kt), "unsupported stem");
+  TORCH_CHECK(acc.numel() >= Cout * kt * 256, "accumulator too small");
+  const int N = dims[0], T = dims[1], Hs = dims[2], Ws = dims[3];
+  stem_s2d_launch(1, bfp(x), nullptr, nullptr, nullptr, bfp(dy), f32(acc), N, T, Hs, Ws, (int)Cout, (int)kt,
+                  cur_stream());
 }
 
 void synth_frames(const at::Tensor& out, int64_t seed) {
@@ -283,5 +310,15 @@ PYBIND11_MODULE(_C, m) {
   m.def("pack_desc_size", &pack_desc_size);
   m.def("video_preprocess", &video_preprocess);
   m.def("synth_frames", &synth_frames);
+  m.def("stem_tiles", [](int64_t Ho, int64_t Wo, int64_t N) { return stem_tiles((int)Ho, (int)Wo, (int)N); });
+  m.def("stem_supported", [](int64_t Cout, int64_t kt) { return stem_s2d_supported((int)Cout, (int)kt); });
+  m.def("stem_fwd", &stem_fwd);
+  m.def("stem_wgrad", &stem_wgrad);
+  m.def("stem_wgrad_convert", [](const at::Tensor& acc, const at::Tensor& grad, int64_t Cout, int64_t kt, double beta) {
+    stem_wgrad_convert_launch(f32(acc), f32(grad), (int)Cout, (int)kt, (float)beta, cur_stream());
+  });
+  m.def("stem_pack", [](const at::Tensor& w, const at::Tensor& out, int64_t Cout, int64_t kt) {
+    stem_pack_launch(f32(w), bfpm(out), (int)Cout, (int)kt, cur_stream());
+  });
   register_clip_reader(m);
 }

@@ -99,9 +99,11 @@ def reference_transform(frames_u8: torch.Tensor, p: ClipParams, crop: int, mean=
 class GpuClipBatch:
     """Runs the fused preprocess kernel for a batch of decoded clips (same source shape)."""
 
-    def __init__(self, device, num_frames: int, crop: int, alpha: Optional[int], mean=MEAN, std=STD):
+    def __init__(self, device, num_frames: int, crop: int, alpha: Optional[int], mean=MEAN, std=STD,
+                 s2d: bool = False):
         from ..ops._ext import require
         self.C = require()
+        self.s2d = s2d  # space-to-depth output for the direct stem kernels (C = 16 at S/2 x S/2)
         self.device = torch.device(device)
         self.T, self.S, self.alpha = num_frames, crop, alpha
         self.mean, self.std = list(mean), list(std)
@@ -115,8 +117,13 @@ class GpuClipBatch:
             self._out[key] = t
         return t
 
-    def _run(self, frames: torch.Tensor, desc: torch.Tensor, tidx: torch.Tensor):
+    def _act(self, buf, B, T):
         from ..ops.conv import Act
+        if self.s2d:
+            return Act(buf.view(-1, 16), B, T, self.S // 2, self.S // 2)
+        return Act(buf, B, T, self.S, self.S)
+
+    def _run(self, frames: torch.Tensor, desc: torch.Tensor, tidx: torch.Tensor):
         B = desc.shape[0]
         outs = []
         if self.alpha:
@@ -124,11 +131,11 @@ class GpuClipBatch:
             stidx = tidx.index_select(1, sel).contiguous()
             Ts = stidx.shape[1]
             slow = self._buf("slow", (B * Ts * self.S * self.S, 4))
-            self.C.video_preprocess(frames, desc, stidx, Ts, self.S, self.mean, self.std, slow)
-            outs.append(Act(slow, B, Ts, self.S, self.S))
+            self.C.video_preprocess(frames, desc, stidx, Ts, self.S, self.mean, self.std, slow, self.s2d)
+            outs.append(self._act(slow, B, Ts))
         fast = self._buf("fast", (B * self.T * self.S * self.S, 4))
-        self.C.video_preprocess(frames, desc, tidx, self.T, self.S, self.mean, self.std, fast)
-        outs.append(Act(fast, B, self.T, self.S, self.S))
+        self.C.video_preprocess(frames, desc, tidx, self.T, self.S, self.mean, self.std, fast, self.s2d)
+        outs.append(self._act(fast, B, self.T))
         return outs
 
     def __call__(self, frames: torch.Tensor, params: Sequence[ClipParams]):

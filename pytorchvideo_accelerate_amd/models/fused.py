@@ -215,22 +215,67 @@ class _ConvBN:
         return a, b
 
 
+def to_s2d(x_ncthw: torch.Tensor) -> Act:
+    """NCTHW float clip -> space-to-depth stem input: 2x2 pixel blocks x RGB0 = 16 bf16 channels."""
+    N, C, T, H, W = x_ncthw.shape
+    x = F.pad(x_ncthw, (0, 0, 0, 0, 0, 0, 0, 4 - C))                  # RGB0
+    x = x.reshape(N, 4, T, H // 2, 2, W // 2, 2).permute(0, 2, 3, 5, 4, 6, 1)  # N,T,Hs,Ws,sy,sx,c
+    x = x.reshape(N * T * (H // 2) * (W // 2), 16).contiguous().to(torch.bfloat16)
+    return Act(x, N, T, H // 2, W // 2)
+
+
 class _Stem:
+    """conv(kt,7,7)/s(1,2,2) + BN + ReLU + MaxPool(1,3,3)/s2.
+
+    With ``eng.stem_s2d`` the conv runs as the direct space-to-depth kernel (csrc/kernels/stem_s2d.hip)
+    on an s2d input Act (C = 16, H/2 x W/2); otherwise as a generic implicit GEMM on RGB0 input."""
+
     def __init__(self, eng, stem: R.ResNetBasicStem, name: str):
         self.u = _ConvBN(eng, stem.conv, stem.norm, name + ".conv", cin_pad=4)
         self.eng, self.name = eng, name
         self.units = [self.u]
+        k = tuple(stem.conv.kernel_size)
+        self.kt = k[0]
+        self.s2d = (eng.stem_s2d and k[1:] == (7, 7) and tuple(stem.conv.stride) == (1, 2, 2)
+                    and tuple(stem.conv.padding) == (self.kt // 2, 3, 3) and stem.conv.in_channels == 3
+                    and eng.C.stem_supported(self.u.C, self.kt))
+        if self.s2d:
+            cpad = (self.u.C + 15) // 16 * 16
+            self.wpack = torch.zeros(cpad * self.kt * 256, device=eng.device, dtype=torch.bfloat16)
 
     def out_channels(self):
         return self.u.C
 
     def out_dims(self, T, H, W):
+        if self.s2d:  # input dims are the s2d grid = conv output grid
+            return T, (H - 1) // 2 + 1, (W - 1) // 2 + 1
         To, Ho, Wo = self.u.spec.out_dims(T, H, W)
         return To, (Ho - 1) // 2 + 1, (Wo - 1) // 2 + 1
 
+    def pack(self):
+        if self.s2d:
+            self.eng.C.stem_pack(self.eng.flat.view(self.u.conv.weight), self.wpack, self.u.C, self.kt)
+
+    def _conv_s2d(self, x: Act, train: bool, tag: str) -> Act:
+        eng, C, u = self.eng, self.eng.C, self.u
+        assert x.C == 16 and x.t.is_contiguous(), "s2d stem expects a dense [M, 16] space-to-depth input"
+        M = x.M
+        y = eng.ws((u.name, "y", tag), (M, u.C), torch.bfloat16)
+        tiles = C.stem_tiles(x.H, x.W, x.N)
+        stats = eng.ws((u.name, "stats"), (tiles, 2, u.C), torch.float32)
+        C.stem_fwd(x.t, self.wpack, y, stats, [x.N, x.T, x.H, x.W], u.C, self.kt)
+        bn = u.bn
+        if train:
+            C.bn_finalize(stats, tiles, u.C, M, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                          bn.num_batches_tracked, bn.momentum if bn.momentum is not None else 0.1, bn.eps,
+                          u.mean, u.rstd, u.scale, u.shift)
+        else:
+            C.bn_eval_affine(bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, u.scale, u.shift)
+        return Act(y, x.N, x.T, x.H, x.W)
+
     def fwd(self, x: Act, out: torch.Tensor, train: bool, tag: str) -> Act:
         C = self.eng.C
-        y = self.u.fwd(x, None, train, tag)
+        y = self._conv_s2d(x, train, tag) if self.s2d else self.u.fwd(x, None, train, tag)
         Ho, Wo = (y.H - 1) // 2 + 1, (y.W - 1) // 2 + 1
         arg = self.eng.ws((self.name, "arg"), (y.N * y.T * Ho * Wo, self.u.C), torch.uint8)
         C.stem_pool_fwd(y.t, self.u.scale, self.u.shift, out, out.stride(0), arg, y.N * y.T, y.H, y.W, Ho, Wo,
@@ -239,12 +284,18 @@ class _Stem:
         return Act(out, y.N, y.T, Ho, Wo)
 
     def bwd(self, dout: Act):
-        C = self.eng.C
+        eng, C = self.eng, self.eng.C
         y = self.y
-        dact = self.eng.ws((self.name, "dact"), (y.M, self.u.C), torch.bfloat16)
+        dact = eng.ws((self.name, "dact"), (y.M, self.u.C), torch.bfloat16)
         C.stem_pool_bwd(dout.t, dout.ld, self.arg, dact, y.N * y.T, y.H, y.W, dout.H, dout.W, self.u.C)
         dy, _ = self.u.bn_backward(Act(dact, y.N, y.T, y.H, y.W), y, 2, None, self.u.xf())
-        self.u.wgrad(dy, self.x, None)
+        if self.s2d:
+            x = self.x
+            acc = eng.scratch("stem_acc_" + self.name, self.u.C * self.kt * 256, zero=True)
+            C.stem_wgrad(x.t, dy.t, acc, [x.N, x.T, x.H, x.W], self.u.C, self.kt)
+            C.stem_wgrad_convert(acc, eng.flat.gview(self.u.conv.weight), self.u.C, self.kt, eng.grad_beta)
+        else:
+            self.u.wgrad(dy, self.x, None)
 
 
 class _ResBlock:
@@ -370,8 +421,9 @@ class _Fuse:
 class FusedNet:
     """Executor bound to a reference ``Net`` (SlowFast or Slow ResNet3D) whose parameters it shares."""
 
-    def __init__(self, model: R.Net, device: torch.device):
+    def __init__(self, model: R.Net, device: torch.device, stem_s2d: bool = True):
         self.C = require()
+        self.stem_s2d = stem_s2d
         self.model = model
         self.device = torch.device(device)
         model.to(self.device)
@@ -494,8 +546,17 @@ class FusedNet:
         self.pack_desc = torch.from_numpy(rec.view(np.uint8).copy()).to(self.device)
 
     def pack(self):
-        """Refresh bf16 packed weights from the fp32 master buffer (one launch)."""
+        """Refresh bf16 packed weights from the fp32 master buffer (one multi-tensor launch + s2d stems)."""
         self.C.pack_weights(self.flat.data, self.pack_fwd, self.pack_dgr, self.pack_desc, len(self.units))
+        for paths, _ in self.stages:
+            for m in paths:
+                if isinstance(m, _Stem):
+                    m.pack()
+
+    @property
+    def input_s2d(self) -> bool:
+        """Whether the stems consume space-to-depth inputs (set GpuClipBatch(s2d=...) accordingly)."""
+        return any(isinstance(m, _Stem) and m.s2d for paths, _ in self.stages for m in paths)
 
     # ------------------------------------------------------------------ forward
     def _forward_backbone(self, xs: List[Act], train: bool) -> List[Act]:
@@ -628,5 +689,7 @@ class FusedNet:
 
     # ------------------------------------------------------------------ misc
     def prepare_inputs(self, xs_ncthw: Sequence[torch.Tensor]) -> List[Act]:
-        """NCTHW float clips (already normalised) -> NDHWC bf16 RGB0 Acts."""
+        """NCTHW float clips (already normalised) -> stem input Acts (s2d or NDHWC RGB0)."""
+        if self.input_s2d:
+            return [to_s2d(x.to(self.device)) for x in xs_ncthw]
         return [Act.from_ncthw(x.to(self.device), c_pad=4) for x in xs_ncthw]

@@ -137,3 +137,40 @@ def test_pack_weights_kernel_matches_host_pack():
         assert torch.equal(u.wf.view_as(wf), wf), u.name
         if u.wd is not None:
             assert torch.equal(u.wd.view_as(wd), wd), u.name
+
+
+@pytest.mark.parametrize("kt,cout", [(5, 8), (1, 64)])
+def test_stem_s2d_fwd_wgrad(kt, cout):
+    from pytorchvideo_accelerate_amd.models.fused import to_s2d
+    from pytorchvideo_accelerate_amd.ops._ext import require
+    C = require()
+    g = torch.Generator(device="cpu").manual_seed(7)
+    N, T, H = 2, 6, 40
+    x = torch.randn(N, 3, T, H, H, generator=g).to(DEV).to(torch.bfloat16).float()
+    w = (torch.randn(cout, 3, kt, 7, 7, generator=g) * 0.05).to(DEV).to(torch.bfloat16).float()
+    ref = torch.nn.functional.conv3d(x, w, None, (1, 2, 2), (kt // 2, 3, 3))
+    xs = to_s2d(x)
+    cpad = (cout + 15) // 16 * 16
+    wp = torch.zeros(cpad * kt * 256, device=DEV, dtype=torch.bfloat16)
+    C.stem_pack(w.contiguous(), wp, cout, kt)
+    M = xs.M
+    y = torch.empty(M, cout, device=DEV, dtype=torch.bfloat16)
+    tiles = C.stem_tiles(xs.H, xs.W, N)
+    stats = torch.empty(tiles, 2, cout, device=DEV)
+    C.stem_fwd(xs.t, wp, y, stats, [N, T, xs.H, xs.W], cout, kt)
+    got = y.float().reshape(N, T, xs.H, xs.W, cout).permute(0, 4, 1, 2, 3)
+    assert rel_err(got, ref) < 1e-2
+    yf = y.float()
+    torch.testing.assert_close(stats.sum(0)[0], yf.sum(0), rtol=1e-3, atol=1e-2)
+    # wgrad
+    wr = w.clone().requires_grad_(True)
+    out = torch.nn.functional.conv3d(x, wr, None, (1, 2, 2), (kt // 2, 3, 3))
+    gy = torch.randn_like(out).to(torch.bfloat16).float()
+    out.backward(gy)
+    dy = gy.permute(0, 2, 3, 4, 1).reshape(M, cout).contiguous().to(torch.bfloat16)
+    acc = torch.zeros(cout * kt * 256, device=DEV)
+    grad = torch.zeros_like(w)
+    C.stem_wgrad(xs.t, dy, acc, [N, T, xs.H, xs.W], cout, kt)
+    C.stem_wgrad_convert(acc, grad, cout, kt, 0.0)
+    assert rel_err(grad, wr.grad) < 1e-2
+    assert acc.abs().max().item() == 0.0  # re-zeroed for the next use

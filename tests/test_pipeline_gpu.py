@@ -74,3 +74,16 @@ def test_run_py_fused_gpu(tmp_path):
 def test_graft_smoke():
     import __graft_entry__ as g
     g.smoke()
+
+
+def test_preprocess_s2d_layout_matches_dense():
+    g = torch.Generator().manual_seed(3)
+    B, Ts, H, W, T, S = 2, 12, 40, 50, 8, 32
+    frames = torch.randint(0, 256, (B, Ts, H, W, 3), generator=g, dtype=torch.uint8).to(DEV)
+    params = [sample_params(Ts, H, W, T, S, True, min_scale=34, max_scale=40, generator=g) for _ in range(B)]
+    dense = GpuClipBatch(DEV, T, S, None)(frames, params)[0]
+    s2d = GpuClipBatch(DEV, T, S, None, s2d=True)(frames, params)[0]
+    from pytorchvideo_accelerate_amd.models.fused import to_s2d
+    ref = to_s2d(dense.to_ncthw().float())
+    assert s2d.C == 16 and (s2d.H, s2d.W) == (S // 2, S // 2)
+    assert torch.equal(s2d.t, ref.t)
