@@ -65,35 +65,63 @@ void conv_igemm_kernel(const ConvParams p) {
   }
 
   // ---- per-slot row coordinates (fixed over the K loop) ----
+  // Everything loop-invariant is precomputed here so the k-loop issues ~1 VALU op per global load:
+  // a chunk's element offset = a_off[s] (row origin) + tap_lin (thread-uniform per k-step) + kc.
   const int col = tid % CPR;
   const int RHW = p.Rh * p.Rw, RTHW = p.Rt * RHW;
   const int GHW = p.Gh * p.Gw, GTHW = p.Gt * GHW;
-  int a_base[A_SLOTS], a_t[A_SLOTS], a_h[A_SLOTS], a_w[A_SLOTS];
+  const bool check = p.check != 0;   // host: false when every gathered coordinate is in range
+  int a_off[A_SLOTS], a_t[A_SLOTS], a_h[A_SLOTS], a_w[A_SLOTS], sa[A_SLOTS];
+  unsigned rowok = 0;
 #pragma unroll
   for (int s = 0; s < A_SLOTS; ++s) {
     const int idx = tid + s * NT;
-    const int m = m0 + idx / CPR;
+    const int row = idx / CPR;
+    const int m = m0 + row;
+    a_off[s] = 0; a_t[s] = 0; a_h[s] = 0; a_w[s] = 0;
     if (idx < A_CHUNKS && m < p.M) {
       const int b = m / RTHW;
       int r = m - b * RTHW;
       const int qt = r / RHW; r -= qt * RHW;
       const int qh = r / p.Rw; const int qw = r - qh * p.Rw;
-      a_base[s] = b * GTHW;
       a_t[s] = qt * p.ast + p.aot; a_h[s] = qh * p.ash + p.aoh; a_w[s] = qw * p.asw + p.aow;
-    } else {
-      a_base[s] = 0; a_t[s] = -(1 << 28); a_h[s] = 0; a_w[s] = 0;
+      a_off[s] = (b * GTHW + (a_t[s] * p.Gh + a_h[s]) * p.Gw + a_w[s]) * p.ldx;
+      rowok |= 1u << s;
     }
+    if constexpr (CH == 8) sa[s] = lds_off<BK>(row, col);
+    else sa[s] = lds_off<BK>(row, col >> 1) + (col & 1) * 8;
+  }
+  int b_off[B_SLOTS], sb[B_SLOTS];
+  unsigned nok = 0;
+#pragma unroll
+  for (int s = 0; s < B_SLOTS; ++s) {
+    const int idx = tid + s * NT;
+    const int row = idx / CPR;
+    const int n = n0 + row;
+    b_off[s] = n * p.Kfull;
+    if (idx < B_CHUNKS && n < p.Ngemm) nok |= 1u << s;
+    if constexpr (CH == 8) sb[s] = lds_off<BK>(row, col);
+    else sb[s] = lds_off<BK>(row, col >> 1) + (col & 1) * 8;
   }
 
-  // ---- k-state of this thread's column: (channel offset, tap) ----
+  // ---- k-state of this thread's column: (channel offset, tap), with derived gather/weight offsets ----
   int kc = col * CH, kdt = 0, kdh = 0, kdw = 0;
+  int tap_lin = 0, tap_w = 0;
+  auto retap = [&]() {
+    tap_lin = p.dir * ((kdt * p.Gh + kdh) * p.Gw + kdw) * p.ldx;
+    tap_w = (((p.bt0 + kdt * p.bts) * p.kh + (p.bh0 + kdh * p.bhs)) * p.kw + (p.bw0 + kdw * p.bws)) * p.Cg;
+  };
   auto kadvance = [&](int by) {
     kc += by;
-    while (kc >= p.Cg) {
-      kc -= p.Cg;
-      if (++kdw == p.nw) { kdw = 0; if (++kdh == p.nh) { kdh = 0; ++kdt; } }
+    if (kc >= p.Cg) {
+      do {
+        kc -= p.Cg;
+        if (++kdw == p.nw) { kdw = 0; if (++kdh == p.nh) { kdh = 0; ++kdt; } }
+      } while (kc >= p.Cg);
+      retap();
     }
   };
+  retap();
   kadvance(0);
 
   VT ra[A_SLOTS], rb[B_SLOTS];
@@ -102,29 +130,26 @@ void conv_igemm_kernel(const ConvParams p) {
 
   auto load = [&]() {
     const bool tap_ok = kdt < p.nt;
-    const int dgt = p.dir * kdt, dgh = p.dir * kdh, dgw = p.dir * kdw;
     ra_c = kc; ra_valid = 0;
+    const int dgt = p.dir * kdt, dgh = p.dir * kdh, dgw = p.dir * kdw;
 #pragma unroll
     for (int s = 0; s < A_SLOTS; ++s) {
-      const int gt = a_t[s] + dgt, gh = a_h[s] + dgh, gw = a_w[s] + dgw;
-      const bool v = tap_ok && (unsigned)gt < (unsigned)p.Gt && (unsigned)gh < (unsigned)p.Gh &&
-                     (unsigned)gw < (unsigned)p.Gw;
+      bool v = tap_ok && (rowok >> s & 1);
+      if (check)
+        v = v && (unsigned)(a_t[s] + dgt) < (unsigned)p.Gt && (unsigned)(a_h[s] + dgh) < (unsigned)p.Gh &&
+            (unsigned)(a_w[s] + dgw) < (unsigned)p.Gw;
       if (v) {
-        const int64_t off = (int64_t)(a_base[s] + (gt * p.Gh + gh) * p.Gw + gw) * p.ldx + kc;
-        ra[s] = *reinterpret_cast<const VT*>(p.x + off);
+        ra[s] = *reinterpret_cast<const VT*>(p.x + (a_off[s] + tap_lin + kc));
         ra_valid |= 1u << s;
       } else {
         ra[s] = VT{};
       }
     }
-    const int tapfull = ((p.bt0 + kdt * p.bts) * p.kh + (p.bh0 + kdh * p.bhs)) * p.kw + (p.bw0 + kdw * p.bws);
-    const int boff = tapfull * p.Cg + kc;
+    const int boff = tap_w + kc;
 #pragma unroll
     for (int s = 0; s < B_SLOTS; ++s) {
-      const int idx = tid + s * NT;
-      const int n = n0 + idx / CPR;
-      if (idx < B_CHUNKS && n < p.Ngemm && tap_ok)
-        rb[s] = *reinterpret_cast<const VT*>(p.w + (int64_t)n * p.Kfull + boff);
+      if (tap_ok && (nok >> s & 1))
+        rb[s] = *reinterpret_cast<const VT*>(p.w + (b_off[s] + boff));
       else
         rb[s] = VT{};
     }
@@ -136,8 +161,7 @@ void conv_igemm_kernel(const ConvParams p) {
     char* B = A + BM * BK * 2;
 #pragma unroll
     for (int s = 0; s < A_SLOTS; ++s) {
-      const int idx = tid + s * NT;
-      if (idx >= A_CHUNKS) break;
+      if (tid + s * NT >= A_CHUNKS) break;
       VT v = ra[s];
       if (affine && (ra_valid >> s & 1)) {
         float f[CH];
@@ -149,17 +173,12 @@ void conv_igemm_kernel(const ConvParams p) {
         }
         if constexpr (CH == 8) v = pack8(f); else v = pack4(f);
       }
-      const int row = idx / CPR;
-      if constexpr (CH == 8) *reinterpret_cast<VT*>(A + lds_off<BK>(row, col)) = v;
-      else *reinterpret_cast<VT*>(A + lds_off<BK>(row, col >> 1) + (col & 1) * 8) = v;
+      *reinterpret_cast<VT*>(A + sa[s]) = v;
     }
 #pragma unroll
     for (int s = 0; s < B_SLOTS; ++s) {
-      const int idx = tid + s * NT;
-      if (idx >= B_CHUNKS) break;
-      const int row = idx / CPR;
-      if constexpr (CH == 8) *reinterpret_cast<VT*>(B + lds_off<BK>(row, col)) = rb[s];
-      else *reinterpret_cast<VT*>(B + lds_off<BK>(row, col >> 1) + (col & 1) * 8) = rb[s];
+      if (tid + s * NT >= B_CHUNKS) break;
+      *reinterpret_cast<VT*>(B + sb[s]) = rb[s];
     }
   };
 
@@ -176,25 +195,26 @@ void conv_igemm_kernel(const ConvParams p) {
   __syncthreads();
 
   const int frow = lane & 15, fslot = lane >> 4;
+  int fa[BK / 32][TM], fb[BK / 32][TN];
+#pragma unroll
+  for (int kk = 0; kk < BK / 32; ++kk) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) fa[kk][i] = lds_off<BK>(wm * WM + i * 16 + frow, fslot + 4 * kk);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) fb[kk][j] = BM * BK * 2 + lds_off<BK>(wn * WN + j * 16 + frow, fslot + 4 * kk);
+  }
   for (int step = 0; step < nsteps; ++step) {
     const int cur = step & 1;
     const bool has_next = step + 1 < nsteps;
     if (has_next) load();
     const char* A = smem + cur * TILE_BYTES;
-    const char* B = A + BM * BK * 2;
 #pragma unroll
     for (int kk = 0; kk < BK / 32; ++kk) {
       bf16x8_t af[TM], bfr[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int row = wm * WM + i * 16 + frow;
-        af[i] = *reinterpret_cast<const bf16x8_t*>(A + lds_off<BK>(row, fslot + 4 * kk));
-      }
+      for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8_t*>(A + fa[kk][i]);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int row = wn * WN + j * 16 + frow;
-        bfr[j] = *reinterpret_cast<const bf16x8_t*>(B + lds_off<BK>(row, fslot + 4 * kk));
-      }
+      for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const bf16x8_t*>(A + fb[kk][j]);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll

@@ -35,6 +35,7 @@ struct ConvParams {
   int nt, nh, nw;           // taps visited per dim
   int kh, kw;               // full kernel extents (weight tap index)
   int bt0, bh0, bw0, bts, bhs, bws;
+  int check;                // 1: gathered coordinates may leave the tensor (padding) -> bounds tests
 };
 
 // Weight gradient: dW[n = cout][k = (tap, cin)] = sum_p dY[p][cout] * im2col(X)[p][k]

@@ -22,10 +22,16 @@ constexpr int BP = 32;  // positions per reduction step (one MFMA k-step)
 
 template <int COLS>
 __device__ __forceinline__ int img_off(int row, int colbyte) {
-  // [BP][COLS] bf16 image; 32-byte segments swizzled by row bits 1 and 3.
+  // [BP][COLS] bf16 image of 32-byte segments.  A 32-lane half of a transpose read touches rows
+  // {r..r+3, r+8..r+11}; the XOR below gives those 8 rows distinct segments of the 256-byte bank row
+  // for every row length (64 B rows: 4 rows share a bank row; 128 B: 2; >= 256 B: 1).
   constexpr int NSEG = COLS * 2 / 32;
   const int seg = colbyte >> 5;
-  const int h = (((row >> 1) & 1) | (((row >> 3) & 1) << 1)) & (NSEG - 1);
+  int h;
+  if constexpr (NSEG >= 8) h = (row & 3) | (((row >> 3) & 1) << 2);
+  else if constexpr (NSEG == 4) h = ((row >> 1) & 1) | (((row >> 3) & 1) << 1);
+  else if constexpr (NSEG == 2) h = (row >> 3) & 1;
+  else h = 0;
   return row * COLS * 2 + (((seg ^ h) << 5) | (colbyte & 31));
 }
 
@@ -65,12 +71,20 @@ void conv_wgrad_kernel(const WgradParams p) {
     for (int i = tid; i < p.Cin; i += NT) { aff[i] = p.in_scale[i]; aff[p.Cin + i] = p.in_shift[i]; }
   }
 
-  // ---- A (dY) slots: fixed column, rows advance by BP ----
+  // ---- A (dY) slots: fixed column; element offsets advance by BP rows per step ----
   const int a_col = tid % A_CPR;
   const int a_n = n0 + a_col * 8;
   const bool a_col_ok = a_n < p.Cout;
+  int a_off[A_SLOTS], a_row[A_SLOTS], sa[A_SLOTS];
+#pragma unroll
+  for (int s = 0; s < A_SLOTS; ++s) {
+    const int idx = tid + s * NT;
+    a_row[s] = idx / A_CPR;
+    a_off[s] = (p_begin + a_row[s]) * p.ldd + a_n;
+    sa[s] = img_off<BMW>(a_row[s], a_col * 16);
+  }
 
-  // ---- B (im2col) slots: fixed (tap, cin) column, rows advance by BP ----
+  // ---- B (im2col) slots: fixed (tap, cin) column per block; positions advance by BP ----
   const int b_col = tid % B_CPR;
   const int kb = k0 + b_col * CH;
   const bool b_col_ok = kb < p.K;
@@ -83,24 +97,37 @@ void conv_wgrad_kernel(const WgradParams p) {
     b_dh = r / p.kw;
     b_dw = r - b_dh * p.kw;
   }
-  // Position decomposition of each B slot's row (advanced incrementally).
+  const int tapoff = ((b_dt * p.Hi + b_dh) * p.Wi + b_dw) * p.ldx + b_c;
+  const bool check = p.pt | p.ph | p.pw;   // taps can only leave the tensor through padding
+  // per-slot output position (pb, pt, ph, pw) and its input origin (bt, bh, bw) / linear offset bio
   const int OHW = p.Ho * p.Wo, OTHW = p.To * OHW;
-  const int IHW = p.Hi * p.Wi, ITHW = p.Ti * IHW;
-  int pb[B_SLOTS], pt_[B_SLOTS], ph_[B_SLOTS], pw_[B_SLOTS];
+  int pt_[B_SLOTS], ph_[B_SLOTS], pw_[B_SLOTS], bt[B_SLOTS], bh[B_SLOTS], bw[B_SLOTS], bio[B_SLOTS],
+      b_row[B_SLOTS], sb[B_SLOTS];
+  // offset deltas of the incremental walk
+  const int dW1 = BP * p.sw * p.ldx;
+  const int dWrap = (p.sh * p.Wi - p.Wo * p.sw) * p.ldx;
+  const int dHrap = (p.st * p.Hi * p.Wi - p.Ho * p.sh * p.Wi) * p.ldx;
+  const int dTrap = (p.Ti * p.Hi * p.Wi - p.To * p.st * p.Hi * p.Wi) * p.ldx;
 #pragma unroll
   for (int s = 0; s < B_SLOTS; ++s) {
-    const int row = (tid + s * NT) / B_CPR;
-    int q = p_begin + row;
+    b_row[s] = (tid + s * NT) / B_CPR;
+    int q = p_begin + b_row[s];
     const int b = q / OTHW; q -= b * OTHW;
     const int t = q / OHW; q -= t * OHW;
     const int h = q / p.Wo;
-    pb[s] = b; pt_[s] = t; ph_[s] = h; pw_[s] = q - h * p.Wo;
+    pt_[s] = t; ph_[s] = h; pw_[s] = q - h * p.Wo;
+    bt[s] = t * p.st - p.pt; bh[s] = h * p.sh - p.ph; bw[s] = pw_[s] * p.sw - p.pw;
+    bio[s] = ((b * p.Ti + bt[s]) * p.Hi + bh[s]) * p.Wi * p.ldx + bw[s] * p.ldx;
+    sb[s] = img_off<BNW>(b_row[s], b_col * CH * 2);
   }
   auto advance_pos = [&](int s) {
-    pw_[s] += BP;
+    pw_[s] += BP; bw[s] += BP * p.sw; bio[s] += dW1;
     while (pw_[s] >= p.Wo) {
-      pw_[s] -= p.Wo;
-      if (++ph_[s] == p.Ho) { ph_[s] = 0; if (++pt_[s] == p.To) { pt_[s] = 0; ++pb[s]; } }
+      pw_[s] -= p.Wo; bw[s] -= p.Wo * p.sw; bh[s] += p.sh; bio[s] += dWrap;
+      if (++ph_[s] == p.Ho) {
+        ph_[s] = 0; bh[s] -= p.Ho * p.sh; bt[s] += p.st; bio[s] += dHrap;
+        if (++pt_[s] == p.To) { pt_[s] = 0; bt[s] -= p.To * p.st; bio[s] += dTrap; }
+      }
     }
   };
 
@@ -112,31 +139,25 @@ void conv_wgrad_kernel(const WgradParams p) {
   auto load = [&]() {
 #pragma unroll
     for (int s = 0; s < A_SLOTS; ++s) {
-      const int idx = tid + s * NT;
-      const int q = pcur + idx / A_CPR;
-      if (idx < A_CHUNKS && a_col_ok && q < p_end)
-        ra[s] = *reinterpret_cast<const uint4*>(p.dy + (int64_t)q * p.ldd + a_n);
+      if (tid + s * NT < A_CHUNKS && a_col_ok && pcur + a_row[s] < p_end)
+        ra[s] = *reinterpret_cast<const uint4*>(p.dy + a_off[s]);
       else
         ra[s] = uint4{0, 0, 0, 0};
+      a_off[s] += BP * p.ldd;
     }
     rb_valid = 0;
 #pragma unroll
     for (int s = 0; s < B_SLOTS; ++s) {
-      const int idx = tid + s * NT;
-      const int q = pcur + idx / B_CPR;
-      bool v = idx < B_CHUNKS && b_col_ok && q < p_end;
+      bool v = tid + s * NT < B_CHUNKS && b_col_ok && pcur + b_row[s] < p_end;
+      if (check)
+        v = v && (unsigned)(bt[s] + b_dt) < (unsigned)p.Ti && (unsigned)(bh[s] + b_dh) < (unsigned)p.Hi &&
+            (unsigned)(bw[s] + b_dw) < (unsigned)p.Wi;
       if (v) {
-        const int ti = pt_[s] * p.st - p.pt + b_dt;
-        const int hi = ph_[s] * p.sh - p.ph + b_dh;
-        const int wi = pw_[s] * p.sw - p.pw + b_dw;
-        v = (unsigned)ti < (unsigned)p.Ti && (unsigned)hi < (unsigned)p.Hi && (unsigned)wi < (unsigned)p.Wi;
-        if (v) {
-          const int64_t off = (int64_t)(pb[s] * ITHW + (ti * p.Hi + hi) * p.Wi + wi) * p.ldx + b_c;
-          rb[s] = *reinterpret_cast<const VT*>(p.x + off);
-          rb_valid |= 1u << s;
-        }
+        rb[s] = *reinterpret_cast<const VT*>(p.x + (bio[s] + tapoff));
+        rb_valid |= 1u << s;
+      } else {
+        rb[s] = VT{};
       }
-      if (!v) rb[s] = VT{};
       advance_pos(s);
     }
     pcur += BP;
@@ -147,14 +168,12 @@ void conv_wgrad_kernel(const WgradParams p) {
     char* B = A + A_BYTES;
 #pragma unroll
     for (int s = 0; s < A_SLOTS; ++s) {
-      const int idx = tid + s * NT;
-      if (idx >= A_CHUNKS) break;
-      *reinterpret_cast<uint4*>(A + img_off<BMW>(idx / A_CPR, a_col * 16)) = ra[s];
+      if (tid + s * NT >= A_CHUNKS) break;
+      *reinterpret_cast<uint4*>(A + sa[s]) = ra[s];
     }
 #pragma unroll
     for (int s = 0; s < B_SLOTS; ++s) {
-      const int idx = tid + s * NT;
-      if (idx >= B_CHUNKS) break;
+      if (tid + s * NT >= B_CHUNKS) break;
       VT v = rb[s];
       if (affine && (rb_valid >> s & 1)) {
         float f[CH];
@@ -166,7 +185,7 @@ void conv_wgrad_kernel(const WgradParams p) {
         }
         if constexpr (CH == 8) v = pack8(f); else v = pack4(f);
       }
-      *reinterpret_cast<VT*>(B + img_off<BNW>(idx / B_CPR, b_col * CH * 2)) = v;
+      *reinterpret_cast<VT*>(B + sb[s]) = v;
     }
   };
 
@@ -185,30 +204,40 @@ void conv_wgrad_kernel(const WgradParams p) {
   __syncthreads();
 
   // tr-read addressing: group g = lane>>4 covers p rows 8g..8g+7; lane i = lane&15 supplies row
-  // (i>>2) of a 4-row block and columns 4*(i&3)..+3 of the 16-column block.
+  // (i>>2) of a 4-row block and columns 4*(i&3)..+3 of the 16-column block.  Offsets precomputed.
   const int g = lane >> 4, li = lane & 15;
   const int tr_row = 8 * g + (li >> 2);
-  const int tr_colb = (li & 3) * 8;  // byte offset inside the 16-column (32-B) block
+  const int tr_colb = (li & 3) * 8;
+  int ta[TM][2], tb[TN][2];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int cb = (wm * WMW + i * 16) * 2 + tr_colb;
+    ta[i][0] = img_off<BMW>(tr_row, cb);
+    ta[i][1] = img_off<BMW>(tr_row + 4, cb);
+  }
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int cb = (wn * WNW + j * 16) * 2 + tr_colb;
+    tb[j][0] = A_BYTES + img_off<BNW>(tr_row, cb);
+    tb[j][1] = A_BYTES + img_off<BNW>(tr_row + 4, cb);
+  }
   for (int step = 0; step < nsteps; ++step) {
     const int cur = step & 1;
     const bool has_next = step + 1 < nsteps;
     if (has_next) load();
     const char* A = smem + cur * TILE;
-    const char* B = A + A_BYTES;
     bf16x8_t af[TM], bfr[TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
-      const int cb = (wm * WMW + i * 16) * 2 + tr_colb;
-      s16x4_t lo = tr_read(A + img_off<BMW>(tr_row, cb));
-      s16x4_t hi = tr_read(A + img_off<BMW>(tr_row + 4, cb));
+      s16x4_t lo = tr_read(A + ta[i][0]);
+      s16x4_t hi = tr_read(A + ta[i][1]);
       s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       af[i] = __builtin_bit_cast(bf16x8_t, v);
     }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      const int cb = (wn * WNW + j * 16) * 2 + tr_colb;
-      s16x4_t lo = tr_read(B + img_off<BNW>(tr_row, cb));
-      s16x4_t hi = tr_read(B + img_off<BNW>(tr_row + 4, cb));
+      s16x4_t lo = tr_read(A + tb[j][0]);
+      s16x4_t hi = tr_read(A + tb[j][1]);
       s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       bfr[j] = __builtin_bit_cast(bf16x8_t, v);
     }

@@ -108,6 +108,18 @@ void conv_igemm(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, c
   p.affine = (int)affine; p.accum = (int)accum;
   int* f = &p.M;
   for (int i = 0; i < 39; ++i) f[i] = (int)g[i];
+  // bounds tests are only needed when some tap can read outside the gathered tensor
+  {
+    auto dim_ok = [](int R, int as, int ao, int dir, int n, int G) {
+      const int lo = ao + (dir < 0 ? -(n - 1) : 0);
+      const int hi = (R - 1) * as + ao + (dir > 0 ? (n - 1) : 0);
+      return n == 0 || (lo >= 0 && hi < G);
+    };
+    p.check = (dim_ok(p.Rt, p.ast, p.aot, p.dir, p.nt, p.Gt) && dim_ok(p.Rh, p.ash, p.aoh, p.dir, p.nh, p.Gh) &&
+               dim_ok(p.Rw, p.asw, p.aow, p.dir, p.nw, p.Gw)) ? 0 : 1;
+  }
+  TORCH_CHECK((int64_t)p.Gt * p.Gh * p.Gw * (x.numel() / std::max<int64_t>(1, (int64_t)p.Gt * p.Gh * p.Gw)) < (1ll << 31) &&
+              x.numel() < (1ll << 31) && y.numel() < (1ll << 31), "tensor too large for 32-bit offsets");
   TORCH_CHECK(p.Cg % chunk == 0 && p.Cg > 0, "gathered channels must be a multiple of the chunk");
   TORCH_CHECK(p.Ngemm % 4 == 0, "output channels must be a multiple of 4");
   TORCH_CHECK(p.ldx % chunk == 0 && p.ldy % 4 == 0, "row strides must keep vector alignment");

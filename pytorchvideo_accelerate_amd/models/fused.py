@@ -128,6 +128,7 @@ class _ConvBN:
     def fwd(self, x: Act, xf: Optional[_Xf], train: bool, tag: str) -> Act:
         C = self.eng.C
         s = self.spec
+        self.eng.mark(self.name + ".fwd")
         To, Ho, Wo = s.out_dims(x.T, x.H, x.W)
         M = x.N * To * Ho * Wo
         y = self.eng.ws((self.name, "y", tag), (M, s.cout), torch.bfloat16)
@@ -154,6 +155,7 @@ class _ConvBN:
     # ---- backward pieces ----
     def wgrad(self, dy: Act, x: Act, xf: Optional[_Xf]):
         eng, s, C = self.eng, self.spec, self.eng.C
+        eng.mark(self.name + ".wgrad")
         K = s.taps * s.cin_pad
         key = (self.name, "wsplit", dy.M)
         sp = eng._splits.get(key)
@@ -172,6 +174,7 @@ class _ConvBN:
 
     def dgrad(self, dy: Act, in_dims, out: torch.Tensor, accum: bool) -> Act:
         s, C = self.spec, self.eng.C
+        self.eng.mark(self.name + ".dgrad")
         Ti, Hi, Wi = in_dims
         key = ("dg", dy.N, tuple(in_dims), dy.ld, out.stride(0))
         geo = self._geo.get(key)
@@ -190,6 +193,7 @@ class _ConvBN:
         eng, C = self.eng, self.eng.C
         M, Cc = y.M, self.C
         blocks, rpb = eng._bn_blocks(M, Cc)
+        eng.mark(self.name + ".bnred")
         part = eng.scratch("bnpart", blocks * 3 * Cc)
         C.bn_bwd_reduce(g.t, g.ld, mask_mode, None if mo is None else mo.t, 0 if mo is None else mo.ld,
                         None if mxf is None else mxf.scale, None if mxf is None else mxf.shift,
@@ -204,6 +208,7 @@ class _ConvBN:
                               fg.gview(other.bn.weight), fg.gview(other.bn.bias), eng.grad_beta, other.coef)
         dy = eng.ws((self.name, "dy"), (M, Cc), torch.bfloat16)
         dy1 = eng.ws((other.name, "dy"), (M, Cc), torch.bfloat16) if other is not None else None
+        eng.mark(self.name + ".bnapply")
         C.bn_bwd_apply(g.t, g.ld, mask_mode, None if mo is None else mo.t, 0 if mo is None else mo.ld,
                        None if mxf is None else mxf.scale, None if mxf is None else mxf.shift,
                        y.t, self.coef, dy, None if other is None else other_y.t,
@@ -263,6 +268,7 @@ class _Stem:
         y = eng.ws((u.name, "y", tag), (M, u.C), torch.bfloat16)
         tiles = C.stem_tiles(x.H, x.W, x.N)
         stats = eng.ws((u.name, "stats"), (tiles, 2, u.C), torch.float32)
+        eng.mark(u.name + ".fwd")
         C.stem_fwd(x.t, self.wpack, y, stats, [x.N, x.T, x.H, x.W], u.C, self.kt)
         bn = u.bn
         if train:
@@ -278,6 +284,7 @@ class _Stem:
         y = self._conv_s2d(x, train, tag) if self.s2d else self.u.fwd(x, None, train, tag)
         Ho, Wo = (y.H - 1) // 2 + 1, (y.W - 1) // 2 + 1
         arg = self.eng.ws((self.name, "arg"), (y.N * y.T * Ho * Wo, self.u.C), torch.uint8)
+        self.eng.mark(self.name + ".pool")
         C.stem_pool_fwd(y.t, self.u.scale, self.u.shift, out, out.stride(0), arg, y.N * y.T, y.H, y.W, Ho, Wo,
                         self.u.C)
         self.x, self.y, self.arg = x, y, arg
@@ -287,11 +294,13 @@ class _Stem:
         eng, C = self.eng, self.eng.C
         y = self.y
         dact = eng.ws((self.name, "dact"), (y.M, self.u.C), torch.bfloat16)
+        eng.mark(self.name + ".poolbwd")
         C.stem_pool_bwd(dout.t, dout.ld, self.arg, dact, y.N * y.T, y.H, y.W, dout.H, dout.W, self.u.C)
         dy, _ = self.u.bn_backward(Act(dact, y.N, y.T, y.H, y.W), y, 2, None, self.u.xf())
         if self.s2d:
             x = self.x
             acc = eng.scratch("stem_acc_" + self.name, self.u.C * self.kt * 256, zero=True)
+            eng.mark(self.u.name + ".wgrad")
             C.stem_wgrad(x.t, dy.t, acc, [x.N, x.T, x.H, x.W], self.u.C, self.kt)
             C.stem_wgrad_convert(acc, eng.flat.gview(self.u.conv.weight), self.u.C, self.kt, eng.grad_beta)
         else:
@@ -321,6 +330,7 @@ class _ResBlock:
         yc = self.c.fwd(yb, self.b.xf(), train, tag)
         y1 = self.one.fwd(x, None, train, tag) if self.one is not None else None
         M = yc.M
+        self.eng.mark(self.name + ".res_out")
         C.res_out(yc.t, self.c.scale, self.c.shift,
                   None if y1 is None else y1.t, None if y1 is None else self.one.scale,
                   None if y1 is None else self.one.shift, None if y1 is not None else x.t, x.ld,
@@ -406,6 +416,7 @@ class _Fuse:
 
     def fwd(self, xf: Act, cat_slice: torch.Tensor, train: bool, tag: str):
         y = self.u.fwd(xf, None, train, tag)
+        self.eng.mark(self.name + ".bn_act")
         self.eng.C.bn_act(y.t, y.ld, cat_slice, cat_slice.stride(0), self.u.scale, self.u.shift, 1, y.M, self.u.C)
         self.xf_in, self.y = xf, y
 
@@ -427,6 +438,7 @@ class FusedNet:
         self.model = model
         self.device = torch.device(device)
         model.to(self.device)
+        self.prof: Optional[List] = None   # [(label, event)] when per-op profiling is enabled
         self._ws: Dict = {}
         self._splits: Dict = {}
         self._bnb: Dict = {}
@@ -488,6 +500,19 @@ class FusedNet:
                     sub.flat_hi = max(self.flat.span(w)[1] for u in sub.units
                                       for w in (u.conv.weight, u.bn.weight, u.bn.bias))
                     sub.eng_progress = self._progress
+
+    def mark(self, label: str):
+        """Per-op profiling: the interval up to the next mark is charged to ``label``."""
+        if self.prof is not None:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            self.prof.append((label, ev))
+
+    def profile_report(self) -> List[Tuple[str, float]]:
+        """(label, ms) for the marks recorded since ``prof`` was set to ``[]`` (synchronizes)."""
+        torch.cuda.synchronize()
+        p = self.prof or []
+        return [(a, e0.elapsed_time(e1)) for (a, e0), (_, e1) in zip(p, p[1:])]
 
     def _progress(self, hi: int):
         if self.grad_hook is not None:
@@ -601,6 +626,7 @@ class FusedNet:
         Ctot = sum(o.C for o in outs)
         N = outs[0].N
         feat = self.ws(("feat", tag), (N, P, Ctot), torch.float32)
+        self.mark("head.pool")
         coff = 0
         for o, k in zip(outs, ks):
             assert o.t.is_contiguous()
@@ -635,6 +661,7 @@ class FusedNet:
             outs = self._forward_backbone(xs, train=True)
             feat, ks = self._pool_features(outs, "t")
         h = self.head
+        self.mark("head.fwdbwd")
         feat_t = feat.detach().requires_grad_(True)
         with torch.enable_grad():
             logits = self._head(feat_t, train=True)
@@ -659,6 +686,7 @@ class FusedNet:
         # head pools -> grads of the last stage outputs
         douts = []
         coff = 0
+        self.mark("head.poolbwd")
         for p, (o, k) in enumerate(zip(outs, ks)):
             d = self.ws(("dlast", p), (o.M, o.C), torch.bfloat16)
             C.avgpool_bwd(gfeat, Ctot, coff, [o.N, o.T, o.H, o.W, o.C], list(k), d)
