@@ -104,7 +104,7 @@ __global__ void bn_act_kernel(const uint16_t* __restrict__ y, int ldy, uint16_t*
 __global__ void res_out_kernel(const uint16_t* __restrict__ yc, const float* __restrict__ sc, const float* __restrict__ hc,
                                const uint16_t* __restrict__ y1, const float* __restrict__ s1, const float* __restrict__ h1,
                                const uint16_t* __restrict__ x, int ldx, uint16_t* __restrict__ out, int ldo,
-                               int64_t M, int C) {
+                               uint8_t* __restrict__ mask, int64_t M, int C) {
   ROW_VEC_SETUP(C);
   float a0[8], a1[8], b0[8], b1[8];
 #pragma unroll
@@ -120,16 +120,28 @@ __global__ void res_out_kernel(const uint16_t* __restrict__ yc, const float* __r
     unpack8(*reinterpret_cast<const uint4*>(sp + m * lds + c), b);
 #pragma unroll
     for (int e = 0; e < 8; ++e) a[e] = fmaxf(a[e] * a0[e] + a1[e] + b[e] * b0[e] + b1[e], 0.f);
-    *reinterpret_cast<uint4*>(out + m * ldo + c) = pack8(a);
+    const uint4 pk = pack8(a);
+    *reinterpret_cast<uint4*>(out + m * ldo + c) = pk;
+    if (mask) {  // ReLU mask of the stored bf16 values: bit e of byte (m, c/8) = out[m][c+e] > 0
+      const uint32_t w[4] = {pk.x, pk.y, pk.z, pk.w};
+      uint32_t bits = 0;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        bits |= ((w[e] & 0x7fffu) != 0 && !(w[e] & 0x8000u)) ? 1u << (2 * e) : 0u;
+        bits |= ((w[e] & 0x7fff0000u) != 0 && !(w[e] & 0x80000000u)) ? 1u << (2 * e + 1) : 0u;
+      }
+      mask[m * (C >> 3) + (c >> 3)] = (uint8_t)bits;
+    }
   }
 }
 
 // ------------------------------------------------------------------------------------------
 // backward reductions
-//   mask_mode 0: dz = g ; 1: dz = g * (mo > 0) ; 2: dz = g * (y0*ms + mh > 0)
+//   mask_mode 0: dz = g ; 1: dz = g * (mo > 0) ; 2: dz = g * (y0*ms + mh > 0) ;
+//   3: dz = g * bit(mo)  (mo = uint8 ReLU mask bits [M][C/8] written by res_out)
 // ------------------------------------------------------------------------------------------
 __global__ void bn_bwd_reduce_kernel(const uint16_t* __restrict__ g, int ldg, int mask_mode,
-                                     const uint16_t* __restrict__ mo, int ldm,
+                                     const void* __restrict__ mo_, int ldm,
                                      const float* __restrict__ ms, const float* __restrict__ mh,
                                      const uint16_t* __restrict__ y0, const float* __restrict__ mean0,
                                      const float* __restrict__ rstd0,
@@ -137,6 +149,8 @@ __global__ void bn_bwd_reduce_kernel(const uint16_t* __restrict__ g, int ldg, in
                                      const float* __restrict__ rstd1,
                                      int64_t M, int C, int rows_per_block, float* __restrict__ part) {
   extern __shared__ __attribute__((aligned(16))) float red[];  // [3][C]
+  const uint16_t* mo = static_cast<const uint16_t*>(mo_);
+  const uint8_t* mb = static_cast<const uint8_t*>(mo_);
   for (int i = threadIdx.x; i < 3 * C; i += NT) red[i] = 0.f;
   __syncthreads();
   const int vecs = C >> 3;
@@ -164,6 +178,10 @@ __global__ void bn_bwd_reduce_kernel(const uint16_t* __restrict__ g, int ldg, in
         unpack8(*reinterpret_cast<const uint4*>(mo + m * ldm + c), o);
 #pragma unroll
         for (int e = 0; e < 8; ++e) dz[e] = o[e] > 0.f ? dz[e] : 0.f;
+      } else if (mask_mode == 3) {
+        const unsigned bits = mb[m * ldm + (c >> 3)];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dz[e] = (bits >> e) & 1u ? dz[e] : 0.f;
       } else if (mask_mode == 2) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) dz[e] = (a[e] * MS[e] + MH[e]) > 0.f ? dz[e] : 0.f;
@@ -177,6 +195,19 @@ __global__ void bn_bwd_reduce_kernel(const uint16_t* __restrict__ g, int ldg, in
         for (int e = 0; e < 8; ++e) s1[e] += dz[e] * (b[e] - m1[e]) * r1[e];
       }
     }
+  }
+  // threads lv, lv+vecs, ... share channel addresses: reduce across the wave before the LDS atomics
+  // (same-address ds_add_f32 lanes serialise; C = 8 would otherwise put all 64 lanes on one address)
+  const bool pow2 = vecs < 64 && (vecs & (vecs - 1)) == 0;
+  if (pow2) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      sdz[e] = wave_sum_stride(sdz[e], vecs);
+      s0[e] = wave_sum_stride(s0[e], vecs);
+      if (y1) s1[e] = wave_sum_stride(s1[e], vecs);
+    }
+  }
+  if (lr < rpi && (!pow2 || (threadIdx.x & 63) < vecs)) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       atomicAdd(&red[c + e], sdz[e]);
@@ -222,7 +253,7 @@ __global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int block
 
 // dy_k = A_k*dz + B_k*y_k + C_k  (k = 0, 1) ; optionally dz itself (identity shortcut gradient)
 __global__ void bn_bwd_apply_kernel(const uint16_t* __restrict__ g, int ldg, int mask_mode,
-                                    const uint16_t* __restrict__ mo, int ldm,
+                                    const void* __restrict__ mo_, int ldm,
                                     const float* __restrict__ ms, const float* __restrict__ mh,
                                     const uint16_t* __restrict__ y0, const float* __restrict__ coef0,
                                     uint16_t* __restrict__ dy0,
@@ -231,6 +262,8 @@ __global__ void bn_bwd_apply_kernel(const uint16_t* __restrict__ g, int ldg, int
                                     uint16_t* __restrict__ dzout, int lddz, int dz_accum,
                                     int64_t M, int C) {
   ROW_VEC_SETUP(C);
+  const uint16_t* mo = static_cast<const uint16_t*>(mo_);
+  const uint8_t* mb = static_cast<const uint8_t*>(mo_);
   float A0[8], B0[8], C0[8], A1[8], B1[8], C1[8], MS[8], MH[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
@@ -247,6 +280,10 @@ __global__ void bn_bwd_apply_kernel(const uint16_t* __restrict__ g, int ldg, int
       unpack8(*reinterpret_cast<const uint4*>(mo + m * ldm + c), o);
 #pragma unroll
       for (int e = 0; e < 8; ++e) dz[e] = o[e] > 0.f ? dz[e] : 0.f;
+    } else if (mask_mode == 3) {
+      const unsigned bits = mb[m * ldm + (c >> 3)];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dz[e] = (bits >> e) & 1u ? dz[e] : 0.f;
     } else if (mask_mode == 2) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) dz[e] = (a[e] * MS[e] + MH[e]) > 0.f ? dz[e] : 0.f;
@@ -452,10 +489,10 @@ void bn_act_launch(const uint16_t* y, int ldy, uint16_t* out, int ldo, const flo
 }
 
 void res_out_launch(const uint16_t* yc, const float* sc, const float* hc, const uint16_t* y1, const float* s1,
-                    const float* h1, const uint16_t* x, int ldx, uint16_t* out, int ldo, int64_t M, int C,
-                    hipStream_t s) {
+                    const float* h1, const uint16_t* x, int ldx, uint16_t* out, int ldo, uint8_t* mask, int64_t M,
+                    int C, hipStream_t s) {
   hipLaunchKernelGGL(res_out_kernel, dim3(grid_rows(M, C)), dim3(NT), 0, s, yc, sc, hc, y1, s1, h1, x, ldx, out,
-                     ldo, M, C);
+                     ldo, mask, M, C);
 }
 
 int bn_bwd_reduce_blocks(int64_t M, int C, int* rows_per_block) {
@@ -469,7 +506,7 @@ int bn_bwd_reduce_blocks(int64_t M, int C, int* rows_per_block) {
   return (int)blocks;
 }
 
-void bn_bwd_reduce_launch(const uint16_t* g, int ldg, int mask_mode, const uint16_t* mo, int ldm, const float* ms,
+void bn_bwd_reduce_launch(const uint16_t* g, int ldg, int mask_mode, const void* mo, int ldm, const float* ms,
                           const float* mh, const uint16_t* y0, const float* mean0, const float* rstd0,
                           const uint16_t* y1, const float* mean1, const float* rstd1, int64_t M, int C, int blocks,
                           int rows_per_block, float* part, hipStream_t s) {
@@ -484,7 +521,7 @@ void bn_bwd_finalize_launch(const float* part, int blocks, int C, int64_t count,
                      dgamma, dbeta, beta_acc, coef);
 }
 
-void bn_bwd_apply_launch(const uint16_t* g, int ldg, int mask_mode, const uint16_t* mo, int ldm, const float* ms,
+void bn_bwd_apply_launch(const uint16_t* g, int ldg, int mask_mode, const void* mo, int ldm, const float* ms,
                          const float* mh, const uint16_t* y0, const float* coef0, uint16_t* dy0, const uint16_t* y1,
                          const float* coef1, uint16_t* dy1, uint16_t* dzout, int lddz, int dz_accum, int64_t M, int C,
                          hipStream_t s) {

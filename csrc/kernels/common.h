@@ -71,6 +71,13 @@ __device__ __forceinline__ float sum16(float v) {
   return v;
 }
 
+// Sum over the lanes of a wave that share (lane % S), S a power of two <= 64 (uniform).  Every lane
+// gets its group's sum.  Used before LDS atomics: same-address ds_add_f32 lanes serialise badly.
+__device__ __forceinline__ float wave_sum_stride(float v, int S) {
+  for (int off = S; off < 64; off <<= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
 // Sum across lanes l, l^16, l^32, l^48 (same lane & 15).
 __device__ __forceinline__ float sum_hi4(float v) {
   v += __shfl_xor(v, 16, 64);

@@ -25,13 +25,18 @@ namespace {
 // LDS tile rows are BK bf16 (64 or 128 bytes) of 16-byte slots, XOR-swizzled so that the 16-lane
 // groups of every ds_read_b128 fragment read hit 16 distinct slots of the 256-byte bank row
 // (brute-force checked against the gfx950 b128 lane groups for both row lengths).
+// LDS bytes before the stats/affine area: the double-buffered k tiles, or (EPI) the fp32 output tile.
+__host__ __device__ constexpr int main_lds_bytes(int BM, int BN, int BK, int EPI) {
+  return (EPI && BM * (BN * 4 + 16) > 2 * (BM + BN) * BK * 2) ? BM * (BN * 4 + 16) : 2 * (BM + BN) * BK * 2;
+}
+
 template <int BK>
 __device__ __forceinline__ int lds_off(int row, int slot) {
   if constexpr (BK == 32) return row * 64 + ((slot ^ (((row >> 2) & 1) << 1)) << 4);
   else return row * 128 + ((slot ^ (row & 6)) << 4);
 }
 
-template <int BM, int BN, int WM, int WN, int CH, int BK>
+template <int BM, int BN, int WM, int WN, int CH, int BK, int EPI>
 __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64)
 void conv_igemm_kernel(const ConvParams p) {
   constexpr int NWN = BN / WN;
@@ -42,12 +47,15 @@ void conv_igemm_kernel(const ConvParams p) {
   constexpr int B_SLOTS = (B_CHUNKS + NT - 1) / NT;
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int TILE_BYTES = (BM + BN) * BK * 2;
+  constexpr int STG_PITCH = BN * 4 + 16;  // EPI staging row pitch (fp32 tile, padded)
+  constexpr int MAIN_BYTES = main_lds_bytes(BM, BN, BK, EPI);
   static_assert(NT % CPR == 0, "thread count must be a multiple of chunks per row");
   using VT = typename std::conditional<CH == 8, uint4, uint2>::type;
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* red = reinterpret_cast<float*>(smem + 2 * TILE_BYTES);        // [2][BN] stats
-  float* aff = red + 2 * BN;                                             // [2][Cg] affine
+  float* red = reinterpret_cast<float*>(smem + MAIN_BYTES);            // [3][BN] stats
+  float* bnp = red + 3 * BN;                                             // EPI: [4][BN] mean0 rstd0 mean1 rstd1
+  float* aff = bnp + (EPI ? 4 * BN : 0);                                 // [2][Cg] affine
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / NWN, wn = wid % NWN;
@@ -57,9 +65,20 @@ void conv_igemm_kernel(const ConvParams p) {
   const int tile_m = t / n_tiles, tile_n = t % n_tiles;
   const int m0 = tile_m * BM, n0 = tile_n * BN;
 
-  const bool do_stats = p.stats != nullptr;
+  const bool do_stats = !EPI && p.stats != nullptr;
+  const bool do_bstats = EPI && p.epart != nullptr;
   const int affine = p.affine;
-  if (do_stats) for (int i = tid; i < 2 * BN; i += NT) red[i] = 0.f;
+  if (do_stats || do_bstats) for (int i = tid; i < 3 * BN; i += NT) red[i] = 0.f;
+  if (do_bstats) {  // this tile's BN constants, read once here so the epilogue never waits on them
+    for (int i = tid; i < BN; i += NT) {
+      const int n = n0 + i;
+      const bool ok = n < p.Ngemm, d = ok && p.ey1 != nullptr;
+      bnp[i] = ok ? p.emean0[n] : 0.f;
+      bnp[BN + i] = ok ? p.erstd0[n] : 0.f;
+      bnp[2 * BN + i] = d ? p.emean1[n] : 0.f;
+      bnp[3 * BN + i] = d ? p.erstd1[n] : 0.f;
+    }
+  }
   if (affine) {
     for (int i = tid; i < p.Cg; i += NT) { aff[i] = p.in_scale[i]; aff[p.Cg + i] = p.in_shift[i]; }
   }
@@ -226,6 +245,8 @@ void conv_igemm_kernel(const ConvParams p) {
   }
 
   // ---- epilogue: D[n][m] fragment: lane holds channels n..n+3 of position m ----
+  // EPI 0: direct fragment stores, cs = sum y, cq = sum y^2 (forward BN statistics)
+  // EPI 1: fp32 tile staged through LDS, then the row-contiguous backward-BN pass below
   float cs[TN][4], cq[TN][4];
 #pragma unroll
   for (int j = 0; j < TN; ++j)
@@ -236,36 +257,158 @@ void conv_igemm_kernel(const ConvParams p) {
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int m = m0 + wm * WM + i * 16 + frow;
-    int64_t pos = m;
+    int pos = m;
     if (!dense_rows && m < p.M) {
       const int b = m / RTHW;
       int r = m - b * RTHW;
       const int qt = r / RHW; r -= qt * RHW;
       const int qh = r / p.Rw; const int qw = r - qh * p.Rw;
-      pos = (((int64_t)b * p.Ot + qt * p.ost + p.ort) * p.Oh + qh * p.osh + p.orh) * p.Ow + qw * p.osw + p.orw;
+      pos = ((b * p.Ot + qt * p.ost + p.ort) * p.Oh + qh * p.osh + p.orh) * p.Ow + qw * p.osw + p.orw;
     }
+    if constexpr (EPI == 0) {
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int n = n0 + wn * WN + j * 16 + 4 * fslot;
-      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      if (m < p.M && n < p.Ngemm) {
-        uint16_t* dst = p.y + pos * p.ldy + n;
-        if (p.accum) {
-          float o[4];
-          unpack4(*reinterpret_cast<const uint2*>(dst), o);
+      for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wn * WN + j * 16 + 4 * fslot;
+        float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        if (m < p.M && n < p.Ngemm) {
+          uint16_t* dst = p.y + pos * p.ldy + n;
+          if (p.accum) {
+            float o[4];
+            unpack4(*reinterpret_cast<const uint2*>(dst), o);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] += o[r];
+            for (int r = 0; r < 4; ++r) v[r] += o[r];
+          }
+          const uint2 pk = pack4(v);
+          *reinterpret_cast<uint2*>(dst) = pk;
+          if (do_stats) {
+            float q[4];
+            unpack4(pk, q);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) { cs[j][r] += q[r]; cq[j][r] += q[r] * q[r]; }
+          }
         }
-        const uint2 pk = pack4(v);
-        *reinterpret_cast<uint2*>(dst) = pk;
-        if (do_stats) {
-          float q[4];
-          unpack4(pk, q);
+      }
+    } else {
+      // stage the fp32 fragment in LDS (k tiles are dead: the main loop ended with a barrier)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) { cs[j][r] += q[r]; cq[j][r] += q[r] * q[r]; }
+      for (int j = 0; j < TN; ++j) {
+        const int row = wm * WM + i * 16 + frow, col = wn * WN + j * 16 + 4 * fslot;
+        *reinterpret_cast<f32x4_t*>(smem + row * STG_PITCH + col * 4) = acc[i][j];
+      }
+    }
+  }
+  if constexpr (EPI == 1) {
+    // row-contiguous pass: each thread owns 8 consecutive channels (16-B global accesses) of every
+    // RPP-th tile row: + old y, + residual, ReLU bits, store, backward-BN partial sums.
+    constexpr int CPRW = BN / 8, RPP = NT / CPRW;
+    static_assert(NT % CPRW == 0, "rows per pass");
+    __syncthreads();
+    const int cg = tid % CPRW, r0 = tid / CPRW;
+    const int n = n0 + cg * 8;
+    // sv = sum v, s0 = sum v*y0, s1 = sum v*y1 ; rebased to sum v*xhat at the end of the tile
+    float sv[8], s0[8], s1[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { sv[e] = 0.f; s0[e] = 0.f; s1[e] = 0.f; }
+    const bool nok = n < p.Ngemm;
+    const bool dual = p.ey1 != nullptr;
+    constexpr int RB = 4;  // rows whose loads are issued together (latency hiding)
+    for (int base = r0; base < BM && nok; base += RB * RPP) {
+      uint4 lo[RB], lr[RB], l0[RB], l1[RB];
+      unsigned bits[RB];
+      int pos[RB];
+      bool ok[RB];
+#pragma unroll
+      for (int u = 0; u < RB; ++u) {
+        const int rr = base + u * RPP;
+        const int m = m0 + rr;
+        ok[u] = rr < BM && m < p.M;
+        int ps = m;
+        if (!dense_rows && ok[u]) {
+          const int b = m / RTHW;
+          int r = m - b * RTHW;
+          const int qt = r / RHW; r -= qt * RHW;
+          const int qh = r / p.Rw; const int qw = r - qh * p.Rw;
+          ps = ((b * p.Ot + qt * p.ost + p.ort) * p.Oh + qh * p.osh + p.orh) * p.Ow + qw * p.osw + p.orw;
+        }
+        pos[u] = ps;
+        lo[u] = lr[u] = l0[u] = l1[u] = uint4{0, 0, 0, 0};
+        bits[u] = 0xffu;
+        if (ok[u]) {
+          if (p.accum) lo[u] = *reinterpret_cast<const uint4*>(p.y + ps * p.ldy + n);
+          if (p.eres) lr[u] = *reinterpret_cast<const uint4*>(p.eres + ps * p.ldr + n);
+          if (p.emask) bits[u] = p.emask[ps * (p.Ngemm >> 3) + (n >> 3)];
+          if (do_bstats) {
+            l0[u] = *reinterpret_cast<const uint4*>(p.ey0 + ps * p.Ngemm + n);
+            if (dual) l1[u] = *reinterpret_cast<const uint4*>(p.ey1 + ps * p.Ngemm + n);
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < RB; ++u) {
+        if (!ok[u]) continue;
+        const int rr = base + u * RPP;
+        const f32x4_t va = *reinterpret_cast<const f32x4_t*>(smem + rr * STG_PITCH + cg * 32);
+        const f32x4_t vb = *reinterpret_cast<const f32x4_t*>(smem + rr * STG_PITCH + cg * 32 + 16);
+        float v[8] = {va[0], va[1], va[2], va[3], vb[0], vb[1], vb[2], vb[3]};
+        float o[8], rs[8];
+        unpack8(lo[u], o);
+        unpack8(lr[u], rs);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float t = v[e] + o[e] + rs[e];
+          v[e] = (bits[u] >> e) & 1u ? t : 0.f;
+        }
+        const uint4 pk = pack8(v);
+        *reinterpret_cast<uint4*>(p.y + pos[u] * p.ldy + n) = pk;
+        if (do_bstats) {
+          float q[8], a[8];
+          unpack8(pk, q);
+          unpack8(l0[u], a);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) { sv[e] += q[e]; s0[e] += q[e] * a[e]; }
+          if (dual) {
+            unpack8(l1[u], a);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) s1[e] += q[e] * a[e];
+          }
         }
       }
     }
+    if (do_bstats && nok) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int c = cg * 8 + e;
+        s0[e] = (s0[e] - bnp[c] * sv[e]) * bnp[BN + c];
+        s1[e] = (s1[e] - bnp[2 * BN + c] * sv[e]) * bnp[3 * BN + c];
+      }
+    }
+    if (do_bstats) {
+      // lanes with the same channel group first reduce across the wave, then one LDS atomic per wave
+      static_assert(CPRW <= 64 && (CPRW & (CPRW - 1)) == 0, "channel groups per row");
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        sv[e] = wave_sum_stride(sv[e], CPRW);
+        s0[e] = wave_sum_stride(s0[e], CPRW);
+        s1[e] = wave_sum_stride(s1[e], CPRW);
+      }
+      if (nok && lane < CPRW) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          atomicAdd(&red[cg * 8 + e], sv[e]);
+          atomicAdd(&red[BN + cg * 8 + e], s0[e]);
+          atomicAdd(&red[2 * BN + cg * 8 + e], s1[e]);
+        }
+      }
+      __syncthreads();
+      for (int i = tid; i < BN; i += NT) {
+        const int nn = n0 + i;
+        if (nn < p.Ngemm) {
+#pragma unroll
+          for (int k = 0; k < 3; ++k) p.epart[(tile_m * 3 + k) * p.Ngemm + nn] = red[k * BN + i];
+        }
+      }
+    }
+    return;
   }
   if (do_stats) {
 #pragma unroll
@@ -284,8 +427,8 @@ void conv_igemm_kernel(const ConvParams p) {
     for (int i = tid; i < BN; i += NT) {
       const int n = n0 + i;
       if (n < p.Ngemm) {
-        p.stats[(int64_t)tile_m * 2 * p.Ngemm + n] = red[i];
-        p.stats[(int64_t)tile_m * 2 * p.Ngemm + p.Ngemm + n] = red[BN + i];
+        p.stats[(tile_m * 2) * p.Ngemm + n] = red[i];
+        p.stats[(tile_m * 2 + 1) * p.Ngemm + n] = red[BN + i];
       }
     }
   }
@@ -295,8 +438,16 @@ template <int BM, int BN, int WM, int WN, int CH, int BK>
 void launch_cfg(const ConvParams& p, hipStream_t stream) {
   constexpr int NT = (BM / WM) * (BN / WN) * 64;
   const int m_tiles = (p.M + BM - 1) / BM, n_tiles = (p.Ngemm + BN - 1) / BN;
-  const size_t lds = 2 * (BM + BN) * BK * 2 + 2 * BN * 4 + (p.affine ? 2 * p.Cg * 4 : 0);
-  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK>), dim3(m_tiles * n_tiles), dim3(NT), lds, stream, p);
+  const bool epi = p.eres || p.emask || p.epart;
+  const size_t lds = main_lds_bytes(BM, BN, BK, epi ? 1 : 0) + (epi ? 7 : 3) * BN * 4 + (p.affine ? 2 * p.Cg * 4 : 0);
+  if (epi) {
+    if constexpr (CH == 8)
+      hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 1>), dim3(m_tiles * n_tiles), dim3(NT), lds,
+                         stream, p);
+  } else {
+    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 0>), dim3(m_tiles * n_tiles), dim3(NT), lds,
+                       stream, p);
+  }
 }
 
 template <int CH, int BK>
@@ -328,6 +479,7 @@ static int g_bk_override = -1;
 void conv_igemm_set_bk(int bk) { g_bk_override = bk; }
 
 void conv_igemm_launch(const ConvParams& p, int chunk, hipStream_t stream) {
+  if ((p.eres || p.emask || p.epart) && chunk != 8) return;  // host binding rejects this combination
   const int v = pick_variant(p.M, p.Ngemm);
   const int K = p.nt * p.nh * p.nw * p.Cg;
   int bk = g_bk_override > 0 ? g_bk_override : ((K >= 1024 && chunk == 8) ? 64 : 32);

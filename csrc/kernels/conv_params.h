@@ -36,6 +36,19 @@ struct ConvParams {
   int kh, kw;               // full kernel extents (weight tap index)
   int bt0, bh0, bw0, bts, bhs, bws;
   int check;                // 1: gathered coordinates may leave the tensor (padding) -> bounds tests
+  // Optional backward-BN epilogue, used by the dgrad that produces the gradient of a residual-unit
+  // output (the next unit's conv_a): v = acc (+ y_old if accum) (+ eres) ; v *= ReLU bit ; store ;
+  // per-column partial sums of v, v*xhat0, v*xhat1 for the producing unit's conv_c / branch1 BNs.
+  const uint16_t* eres;     // residual gradient rows (row stride ldr), same row mapping as y
+  int ldr;
+  const uint8_t* emask;     // ReLU mask bits [rows][Ngemm/8]
+  const uint16_t* ey0;      // BN inputs [rows][Ngemm] (raw conv outputs)
+  const uint16_t* ey1;
+  const float* emean0;
+  const float* erstd0;
+  const float* emean1;
+  const float* erstd1;
+  float* epart;             // [m_tiles][3][Ngemm] partial (sum v, sum v*xhat0, sum v*xhat1)
 };
 
 // Weight gradient: dW[n = cout][k = (tap, cin)] = sum_p dY[p][cout] * im2col(X)[p][k]

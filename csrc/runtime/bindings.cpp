@@ -29,17 +29,17 @@ void bn_eval_affine_launch(int C, const float* gamma, const float* beta, const f
 void bn_act_launch(const uint16_t* y, int ldy, uint16_t* out, int ldo, const float* scale, const float* shift,
                    int relu, int64_t M, int C, hipStream_t s);
 void res_out_launch(const uint16_t* yc, const float* sc, const float* hc, const uint16_t* y1, const float* s1,
-                    const float* h1, const uint16_t* x, int ldx, uint16_t* out, int ldo, int64_t M, int C,
-                    hipStream_t s);
+                    const float* h1, const uint16_t* x, int ldx, uint16_t* out, int ldo, uint8_t* mask, int64_t M,
+                    int C, hipStream_t s);
 int bn_bwd_reduce_blocks(int64_t M, int C, int* rows_per_block);
-void bn_bwd_reduce_launch(const uint16_t* g, int ldg, int mask_mode, const uint16_t* mo, int ldm, const float* ms,
+void bn_bwd_reduce_launch(const uint16_t* g, int ldg, int mask_mode, const void* mo, int ldm, const float* ms,
                           const float* mh, const uint16_t* y0, const float* mean0, const float* rstd0,
                           const uint16_t* y1, const float* mean1, const float* rstd1, int64_t M, int C, int blocks,
                           int rows_per_block, float* part, hipStream_t s);
 void bn_bwd_finalize_launch(const float* part, int blocks, int C, int64_t count, int which, const float* gamma,
                             const float* mean, const float* rstd, float* dgamma, float* dbeta, float beta_acc,
                             float* coef, hipStream_t s);
-void bn_bwd_apply_launch(const uint16_t* g, int ldg, int mask_mode, const uint16_t* mo, int ldm, const float* ms,
+void bn_bwd_apply_launch(const uint16_t* g, int ldg, int mask_mode, const void* mo, int ldm, const float* ms,
                          const float* mh, const uint16_t* y0, const float* coef0, uint16_t* dy0, const uint16_t* y1,
                          const float* coef1, uint16_t* dy1, uint16_t* dzout, int lddz, int dz_accum, int64_t M, int C,
                          hipStream_t s);
@@ -97,34 +97,64 @@ inline float* f32o(const OptT& t) { return t.has_value() ? f32(*t) : nullptr; }
 // geometry vector (39): [M, Ngemm, Kfull, Cg, ldx, ldy, Gt, Gh, Gw, Rt, Rh, Rw, Ot, Oh, Ow,
 //   ost, osh, osw, ort, orh, orw, ast, ash, asw, aot, aoh, aow, dir, nt, nh, nw, kh, kw,
 //   bt0, bh0, bw0, bts, bhs, bws]   (see ConvParams; built by ops/conv.py)
-void conv_igemm(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, const OptT& stats,
-                const OptT& scale, const OptT& shift, int64_t affine, int64_t accum, std::vector<int64_t> g,
-                int64_t chunk) {
+static ConvParams conv_params(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, int64_t accum,
+                              const std::vector<int64_t>& g, int64_t chunk) {
   TORCH_CHECK(g.size() == 39, "conv geometry must have 39 entries");
   ConvParams p{};
   p.x = bfp(x); p.w = bfp(w); p.y = bfpm(y);
-  p.stats = f32o(stats);
-  p.in_scale = f32o(scale); p.in_shift = f32o(shift);
-  p.affine = (int)affine; p.accum = (int)accum;
+  p.accum = (int)accum;
   int* f = &p.M;
   for (int i = 0; i < 39; ++i) f[i] = (int)g[i];
   // bounds tests are only needed when some tap can read outside the gathered tensor
-  {
-    auto dim_ok = [](int R, int as, int ao, int dir, int n, int G) {
-      const int lo = ao + (dir < 0 ? -(n - 1) : 0);
-      const int hi = (R - 1) * as + ao + (dir > 0 ? (n - 1) : 0);
-      return n == 0 || (lo >= 0 && hi < G);
-    };
-    p.check = (dim_ok(p.Rt, p.ast, p.aot, p.dir, p.nt, p.Gt) && dim_ok(p.Rh, p.ash, p.aoh, p.dir, p.nh, p.Gh) &&
-               dim_ok(p.Rw, p.asw, p.aow, p.dir, p.nw, p.Gw)) ? 0 : 1;
-  }
-  TORCH_CHECK((int64_t)p.Gt * p.Gh * p.Gw * (x.numel() / std::max<int64_t>(1, (int64_t)p.Gt * p.Gh * p.Gw)) < (1ll << 31) &&
-              x.numel() < (1ll << 31) && y.numel() < (1ll << 31), "tensor too large for 32-bit offsets");
+  auto dim_ok = [](int R, int as, int ao, int dir, int n, int G) {
+    const int lo = ao + (dir < 0 ? -(n - 1) : 0);
+    const int hi = (R - 1) * as + ao + (dir > 0 ? (n - 1) : 0);
+    return n == 0 || (lo >= 0 && hi < G);
+  };
+  p.check = (dim_ok(p.Rt, p.ast, p.aot, p.dir, p.nt, p.Gt) && dim_ok(p.Rh, p.ash, p.aoh, p.dir, p.nh, p.Gh) &&
+             dim_ok(p.Rw, p.asw, p.aow, p.dir, p.nw, p.Gw)) ? 0 : 1;
+  TORCH_CHECK(x.numel() < (1ll << 31) && y.numel() < (1ll << 31), "tensor too large for 32-bit offsets");
   TORCH_CHECK(p.Cg % chunk == 0 && p.Cg > 0, "gathered channels must be a multiple of the chunk");
   TORCH_CHECK(p.Ngemm % 4 == 0, "output channels must be a multiple of 4");
   TORCH_CHECK(p.ldx % chunk == 0 && p.ldy % 4 == 0, "row strides must keep vector alignment");
-  TORCH_CHECK(!affine || (scale.has_value() && shift.has_value()), "affine needs scale/shift");
   TORCH_CHECK(w.numel() >= (int64_t)p.Ngemm * p.Kfull, "packed weight too small");
+  return p;
+}
+
+void conv_igemm(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, const OptT& stats,
+                const OptT& scale, const OptT& shift, int64_t affine, int64_t accum, std::vector<int64_t> g,
+                int64_t chunk) {
+  ConvParams p = conv_params(x, w, y, accum, g, chunk);
+  p.stats = f32o(stats);
+  p.in_scale = f32o(scale); p.in_shift = f32o(shift);
+  p.affine = (int)affine;
+  TORCH_CHECK(!affine || (scale.has_value() && shift.has_value()), "affine needs scale/shift");
+  if (p.M == 0) return;
+  conv_igemm_launch(p, (int)chunk, cur_stream());
+}
+
+// dgrad with the backward-BN epilogue (see ConvParams): residual add, ReLU-bit mask, and partial sums
+// [m_tiles][3][Ngemm] of (v, v*xhat0, v*xhat1) over this launch's rows (which must be dense: one phase).
+void conv_igemm_epi(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, int64_t accum,
+                    std::vector<int64_t> g, int64_t chunk, const OptT& res, int64_t ldr, const OptT& mask,
+                    const OptT& y0, const OptT& mean0, const OptT& rstd0, const OptT& y1, const OptT& mean1,
+                    const OptT& rstd1, const OptT& part) {
+  ConvParams p = conv_params(x, w, y, accum, g, chunk);
+  p.eres = bfo(res); p.ldr = (int)ldr;
+  TORCH_CHECK(!res.has_value() || ldr % 4 == 0, "residual row stride alignment");
+  if (mask.has_value()) {
+    TORCH_CHECK(mask->scalar_type() == at::kByte && p.Ngemm % 8 == 0, "mask must be uint8 bits [rows][C/8]");
+    p.emask = mask->data_ptr<uint8_t>();
+  }
+  if (part.has_value()) {
+    TORCH_CHECK(y0.has_value() && mean0.has_value() && rstd0.has_value(), "BN epilogue needs y0/mean0/rstd0");
+    TORCH_CHECK(!y1.has_value() || (mean1.has_value() && rstd1.has_value()), "BN epilogue needs mean1/rstd1");
+    TORCH_CHECK(y0->size(-1) == p.Ngemm, "BN epilogue inputs must be dense [rows][Ngemm]");
+    p.ey0 = bfp(*y0); p.ey1 = bfo(y1);
+    p.emean0 = f32(*mean0); p.erstd0 = f32(*rstd0); p.emean1 = f32o(mean1); p.erstd1 = f32o(rstd1);
+    p.epart = f32(*part);
+    TORCH_CHECK(part->numel() >= (int64_t)conv_igemm_m_tiles(p.M, p.Ngemm) * 3 * p.Ngemm, "partials too small");
+  }
   if (p.M == 0) return;
   conv_igemm_launch(p, (int)chunk, cur_stream());
 }
@@ -181,10 +211,23 @@ void bn_act(const at::Tensor& y, int64_t ldy, const at::Tensor& out, int64_t ldo
 }
 
 void res_out(const at::Tensor& yc, const at::Tensor& sc, const at::Tensor& hc, const OptT& y1, const OptT& s1,
-             const OptT& h1, const OptT& x, int64_t ldx, const at::Tensor& out, int64_t ldo, int64_t M, int64_t C) {
+             const OptT& h1, const OptT& x, int64_t ldx, const at::Tensor& out, int64_t ldo, int64_t M, int64_t C,
+             const OptT& mask) {
   TORCH_CHECK(y1.has_value() || x.has_value(), "res_out needs a shortcut");
-  res_out_launch(bfp(yc), f32(sc), f32(hc), bfo(y1), f32o(s1), f32o(h1), bfo(x), (int)ldx, bfpm(out), (int)ldo, M,
-                 (int)C, cur_stream());
+  TORCH_CHECK(!mask.has_value() || (mask->scalar_type() == at::kByte && mask->numel() >= M * (C / 8)),
+              "res_out mask must be uint8 [M, C/8]");
+  res_out_launch(bfp(yc), f32(sc), f32(hc), bfo(y1), f32o(s1), f32o(h1), bfo(x), (int)ldx, bfpm(out), (int)ldo,
+                 mask.has_value() ? mask->data_ptr<uint8_t>() : nullptr, M, (int)C, cur_stream());
+}
+
+// mask operand of the BN-backward kernels: bf16 block output (mode 1) or uint8 ReLU bits (mode 3)
+static const void* mask_ptr(int64_t mode, const OptT& mo) {
+  if (mode == 1) return bfo(mo);
+  if (mode == 3) {
+    TORCH_CHECK(mo.has_value() && mo->scalar_type() == at::kByte, "mask mode 3 needs uint8 mask bits");
+    return mo->data_ptr<uint8_t>();
+  }
+  return nullptr;
 }
 
 std::vector<int64_t> bn_bwd_blocks(int64_t M, int64_t C) {
@@ -198,7 +241,7 @@ void bn_bwd_reduce(const at::Tensor& g, int64_t ldg, int64_t mask_mode, const Op
                    const OptT& y1, const OptT& mean1, const OptT& rstd1, int64_t M, int64_t C, int64_t blocks,
                    int64_t rpb, const at::Tensor& part) {
   TORCH_CHECK(C % 8 == 0 && C <= 2048, "bn_bwd_reduce channel constraint");
-  bn_bwd_reduce_launch(bfp(g), (int)ldg, (int)mask_mode, bfo(mo), (int)ldm, f32o(ms), f32o(mh), bfp(y0), f32(mean0),
+  bn_bwd_reduce_launch(bfp(g), (int)ldg, (int)mask_mode, mask_ptr(mask_mode, mo), (int)ldm, f32o(ms), f32o(mh), bfp(y0), f32(mean0),
                        f32(rstd0), bfo(y1), f32o(mean1), f32o(rstd1), M, (int)C, (int)blocks, (int)rpb, f32(part),
                        cur_stream());
 }
@@ -214,7 +257,7 @@ void bn_bwd_apply(const at::Tensor& g, int64_t ldg, int64_t mask_mode, const Opt
                   const OptT& mh, const at::Tensor& y0, const at::Tensor& coef0, const at::Tensor& dy0,
                   const OptT& y1, const OptT& coef1, const OptT& dy1, const OptT& dzout, int64_t lddz,
                   int64_t dz_accum, int64_t M, int64_t C) {
-  bn_bwd_apply_launch(bfp(g), (int)ldg, (int)mask_mode, bfo(mo), (int)ldm, f32o(ms), f32o(mh), bfp(y0), f32(coef0),
+  bn_bwd_apply_launch(bfp(g), (int)ldg, (int)mask_mode, mask_ptr(mask_mode, mo), (int)ldm, f32o(ms), f32o(mh), bfp(y0), f32(coef0),
                       bfpm(dy0), bfo(y1), f32o(coef1), bfom(dy1), bfom(dzout), (int)lddz, (int)dz_accum, M, (int)C,
                       cur_stream());
 }
@@ -300,6 +343,7 @@ void synth_frames(const at::Tensor& out, int64_t seed) {
 PYBIND11_MODULE(_C, m) {
   m.doc() = "gfx950 HIP kernels for pytorchvideo_accelerate_amd";
   m.def("conv_igemm", &conv_igemm);
+  m.def("conv_igemm_epi", &conv_igemm_epi);
   m.def("conv_m_tiles", &conv_m_tiles);
   m.def("conv_set_bk", [](int64_t bk) { conv_igemm_set_bk((int)bk); });
   m.def("wgrad_tile", &wgrad_tile);

@@ -172,7 +172,12 @@ class _ConvBN:
         C.wgrad_reduce(part, eng.flat.gview(self.conv.weight), splits, s.cout, s.taps, s.cin_pad, s.cin, 1.0,
                        eng.grad_beta)
 
-    def dgrad(self, dy: Act, in_dims, out: torch.Tensor, accum: bool) -> Act:
+    def dgrad(self, dy: Act, in_dims, out: torch.Tensor, accum: bool, res: Optional[Act] = None,
+              epi: Optional["_ResBlock"] = None):
+        """grad wrt the conv input into ``out`` (``accum``: added).  With ``res`` / ``epi`` the single-phase
+        launch also adds the residual gradient ``res``, applies the ReLU mask of residual unit ``epi``'s
+        output and emits the partial sums of ``epi``'s conv_c (+branch1) BN backward; returns
+        (partials, tiles) for ``epi.bwd(pre=...)``."""
         s, C = self.spec, self.eng.C
         self.eng.mark(self.name + ".dgrad")
         Ti, Hi, Wi = in_dims
@@ -180,26 +185,52 @@ class _ConvBN:
         geo = self._geo.get(key)
         if geo is None:
             geo = self._geo[key] = dgrad_phases(s, dy.N, tuple(in_dims), (dy.T, dy.H, dy.W), dy.ld, out.stride(0))
+        if res is not None or epi is not None:
+            assert len(geo) == 1, "fused dgrad epilogue needs a single-phase (stride-1) dgrad"
+            g = geo[0]
+            part, tiles = None, 0
+            if epi is not None:
+                tiles = C.conv_m_tiles(g[0], g[1])
+                part = self.eng.scratch("bnepi", tiles * 3 * g[1])
+                c, one = epi.c, epi.one
+            C.conv_igemm_epi(dy.t, self.wd, out, 1 if accum else 0, g, 8,
+                             None if res is None else res.t, 0 if res is None else res.ld,
+                             None if epi is None else epi.mask, None if epi is None else epi.yc.t,
+                             None if epi is None else c.mean, None if epi is None else c.rstd,
+                             None if epi is None or one is None else epi.y1.t,
+                             None if epi is None or one is None else one.mean,
+                             None if epi is None or one is None else one.rstd, part)
+            return (part, tiles) if epi is not None else None
         for g in geo:
             if accum and g[28] == 0:
                 continue
             C.conv_igemm(dy.t, self.wd, out, None, None, None, 0, 1 if accum else 0, g, 8)
-        return Act(out, dy.N, Ti, Hi, Wi)
+        return None
 
     def bn_backward(self, g: Act, y: Act, mask_mode: int, mo: Optional[Act], mxf: Optional[_Xf],
                     dz_out: Optional[Act] = None, dz_accum: bool = False, other: Optional["_ConvBN"] = None,
-                    other_y: Optional[Act] = None) -> Tuple[Act, Optional[Act]]:
-        """dz = g*mask ; returns (dy_self, dy_other) for one or two BNs sharing dz."""
+                    other_y: Optional[Act] = None, pre=None) -> Tuple[Act, Optional[Act]]:
+        """dz = g*mask ; returns (dy_self, dy_other) for one or two BNs sharing dz.
+
+        mask_mode 0: none, 1: ``mo`` (Act) > 0, 2: affine(y) > 0, 3: ``mo`` = uint8 ReLU bits [M, C/8].
+        ``pre`` = (partials, tiles) already produced by a consumer dgrad epilogue: skips the reduce."""
         eng, C = self.eng, self.eng.C
         M, Cc = y.M, self.C
-        blocks, rpb = eng._bn_blocks(M, Cc)
-        eng.mark(self.name + ".bnred")
-        part = eng.scratch("bnpart", blocks * 3 * Cc)
-        C.bn_bwd_reduce(g.t, g.ld, mask_mode, None if mo is None else mo.t, 0 if mo is None else mo.ld,
-                        None if mxf is None else mxf.scale, None if mxf is None else mxf.shift,
-                        y.t, self.mean, self.rstd,
-                        None if other is None else other_y.t, None if other is None else other.mean,
-                        None if other is None else other.rstd, M, Cc, blocks, rpb, part)
+        if isinstance(mo, Act):
+            mo_t, mo_ld = mo.t, mo.ld
+        else:
+            mo_t, mo_ld = mo, (0 if mo is None else mo.shape[1])
+        if pre is not None:
+            part, blocks = pre
+        else:
+            blocks, rpb = eng._bn_blocks(M, Cc)
+            eng.mark(self.name + ".bnred")
+            part = eng.scratch("bnpart", blocks * 3 * Cc)
+            C.bn_bwd_reduce(g.t, g.ld, mask_mode, mo_t, mo_ld,
+                            None if mxf is None else mxf.scale, None if mxf is None else mxf.shift,
+                            y.t, self.mean, self.rstd,
+                            None if other is None else other_y.t, None if other is None else other.mean,
+                            None if other is None else other.rstd, M, Cc, blocks, rpb, part)
         fg = eng.flat
         C.bn_bwd_finalize(part, blocks, Cc, M, 0, self.bn.weight, self.mean, self.rstd,
                           fg.gview(self.bn.weight), fg.gview(self.bn.bias), eng.grad_beta, self.coef)
@@ -209,7 +240,7 @@ class _ConvBN:
         dy = eng.ws((self.name, "dy"), (M, Cc), torch.bfloat16)
         dy1 = eng.ws((other.name, "dy"), (M, Cc), torch.bfloat16) if other is not None else None
         eng.mark(self.name + ".bnapply")
-        C.bn_bwd_apply(g.t, g.ld, mask_mode, None if mo is None else mo.t, 0 if mo is None else mo.ld,
+        C.bn_bwd_apply(g.t, g.ld, mask_mode, mo_t, mo_ld,
                        None if mxf is None else mxf.scale, None if mxf is None else mxf.shift,
                        y.t, self.coef, dy, None if other is None else other_y.t,
                        None if other is None else other.coef, dy1,
@@ -331,25 +362,36 @@ class _ResBlock:
         y1 = self.one.fwd(x, None, train, tag) if self.one is not None else None
         M = yc.M
         self.eng.mark(self.name + ".res_out")
+        mask = self.eng.ws((self.name, "mask"), (M, self.c.C // 8), torch.uint8) if train else None
         C.res_out(yc.t, self.c.scale, self.c.shift,
                   None if y1 is None else y1.t, None if y1 is None else self.one.scale,
                   None if y1 is None else self.one.shift, None if y1 is not None else x.t, x.ld,
-                  out, out.stride(0), M, self.c.C)
+                  out, out.stride(0), M, self.c.C, mask)
+        self.mask = mask
         o = Act(out, yc.N, yc.T, yc.H, yc.W)
         self.x, self.ya, self.yb, self.yc, self.y1, self.out = x, ya, yb, yc, y1, o
         return o
 
-    def bwd(self, dout: Act, dx: torch.Tensor, dx_accum: bool):
-        """dout: grad wrt block output; dx: [M_in, C_in] buffer receiving grad wrt block input."""
+    def bwd(self, dout: Act, dx: torch.Tensor, dx_accum: bool, pre=None, prev: Optional["_ResBlock"] = None):
+        """dout: grad wrt block output; dx: [M_in, C_in] buffer receiving grad wrt block input.
+
+        ``pre``: ``dout`` is already the ReLU-masked gradient and its conv_c/branch1 BN partial sums were
+        emitted by the following unit's conv_a dgrad epilogue.  ``prev``: the preceding unit of the same
+        stage — this unit's final dgrad then produces ``prev``'s masked gradient and partial sums (returned,
+        to be passed as ``prev.bwd(pre=...)``)."""
         eng = self.eng
         x, ya, yb, yc, y1 = self.x, self.ya, self.yb, self.yc, self.y1
         dxa = Act(dx, x.N, x.T, x.H, x.W)
-        if self.one is None:
+        res = None
+        if pre is not None:
+            dyc, dy1 = self.c.bn_backward(dout, yc, 0, None, None, other=self.one, other_y=y1, pre=pre)
+            if self.one is None:
+                res = dout          # identity shortcut: the masked gradient is added by conv_a's dgrad
+        elif self.one is None:
             # identity shortcut: dz goes straight to dx
-            dyc, _ = self.c.bn_backward(dout, yc, 1, self.out, None, dz_out=dxa, dz_accum=dx_accum)
-            dy1 = None
+            dyc, _ = self.c.bn_backward(dout, yc, 3, self.mask, None, dz_out=dxa, dz_accum=dx_accum)
         else:
-            dyc, dy1 = self.c.bn_backward(dout, yc, 1, self.out, None, other=self.one, other_y=y1)
+            dyc, dy1 = self.c.bn_backward(dout, yc, 3, self.mask, None, other=self.one, other_y=y1)
         self.c.wgrad(dyc, yb, self.b.xf())
         dab = eng.ws((self.name, "dab"), (yb.M, self.b.C), torch.bfloat16)
         self.c.dgrad(dyc, (yb.T, yb.H, yb.W), dab, False)
@@ -359,12 +401,23 @@ class _ResBlock:
         self.b.dgrad(dyb, (ya.T, ya.H, ya.W), daa, False)
         dya, _ = self.a.bn_backward(Act(daa, ya.N, ya.T, ya.H, ya.W), ya, 2, None, self.a.xf())
         self.a.wgrad(dya, x, None)
-        acc = True if self.one is None else dx_accum
         if self.one is not None:
             self.one.wgrad(dy1, x, None)
             self.one.dgrad(dy1, (x.T, x.H, x.W), dx, dx_accum)
             acc = True
-        self.a.dgrad(dya, (x.T, x.H, x.W), dx, acc)
+        else:
+            acc = dx_accum if pre is not None else True
+        if prev is not None and not self._epi_ok(prev):
+            prev = None
+        if res is None and prev is None:
+            self.a.dgrad(dya, (x.T, x.H, x.W), dx, acc)
+            return None
+        return self.a.dgrad(dya, (x.T, x.H, x.W), dx, acc, res=res, epi=prev)
+
+    def _epi_ok(self, prev: "_ResBlock") -> bool:
+        s = self.a.spec
+        return (tuple(s.stride) == (1, 1, 1) and prev.out.t.is_contiguous() and prev.c.C % 8 == 0
+                and prev.mask is not None)
 
 
 class _Stage:
@@ -394,6 +447,7 @@ class _Stage:
 
     def bwd(self, dout: Act, dx: torch.Tensor, dx_accum: bool):
         eng = self.eng
+        pre = None
         for i in range(len(self.blocks) - 1, -1, -1):
             b = self.blocks[i]
             if i == 0:
@@ -401,7 +455,7 @@ class _Stage:
             else:
                 xin = b.x
                 tgt, acc = eng.ws((b.name, "dx"), (xin.M, xin.C), torch.bfloat16), False
-            b.bwd(dout, tgt, acc)
+            pre = b.bwd(dout, tgt, acc, pre=pre, prev=self.blocks[i - 1] if i > 0 else None)
             b.eng_progress(b.flat_hi)
             if i > 0:
                 xin = b.x

@@ -96,6 +96,69 @@ def test_conv_dgrad(case):
     assert rel_err(dx2.to_ncthw(), 2 * x.grad) < 1.5e-2
 
 
+def _bits(mask):
+    """bool [M, C] -> uint8 [M, C/8] with bit e of byte j = mask[:, 8j+e] (res_out's layout)."""
+    M, C = mask.shape
+    w = (1 << torch.arange(8, device=mask.device)).to(torch.int32)
+    return (mask.view(M, C // 8, 8).to(torch.int32) * w).sum(-1).to(torch.uint8)
+
+
+@pytest.mark.parametrize("case,dual,accum", [(CASES[1], True, False), (CASES[0], False, True),
+                                             (CASES[8], True, True)])
+def test_conv_dgrad_bn_epilogue(case, dual, accum):
+    """dgrad + residual + ReLU-bit mask + backward-BN partial sums (sum v, sum v*xhat0, sum v*xhat1)."""
+    from pytorchvideo_accelerate_amd.ops._ext import require
+    from pytorchvideo_accelerate_amd.ops.conv import conv_m_tiles, dgrad_phases
+    C = require()
+    x, w, spec = _mk(case, seed=5)
+    N, Ci, T, H, W = x.shape
+    ref_y = torch.nn.functional.conv3d(x, w, None, spec.stride, spec.pad)
+    gy = torch.randn_like(ref_y).to(torch.bfloat16).float()
+    dx_ref = torch.nn.grad.conv3d_input(x.shape, w, gy, spec.stride, spec.pad)
+    M = N * T * H * W
+    g = torch.Generator(device="cpu").manual_seed(6)
+    bf = lambda *s: torch.randn(*s, generator=g).to(torch.bfloat16).to(DEV)
+    res, old, y0, y1 = bf(M, Ci), bf(M, Ci), bf(M, Ci) * 2 + 0.5, bf(M, Ci)
+    mask = torch.rand(M, Ci, generator=g).to(DEV) > 0.4
+    mean0, rstd0 = torch.randn(Ci, device=DEV) * 0.3, torch.rand(Ci, device=DEV) + 0.5
+    mean1, rstd1 = torch.randn(Ci, device=DEV) * 0.3, torch.rand(Ci, device=DEV) + 0.5
+    _, wd = pack_weight(w, spec)
+    dy = Act.from_ncthw(gy)
+    out = old.clone()
+    geo = dgrad_phases(spec, N, (T, H, W), (dy.T, dy.H, dy.W), dy.ld, Ci)
+    assert len(geo) == 1
+    tiles = conv_m_tiles(M, Ci)
+    part = torch.full((tiles, 3, Ci), float("nan"), device=DEV)
+    C.conv_igemm_epi(dy.t, wd, out, 1 if accum else 0, geo[0], 8, res, Ci, _bits(mask), y0, mean0, rstd0,
+                     y1 if dual else None, mean1 if dual else None, rstd1 if dual else None, part)
+    dxr = dx_ref.permute(0, 2, 3, 4, 1).reshape(M, Ci)
+    v = (dxr + (old.float() if accum else 0) + res.float()) * mask
+    assert rel_err(out, v) < 1.5e-2
+    q = out.float()
+    s = part.sum(0)
+    tol = 2e-2 * (q.abs() * (y0.float() - mean0).abs() * rstd0).sum(0).max().item() / M ** 0.5
+    torch.testing.assert_close(s[0], q.sum(0), rtol=1e-3, atol=1e-2 * q.abs().sum(0).max().item() / M ** 0.5)
+    torch.testing.assert_close(s[1], (q * (y0.float() - mean0) * rstd0).sum(0), rtol=1e-3, atol=tol)
+    if dual:
+        torch.testing.assert_close(s[2], (q * (y1.float() - mean1) * rstd1).sum(0), rtol=1e-3, atol=tol)
+
+
+def test_res_out_mask_bits():
+    from pytorchvideo_accelerate_amd.ops._ext import require
+    C = require()
+    M, Ch = 1000, 64
+    g = torch.Generator(device="cpu").manual_seed(7)
+    yc = torch.randn(M, Ch, generator=g).to(torch.bfloat16).to(DEV)
+    x = torch.randn(M, Ch, generator=g).to(torch.bfloat16).to(DEV)
+    sc, sh = torch.rand(Ch, device=DEV) + 0.5, torch.randn(Ch, device=DEV) * 0.1
+    out = torch.empty(M, Ch, device=DEV, dtype=torch.bfloat16)
+    mask = torch.zeros(M, Ch // 8, device=DEV, dtype=torch.uint8)
+    C.res_out(yc, sc, sh, None, None, None, x, Ch, out, Ch, M, Ch, mask)
+    ref = torch.relu(yc.float() * sc + sh + x.float())
+    assert rel_err(out, ref) < 1e-2
+    assert torch.equal(mask, _bits(out.float() > 0))
+
+
 @pytest.mark.parametrize("case", CASES + STEMS)
 def test_conv_wgrad(case):
     x, w, spec = _mk(case, seed=3)
