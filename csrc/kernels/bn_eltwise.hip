@@ -148,11 +148,9 @@ __global__ void bn_bwd_reduce_kernel(const uint16_t* __restrict__ g, int ldg, in
                                      const uint16_t* __restrict__ y1, const float* __restrict__ mean1,
                                      const float* __restrict__ rstd1,
                                      int64_t M, int C, int rows_per_block, float* __restrict__ part) {
-  extern __shared__ __attribute__((aligned(16))) float red[];  // [3][C]
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [slots][3][C], NT*96 bytes
   const uint16_t* mo = static_cast<const uint16_t*>(mo_);
   const uint8_t* mb = static_cast<const uint8_t*>(mo_);
-  for (int i = threadIdx.x; i < 3 * C; i += NT) red[i] = 0.f;
-  __syncthreads();
   const int vecs = C >> 3;
   const int rpi = NT / vecs;  // rows per iteration
   const int lv = threadIdx.x % vecs, lr = threadIdx.x / vecs;
@@ -196,27 +194,31 @@ __global__ void bn_bwd_reduce_kernel(const uint16_t* __restrict__ g, int ldg, in
       }
     }
   }
-  // threads lv, lv+vecs, ... share channel addresses: reduce across the wave before the LDS atomics
-  // (same-address ds_add_f32 lanes serialise; C = 8 would otherwise put all 64 lanes on one address)
-  const bool pow2 = vecs < 64 && (vecs & (vecs - 1)) == 0;
-  if (pow2) {
+  // Deterministic block reduction (no float atomics): threads lv, lv+vecs, ... share channels.  With
+  // vecs < 64 (power of two) a wave first reduces across its lanes and each wave owns one slot;
+  // otherwise every row group lr owns a slot.  Slots are summed in a fixed order.
+  const bool wred = vecs < 64 && (vecs & (vecs - 1)) == 0;
+  if (wred) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       sdz[e] = wave_sum_stride(sdz[e], vecs);
       s0[e] = wave_sum_stride(s0[e], vecs);
-      if (y1) s1[e] = wave_sum_stride(s1[e], vecs);
+      s1[e] = wave_sum_stride(s1[e], vecs);
     }
   }
-  if (lr < rpi && (!pow2 || (threadIdx.x & 63) < vecs)) {
+  const int nslots = wred ? NT / 64 : rpi;
+  const int slot = wred ? (int)(threadIdx.x >> 6) : lr;
+  if (lr < rpi && (!wred || (threadIdx.x & 63) < vecs)) {
+    float* o = red + slot * 3 * C;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      atomicAdd(&red[c + e], sdz[e]);
-      atomicAdd(&red[C + c + e], s0[e]);
-      if (y1) atomicAdd(&red[2 * C + c + e], s1[e]);
-    }
+    for (int e = 0; e < 8; ++e) { o[c + e] = sdz[e]; o[C + c + e] = s0[e]; o[2 * C + c + e] = s1[e]; }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < 3 * C; i += NT) part[(int64_t)blockIdx.x * 3 * C + i] = red[i];
+  for (int i = threadIdx.x; i < 3 * C; i += NT) {
+    float t = 0.f;
+    for (int k = 0; k < nslots; ++k) t += red[k * 3 * C + i];
+    part[(int64_t)blockIdx.x * 3 * C + i] = t;
+  }
 }
 
 // per channel: sums over blocks -> dgamma/dbeta (grad buffers, accumulate with beta_acc) + apply coeffs
@@ -510,7 +512,7 @@ void bn_bwd_reduce_launch(const uint16_t* g, int ldg, int mask_mode, const void*
                           const float* mh, const uint16_t* y0, const float* mean0, const float* rstd0,
                           const uint16_t* y1, const float* mean1, const float* rstd1, int64_t M, int C, int blocks,
                           int rows_per_block, float* part, hipStream_t s) {
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(blocks), dim3(NT), 3 * C * sizeof(float), s, g, ldg, mask_mode, mo,
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(blocks), dim3(NT), NT * 96, s, g, ldg, mask_mode, mo,
                      ldm, ms, mh, y0, mean0, rstd0, y1, mean1, rstd1, M, C, rows_per_block, part);
 }
 

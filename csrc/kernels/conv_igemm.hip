@@ -53,8 +53,12 @@ void conv_igemm_kernel(const ConvParams p) {
   using VT = typename std::conditional<CH == 8, uint4, uint2>::type;
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* red = reinterpret_cast<float*>(smem + MAIN_BYTES);            // [3][BN] stats
-  float* bnp = red + 3 * BN;                                             // EPI: [4][BN] mean0 rstd0 mean1 rstd1
+  // stats slots, one per wave row (EPI 0: [BM/WM][2][BN]) or per wave (EPI 1: [NW][3][BN]); summed in a fixed
+  // order, so the BN statistics are bitwise deterministic (no float atomics)
+  constexpr int NWAVES = (BM / WM) * NWN;
+  constexpr int RED_FLOATS = EPI ? NWAVES * 3 * BN : (BM / WM) * 2 * BN;
+  float* red = reinterpret_cast<float*>(smem + MAIN_BYTES);
+  float* bnp = red + RED_FLOATS;                                         // EPI: [4][BN] mean0 rstd0 mean1 rstd1
   float* aff = bnp + (EPI ? 4 * BN : 0);                                 // [2][Cg] affine
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -68,7 +72,6 @@ void conv_igemm_kernel(const ConvParams p) {
   const bool do_stats = !EPI && p.stats != nullptr;
   const bool do_bstats = EPI && p.epart != nullptr;
   const int affine = p.affine;
-  if (do_stats || do_bstats) for (int i = tid; i < 3 * BN; i += NT) red[i] = 0.f;
   if (do_bstats) {  // this tile's BN constants, read once here so the epilogue never waits on them
     for (int i = tid; i < BN; i += NT) {
       const int n = n0 + i;
@@ -391,12 +394,13 @@ void conv_igemm_kernel(const ConvParams p) {
         s0[e] = wave_sum_stride(s0[e], CPRW);
         s1[e] = wave_sum_stride(s1[e], CPRW);
       }
-      if (nok && lane < CPRW) {
+      if (lane < CPRW) {
+        float* slot = red + wid * 3 * BN;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          atomicAdd(&red[cg * 8 + e], sv[e]);
-          atomicAdd(&red[BN + cg * 8 + e], s0[e]);
-          atomicAdd(&red[2 * BN + cg * 8 + e], s1[e]);
+          slot[cg * 8 + e] = sv[e];
+          slot[BN + cg * 8 + e] = s0[e];
+          slot[2 * BN + cg * 8 + e] = s1[e];
         }
       }
       __syncthreads();
@@ -404,7 +408,12 @@ void conv_igemm_kernel(const ConvParams p) {
         const int nn = n0 + i;
         if (nn < p.Ngemm) {
 #pragma unroll
-          for (int k = 0; k < 3; ++k) p.epart[(tile_m * 3 + k) * p.Ngemm + nn] = red[k * BN + i];
+          for (int k = 0; k < 3; ++k) {
+            float t = 0.f;
+#pragma unroll
+            for (int w = 0; w < NWAVES; ++w) t += red[(w * 3 + k) * BN + i];
+            p.epart[(tile_m * 3 + k) * p.Ngemm + nn] = t;
+          }
         }
       }
     }
@@ -417,18 +426,21 @@ void conv_igemm_kernel(const ConvParams p) {
       for (int r = 0; r < 4; ++r) {
         const float s = sum16(cs[j][r]);
         const float q = sum16(cq[j][r]);
-        if (frow == 0) {
+        if (frow == 0) {  // (wm, column) slots are written by exactly one lane
           const int nl = wn * WN + j * 16 + 4 * fslot + r;
-          atomicAdd(&red[nl], s);
-          atomicAdd(&red[BN + nl], q);
+          red[wm * 2 * BN + nl] = s;
+          red[wm * 2 * BN + BN + nl] = q;
         }
       }
     __syncthreads();
     for (int i = tid; i < BN; i += NT) {
       const int n = n0 + i;
       if (n < p.Ngemm) {
-        p.stats[(tile_m * 2) * p.Ngemm + n] = red[i];
-        p.stats[(tile_m * 2 + 1) * p.Ngemm + n] = red[BN + i];
+        float s = 0.f, q = 0.f;
+#pragma unroll
+        for (int w = 0; w < BM / WM; ++w) { s += red[w * 2 * BN + i]; q += red[w * 2 * BN + BN + i]; }
+        p.stats[(tile_m * 2) * p.Ngemm + n] = s;
+        p.stats[(tile_m * 2 + 1) * p.Ngemm + n] = q;
       }
     }
   }
@@ -439,7 +451,9 @@ void launch_cfg(const ConvParams& p, hipStream_t stream) {
   constexpr int NT = (BM / WM) * (BN / WN) * 64;
   const int m_tiles = (p.M + BM - 1) / BM, n_tiles = (p.Ngemm + BN - 1) / BN;
   const bool epi = p.eres || p.emask || p.epart;
-  const size_t lds = main_lds_bytes(BM, BN, BK, epi ? 1 : 0) + (epi ? 7 : 3) * BN * 4 + (p.affine ? 2 * p.Cg * 4 : 0);
+  constexpr int NW = (BM / WM) * (BN / WN);
+  const size_t red_bytes = epi ? (NW * 3 + 4) * BN * 4 : (BM / WM) * 2 * BN * 4;
+  const size_t lds = main_lds_bytes(BM, BN, BK, epi ? 1 : 0) + red_bytes + (p.affine ? 2 * p.Cg * 4 : 0);
   if (epi) {
     if constexpr (CH == 8)
       hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 1>), dim3(m_tiles * n_tiles), dim3(NT), lds,

@@ -67,4 +67,5 @@ struct WgradParams {
   int To, Ho, Wo;
   int kt, kh, kw, st, sh, sw, pt, ph, pw;
   int splits, p_per_split;
+  int slab;                 // 1: deterministic mode — split s stores into partial + s*Cout*K (no atomics)
 };

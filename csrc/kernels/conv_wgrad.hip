@@ -253,8 +253,9 @@ void conv_wgrad_kernel(const WgradParams p) {
   // D[n][k]: lane holds k = col (lane&15), n = 4*(lane>>4) + r.  With one slab the tile is stored;
   // with several, slabs accumulate into one zero-initialised fp32 buffer with no-return
   // global_atomic_add_f32 (each wave-instruction = 4 rows x 64 contiguous bytes).
-  float* out = p.partial;
-  const bool atomic = p.splits > 1;
+  // deterministic (slab) mode: every split stores its own slab; the convert kernel sums them in order
+  float* out = p.partial + (p.slab ? (int64_t)blockIdx.z * p.Cout * p.K : 0);
+  const bool atomic = p.splits > 1 && !p.slab;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -282,7 +283,8 @@ void launch_w(const WgradParams& p, hipStream_t stream) {
 // dW accumulator [Cout][taps][Cin_pad] -> grad[Cout][Cin][taps] (PyTorch layout),
 // grad = beta * grad + scale * acc ; the accumulator is re-zeroed for the next layer (atomic mode).
 __global__ void wgrad_convert_kernel(float* __restrict__ accbuf, float* __restrict__ grad, int total,
-                                     int taps, int Cin, int Cin_real, float scale, float beta, int rezero) {
+                                     int taps, int Cin, int Cin_real, float scale, float beta, int rezero,
+                                     int slabs, int64_t slab_stride) {
   const int per_n = Cin_real * taps;
   for (int o = blockIdx.x * blockDim.x + threadIdx.x; o < total; o += gridDim.x * blockDim.x) {
     const int n = o / per_n;
@@ -290,7 +292,8 @@ __global__ void wgrad_convert_kernel(float* __restrict__ accbuf, float* __restri
     const int c = rem / taps;
     const int tap = rem - c * taps;
     const int a = (n * taps + tap) * Cin + c;
-    const float v = accbuf[a];
+    float v = accbuf[a];
+    for (int s = 1; s < slabs; ++s) v += accbuf[s * slab_stride + a];  // fixed order
     if (rezero) accbuf[a] = 0.f;
     grad[o] = (beta == 0.f ? 0.f : beta * grad[o]) + scale * v;
   }
@@ -335,10 +338,11 @@ void conv_wgrad_launch(const WgradParams& p, int chunk, hipStream_t stream) {
 }
 
 void wgrad_reduce_launch(float* accbuf, float* grad, int splits, int Cout, int taps, int Cin, int Cin_real,
-                         float scale, float beta, hipStream_t stream) {
+                         float scale, float beta, int slab, hipStream_t stream) {
+  // atomic mode: one accumulator, re-zeroed here; slab mode: `splits` slabs fully overwritten by the kernel
   const int total = Cout * taps * Cin_real;
   int blocks = std::min((total + 255) / 256, 4096);
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(wgrad_convert_kernel, dim3(blocks), dim3(256), 0, stream, accbuf, grad, total, taps, Cin,
-                     Cin_real, scale, beta, 1);
+                     Cin_real, scale, beta, slab ? 0 : 1, slab ? splits : 1, (int64_t)Cout * taps * Cin);
 }

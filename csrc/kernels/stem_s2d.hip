@@ -75,7 +75,7 @@ __global__ __launch_bounds__(256) void stem_fwd_kernel(const StemParams p) {
   constexpr int KSTEPS = TAPS * 16 / 32;  // 2 taps per MFMA k-step
   constexpr int SLOTS = KT + 1;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* red = reinterpret_cast<float*>(smem + SLOTS * FRAME_BYTES);  // [2][COT*16]
+  float* red = reinterpret_cast<float*>(smem + SLOTS * FRAME_BYTES);  // [4 waves][2][COT*16]
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
@@ -84,7 +84,6 @@ __global__ __launch_bounds__(256) void stem_fwd_kernel(const StemParams p) {
   const int th = b % p.tiles_h;
   const int n = b / p.tiles_h;
   const int ho0 = th * TH, wo0 = tw * TW;
-  for (int i = tid; i < 2 * COT * 16; i += 256) red[i] = 0.f;
 
   // weight fragments (A operand: lane holds W[co = 16*c + li][k = 32*ks + 8*g .. +8])
   bf16x8_t wa[COT][KSTEPS];
@@ -161,21 +160,25 @@ __global__ __launch_bounds__(256) void stem_fwd_kernel(const StemParams p) {
       __syncthreads();
     }
   }
-  // BN partial sums of this workgroup
+  // BN partial sums of this workgroup: one slot per wave, summed in wave order (deterministic)
+  constexpr int CT = COT * 16;
 #pragma unroll
   for (int c = 0; c < COT; ++c)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const float s = sum16(cs[c][r]), q = sum16(cq[c][r]);
       if (li == 0) {
-        atomicAdd(&red[16 * c + 4 * g + r], s);
-        atomicAdd(&red[COT * 16 + 16 * c + 4 * g + r], q);
+        red[w * 2 * CT + 16 * c + 4 * g + r] = s;
+        red[w * 2 * CT + CT + 16 * c + 4 * g + r] = q;
       }
     }
   __syncthreads();
   for (int i = tid; i < p.Cout; i += 256) {
-    p.stats[(int64_t)blockIdx.x * 2 * p.Cout + i] = red[i];
-    p.stats[(int64_t)blockIdx.x * 2 * p.Cout + p.Cout + i] = red[COT * 16 + i];
+    float s = 0.f, q = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { s += red[k * 2 * CT + i]; q += red[k * 2 * CT + CT + i]; }
+    p.stats[(int64_t)blockIdx.x * 2 * p.Cout + i] = s;
+    p.stats[(int64_t)blockIdx.x * 2 * p.Cout + p.Cout + i] = q;
   }
 }
 
@@ -320,7 +323,7 @@ __global__ void stem_pack_kernel(const float* __restrict__ w, uint16_t* __restri
 
 template <int KT, int COT>
 void launch_fwd(const StemParams& p, hipStream_t s) {
-  const size_t lds = (KT + 1) * FRAME_BYTES + 2 * COT * 16 * 4;
+  const size_t lds = (KT + 1) * FRAME_BYTES + 4 * 2 * COT * 16 * 4;
   hipLaunchKernelGGL((stem_fwd_kernel<KT, COT>), dim3(p.N * p.tiles_h * p.tiles_w), dim3(256), lds, s, p);
 }
 

@@ -20,7 +20,7 @@ void conv_igemm_set_bk(int bk);
 void conv_wgrad_launch(const WgradParams& p, int chunk, hipStream_t stream);
 void conv_wgrad_tile(int Cout, int K, int* bmw, int* bnw);
 void wgrad_reduce_launch(float* accbuf, float* grad, int splits, int Cout, int taps, int Cin, int Cin_real,
-                         float scale, float beta, hipStream_t stream);
+                         float scale, float beta, int slab, hipStream_t stream);
 void bn_finalize_launch(const float* part, int tiles, int C, int64_t count, const float* gamma, const float* beta,
                         float* rm, float* rv, int64_t* nbt, float momentum, float eps, float* smean, float* srstd,
                         float* scale, float* shift, hipStream_t s);
@@ -169,7 +169,7 @@ std::vector<int64_t> wgrad_tile(int64_t Cout, int64_t K) {
 
 // geometry: [P, Cout, K, Cin, ldd, ldx, Ti, Hi, Wi, To, Ho, Wo, kt, kh, kw, st, sh, sw, pt, ph, pw, splits, pps]
 void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& partial, const OptT& scale,
-                const OptT& shift, int64_t affine, std::vector<int64_t> g, int64_t chunk) {
+                const OptT& shift, int64_t affine, std::vector<int64_t> g, int64_t chunk, int64_t slab) {
   TORCH_CHECK(g.size() == 23, "wgrad geometry must have 23 entries");
   WgradParams p{};
   p.dy = bfp(dy); p.x = bfp(x); p.partial = f32(partial);
@@ -180,14 +180,16 @@ void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& par
   p.pt = g[18]; p.ph = g[19]; p.pw = g[20]; p.splits = g[21]; p.p_per_split = g[22];
   TORCH_CHECK(p.Cin % chunk == 0 && p.Cout % 8 == 0, "wgrad channel alignment");
   TORCH_CHECK(p.p_per_split % 32 == 0, "p_per_split must be a multiple of 32");
-  TORCH_CHECK(partial.numel() >= (int64_t)p.Cout * p.K, "wgrad accumulator too small");
+  p.slab = (int)slab;
+  TORCH_CHECK(partial.numel() >= (int64_t)p.Cout * p.K * (slab ? p.splits : 1), "wgrad accumulator too small");
   conv_wgrad_launch(p, (int)chunk, cur_stream());
 }
 
 void wgrad_reduce(const at::Tensor& partial, const at::Tensor& grad, int64_t splits, int64_t Cout, int64_t taps,
-                  int64_t Cin, int64_t Cin_real, double scale, double beta) {
+                  int64_t Cin, int64_t Cin_real, double scale, double beta, int64_t slab) {
+  TORCH_CHECK(!slab || partial.numel() >= splits * Cout * taps * Cin, "slab accumulator too small");
   wgrad_reduce_launch(f32(partial), f32(grad), (int)splits, (int)Cout, (int)taps, (int)Cin, (int)Cin_real,
-                      (float)scale, (float)beta, cur_stream());
+                      (float)scale, (float)beta, (int)slab, cur_stream());
 }
 
 void bn_finalize(const at::Tensor& part, int64_t tiles, int64_t C, int64_t count, const at::Tensor& gamma,
@@ -347,8 +349,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_m_tiles", &conv_m_tiles);
   m.def("conv_set_bk", [](int64_t bk) { conv_igemm_set_bk((int)bk); });
   m.def("wgrad_tile", &wgrad_tile);
-  m.def("conv_wgrad", &conv_wgrad);
-  m.def("wgrad_reduce", &wgrad_reduce);
+  m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("partial"), py::arg("scale"),
+        py::arg("shift"), py::arg("affine"), py::arg("g"), py::arg("chunk"), py::arg("slab") = 0);
+  m.def("wgrad_reduce", &wgrad_reduce, py::arg("partial"), py::arg("grad"), py::arg("splits"), py::arg("Cout"),
+        py::arg("taps"), py::arg("Cin"), py::arg("Cin_real"), py::arg("scale"), py::arg("beta"), py::arg("slab") = 0);
   m.def("bn_finalize", &bn_finalize);
   m.def("bn_eval_affine", &bn_eval_affine);
   m.def("bn_act", &bn_act);

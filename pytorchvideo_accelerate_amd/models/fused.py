@@ -161,16 +161,20 @@ class _ConvBN:
         sp = eng._splits.get(key)
         if sp is None:
             from ..ops.conv import wgrad_splits
-            sp = eng._splits[key] = wgrad_splits(dy.M, s.cout, K)
+            sp = eng._splits[key] = wgrad_splits(dy.M, s.cout, K, target_blocks=256 if eng.deterministic else 1024)
         splits, pps = sp
-        part = eng.scratch("wgrad_acc", s.cout * K, zero=True)
+        slab = 1 if eng.deterministic else 0
+        if slab:  # per-split slabs summed in a fixed order: bitwise reproducible weight gradients
+            part = eng.scratch("wgrad_slab", splits * s.cout * K)
+        else:     # fp32 atomics into one zeroed accumulator (kept zero by wgrad_reduce)
+            part = eng.scratch("wgrad_acc", s.cout * K, zero=True)
         aff = 0 if xf is None else (2 if xf.relu else 1)
         g = [dy.M, s.cout, K, s.cin_pad, dy.ld, x.ld, x.T, x.H, x.W, dy.T, dy.H, dy.W,
              *s.k, *s.stride, *s.pad, splits, pps]
         C.conv_wgrad(dy.t, x.t, part, None if xf is None else xf.scale, None if xf is None else xf.shift, aff, g,
-                     s.chunk)
+                     s.chunk, slab)
         C.wgrad_reduce(part, eng.flat.gview(self.conv.weight), splits, s.cout, s.taps, s.cin_pad, s.cin, 1.0,
-                       eng.grad_beta)
+                       eng.grad_beta, slab)
 
     def dgrad(self, dy: Act, in_dims, out: torch.Tensor, accum: bool, res: Optional[Act] = None,
               epi: Optional["_ResBlock"] = None):
@@ -486,9 +490,12 @@ class _Fuse:
 class FusedNet:
     """Executor bound to a reference ``Net`` (SlowFast or Slow ResNet3D) whose parameters it shares."""
 
-    def __init__(self, model: R.Net, device: torch.device, stem_s2d: bool = True):
+    def __init__(self, model: R.Net, device: torch.device, stem_s2d: bool = True, deterministic: bool = False):
+        """``deterministic``: bitwise-reproducible gradients (slab wgrad reduction, generic stems; BN
+        statistics are always reduced in a fixed order).  Costs a little speed."""
         self.C = require()
-        self.stem_s2d = stem_s2d
+        self.deterministic = deterministic
+        self.stem_s2d = stem_s2d and not deterministic
         self.model = model
         self.device = torch.device(device)
         model.to(self.device)
