@@ -53,6 +53,7 @@ class Accelerator:
                  logging_dir: str = ".", kernels: str = "auto", bucket_mb: float = 32.0):
         if mixed_precision is None:
             mixed_precision = os.environ.get("ACCELERATE_MIXED_PRECISION", "no")
+        cpu = cpu or os.environ.get("ACCELERATE_USE_CPU", "").lower() in ("1", "true", "yes")
         self.mixed_precision = mixed_precision
         self.state = DistState.from_env(cpu=cpu)
         self.device = self.state.device

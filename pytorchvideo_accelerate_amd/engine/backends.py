@@ -39,6 +39,7 @@ class TorchBackend:
         self.mp = mixed_precision
         self.amp_dtype = {"bf16": torch.bfloat16, "fp16": torch.float16}.get(mixed_precision)
         self.scaler = None
+        self.timer = None
         if mixed_precision == "fp16" and self.device.type == "cuda":
             self.scaler = torch.amp.GradScaler("cuda")
 
@@ -73,7 +74,8 @@ class TorchBackend:
         scaled.backward()
         self.flat.rebind()
         self.sync.begin(sync)
-        self.sync.finish()
+        with (self.timer.phase("comm") if self.timer else contextlib.nullcontext()):
+            self.sync.finish()
         return loss.detach(), out.detach().float()
 
     @torch.no_grad()
@@ -100,6 +102,7 @@ class FusedBackend:
         self.net.grad_hook = self.sync.progress
         self.scaler = None
         self._training = True
+        self.timer = None   # utils.profiling.StepTimer (optional)
 
     def train(self):
         self._training = True
@@ -110,9 +113,12 @@ class FusedBackend:
         self.model.eval()
 
     def train_step(self, video, labels, loss_scale: float = 1.0, sync: bool = True):
-        self.sync.begin(sync)
-        loss, logits = self.net.forward_backward(video, labels.to(self.device), loss_scale)
-        self.sync.finish()
+        t = self.timer
+        with (t.phase("fwd_bwd") if t else contextlib.nullcontext()):
+            self.sync.begin(sync)
+            loss, logits = self.net.forward_backward(video, labels.to(self.device), loss_scale)
+        with (t.phase("comm") if t else contextlib.nullcontext()):
+            self.sync.finish()
         return loss, logits
 
     @torch.no_grad()

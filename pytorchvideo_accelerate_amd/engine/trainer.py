@@ -33,7 +33,27 @@ import torch
 from ..data.kinetics import LabeledVideoPaths, SyntheticVideoPaths, VideoClipDataset
 from ..models import reference as R
 from ..utils.misc import set_seed
+from ..utils.metrics import Accuracy
+from ..utils.profiling import StepTimer
 from .accelerator import Accelerator
+
+
+class InjectedFault(RuntimeError):
+    """Raised by ``PVA_FAULT_AT_STEP`` (fault-injection test hook for elastic restarts)."""
+
+
+def _maybe_inject_fault(global_step: int, output_dir: str):
+    """``PVA_FAULT_AT_STEP=N``: fail once when global step N completes (a marker file in ``output_dir``
+    makes the restarted run pass through)."""
+    at = os.environ.get("PVA_FAULT_AT_STEP")
+    if not at or global_step != int(at):
+        return
+    marker = os.path.join(output_dir or ".", f".fault_injected_{os.environ.get('RANK', '0')}")
+    if os.path.exists(marker):
+        return
+    os.makedirs(os.path.dirname(marker), exist_ok=True)
+    open(marker, "w").close()
+    raise InjectedFault(f"injected fault at global step {global_step}")
 
 
 def parse_checkpointing_steps(v):
@@ -157,6 +177,10 @@ def training_function(args: Namespace) -> dict:
     starting_epoch = 0
     resume_step = None
     resume = args.resume_from_checkpoint
+    if not resume and os.environ.get("PVA_AUTO_RESUME") == "1":
+        # elastic restart (launch.py --auto_resume): continue from the newest checkpoint if there is one
+        from ..ckpt.state import latest_checkpoint
+        resume = latest_checkpoint(args.output_dir or ".") or None
     if resume:
         if resume == "latest":
             from ..ckpt.state import latest_checkpoint
@@ -181,7 +205,10 @@ def training_function(args: Namespace) -> dict:
         acc.init_trackers(run, vars(args))
 
     gas = args.gradient_accumulation_steps
-    history = {"train_loss_epoch": [], "accuracy": [], "clips_per_sec": []}
+    history = {"train_loss_epoch": [], "accuracy": [], "clips_per_sec": [], "perf": []}
+    timer = StepTimer(acc.device)
+    backend.timer = timer
+    val_metric = Accuracy(acc.device, acc.state)
     output_dir = None
     show = acc.is_main_process and not getattr(args, "quiet", False)
     for epoch in range(starting_epoch, args.num_epochs):
@@ -193,21 +220,32 @@ def training_function(args: Namespace) -> dict:
         if skip:
             # skip without decoding: drop the first `skip` batches of the epoch plan
             train_ds.items = train_ds.items[skip * args.batch_size:]
-        for i, batch in enumerate(train_loader):
+        it = iter(train_loader)
+        i = -1
+        while True:
+            timer.begin_step()
+            with timer.host("data"):
+                batch = next(it, None)
+            if batch is None:
+                timer._cur = None
+                break
+            i += 1
             step = i + skip
             boundary = step % gas == 0
             loss, _ = backend.train_step(batch["video"], batch["label"], 1.0 / gas, sync=boundary)
             if boundary:
-                sc = getattr(backend, "scaler", None)
-                if sc is not None:
-                    scale0 = sc.get_scale()
-                    sc.step(optimizer)
-                    sc.update()
-                    optimizer.step_was_skipped = sc.get_scale() < scale0
-                else:
-                    optimizer.step()
-                scheduler.step()
-                optimizer.zero_grad()
+                with timer.phase("opt"):
+                    sc = getattr(backend, "scaler", None)
+                    if sc is not None:
+                        scale0 = sc.get_scale()
+                        sc.step(optimizer)
+                        sc.update()
+                        optimizer.step_was_skipped = sc.get_scale() < scale0
+                    else:
+                        optimizer.step()
+                    scheduler.step()
+                    optimizer.zero_grad()
+            timer.end_step(batch["label"].shape[0] * acc.num_processes)
             global_step += 1
             acc.step = global_step
             clips += batch["label"].shape[0] * acc.num_processes
@@ -215,7 +253,9 @@ def training_function(args: Namespace) -> dict:
             if args.with_tracking:
                 total_loss += step_loss
                 if (step + 1) % args.log_every == 0:
-                    acc.log({"train_loss_step": step_loss.item(), "lr": optimizer.param_groups[0]["lr"]},
+                    perf = timer.summary()
+                    history["perf"].append(perf)
+                    acc.log({"train_loss_step": step_loss.item(), "lr": optimizer.param_groups[0]["lr"], **perf},
                             step=global_step)
             if show and (step + 1) % max(args.log_every, 1) == 0:
                 print(f"epoch {epoch} step {step + 1}/{steps_per_epoch} loss {step_loss.item():.4f} "
@@ -224,6 +264,7 @@ def training_function(args: Namespace) -> dict:
                 output_dir = os.path.join(args.output_dir or ".", f"step_{global_step}")
                 acc.save_state(output_dir)
                 acc.print(f"Saving checkpoint to {output_dir}")
+            _maybe_inject_fault(global_step, args.output_dir)
             if step == args.limit_train_batches:
                 break
         if acc.device.type == "cuda":
@@ -236,18 +277,13 @@ def training_function(args: Namespace) -> dict:
         # ---------------- evaluation
         acc.sync_buffers()
         backend.eval()
-        correct = torch.zeros((), device=acc.device, dtype=torch.long)
-        total = torch.zeros((), device=acc.device, dtype=torch.long)
+        val_metric.reset()
         for step, batch in enumerate(val_loader):
             logits = backend.eval_step(batch["video"])
-            labels = batch["label"].to(acc.device)
-            correct += (logits.argmax(-1) == labels).sum()
-            total += labels.numel()
+            val_metric.update(logits, batch["label"])
             if step == args.limit_val_batches:
                 break
-        acc.reduce(correct, "sum")
-        acc.reduce(total, "sum")
-        val_acc = (correct.float() / total.clamp_min(1).float()).item()
+        val_acc = val_metric.compute().item()
         history["accuracy"].append(val_acc)
         tl = (total_loss / max(steps_per_epoch, 1)).item() if args.with_tracking else float("nan")
         history["train_loss_epoch"].append(tl)

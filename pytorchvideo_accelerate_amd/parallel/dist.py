@@ -57,8 +57,15 @@ class DistState:
                 kw = {}
                 if use_gpu:
                     kw["device_id"] = st.device
-                dist.init_process_group(st.backend, rank=rank, world_size=ws,
-                                        timeout=datetime.timedelta(seconds=timeout_s), **kw)
+                timeout = datetime.timedelta(seconds=timeout_s)
+                if os.environ.get("TORCHELASTIC_USE_AGENT_STORE") == "True":
+                    # under the torchrun agent: join its TCPStore with a per-attempt prefix so an elastic
+                    # restart never reads the previous attempt's connection keys (stale gloo/RCCL peers)
+                    base = dist.TCPStore(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]), ws, False,
+                                         timeout=timeout)
+                    attempt = os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")
+                    kw["store"] = dist.PrefixStore(f"pva/attempt_{attempt}/", base)
+                dist.init_process_group(st.backend, rank=rank, world_size=ws, timeout=timeout, **kw)
         return st
 
     # -------------------------------------------------------------- collectives

@@ -4,6 +4,7 @@ Same flags and defaults as the reference ``run.py`` (``main`` kwargs, Fire seman
 additions.  Launch like the reference:
 
     python run.py --is_slowfast --num_frames 32 --sampling_rate 2 --mixed_precision bf16 ...
+    python -m pytorchvideo_accelerate_amd.launch --multi_gpu --num_processes 8 run.py ...   # or
     accelerate launch --multi_gpu --num_processes 8 run.py ...      # or
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 run.py ...
 """
@@ -62,6 +63,8 @@ def main(
       kernels            auto | fused | torch  (fused = gfx950 HIP kernels, bf16)
       reference_val      evaluate only one clip per video (reference LimitDataset behaviour)
       pretrained_path    local weights for --pretrained (no network)
+    As in the reference, the script flag decides mixed precision (default "no"): the launcher's
+    --mixed_precision only reaches programmatic Accelerator(mixed_precision=None) users.
     """
     args = Namespace(**{k: v for k, v in locals().items()})
     return training_function(args)

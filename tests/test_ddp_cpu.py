@@ -57,6 +57,15 @@ def test_gradsync_equals_big_batch(tmp_path):
     assert res["params_equal"] and res["avg"] == 1.5 and res["gather"] == [0, 1]
 
 
+def test_gradsync_stress_random_timing(tmp_path):
+    """3 ranks, random chunked backward with random delays / stale progress reports, no_sync accumulation,
+    restricted span: the all-reduced gradients are exact (float64 payload)."""
+    out = str(tmp_path / "stress.json")
+    _launch([os.path.join(HERE, "scripts", "comm_stress_worker.py"), out], nproc=3)
+    res = json.load(open(out))
+    assert res["max_err"] == 0.0 and res["ok_span"] and res["buckets"] >= 10
+
+
 @pytest.mark.slow
 def test_run_py_two_ranks_cpu(tmp_path):
     args = [os.path.join(REPO, "run.py"), "--cpu", "--synthetic", "--synthetic_videos", "8", "--synthetic_classes",
