@@ -38,6 +38,29 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
   return make_uint4(pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7]));
 }
 
+typedef __attribute__((ext_vector_type(2))) float f32x2_t;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+typedef __attribute__((ext_vector_type(2))) short s16x2_t;
+
+// 2 x f32 -> packed bf16 pair in ONE v_cvt_pk_bf16_f32 (RNE, NaN-preserving)
+__device__ __forceinline__ uint32_t cvt_pk_bf16(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){a, b}, bf16x2_t));
+}
+
+__device__ __forceinline__ uint4 pack8_fast(const float* f) {
+  return make_uint4(cvt_pk_bf16(f[0], f[1]), cvt_pk_bf16(f[2], f[3]), cvt_pk_bf16(f[4], f[5]), cvt_pk_bf16(f[6], f[7]));
+}
+
+// ReLU on packed bf16: bf16 is sign-magnitude, so max as signed int16 against 0 zeroes every negative
+// (and -0) lane and keeps positives: one v_pk_max_i16 per pair.
+__device__ __forceinline__ uint32_t relu_bf16x2(uint32_t w) {
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(s16x2_t, w), (s16x2_t){0, 0}));
+}
+
+__device__ __forceinline__ uint4 relu_bf16x8(const uint4& v) {
+  return make_uint4(relu_bf16x2(v.x), relu_bf16x2(v.y), relu_bf16x2(v.z), relu_bf16x2(v.w));
+}
+
 __device__ __forceinline__ void unpack4(const uint2& v, float* f) {
   f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
   f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);

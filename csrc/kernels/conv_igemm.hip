@@ -36,7 +36,7 @@ __device__ __forceinline__ int lds_off(int row, int slot) {
   else return row * 128 + ((slot ^ (row & 6)) << 4);
 }
 
-template <int BM, int BN, int WM, int WN, int CH, int BK, int EPI>
+template <int BM, int BN, int WM, int WN, int CH, int BK, int EPI, int UT>
 __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64)
 void conv_igemm_kernel(const ConvParams p) {
   constexpr int NWN = BN / WN;
@@ -56,10 +56,10 @@ void conv_igemm_kernel(const ConvParams p) {
   // stats slots, one per wave row (EPI 0: [BM/WM][2][BN]) or per wave (EPI 1: [NW][3][BN]); summed in a fixed
   // order, so the BN statistics are bitwise deterministic (no float atomics)
   constexpr int NWAVES = (BM / WM) * NWN;
-  constexpr int RED_FLOATS = EPI ? NWAVES * 3 * BN : (BM / WM) * 2 * BN;
+  constexpr int RED_FLOATS = EPI == 1 ? NWAVES * 3 * BN : (BM / WM) * 2 * BN;
   float* red = reinterpret_cast<float*>(smem + MAIN_BYTES);
   float* bnp = red + RED_FLOATS;                                         // EPI: [4][BN] mean0 rstd0 mean1 rstd1
-  float* aff = bnp + (EPI ? 4 * BN : 0);                                 // [2][Cg] affine
+  float* aff = bnp + (EPI == 1 ? 4 * BN : 0);                            // [2][Cg] affine
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / NWN, wn = wid % NWN;
@@ -69,8 +69,8 @@ void conv_igemm_kernel(const ConvParams p) {
   const int tile_m = t / n_tiles, tile_n = t % n_tiles;
   const int m0 = tile_m * BM, n0 = tile_n * BN;
 
-  const bool do_stats = !EPI && p.stats != nullptr;
-  const bool do_bstats = EPI && p.epart != nullptr;
+  const bool do_stats = EPI == 0 && p.stats != nullptr;
+  const bool do_bstats = EPI == 1 && p.epart != nullptr;
   const int affine = p.affine;
   if (do_bstats) {  // this tile's BN constants, read once here so the epilogue never waits on them
     for (int i = tid; i < BN; i += NT) {
@@ -86,136 +86,12 @@ void conv_igemm_kernel(const ConvParams p) {
     for (int i = tid; i < p.Cg; i += NT) { aff[i] = p.in_scale[i]; aff[p.Cg + i] = p.in_shift[i]; }
   }
 
-  // ---- per-slot row coordinates (fixed over the K loop) ----
-  // Everything loop-invariant is precomputed here so the k-loop issues ~1 VALU op per global load:
-  // a chunk's element offset = a_off[s] (row origin) + tap_lin (thread-uniform per k-step) + kc.
-  const int col = tid % CPR;
   const int RHW = p.Rh * p.Rw, RTHW = p.Rt * RHW;
-  const int GHW = p.Gh * p.Gw, GTHW = p.Gt * GHW;
-  const bool check = p.check != 0;   // host: false when every gathered coordinate is in range
-  int a_off[A_SLOTS], a_t[A_SLOTS], a_h[A_SLOTS], a_w[A_SLOTS], sa[A_SLOTS];
-  unsigned rowok = 0;
-#pragma unroll
-  for (int s = 0; s < A_SLOTS; ++s) {
-    const int idx = tid + s * NT;
-    const int row = idx / CPR;
-    const int m = m0 + row;
-    a_off[s] = 0; a_t[s] = 0; a_h[s] = 0; a_w[s] = 0;
-    if (idx < A_CHUNKS && m < p.M) {
-      const int b = m / RTHW;
-      int r = m - b * RTHW;
-      const int qt = r / RHW; r -= qt * RHW;
-      const int qh = r / p.Rw; const int qw = r - qh * p.Rw;
-      a_t[s] = qt * p.ast + p.aot; a_h[s] = qh * p.ash + p.aoh; a_w[s] = qw * p.asw + p.aow;
-      a_off[s] = (b * GTHW + (a_t[s] * p.Gh + a_h[s]) * p.Gw + a_w[s]) * p.ldx;
-      rowok |= 1u << s;
-    }
-    if constexpr (CH == 8) sa[s] = lds_off<BK>(row, col);
-    else sa[s] = lds_off<BK>(row, col >> 1) + (col & 1) * 8;
-  }
-  int b_off[B_SLOTS], sb[B_SLOTS];
-  unsigned nok = 0;
-#pragma unroll
-  for (int s = 0; s < B_SLOTS; ++s) {
-    const int idx = tid + s * NT;
-    const int row = idx / CPR;
-    const int n = n0 + row;
-    b_off[s] = n * p.Kfull;
-    if (idx < B_CHUNKS && n < p.Ngemm) nok |= 1u << s;
-    if constexpr (CH == 8) sb[s] = lds_off<BK>(row, col);
-    else sb[s] = lds_off<BK>(row, col >> 1) + (col & 1) * 8;
-  }
-
-  // ---- k-state of this thread's column: (channel offset, tap), with derived gather/weight offsets ----
-  int kc = col * CH, kdt = 0, kdh = 0, kdw = 0;
-  int tap_lin = 0, tap_w = 0;
-  auto retap = [&]() {
-    tap_lin = p.dir * ((kdt * p.Gh + kdh) * p.Gw + kdw) * p.ldx;
-    tap_w = (((p.bt0 + kdt * p.bts) * p.kh + (p.bh0 + kdh * p.bhs)) * p.kw + (p.bw0 + kdw * p.bws)) * p.Cg;
-  };
-  auto kadvance = [&](int by) {
-    kc += by;
-    if (kc >= p.Cg) {
-      do {
-        kc -= p.Cg;
-        if (++kdw == p.nw) { kdw = 0; if (++kdh == p.nh) { kdh = 0; ++kdt; } }
-      } while (kc >= p.Cg);
-      retap();
-    }
-  };
-  retap();
-  kadvance(0);
-
-  VT ra[A_SLOTS], rb[B_SLOTS];
-  int ra_c = 0;            // channel offset of the staged A chunks
-  unsigned ra_valid = 0;   // bit s: slot s loaded real data
-
-  auto load = [&]() {
-    const bool tap_ok = kdt < p.nt;
-    ra_c = kc; ra_valid = 0;
-    const int dgt = p.dir * kdt, dgh = p.dir * kdh, dgw = p.dir * kdw;
-#pragma unroll
-    for (int s = 0; s < A_SLOTS; ++s) {
-      bool v = tap_ok && (rowok >> s & 1);
-      if (check)
-        v = v && (unsigned)(a_t[s] + dgt) < (unsigned)p.Gt && (unsigned)(a_h[s] + dgh) < (unsigned)p.Gh &&
-            (unsigned)(a_w[s] + dgw) < (unsigned)p.Gw;
-      if (v) {
-        ra[s] = *reinterpret_cast<const VT*>(p.x + (a_off[s] + tap_lin + kc));
-        ra_valid |= 1u << s;
-      } else {
-        ra[s] = VT{};
-      }
-    }
-    const int boff = tap_w + kc;
-#pragma unroll
-    for (int s = 0; s < B_SLOTS; ++s) {
-      if (tap_ok && (nok >> s & 1))
-        rb[s] = *reinterpret_cast<const VT*>(p.w + (b_off[s] + boff));
-      else
-        rb[s] = VT{};
-    }
-    kadvance(BK);
-  };
-
-  auto store_lds = [&](int buf) {
-    char* A = smem + buf * TILE_BYTES;
-    char* B = A + BM * BK * 2;
-#pragma unroll
-    for (int s = 0; s < A_SLOTS; ++s) {
-      if (tid + s * NT >= A_CHUNKS) break;
-      VT v = ra[s];
-      if (affine && (ra_valid >> s & 1)) {
-        float f[CH];
-        if constexpr (CH == 8) unpack8(v, f); else unpack4(v, f);
-#pragma unroll
-        for (int e = 0; e < CH; ++e) {
-          float z = f[e] * aff[ra_c + e] + aff[p.Cg + ra_c + e];
-          f[e] = (affine == 2) ? fmaxf(z, 0.f) : z;
-        }
-        if constexpr (CH == 8) v = pack8(f); else v = pack4(f);
-      }
-      *reinterpret_cast<VT*>(A + sa[s]) = v;
-    }
-#pragma unroll
-    for (int s = 0; s < B_SLOTS; ++s) {
-      if (tid + s * NT >= B_CHUNKS) break;
-      *reinterpret_cast<VT*>(B + sb[s]) = rb[s];
-    }
-  };
-
   f32x4_t acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-  const int nsteps = (p.nt * p.nh * p.nw * p.Cg + BK - 1) / BK;
-  __syncthreads();  // affine table ready
-  load();
-  store_lds(0);
-  __syncthreads();
-
   const int frow = lane & 15, fslot = lane >> 4;
   int fa[BK / 32][TM], fb[BK / 32][TN];
 #pragma unroll
@@ -225,26 +101,303 @@ void conv_igemm_kernel(const ConvParams p) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) fb[kk][j] = BM * BK * 2 + lds_off<BK>(wn * WN + j * 16 + frow, fslot + 4 * kk);
   }
-  for (int step = 0; step < nsteps; ++step) {
-    const int cur = step & 1;
-    const bool has_next = step + 1 < nsteps;
-    if (has_next) load();
-    const char* A = smem + cur * TILE_BYTES;
+
+  if constexpr (UT) {
+    // ================= uniform-tap loader (Cg % BK == 0, CH == 8) =================
+    // Every k-step of the block lies inside one tap, so the tap / channel cursor is wave-uniform (SGPRs).
+    // Raw buffer loads: weights = per-slot VGPR row offset + SGPR (tap, channel) offset -> no VALU;
+    // activations without reachable padding likewise; with padding, a per-slot valid-tap bitmask (built
+    // once) picks the row offset or an out-of-range offset (the buffer unit returns zeros).
+    static_assert(CH == 8, "uniform-tap loader stages 16-B chunks");
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, (int)p.xbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, (int)p.wbytes, 0x00020000);
+    constexpr unsigned OOB = 0xFFFFFFF0u;
+    const int col = tid % CPR;
+    const bool check = p.check != 0;
+    const int GHW = p.Gh * p.Gw, GTHW = p.Gt * GHW;
+    // most negative tap offset (dgrad walks taps backwards): the no-check form adds taps as a >= 0 soffset
+    const int tmin = p.dir < 0 ? -(((p.nt - 1) * p.Gh + (p.nh - 1)) * p.Gw + (p.nw - 1)) * p.ldx : 0;
+    int a_vo[A_SLOTS], sa[A_SLOTS];
+    unsigned tmask[A_SLOTS];
 #pragma unroll
-    for (int kk = 0; kk < BK / 32; ++kk) {
-      bf16x8_t af[TM], bfr[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8_t*>(A + fa[kk][i]);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const bf16x8_t*>(A + fb[kk][j]);
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+    for (int s = 0; s < A_SLOTS; ++s) {
+      const int idx = tid + s * NT;
+      const int row = idx / CPR;
+      const int m = m0 + row;
+      const bool rv = idx < A_CHUNKS && m < p.M;
+      int at = 0, ah = 0, aw = 0, off = 0;
+      if (rv) {
+        const int b = m / RTHW;
+        int r = m - b * RTHW;
+        const int qt = r / RHW; r -= qt * RHW;
+        const int qh = r / p.Rw; const int qw = r - qh * p.Rw;
+        at = qt * p.ast + p.aot; ah = qh * p.ash + p.aoh; aw = qw * p.asw + p.aow;
+        off = (b * GTHW + (at * p.Gh + ah) * p.Gw + aw) * p.ldx + col * 8;
+      }
+      unsigned msk = 0;
+      if (check && rv) {
+        int t = 0;
+        for (int jt = 0; jt < p.nt; ++jt)
+          for (int jh = 0; jh < p.nh; ++jh)
+            for (int jw = 0; jw < p.nw; ++jw, ++t)
+              if ((unsigned)(at + p.dir * jt) < (unsigned)p.Gt && (unsigned)(ah + p.dir * jh) < (unsigned)p.Gh &&
+                  (unsigned)(aw + p.dir * jw) < (unsigned)p.Gw)
+                msk |= 1u << t;
+      }
+      tmask[s] = msk;
+      // no-check: rows past M read a real (ignored) address — never rely on range checks there
+      a_vo[s] = check ? off * 2 : (rv ? (off + tmin) * 2 : 0);
+      sa[s] = lds_off<BK>(row, col);
     }
-    if (has_next) store_lds(cur ^ 1);
+    int b_vo[B_SLOTS], sb[B_SLOTS];
+#pragma unroll
+    for (int s = 0; s < B_SLOTS; ++s) {
+      const int idx = tid + s * NT;
+      const int row = idx / CPR;
+      const int n = n0 + row;
+      b_vo[s] = (idx < B_CHUNKS && n < p.Ngemm) ? (n * p.Kfull + col * 8) * 2 : 0;  // columns >= N: ignored
+      sb[s] = lds_off<BK>(row, col);
+    }
+    // uniform k cursor
+    int kt_ = 0, kh_ = 0, kw_ = 0, t_ = 0, kb = 0, tapA = 0, tapW = 0;
+    auto retap = [&]() {
+      tapA = p.dir * ((kt_ * p.Gh + kh_) * p.Gw + kw_) * p.ldx;
+      tapW = (((p.bt0 + kt_ * p.bts) * p.kh + (p.bh0 + kh_ * p.bhs)) * p.kw + (p.bw0 + kw_ * p.bws)) * p.Cg;
+    };
+    retap();
+    uint4 ra[A_SLOTS], rb[B_SLOTS];
+    int ra_c = 0;
+    unsigned ra_valid = 0;
+    auto load = [&]() {
+      const int ta = tapA + kb;
+      ra_c = kb;
+      ra_valid = 0;
+#pragma unroll
+      for (int s = 0; s < A_SLOTS; ++s) {
+        if (check) {
+          const bool v = (tmask[s] >> t_) & 1u;
+          ra[s] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, v ? a_vo[s] + ta * 2 : (int)OOB, 0, 0));
+          ra_valid |= (unsigned)v << s;
+        } else {
+          ra[s] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, a_vo[s], (ta - tmin) * 2, 0));
+        }
+      }
+      const int wso = (tapW + kb) * 2;
+#pragma unroll
+      for (int s = 0; s < B_SLOTS; ++s)
+        rb[s] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wr, b_vo[s], wso, 0));
+      kb += BK;
+      if (kb == p.Cg) {
+        kb = 0;
+        ++t_;
+        if (++kw_ == p.nw) { kw_ = 0; if (++kh_ == p.nh) { kh_ = 0; ++kt_; } }
+        retap();
+      }
+    };
+    auto store_lds = [&](int buf) {
+      char* A = smem + buf * TILE_BYTES;
+      char* B = A + BM * BK * 2;
+#pragma unroll
+      for (int s = 0; s < A_SLOTS; ++s) {
+        if (tid + s * NT >= A_CHUNKS) break;
+        uint4 v = ra[s];
+        if (affine) {
+          // packed consumer-side BN(+ReLU): 8 unpacks, 8 FMAs, 4 cvt_pk_bf16_f32, 4 v_pk_max_i16
+          const float* sc = aff + ra_c + col * 8;
+          const f32x4_t s0 = *reinterpret_cast<const f32x4_t*>(sc), s1 = *reinterpret_cast<const f32x4_t*>(sc + 4);
+          const f32x4_t h0 = *reinterpret_cast<const f32x4_t*>(sc + p.Cg);
+          const f32x4_t h1 = *reinterpret_cast<const f32x4_t*>(sc + p.Cg + 4);
+          float f[8];
+          unpack8(v, f);
+          const float sc8[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
+          const float sh8[8] = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+#pragma unroll
+          for (int e = 0; e < 8; ++e) f[e] = __builtin_fmaf(f[e], sc8[e], sh8[e]);
+          v = pack8_fast(f);
+          if (affine == 2) v = relu_bf16x8(v);
+          if (check && !((ra_valid >> s) & 1u)) v = uint4{0, 0, 0, 0};  // zero padding of the activation
+        }
+        *reinterpret_cast<uint4*>(A + sa[s]) = v;
+      }
+#pragma unroll
+      for (int s = 0; s < B_SLOTS; ++s) {
+        if (tid + s * NT >= B_CHUNKS) break;
+        *reinterpret_cast<uint4*>(B + sb[s]) = rb[s];
+      }
+    };
+    const int nsteps = (p.nt * p.nh * p.nw * p.Cg) / BK;
+    __syncthreads();  // affine table ready
+    load();
+    store_lds(0);
     __syncthreads();
+    for (int step = 0; step < nsteps; ++step) {
+      const int cur = step & 1;
+      const bool has_next = step + 1 < nsteps;
+      if (has_next) load();
+      const char* A = smem + cur * TILE_BYTES;
+#pragma unroll
+      for (int kk = 0; kk < BK / 32; ++kk) {
+        bf16x8_t af[TM], bfr[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8_t*>(A + fa[kk][i]);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const bf16x8_t*>(A + fb[kk][j]);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+      }
+      if (has_next) store_lds(cur ^ 1);
+      __syncthreads();
+    }
+  } else {
+  // ---- per-slot row coordinates (fixed over the K loop) ----
+    // Everything loop-invariant is precomputed here so the k-loop issues ~1 VALU op per global load:
+    // a chunk's element offset = a_off[s] (row origin) + tap_lin (thread-uniform per k-step) + kc.
+    const int col = tid % CPR;
+    const int GHW = p.Gh * p.Gw, GTHW = p.Gt * GHW;
+    const bool check = p.check != 0;   // host: false when every gathered coordinate is in range
+    int a_off[A_SLOTS], a_t[A_SLOTS], a_h[A_SLOTS], a_w[A_SLOTS], sa[A_SLOTS];
+    unsigned rowok = 0;
+  #pragma unroll
+    for (int s = 0; s < A_SLOTS; ++s) {
+      const int idx = tid + s * NT;
+      const int row = idx / CPR;
+      const int m = m0 + row;
+      a_off[s] = 0; a_t[s] = 0; a_h[s] = 0; a_w[s] = 0;
+      if (idx < A_CHUNKS && m < p.M) {
+        const int b = m / RTHW;
+        int r = m - b * RTHW;
+        const int qt = r / RHW; r -= qt * RHW;
+        const int qh = r / p.Rw; const int qw = r - qh * p.Rw;
+        a_t[s] = qt * p.ast + p.aot; a_h[s] = qh * p.ash + p.aoh; a_w[s] = qw * p.asw + p.aow;
+        a_off[s] = (b * GTHW + (a_t[s] * p.Gh + a_h[s]) * p.Gw + a_w[s]) * p.ldx;
+        rowok |= 1u << s;
+      }
+      if constexpr (CH == 8) sa[s] = lds_off<BK>(row, col);
+      else sa[s] = lds_off<BK>(row, col >> 1) + (col & 1) * 8;
+    }
+    int b_off[B_SLOTS], sb[B_SLOTS];
+    unsigned nok = 0;
+  #pragma unroll
+    for (int s = 0; s < B_SLOTS; ++s) {
+      const int idx = tid + s * NT;
+      const int row = idx / CPR;
+      const int n = n0 + row;
+      b_off[s] = n * p.Kfull;
+      if (idx < B_CHUNKS && n < p.Ngemm) nok |= 1u << s;
+      if constexpr (CH == 8) sb[s] = lds_off<BK>(row, col);
+      else sb[s] = lds_off<BK>(row, col >> 1) + (col & 1) * 8;
+    }
+  
+    // ---- k-state of this thread's column: (channel offset, tap), with derived gather/weight offsets ----
+    int kc = col * CH, kdt = 0, kdh = 0, kdw = 0;
+    int tap_lin = 0, tap_w = 0;
+    auto retap = [&]() {
+      tap_lin = p.dir * ((kdt * p.Gh + kdh) * p.Gw + kdw) * p.ldx;
+      tap_w = (((p.bt0 + kdt * p.bts) * p.kh + (p.bh0 + kdh * p.bhs)) * p.kw + (p.bw0 + kdw * p.bws)) * p.Cg;
+    };
+    auto kadvance = [&](int by) {
+      kc += by;
+      if (kc >= p.Cg) {
+        do {
+          kc -= p.Cg;
+          if (++kdw == p.nw) { kdw = 0; if (++kdh == p.nh) { kdh = 0; ++kdt; } }
+        } while (kc >= p.Cg);
+        retap();
+      }
+    };
+    retap();
+    kadvance(0);
+  
+    VT ra[A_SLOTS], rb[B_SLOTS];
+    int ra_c = 0;            // channel offset of the staged A chunks
+    unsigned ra_valid = 0;   // bit s: slot s loaded real data
+  
+    auto load = [&]() {
+      const bool tap_ok = kdt < p.nt;
+      ra_c = kc; ra_valid = 0;
+      const int dgt = p.dir * kdt, dgh = p.dir * kdh, dgw = p.dir * kdw;
+  #pragma unroll
+      for (int s = 0; s < A_SLOTS; ++s) {
+        bool v = tap_ok && (rowok >> s & 1);
+        if (check)
+          v = v && (unsigned)(a_t[s] + dgt) < (unsigned)p.Gt && (unsigned)(a_h[s] + dgh) < (unsigned)p.Gh &&
+              (unsigned)(a_w[s] + dgw) < (unsigned)p.Gw;
+        if (v) {
+          ra[s] = *reinterpret_cast<const VT*>(p.x + (a_off[s] + tap_lin + kc));
+          ra_valid |= 1u << s;
+        } else {
+          ra[s] = VT{};
+        }
+      }
+      const int boff = tap_w + kc;
+  #pragma unroll
+      for (int s = 0; s < B_SLOTS; ++s) {
+        if (tap_ok && (nok >> s & 1))
+          rb[s] = *reinterpret_cast<const VT*>(p.w + (b_off[s] + boff));
+        else
+          rb[s] = VT{};
+      }
+      kadvance(BK);
+    };
+  
+    auto store_lds = [&](int buf) {
+      char* A = smem + buf * TILE_BYTES;
+      char* B = A + BM * BK * 2;
+  #pragma unroll
+      for (int s = 0; s < A_SLOTS; ++s) {
+        if (tid + s * NT >= A_CHUNKS) break;
+        VT v = ra[s];
+        if (affine && (ra_valid >> s & 1)) {
+          float f[CH];
+          if constexpr (CH == 8) unpack8(v, f); else unpack4(v, f);
+  #pragma unroll
+          for (int e = 0; e < CH; ++e) {
+            float z = f[e] * aff[ra_c + e] + aff[p.Cg + ra_c + e];
+            f[e] = (affine == 2) ? fmaxf(z, 0.f) : z;
+          }
+          if constexpr (CH == 8) v = pack8(f); else v = pack4(f);
+        }
+        *reinterpret_cast<VT*>(A + sa[s]) = v;
+      }
+  #pragma unroll
+      for (int s = 0; s < B_SLOTS; ++s) {
+        if (tid + s * NT >= B_CHUNKS) break;
+        *reinterpret_cast<VT*>(B + sb[s]) = rb[s];
+      }
+    };
+  
+  
+    const int nsteps = (p.nt * p.nh * p.nw * p.Cg + BK - 1) / BK;
+    __syncthreads();  // affine table ready
+    load();
+    store_lds(0);
+    __syncthreads();
+  
+    for (int step = 0; step < nsteps; ++step) {
+      const int cur = step & 1;
+      const bool has_next = step + 1 < nsteps;
+      if (has_next) load();
+      const char* A = smem + cur * TILE_BYTES;
+  #pragma unroll
+      for (int kk = 0; kk < BK / 32; ++kk) {
+        bf16x8_t af[TM], bfr[TN];
+  #pragma unroll
+        for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8_t*>(A + fa[kk][i]);
+  #pragma unroll
+        for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const bf16x8_t*>(A + fb[kk][j]);
+  #pragma unroll
+        for (int i = 0; i < TM; ++i)
+  #pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+      }
+      if (has_next) store_lds(cur ^ 1);
+      __syncthreads();
+    }
+  
   }
 
   // ---- epilogue: D[n][m] fragment: lane holds channels n..n+3 of position m ----
@@ -446,6 +599,9 @@ void conv_igemm_kernel(const ConvParams p) {
   }
 }
 
+// uniform-tap loader use: 0 never, 1 where it measured faster (default), 2 whenever legal
+static int g_ut_mode = 1;
+
 template <int BM, int BN, int WM, int WN, int CH, int BK>
 void launch_cfg(const ConvParams& p, hipStream_t stream) {
   constexpr int NT = (BM / WM) * (BN / WN) * 64;
@@ -454,13 +610,23 @@ void launch_cfg(const ConvParams& p, hipStream_t stream) {
   constexpr int NW = (BM / WM) * (BN / WN);
   const size_t red_bytes = epi ? (NW * 3 + 4) * BN * 4 : (BM / WM) * 2 * BN * 4;
   const size_t lds = main_lds_bytes(BM, BN, BK, epi ? 1 : 0) + red_bytes + (p.affine ? 2 * p.Cg * 4 : 0);
-  if (epi) {
-    if constexpr (CH == 8)
-      hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 1>), dim3(m_tiles * n_tiles), dim3(NT), lds,
-                         stream, p);
+  const dim3 grid(m_tiles * n_tiles), block(NT);
+  // measured (scripts/conv_bench.py --ut 0/1/2): the uniform-tap loader wins without reachable padding
+  // and for spatial (1,k,k) unit-stride gathers (most with the consumer-side BN fold: 3x3 conv_b -20..25 %);
+  // it loses on padded temporal (k,1,1) and strided gathers, which keep the per-lane loader
+  const bool ut_legal = CH == 8 && p.Cg % BK == 0 && p.nt * p.nh * p.nw <= 32;
+  const bool ut_pays = !p.check || (p.nt == 1 && p.ash == 1 && p.asw == 1);
+  const bool ut = ut_legal && (g_ut_mode == 2 || (g_ut_mode == 1 && ut_pays));
+  if constexpr (CH == 8) {
+    if (epi) {
+      if (ut) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 1, 1>), grid, block, lds, stream, p);
+      else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 1, 0>), grid, block, lds, stream, p);
+    } else {
+      if (ut) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 0, 1>), grid, block, lds, stream, p);
+      else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 0, 0>), grid, block, lds, stream, p);
+    }
   } else {
-    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 0>), dim3(m_tiles * n_tiles), dim3(NT), lds,
-                       stream, p);
+    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 0, 0>), grid, block, lds, stream, p);
   }
 }
 
@@ -490,6 +656,7 @@ int conv_igemm_m_tiles(int M, int N) {
 }
 
 static int g_bk_override = -1;
+void conv_igemm_set_ut(int mode) { g_ut_mode = mode; }
 void conv_igemm_set_bk(int bk) { g_bk_override = bk; }
 
 void conv_igemm_launch(const ConvParams& p, int chunk, hipStream_t stream) {

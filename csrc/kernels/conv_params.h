@@ -49,6 +49,7 @@ struct ConvParams {
   const float* emean1;
   const float* erstd1;
   float* epart;             // [m_tiles][3][Ngemm] partial (sum v, sum v*xhat0, sum v*xhat1)
+  unsigned xbytes, wbytes;  // buffer-resource extents of x and w (uniform-tap loader)
 };
 
 // Weight gradient: dW[n = cout][k = (tap, cin)] = sum_p dY[p][cout] * im2col(X)[p][k]

@@ -15,6 +15,7 @@ static_assert(offsetof(ConvParams, bws) - offsetof(ConvParams, M) == 38 * sizeof
 
 // ---- kernel launchers (defined in csrc/kernels/*.hip) ----
 void conv_igemm_launch(const ConvParams& p, int chunk, hipStream_t stream);
+void conv_igemm_set_ut(int mode);
 int conv_igemm_m_tiles(int M, int N);
 void conv_igemm_set_bk(int bk);
 void conv_wgrad_launch(const WgradParams& p, int chunk, hipStream_t stream);
@@ -114,6 +115,9 @@ static ConvParams conv_params(const at::Tensor& x, const at::Tensor& w, const at
   p.check = (dim_ok(p.Rt, p.ast, p.aot, p.dir, p.nt, p.Gt) && dim_ok(p.Rh, p.ash, p.aoh, p.dir, p.nh, p.Gh) &&
              dim_ok(p.Rw, p.asw, p.aow, p.dir, p.nw, p.Gw)) ? 0 : 1;
   TORCH_CHECK(x.numel() < (1ll << 31) && y.numel() < (1ll << 31), "tensor too large for 32-bit offsets");
+  TORCH_CHECK(x.numel() * 2 < 0xFFFFFF00ll && w.numel() * 2 < 0xFFFFFF00ll, "buffer extents must fit 32 bits");
+  p.xbytes = (unsigned)(x.numel() * 2);
+  p.wbytes = (unsigned)(w.numel() * 2);
   TORCH_CHECK(p.Cg % chunk == 0 && p.Cg > 0, "gathered channels must be a multiple of the chunk");
   TORCH_CHECK(p.Ngemm % 4 == 0, "output channels must be a multiple of 4");
   TORCH_CHECK(p.ldx % chunk == 0 && p.ldy % 4 == 0, "row strides must keep vector alignment");
@@ -348,6 +352,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_igemm_epi", &conv_igemm_epi);
   m.def("conv_m_tiles", &conv_m_tiles);
   m.def("conv_set_bk", [](int64_t bk) { conv_igemm_set_bk((int)bk); });
+  m.def("conv_set_ut", [](int64_t mode) { conv_igemm_set_ut((int)mode); });
   m.def("wgrad_tile", &wgrad_tile);
   m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("partial"), py::arg("scale"),
         py::arg("shift"), py::arg("affine"), py::arg("g"), py::arg("chunk"), py::arg("slab") = 0);

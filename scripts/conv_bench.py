@@ -54,10 +54,13 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default="")
     ap.add_argument("--bk", type=int, default=-1)
+    ap.add_argument("--affine", type=int, default=0, help="1: forward applies consumer-side BN+ReLU to its input")
+    ap.add_argument("--ut", type=int, default=1, help="uniform-tap loader: 0 never, 1 heuristic (default), 2 always")
     a = ap.parse_args()
+    from pytorchvideo_accelerate_amd.ops._ext import require
     if a.bk > 0:
-        from pytorchvideo_accelerate_amd.ops._ext import require
         require().conv_set_bk(a.bk)
+    require().conv_set_ut(a.ut)
     dev = "cuda"
     tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0}
     print(f"{'layer':18s} {'M':>8s} {'N':>5s} {'K':>5s} | {'fwd us':>8s} {'TF':>6s} | {'dgrad us':>8s} {'TF':>6s} | {'wgrad us':>8s} {'TF':>6s}")
@@ -74,7 +77,12 @@ def main():
         M = N * To * Ho * Wo
         flops = spec.flops(N, T, H, W)
         out = torch.empty(M, cout, device=dev, dtype=torch.bfloat16)
-        tf = timeit(lambda: conv_fwd(xa, wf, spec, out=out), a.iters)
+        if a.affine:
+            sc = torch.rand(spec.cin_pad or cin, device=dev) + 0.5
+            sh = torch.randn(spec.cin_pad or cin, device=dev) * 0.1
+            tf = timeit(lambda: conv_fwd(xa, wf, spec, out=out, in_scale=sc, in_shift=sh, in_relu=True), a.iters)
+        else:
+            tf = timeit(lambda: conv_fwd(xa, wf, spec, out=out), a.iters)
         dy = Act(torch.randn(M, cout, device=dev).to(torch.bfloat16), N, To, Ho, Wo)
         if cin % 8 == 0:
             dx = torch.empty(xa.M, cin, device=dev, dtype=torch.bfloat16)
