@@ -69,4 +69,5 @@ struct WgradParams {
   int kt, kh, kw, st, sh, sw, pt, ph, pw;
   int splits, p_per_split;
   int slab;                 // 1: deterministic mode — split s stores into partial + s*Cout*K (no atomics)
+  unsigned dybytes, xbytes; // buffer-resource extents
 };

@@ -40,7 +40,9 @@ __device__ __forceinline__ s16x4_t tr_read(const char* base) {
       (__attribute__((address_space(3))) s16x4_t*)(base));
 }
 
-template <int BMW, int BNW, int WMW, int WNW, int CH>
+// DENSE: 1x1x1, stride 1, no padding — the im2col row of position p is x row p, so both operands stream
+// with raw buffer loads whose per-step advance is one SGPR offset (no per-lane address math).
+template <int BMW, int BNW, int WMW, int WNW, int CH, int DENSE>
 __global__ __launch_bounds__((BMW / WMW) * (BNW / WNW) * 64)
 void conv_wgrad_kernel(const WgradParams p) {
   constexpr int NWN = BNW / WNW;
@@ -57,7 +59,6 @@ void conv_wgrad_kernel(const WgradParams p) {
   using VT = typename std::conditional<CH == 8, uint4, uint2>::type;
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* aff = reinterpret_cast<float*>(smem + 2 * TILE);
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / NWN, wn = wid % NWN;
@@ -67,20 +68,25 @@ void conv_wgrad_kernel(const WgradParams p) {
   const int p_begin = split * p.p_per_split;
   const int p_end = min(p.P, p_begin + p.p_per_split);
   const int affine = p.affine;
-  if (affine) {
-    for (int i = tid; i < p.Cin; i += NT) { aff[i] = p.in_scale[i]; aff[p.Cin + i] = p.in_shift[i]; }
-  }
+  const __amdgpu_buffer_rsrc_t dyr = __builtin_amdgcn_make_buffer_rsrc((void*)p.dy, (short)0, (int)p.dybytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, (int)p.xbytes, 0x00020000);
+  constexpr unsigned OOB = 0xFFFFFFF0u;
+  // every step is full when P is a multiple of BP (p_per_split always is): no row masks at all
+  const bool exact = (p.P % BP) == 0;
 
   // ---- A (dY) slots: fixed column; element offsets advance by BP rows per step ----
   const int a_col = tid % A_CPR;
   const int a_n = n0 + a_col * 8;
   const bool a_col_ok = a_n < p.Cout;
-  int a_off[A_SLOTS], a_row[A_SLOTS], sa[A_SLOTS];
+  int a_vo[A_SLOTS], a_row[A_SLOTS], sa[A_SLOTS];
 #pragma unroll
   for (int s = 0; s < A_SLOTS; ++s) {
     const int idx = tid + s * NT;
     a_row[s] = idx / A_CPR;
-    a_off[s] = (p_begin + a_row[s]) * p.ldd + a_n;
+    // element offset of the slot's dY row (DENSE: byte offset for the buffer loads; columns past Cout
+    // read a real, ignored address — those dW rows are never stored)
+    a_vo[s] = (p_begin + a_row[s]) * p.ldd + a_n;
+    if constexpr (DENSE) a_vo[s] = (idx < A_CHUNKS && a_col_ok) ? a_vo[s] * 2 : 0;
     sa[s] = img_off<BMW>(a_row[s], a_col * 16);
   }
 
@@ -98,6 +104,13 @@ void conv_wgrad_kernel(const WgradParams p) {
     b_dw = r - b_dh * p.kw;
   }
   const int tapoff = ((b_dt * p.Hi + b_dh) * p.Wi + b_dw) * p.ldx + b_c;
+  // the block's im2col column is fixed, so this thread's 8 BN scale/shift values are too: registers
+  float asc[CH], ash[CH];
+#pragma unroll
+  for (int e = 0; e < CH; ++e) {
+    asc[e] = (affine && b_col_ok) ? p.in_scale[b_c + e] : 0.f;
+    ash[e] = (affine && b_col_ok) ? p.in_shift[b_c + e] : 0.f;
+  }
   const bool check = p.pt | p.ph | p.pw;   // taps can only leave the tensor through padding
   // per-slot output position (pb, pt, ph, pw) and its input origin (bt, bh, bw) / linear offset bio
   const int OHW = p.Ho * p.Wo, OTHW = p.To * OHW;
@@ -136,16 +149,47 @@ void conv_wgrad_kernel(const WgradParams p) {
   unsigned rb_valid = 0;
   int pcur = p_begin;
 
+  int b_vo[B_SLOTS];
+#pragma unroll
+  for (int s = 0; s < B_SLOTS; ++s)
+    b_vo[s] = (DENSE && tid + s * NT < B_CHUNKS && b_col_ok) ? ((p_begin + b_row[s]) * p.ldx + b_c) * 2 : 0;
+
   auto load = [&]() {
+    const int pd = pcur - p_begin;  // uniform step offset (positions)
+    rb_valid = 0;
+    if constexpr (DENSE && CH == 8) {
+#pragma unroll
+      for (int s = 0; s < A_SLOTS; ++s) {
+        if (exact) {
+          ra[s] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(dyr, a_vo[s], pd * p.ldd * 2, 0));
+        } else {
+          const bool v = pcur + a_row[s] < p_end;
+          ra[s] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+              dyr, v ? a_vo[s] + pd * p.ldd * 2 : (int)OOB, 0, 0));
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < B_SLOTS; ++s) {
+        if (exact) {
+          rb[s] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, b_vo[s], pd * p.ldx * 2, 0));
+        } else {
+          const bool v = pcur + b_row[s] < p_end;
+          rb[s] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+              xr, v ? b_vo[s] + pd * p.ldx * 2 : (int)OOB, 0, 0));
+        }
+      }
+      rb_valid = ~0u;
+      pcur += BP;
+      return;
+    }
 #pragma unroll
     for (int s = 0; s < A_SLOTS; ++s) {
       if (tid + s * NT < A_CHUNKS && a_col_ok && pcur + a_row[s] < p_end)
-        ra[s] = *reinterpret_cast<const uint4*>(p.dy + a_off[s]);
+        ra[s] = *reinterpret_cast<const uint4*>(p.dy + a_vo[s]);
       else
         ra[s] = uint4{0, 0, 0, 0};
-      a_off[s] += BP * p.ldd;
+      a_vo[s] += BP * p.ldd;
     }
-    rb_valid = 0;
 #pragma unroll
     for (int s = 0; s < B_SLOTS; ++s) {
       bool v = tid + s * NT < B_CHUNKS && b_col_ok && pcur + b_row[s] < p_end;
@@ -175,15 +219,22 @@ void conv_wgrad_kernel(const WgradParams p) {
     for (int s = 0; s < B_SLOTS; ++s) {
       if (tid + s * NT >= B_CHUNKS) break;
       VT v = rb[s];
-      if (affine && (rb_valid >> s & 1)) {
+      if (affine) {
+        // recompute the producer's BN(+ReLU) on the fly: packed cvt + v_pk_max_i16 ReLU
         float f[CH];
         if constexpr (CH == 8) unpack8(v, f); else unpack4(v, f);
 #pragma unroll
-        for (int e = 0; e < CH; ++e) {
-          const float z = f[e] * aff[b_c + e] + aff[p.Cin + b_c + e];
-          f[e] = (affine == 2) ? fmaxf(z, 0.f) : z;
+        for (int e = 0; e < CH; ++e) f[e] = __builtin_fmaf(f[e], asc[e], ash[e]);
+        if constexpr (CH == 8) {
+          v = pack8_fast(f);
+          if (affine == 2) v = relu_bf16x8(v);
+          if (!DENSE && !((rb_valid >> s) & 1u)) v = uint4{0, 0, 0, 0};   // zero padding stays zero
+        } else {
+          if (affine == 2)
+            for (int e = 0; e < CH; ++e) f[e] = fmaxf(f[e], 0.f);
+          v = pack4(f);
+          if (!((rb_valid >> s) & 1u)) v = VT{};
         }
-        if constexpr (CH == 8) v = pack8(f); else v = pack4(f);
       }
       *reinterpret_cast<VT*>(B + sb[s]) = v;
     }
@@ -276,8 +327,16 @@ template <int BMW, int BNW, int WMW, int WNW, int CH>
 void launch_w(const WgradParams& p, hipStream_t stream) {
   constexpr int NT = (BMW / WMW) * (BNW / WNW) * 64;
   dim3 grid((p.Cout + BMW - 1) / BMW, (p.K + BNW - 1) / BNW, p.splits);
-  const size_t lds = 2 * BP * (BMW + BNW) * 2 + (p.affine ? 2 * p.Cin * 4 : 0);
-  hipLaunchKernelGGL((conv_wgrad_kernel<BMW, BNW, WMW, WNW, CH>), grid, dim3(NT), lds, stream, p);
+  const size_t lds = 2 * BP * (BMW + BNW) * 2;
+  const bool dense = p.kt == 1 && p.kh == 1 && p.kw == 1 && p.st == 1 && p.sh == 1 && p.sw == 1 &&
+                     p.pt == 0 && p.ph == 0 && p.pw == 0;
+  if constexpr (CH == 8) {
+    if (dense) {
+      hipLaunchKernelGGL((conv_wgrad_kernel<BMW, BNW, WMW, WNW, CH, 1>), grid, dim3(NT), lds, stream, p);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((conv_wgrad_kernel<BMW, BNW, WMW, WNW, CH, 0>), grid, dim3(NT), lds, stream, p);
 }
 
 // dW accumulator [Cout][taps][Cin_pad] -> grad[Cout][Cin][taps] (PyTorch layout),

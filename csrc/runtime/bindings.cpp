@@ -185,6 +185,9 @@ void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& par
   TORCH_CHECK(p.Cin % chunk == 0 && p.Cout % 8 == 0, "wgrad channel alignment");
   TORCH_CHECK(p.p_per_split % 32 == 0, "p_per_split must be a multiple of 32");
   p.slab = (int)slab;
+  TORCH_CHECK(dy.numel() * 2 < 0xFFFFFF00ll && x.numel() * 2 < 0xFFFFFF00ll, "buffer extents must fit 32 bits");
+  p.dybytes = (unsigned)(dy.numel() * 2);
+  p.xbytes = (unsigned)(x.numel() * 2);
   TORCH_CHECK(partial.numel() >= (int64_t)p.Cout * p.K * (slab ? p.splits : 1), "wgrad accumulator too small");
   conv_wgrad_launch(p, (int)chunk, cur_stream());
 }
