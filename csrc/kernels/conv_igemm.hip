@@ -58,8 +58,8 @@ void conv_igemm_kernel(const ConvParams p) {
   constexpr int NWAVES = (BM / WM) * NWN;
   constexpr int RED_FLOATS = EPI == 1 ? NWAVES * 3 * BN : (BM / WM) * 2 * BN;
   float* red = reinterpret_cast<float*>(smem + MAIN_BYTES);
-  float* bnp = red + RED_FLOATS;                                         // EPI: [4][BN] mean0 rstd0 mean1 rstd1
-  float* aff = bnp + (EPI == 1 ? 4 * BN : 0);                            // [2][Cg] affine
+  float* bnp = red + RED_FLOATS;  // EPI: [6][BN] mean0 rstd0 mean1 rstd1 mask-scale mask-shift
+  float* aff = bnp + (EPI == 1 ? 6 * BN : 0);                            // [2][Cg] affine
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / NWN, wn = wid % NWN;
@@ -80,6 +80,8 @@ void conv_igemm_kernel(const ConvParams p) {
       bnp[BN + i] = ok ? p.erstd0[n] : 0.f;
       bnp[2 * BN + i] = d ? p.emean1[n] : 0.f;
       bnp[3 * BN + i] = d ? p.erstd1[n] : 0.f;
+      bnp[4 * BN + i] = (ok && p.emsc) ? p.emsc[n] : 0.f;
+      bnp[5 * BN + i] = (ok && p.emsh) ? p.emsh[n] : 0.f;
     }
   }
   if (affine) {
@@ -467,6 +469,7 @@ void conv_igemm_kernel(const ConvParams p) {
     for (int e = 0; e < 8; ++e) { sv[e] = 0.f; s0[e] = 0.f; s1[e] = 0.f; }
     const bool nok = n < p.Ngemm;
     const bool dual = p.ey1 != nullptr;
+    const bool masky = do_bstats && p.emsc != nullptr;
     constexpr int RB = 4;  // rows whose loads are issued together (latency hiding)
     for (int base = r0; base < BM && nok; base += RB * RPP) {
       uint4 lo[RB], lr[RB], l0[RB], l1[RB];
@@ -509,6 +512,13 @@ void conv_igemm_kernel(const ConvParams p) {
         float o[8], rs[8];
         unpack8(lo[u], o);
         unpack8(lr[u], rs);
+        if (masky) {  // mask mode 2: ReLU of this BN's own affine output
+          float a[8];
+          unpack8(l0[u], a);
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (!(a[e] * bnp[4 * BN + cg * 8 + e] + bnp[5 * BN + cg * 8 + e] > 0.f)) bits[u] &= ~(1u << e);
+        }
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const float t = v[e] + o[e] + rs[e];
@@ -608,7 +618,7 @@ void launch_cfg(const ConvParams& p, hipStream_t stream) {
   const int m_tiles = (p.M + BM - 1) / BM, n_tiles = (p.Ngemm + BN - 1) / BN;
   const bool epi = p.eres || p.emask || p.epart;
   constexpr int NW = (BM / WM) * (BN / WN);
-  const size_t red_bytes = epi ? (NW * 3 + 4) * BN * 4 : (BM / WM) * 2 * BN * 4;
+  const size_t red_bytes = epi ? (NW * 3 + 6) * BN * 4 : (BM / WM) * 2 * BN * 4;
   const size_t lds = main_lds_bytes(BM, BN, BK, epi ? 1 : 0) + red_bytes + (p.affine ? 2 * p.Cg * 4 : 0);
   const dim3 grid(m_tiles * n_tiles), block(NT);
   // measured (scripts/conv_bench.py --ut 0/1/2): the uniform-tap loader wins without reachable padding

@@ -49,6 +49,8 @@ struct ConvParams {
   const float* emean1;
   const float* erstd1;
   float* epart;             // [m_tiles][3][Ngemm] partial (sum v, sum v*xhat0, sum v*xhat1)
+  const float* emsc;        // optional ReLU mask from the BN input itself: v *= (y0*emsc + emsh > 0)
+  const float* emsh;        //   (mask mode 2: the gradient of a BN whose ReLU output feeds this conv)
   unsigned xbytes, wbytes;  // buffer-resource extents of x and w (uniform-tap loader)
 };
 

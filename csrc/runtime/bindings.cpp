@@ -142,7 +142,7 @@ void conv_igemm(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, c
 void conv_igemm_epi(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, int64_t accum,
                     std::vector<int64_t> g, int64_t chunk, const OptT& res, int64_t ldr, const OptT& mask,
                     const OptT& y0, const OptT& mean0, const OptT& rstd0, const OptT& y1, const OptT& mean1,
-                    const OptT& rstd1, const OptT& part) {
+                    const OptT& rstd1, const OptT& part, const OptT& msc, const OptT& msh) {
   ConvParams p = conv_params(x, w, y, accum, g, chunk);
   p.eres = bfo(res); p.ldr = (int)ldr;
   TORCH_CHECK(!res.has_value() || ldr % 4 == 0, "residual row stride alignment");
@@ -157,6 +157,8 @@ void conv_igemm_epi(const at::Tensor& x, const at::Tensor& w, const at::Tensor& 
     p.ey0 = bfp(*y0); p.ey1 = bfo(y1);
     p.emean0 = f32(*mean0); p.erstd0 = f32(*rstd0); p.emean1 = f32o(mean1); p.erstd1 = f32o(rstd1);
     p.epart = f32(*part);
+    TORCH_CHECK(msc.has_value() == msh.has_value(), "mask affine needs scale and shift");
+    p.emsc = f32o(msc); p.emsh = f32o(msh);
     TORCH_CHECK(part->numel() >= (int64_t)conv_igemm_m_tiles(p.M, p.Ngemm) * 3 * p.Ngemm, "partials too small");
   }
   if (p.M == 0) return;
@@ -352,7 +354,10 @@ void synth_frames(const at::Tensor& out, int64_t seed) {
 PYBIND11_MODULE(_C, m) {
   m.doc() = "gfx950 HIP kernels for pytorchvideo_accelerate_amd";
   m.def("conv_igemm", &conv_igemm);
-  m.def("conv_igemm_epi", &conv_igemm_epi);
+  m.def("conv_igemm_epi", &conv_igemm_epi, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("accum"), py::arg("g"),
+        py::arg("chunk"), py::arg("res"), py::arg("ldr"), py::arg("mask"), py::arg("y0"), py::arg("mean0"),
+        py::arg("rstd0"), py::arg("y1"), py::arg("mean1"), py::arg("rstd1"), py::arg("part"),
+        py::arg("msc") = py::none(), py::arg("msh") = py::none());
   m.def("conv_m_tiles", &conv_m_tiles);
   m.def("conv_set_bk", [](int64_t bk) { conv_igemm_set_bk((int)bk); });
   m.def("conv_set_ut", [](int64_t mode) { conv_igemm_set_ut((int)mode); });

@@ -177,11 +177,13 @@ class _ConvBN:
                        eng.grad_beta, slab)
 
     def dgrad(self, dy: Act, in_dims, out: torch.Tensor, accum: bool, res: Optional[Act] = None,
-              epi: Optional["_ResBlock"] = None):
+              epi: Optional["_ResBlock"] = None, bn: Optional[Tuple["_ConvBN", Act]] = None):
         """grad wrt the conv input into ``out`` (``accum``: added).  With ``res`` / ``epi`` the single-phase
         launch also adds the residual gradient ``res``, applies the ReLU mask of residual unit ``epi``'s
         output and emits the partial sums of ``epi``'s conv_c (+branch1) BN backward; returns
-        (partials, tiles) for ``epi.bwd(pre=...)``."""
+        (partials, tiles) for ``epi.bwd(pre=...)``.  With ``bn = (unit, y)`` (this conv's input is
+        relu(BN_unit(y))) it applies that ReLU mask and emits ``unit``'s BN-backward partial sums instead;
+        returns (partials, tiles) for ``unit.bn_backward(pre=...)``, or None when not fusable."""
         s, C = self.spec, self.eng.C
         self.eng.mark(self.name + ".dgrad")
         Ti, Hi, Wi = in_dims
@@ -189,6 +191,14 @@ class _ConvBN:
         geo = self._geo.get(key)
         if geo is None:
             geo = self._geo[key] = dgrad_phases(s, dy.N, tuple(in_dims), (dy.T, dy.H, dy.W), dy.ld, out.stride(0))
+        if bn is not None and res is None and epi is None and len(geo) == 1 and not accum:
+            u, y = bn
+            g = geo[0]
+            tiles = C.conv_m_tiles(g[0], g[1])
+            part = self.eng.scratch("bnepi", tiles * 3 * g[1])
+            C.conv_igemm_epi(dy.t, self.wd, out, 0, g, 8, None, 0, None, y.t, u.mean, u.rstd, None, None, None,
+                             part, u.scale, u.shift)
+            return part, tiles
         if res is not None or epi is not None:
             assert len(geo) == 1, "fused dgrad epilogue needs a single-phase (stride-1) dgrad"
             g = geo[0]
@@ -398,12 +408,15 @@ class _ResBlock:
             dyc, dy1 = self.c.bn_backward(dout, yc, 3, self.mask, None, other=self.one, other_y=y1)
         self.c.wgrad(dyc, yb, self.b.xf())
         dab = eng.ws((self.name, "dab"), (yb.M, self.b.C), torch.bfloat16)
-        self.c.dgrad(dyc, (yb.T, yb.H, yb.W), dab, False)
-        dyb, _ = self.b.bn_backward(Act(dab, yb.N, yb.T, yb.H, yb.W), yb, 2, None, self.b.xf())
+        # the dgrad epilogues apply the b / a ReLU masks and reduce their BN-backward sums (no separate pass)
+        pb = self.c.dgrad(dyc, (yb.T, yb.H, yb.W), dab, False, bn=(self.b, yb))
+        dyb, _ = self.b.bn_backward(Act(dab, yb.N, yb.T, yb.H, yb.W), yb, 0 if pb else 2, None,
+                                    None if pb else self.b.xf(), pre=pb)
         self.b.wgrad(dyb, ya, self.a.xf())
         daa = eng.ws((self.name, "daa"), (ya.M, self.a.C), torch.bfloat16)
-        self.b.dgrad(dyb, (ya.T, ya.H, ya.W), daa, False)
-        dya, _ = self.a.bn_backward(Act(daa, ya.N, ya.T, ya.H, ya.W), ya, 2, None, self.a.xf())
+        pa = self.b.dgrad(dyb, (ya.T, ya.H, ya.W), daa, False, bn=(self.a, ya))
+        dya, _ = self.a.bn_backward(Act(daa, ya.N, ya.T, ya.H, ya.W), ya, 0 if pa else 2, None,
+                                    None if pa else self.a.xf(), pre=pa)
         self.a.wgrad(dya, x, None)
         if self.one is not None:
             self.one.wgrad(dy1, x, None)

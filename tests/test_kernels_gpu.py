@@ -143,6 +143,39 @@ def test_conv_dgrad_bn_epilogue(case, dual, accum):
         torch.testing.assert_close(s[2], (q * (y1.float() - mean1) * rstd1).sum(0), rtol=1e-3, atol=tol)
 
 
+@pytest.mark.parametrize("case", [CASES[0], CASES[2], CASES[6]])
+def test_conv_dgrad_bn_epilogue_affine_mask(case):
+    """dgrad epilogue for a conv whose input is relu(BN(y)): v *= (y*scale + shift > 0) + BN partial sums."""
+    from pytorchvideo_accelerate_amd.ops._ext import require
+    from pytorchvideo_accelerate_amd.ops.conv import conv_m_tiles, dgrad_phases
+    C = require()
+    x, w, spec = _mk(case, seed=11)
+    N, Ci, T, H, W = x.shape
+    ref_y = torch.nn.functional.conv3d(x, w, None, spec.stride, spec.pad)
+    gy = torch.randn_like(ref_y).to(torch.bfloat16).float()
+    dx_ref = torch.nn.grad.conv3d_input(x.shape, w, gy, spec.stride, spec.pad)
+    M = N * T * H * W
+    g = torch.Generator(device="cpu").manual_seed(12)
+    y0 = (torch.randn(M, Ci, generator=g) * 2 + 0.3).to(torch.bfloat16).to(DEV)
+    mean0, rstd0 = torch.randn(Ci, device=DEV) * 0.3, torch.rand(Ci, device=DEV) + 0.5
+    msc, msh = torch.rand(Ci, device=DEV) + 0.2, torch.randn(Ci, device=DEV) * 0.5
+    _, wd = pack_weight(w, spec)
+    dy = Act.from_ncthw(gy)
+    out = torch.empty(M, Ci, device=DEV, dtype=torch.bfloat16)
+    geo = dgrad_phases(spec, N, (T, H, W), (dy.T, dy.H, dy.W), dy.ld, Ci)
+    part = torch.full((conv_m_tiles(M, Ci), 3, Ci), float("nan"), device=DEV)
+    C.conv_igemm_epi(dy.t, wd, out, 0, geo[0], 8, None, 0, None, y0, mean0, rstd0, None, None, None, part,
+                     msc, msh)
+    mask = (y0.float() * msc + msh) > 0
+    v = dx_ref.permute(0, 2, 3, 4, 1).reshape(M, Ci) * mask
+    assert rel_err(out, v) < 1.5e-2
+    q = out.float()
+    s = part.sum(0)
+    tol = 2e-2 * (q.abs() * (y0.float() - mean0).abs() * rstd0).sum(0).max().item() / M ** 0.5
+    torch.testing.assert_close(s[0], q.sum(0), rtol=1e-3, atol=1e-2 * q.abs().sum(0).max().item() / M ** 0.5)
+    torch.testing.assert_close(s[1], (q * (y0.float() - mean0) * rstd0).sum(0), rtol=1e-3, atol=tol)
+
+
 def test_res_out_mask_bits():
     from pytorchvideo_accelerate_amd.ops._ext import require
     C = require()
