@@ -15,7 +15,7 @@ import torch
 import torch.nn.functional as F
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from pytorchvideo_accelerate_amd.models.reference import slowfast_r50, slow_r50  # noqa: E402
+from pytorchvideo_accelerate_amd.models.reference import create_slowfast, slow_r50  # noqa: E402
 
 
 def main():
@@ -27,13 +27,14 @@ def main():
     ap.add_argument("--crop", type=int, default=224)
     ap.add_argument("--alpha", type=int, default=4)
     ap.add_argument("--classes", type=int, default=400)
+    ap.add_argument("--depth", type=int, default=50)
     ap.add_argument("--channels-last", action="store_true")
     ap.add_argument("--slow", action="store_true")
     ap.add_argument("--dtype", default="bf16")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
-    model = (slow_r50(a.classes) if a.slow else slowfast_r50(a.classes)).to(dev)
+    model = (slow_r50(a.classes) if a.slow else create_slowfast(a.depth, a.classes)).to(dev)
     if a.channels_last:
         model = model.to(memory_format=torch.channels_last_3d)
     opt = torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
