@@ -612,8 +612,12 @@ void conv_igemm_kernel(const ConvParams p) {
 // uniform-tap loader use: 0 never, 1 where it measured faster (default), 2 whenever legal
 static int g_ut_mode = 1;
 
+inline bool conv_ut_legal(const ConvParams& p, int ch, int bk) {
+  return ch == 8 && p.Cg % bk == 0 && p.nt * p.nh * p.nw <= 32;
+}
+
 template <int BM, int BN, int WM, int WN, int CH, int BK>
-void launch_cfg(const ConvParams& p, hipStream_t stream) {
+void launch_cfg(const ConvParams& p, int ut_force, hipStream_t stream) {
   constexpr int NT = (BM / WM) * (BN / WN) * 64;
   const int m_tiles = (p.M + BM - 1) / BM, n_tiles = (p.Ngemm + BN - 1) / BN;
   const bool epi = p.eres || p.emask || p.epart;
@@ -621,12 +625,13 @@ void launch_cfg(const ConvParams& p, hipStream_t stream) {
   const size_t red_bytes = epi ? (NW * 3 + 6) * BN * 4 : (BM / WM) * 2 * BN * 4;
   const size_t lds = main_lds_bytes(BM, BN, BK, epi ? 1 : 0) + red_bytes + (p.affine ? 2 * p.Cg * 4 : 0);
   const dim3 grid(m_tiles * n_tiles), block(NT);
-  // measured (scripts/conv_bench.py --ut 0/1/2): the uniform-tap loader wins without reachable padding
-  // and for spatial (1,k,k) unit-stride gathers (most with the consumer-side BN fold: 3x3 conv_b -20..25 %);
-  // it loses on padded temporal (k,1,1) and strided gathers, which keep the per-lane loader
-  const bool ut_legal = CH == 8 && p.Cg % BK == 0 && p.nt * p.nh * p.nw <= 32;
+  // heuristic (ut_force < 0), measured with scripts/conv_bench.py --ut 0/1/2: the uniform-tap loader wins
+  // without reachable padding and for spatial (1,k,k) unit-stride gathers (with the consumer-side BN fold
+  // 3x3 conv_b -20..25 %); it loses on padded temporal (k,1,1) and strided gathers.  The autotuner
+  // (models/fused.ConvTuner) passes ut_force = 0 / 1 per conv instead.
+  const bool ut_legal = conv_ut_legal(p, CH, BK);
   const bool ut_pays = !p.check || (p.nt == 1 && p.ash == 1 && p.asw == 1);
-  const bool ut = ut_legal && (g_ut_mode == 2 || (g_ut_mode == 1 && ut_pays));
+  const bool ut = ut_legal && (ut_force >= 0 ? ut_force == 1 : (g_ut_mode == 2 || (g_ut_mode == 1 && ut_pays)));
   if constexpr (CH == 8) {
     if (epi) {
       if (ut) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 1, 1>), grid, block, lds, stream, p);
@@ -641,12 +646,12 @@ void launch_cfg(const ConvParams& p, hipStream_t stream) {
 }
 
 template <int CH, int BK>
-void launch_variant(int v, const ConvParams& p, hipStream_t stream) {
+void launch_variant(int v, const ConvParams& p, int ut_force, hipStream_t stream) {
   switch (v) {
-    case 0: launch_cfg<128, 128, 64, 64, CH, BK>(p, stream); break;
-    case 1: launch_cfg<128, 64, 64, 32, CH, BK>(p, stream); break;
-    case 2: launch_cfg<256, 32, 64, 32, CH, BK>(p, stream); break;
-    default: launch_cfg<256, 16, 64, 16, CH, BK>(p, stream); break;
+    case 0: launch_cfg<128, 128, 64, 64, CH, BK>(p, ut_force, stream); break;
+    case 1: launch_cfg<128, 64, 64, 32, CH, BK>(p, ut_force, stream); break;
+    case 2: launch_cfg<256, 32, 64, 32, CH, BK>(p, ut_force, stream); break;
+    default: launch_cfg<256, 16, 64, 16, CH, BK>(p, ut_force, stream); break;
   }
 }
 
@@ -659,24 +664,43 @@ static int pick_variant(int M, int N) {
   return 3;                   // 256 x 16
 }
 
+// Launch configuration word: tile variant (bits 0-1: 128x128, 128x64, 256x32, 256x16), BK (bit 2: 32 / 64),
+// uniform-tap loader (bit 3), bit 4 set = explicit (else the built-in heuristic).  -1 = heuristic.
+int conv_cfg_bm(int cfg, int N) {
+  const int v = (cfg >= 0 && (cfg & 16)) ? (cfg & 3) : pick_variant(0, N);
+  return v <= 1 ? 128 : 256;
+}
+
 int conv_igemm_m_tiles(int M, int N) {
-  const int v = pick_variant(M, N);
-  const int bm = (v <= 1) ? 128 : 256;
+  const int bm = conv_cfg_bm(-1, N);
   return (M + bm - 1) / bm;
 }
+
+int conv_igemm_m_tiles_k(int M, int N, int /*K*/, int /*Cg*/) { return conv_igemm_m_tiles(M, N); }
 
 static int g_bk_override = -1;
 void conv_igemm_set_ut(int mode) { g_ut_mode = mode; }
 void conv_igemm_set_bk(int bk) { g_bk_override = bk; }
 
-void conv_igemm_launch(const ConvParams& p, int chunk, hipStream_t stream) {
+// 1 when the uniform-tap loader may run this launch with that BK
+int conv_igemm_ut_legal(const ConvParams& p, int chunk, int bk) { return conv_ut_legal(p, chunk, bk) ? 1 : 0; }
+
+void conv_igemm_launch(const ConvParams& p, int chunk, hipStream_t stream, int cfg) {
   if ((p.eres || p.emask || p.epart) && chunk != 8) return;  // host binding rejects this combination
-  const int v = pick_variant(p.M, p.Ngemm);
-  const int K = p.nt * p.nh * p.nw * p.Cg;
-  int bk = g_bk_override > 0 ? g_bk_override : ((K >= 1024 && chunk == 8) ? 64 : 32);
-  if (chunk == 8) {
-    if (bk == 64) launch_variant<8, 64>(v, p, stream); else launch_variant<8, 32>(v, p, stream);
+  int v, bk, ut_force;
+  if (cfg >= 0 && (cfg & 16)) {
+    v = cfg & 3;
+    bk = (cfg & 4) ? 64 : 32;
+    ut_force = (cfg >> 3) & 1;
   } else {
-    if (bk == 64) launch_variant<4, 64>(v, p, stream); else launch_variant<4, 32>(v, p, stream);
+    v = pick_variant(p.M, p.Ngemm);
+    const int K = p.nt * p.nh * p.nw * p.Cg;
+    bk = g_bk_override > 0 ? g_bk_override : ((K >= 1024 && chunk == 8) ? 64 : 32);
+    ut_force = -1;
+  }
+  if (chunk == 8) {
+    if (bk == 64) launch_variant<8, 64>(v, p, ut_force, stream); else launch_variant<8, 32>(v, p, ut_force, stream);
+  } else {
+    if (bk == 64) launch_variant<4, 64>(v, p, ut_force, stream); else launch_variant<4, 32>(v, p, ut_force, stream);
   }
 }

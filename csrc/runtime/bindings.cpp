@@ -14,9 +14,12 @@ static_assert(offsetof(ConvParams, bws) - offsetof(ConvParams, M) == 38 * sizeof
               "ConvParams integer block must be contiguous (filled from a 39-int geometry vector)");
 
 // ---- kernel launchers (defined in csrc/kernels/*.hip) ----
-void conv_igemm_launch(const ConvParams& p, int chunk, hipStream_t stream);
+void conv_igemm_launch(const ConvParams& p, int chunk, hipStream_t stream, int cfg);
+int conv_cfg_bm(int cfg, int N);
+int conv_igemm_ut_legal(const ConvParams& p, int chunk, int bk);
 void conv_igemm_set_ut(int mode);
 int conv_igemm_m_tiles(int M, int N);
+int conv_igemm_m_tiles_k(int M, int N, int K, int Cg);
 void conv_igemm_set_bk(int bk);
 void conv_wgrad_launch(const WgradParams& p, int chunk, hipStream_t stream);
 void conv_wgrad_tile(int Cout, int K, int* bmw, int* bnw);
@@ -127,14 +130,14 @@ static ConvParams conv_params(const at::Tensor& x, const at::Tensor& w, const at
 
 void conv_igemm(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, const OptT& stats,
                 const OptT& scale, const OptT& shift, int64_t affine, int64_t accum, std::vector<int64_t> g,
-                int64_t chunk) {
+                int64_t chunk, int64_t cfg) {
   ConvParams p = conv_params(x, w, y, accum, g, chunk);
   p.stats = f32o(stats);
   p.in_scale = f32o(scale); p.in_shift = f32o(shift);
   p.affine = (int)affine;
   TORCH_CHECK(!affine || (scale.has_value() && shift.has_value()), "affine needs scale/shift");
   if (p.M == 0) return;
-  conv_igemm_launch(p, (int)chunk, cur_stream());
+  conv_igemm_launch(p, (int)chunk, cur_stream(), (int)cfg);
 }
 
 // dgrad with the backward-BN epilogue (see ConvParams): residual add, ReLU-bit mask, and partial sums
@@ -142,7 +145,7 @@ void conv_igemm(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, c
 void conv_igemm_epi(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, int64_t accum,
                     std::vector<int64_t> g, int64_t chunk, const OptT& res, int64_t ldr, const OptT& mask,
                     const OptT& y0, const OptT& mean0, const OptT& rstd0, const OptT& y1, const OptT& mean1,
-                    const OptT& rstd1, const OptT& part, const OptT& msc, const OptT& msh) {
+                    const OptT& rstd1, const OptT& part, const OptT& msc, const OptT& msh, int64_t cfg) {
   ConvParams p = conv_params(x, w, y, accum, g, chunk);
   p.eres = bfo(res); p.ldr = (int)ldr;
   TORCH_CHECK(!res.has_value() || ldr % 4 == 0, "residual row stride alignment");
@@ -159,13 +162,18 @@ void conv_igemm_epi(const at::Tensor& x, const at::Tensor& w, const at::Tensor& 
     p.epart = f32(*part);
     TORCH_CHECK(msc.has_value() == msh.has_value(), "mask affine needs scale and shift");
     p.emsc = f32o(msc); p.emsh = f32o(msh);
-    TORCH_CHECK(part->numel() >= (int64_t)conv_igemm_m_tiles(p.M, p.Ngemm) * 3 * p.Ngemm, "partials too small");
+    const int bm = conv_cfg_bm((int)cfg, p.Ngemm);
+    TORCH_CHECK(part->numel() >= (int64_t)((p.M + bm - 1) / bm) * 3 * p.Ngemm, "partials too small");
   }
   if (p.M == 0) return;
-  conv_igemm_launch(p, (int)chunk, cur_stream());
+  conv_igemm_launch(p, (int)chunk, cur_stream(), (int)cfg);
 }
 
-int64_t conv_m_tiles(int64_t M, int64_t N) { return conv_igemm_m_tiles((int)M, (int)N); }
+// row tiles of the BN partial-sum buffer a conv launch writes; pass K (= taps * Cg) and Cg for forward
+// launches so the small-channel streaming kernel's 128-row tiles are accounted for
+int64_t conv_m_tiles(int64_t M, int64_t N, int64_t K, int64_t Cg) {
+  return K > 0 ? conv_igemm_m_tiles_k((int)M, (int)N, (int)K, (int)Cg) : conv_igemm_m_tiles((int)M, (int)N);
+}
 
 std::vector<int64_t> wgrad_tile(int64_t Cout, int64_t K) {
   int a, b;
@@ -353,12 +361,21 @@ void synth_frames(const at::Tensor& out, int64_t seed) {
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "gfx950 HIP kernels for pytorchvideo_accelerate_amd";
-  m.def("conv_igemm", &conv_igemm);
+  m.def("conv_igemm", &conv_igemm, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("stats"), py::arg("scale"),
+        py::arg("shift"), py::arg("affine"), py::arg("accum"), py::arg("g"), py::arg("chunk"), py::arg("cfg") = -1);
+  // launch-config helpers for the autotuner
+  m.def("conv_cfg_bm", [](int64_t cfg, int64_t N) { return (int64_t)conv_cfg_bm((int)cfg, (int)N); });
+  m.def("conv_ut_legal", [](std::vector<int64_t> g, int64_t chunk, int64_t bk) {
+    ConvParams q{};
+    int* f = &q.M;
+    for (int i = 0; i < 39 && i < (int)g.size(); ++i) f[i] = (int)g[i];
+    return (int64_t)conv_igemm_ut_legal(q, (int)chunk, (int)bk);
+  });
   m.def("conv_igemm_epi", &conv_igemm_epi, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("accum"), py::arg("g"),
         py::arg("chunk"), py::arg("res"), py::arg("ldr"), py::arg("mask"), py::arg("y0"), py::arg("mean0"),
         py::arg("rstd0"), py::arg("y1"), py::arg("mean1"), py::arg("rstd1"), py::arg("part"),
-        py::arg("msc") = py::none(), py::arg("msh") = py::none());
-  m.def("conv_m_tiles", &conv_m_tiles);
+        py::arg("msc") = py::none(), py::arg("msh") = py::none(), py::arg("cfg") = -1);
+  m.def("conv_m_tiles", &conv_m_tiles, py::arg("M"), py::arg("N"), py::arg("K") = 0, py::arg("Cg") = 0);
   m.def("conv_set_bk", [](int64_t bk) { conv_igemm_set_bk((int)bk); });
   m.def("conv_set_ut", [](int64_t mode) { conv_igemm_set_ut((int)mode); });
   m.def("wgrad_tile", &wgrad_tile);

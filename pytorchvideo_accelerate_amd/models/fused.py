@@ -133,19 +133,25 @@ class _ConvBN:
         M = x.N * To * Ho * Wo
         y = self.eng.ws((self.name, "y", tag), (M, s.cout), torch.bfloat16)
         stats = None
-        if train:
-            tiles = C.conv_m_tiles(M, s.cout)
-            stats = self.eng.ws((self.name, "stats"), (tiles, 2, s.cout), torch.float32)
+        if train:  # sized for the smallest row tile (128); the launch writes ceil(M / BM) of them
+            stats = self.eng.ws((self.name, "stats"), ((M + 127) // 128, 2, s.cout), torch.float32)
         aff = 0 if xf is None else (2 if xf.relu else 1)
         key = ("fg", x.N, x.T, x.H, x.W, x.ld)
         g = self._geo.get(key)
         if g is None:
             g = self._geo[key] = fwd_geometry(s, x.N, x.T, x.H, x.W, x.ld, s.cout)
-        C.conv_igemm(x.t, self.wf, y, stats, None if xf is None else xf.scale, None if xf is None else xf.shift,
-                     aff, 0, g, s.chunk)
+        sc_, sh_ = (None, None) if xf is None else (xf.scale, xf.shift)
+        tuner = self.eng.tuner
+
+        def run(cfg, scratch):
+            C.conv_igemm(x.t, self.wf, tuner.scratch_like(y) if scratch else y,
+                         None if stats is None else (tuner.scratch_like(stats) if scratch else stats),
+                         sc_, sh_, aff, 0, g, s.chunk, cfg)
+        cfg = tuner.launch(("f", s.chunk, aff, train) + tuple(g), g, s.chunk, run)
         bn = self.bn
         if train:
-            C.bn_finalize(stats, stats.shape[0], s.cout, M, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+            tiles = (M + tuner.bm(cfg, s.cout) - 1) // tuner.bm(cfg, s.cout)
+            C.bn_finalize(stats, tiles, s.cout, M, bn.weight, bn.bias, bn.running_mean, bn.running_var,
                           bn.num_batches_tracked, bn.momentum if bn.momentum is not None else 0.1, bn.eps,
                           self.mean, self.rstd, self.scale, self.shift)
         else:
@@ -191,34 +197,51 @@ class _ConvBN:
         geo = self._geo.get(key)
         if geo is None:
             geo = self._geo[key] = dgrad_phases(s, dy.N, tuple(in_dims), (dy.T, dy.H, dy.W), dy.ld, out.stride(0))
+        tuner = self.eng.tuner
         if bn is not None and res is None and epi is None and len(geo) == 1 and not accum:
             u, y = bn
             g = geo[0]
-            tiles = C.conv_m_tiles(g[0], g[1])
-            part = self.eng.scratch("bnepi", tiles * 3 * g[1])
-            C.conv_igemm_epi(dy.t, self.wd, out, 0, g, 8, None, 0, None, y.t, u.mean, u.rstd, None, None, None,
-                             part, u.scale, u.shift)
-            return part, tiles
+            part = self.eng.scratch("bnepi", ((g[0] + 127) // 128) * 3 * g[1])
+
+            def run(cfg, scratch):
+                C.conv_igemm_epi(dy.t, self.wd, tuner.scratch_like(out) if scratch else out, 0, g, 8, None, 0, None,
+                                 y.t, u.mean, u.rstd, None, None, None,
+                                 tuner.scratch_like(part) if scratch else part, u.scale, u.shift, cfg)
+            cfg = tuner.launch(("eb",) + tuple(g), g, 8, run)
+            bm = tuner.bm(cfg, g[1])
+            return part, (g[0] + bm - 1) // bm
         if res is not None or epi is not None:
             assert len(geo) == 1, "fused dgrad epilogue needs a single-phase (stride-1) dgrad"
             g = geo[0]
-            part, tiles = None, 0
+            part, c, one = None, None, None
             if epi is not None:
-                tiles = C.conv_m_tiles(g[0], g[1])
-                part = self.eng.scratch("bnepi", tiles * 3 * g[1])
+                part = self.eng.scratch("bnepi", ((g[0] + 127) // 128) * 3 * g[1])
                 c, one = epi.c, epi.one
-            C.conv_igemm_epi(dy.t, self.wd, out, 1 if accum else 0, g, 8,
-                             None if res is None else res.t, 0 if res is None else res.ld,
-                             None if epi is None else epi.mask, None if epi is None else epi.yc.t,
-                             None if epi is None else c.mean, None if epi is None else c.rstd,
-                             None if epi is None or one is None else epi.y1.t,
-                             None if epi is None or one is None else one.mean,
-                             None if epi is None or one is None else one.rstd, part)
-            return (part, tiles) if epi is not None else None
+
+            def run(cfg, scratch):
+                C.conv_igemm_epi(dy.t, self.wd, tuner.scratch_like(out) if scratch else out, 1 if accum else 0, g, 8,
+                                 None if res is None else res.t, 0 if res is None else res.ld,
+                                 None if epi is None else epi.mask, None if epi is None else epi.yc.t,
+                                 None if epi is None else c.mean, None if epi is None else c.rstd,
+                                 None if epi is None or one is None else epi.y1.t,
+                                 None if epi is None or one is None else one.mean,
+                                 None if epi is None or one is None else one.rstd,
+                                 None if part is None else (tuner.scratch_like(part) if scratch else part),
+                                 None, None, cfg)
+            cfg = tuner.launch(("er", accum, res is not None, epi is not None,
+                                epi is not None and one is not None) + tuple(g), g, 8, run)
+            if epi is None:
+                return None
+            bm = tuner.bm(cfg, g[1])
+            return part, (g[0] + bm - 1) // bm
         for g in geo:
             if accum and g[28] == 0:
                 continue
-            C.conv_igemm(dy.t, self.wd, out, None, None, None, 0, 1 if accum else 0, g, 8)
+
+            def run(cfg, scratch, g=g):
+                C.conv_igemm(dy.t, self.wd, tuner.scratch_like(out) if scratch else out, None, None, None, 0,
+                             1 if accum else 0, g, 8, cfg)
+            tuner.launch(("d", accum) + tuple(g), g, 8, run)
         return None
 
     def bn_backward(self, g: Act, y: Act, mask_mode: int, mo: Optional[Act], mxf: Optional[_Xf],
@@ -513,6 +536,8 @@ class FusedNet:
         self.device = torch.device(device)
         model.to(self.device)
         self.prof: Optional[List] = None   # [(label, event)] when per-op profiling is enabled
+        from ..ops.tune import ConvTuner
+        self.tuner = ConvTuner(require(), enabled=not deterministic and torch.device(device).type == "cuda")
         self._ws: Dict = {}
         self._splits: Dict = {}
         self._bnb: Dict = {}

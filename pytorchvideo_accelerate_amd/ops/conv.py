@@ -150,8 +150,11 @@ def dgrad_phases(spec: ConvSpec, N: int, in_dims: Triple, out_dims: Triple, ldx:
     return geo
 
 
-def conv_m_tiles(M: int, N: int) -> int:
-    return require().conv_m_tiles(M, N)
+def conv_m_tiles(M: int, N: int, spec: Optional["ConvSpec"] = None) -> int:
+    """Row tiles of the forward BN partial sums (``spec`` selects the kernel family the launch will use)."""
+    if spec is None:
+        return require().conv_m_tiles(M, N)
+    return require().conv_m_tiles(M, N, spec.taps * spec.cin_pad, spec.cin_pad)
 
 
 def conv_fwd(x: Act, wpack: torch.Tensor, spec: ConvSpec, out: Optional[torch.Tensor] = None,

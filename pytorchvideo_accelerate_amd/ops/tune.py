@@ -1,0 +1,101 @@
+"""First-use autotuning of implicit-GEMM conv launch configurations (cuDNN-benchmark-mode analogue).
+
+The gfx950 conv kernel (csrc/kernels/conv_igemm.hip) has several launch configurations per conv: output
+tile (128x128, 128x64, 256x32, 256x16), K depth per LDS stage (BK 32 / 64) and the uniform-tap loader
+on or off.  Which one wins depends on the layer (measured: the uniform-tap loader is 20-25 % faster on
+3x3 convs with the consumer-side BN fold and 15-30 % slower on padded temporal convs; BK=64 wins only for
+deep K).  The first time a geometry is launched, :class:`ConvTuner` times every legal configuration on
+scratch outputs (same shapes and strides, so inputs and real outputs are untouched — including
+accumulating dgrads), caches the fastest and launches it for real.  Every configuration accumulates K in
+the same order, so the result does not depend on the choice.
+
+Disabled by ``PVA_AUTOTUNE=0`` and in deterministic mode (the built-in heuristic is used instead).
+"""
+from __future__ import annotations
+
+import os
+from typing import Callable, Dict, List, Sequence, Tuple
+
+import torch
+
+EXPLICIT = 16          # cfg bit: explicit configuration (else the kernel's heuristic)
+BK64 = 4
+UT = 8
+TILE_BN = (128, 64, 32, 16)   # variants 0..3
+TILE_BM = (128, 128, 256, 256)
+
+
+def cfg_word(variant: int, bk: int, ut: bool) -> int:
+    return EXPLICIT | variant | (BK64 if bk == 64 else 0) | (UT if ut else 0)
+
+
+class ConvTuner:
+    def __init__(self, C, enabled: bool = True, reps: int = 3):
+        self.C = C
+        self.enabled = enabled and os.environ.get("PVA_AUTOTUNE", "1") != "0"
+        self.reps = reps
+        self.cache: Dict[Tuple, int] = {}
+        self._scratch: Dict[Tuple, torch.Tensor] = {}
+
+    # ---------------------------------------------------------------- candidates
+    def candidates(self, g: Sequence[int], chunk: int) -> List[int]:
+        N, Cg = g[1], g[3]
+        K = g[28] * g[29] * g[30] * Cg
+        out = []
+        for v, bn in enumerate(TILE_BN):
+            if bn > 16 and bn >= 2 * N:      # tile much wider than the output channels
+                continue
+            if bn * 8 < N:                   # tile far narrower than N: many redundant A re-reads
+                continue
+            for bk in (32, 64):
+                if bk == 64 and (chunk != 8 or K < 64):
+                    continue
+                uts = [False]
+                if chunk == 8 and self.C.conv_ut_legal(list(g), chunk, bk):
+                    uts.append(True)
+                for ut in uts:
+                    out.append(cfg_word(v, bk, ut))
+        return out
+
+    def bm(self, cfg: int, N: int) -> int:
+        return int(self.C.conv_cfg_bm(cfg, N))
+
+    def scratch_like(self, t: torch.Tensor) -> torch.Tensor:
+        key = (tuple(t.shape), tuple(t.stride()), t.dtype, t.device)
+        s = self._scratch.get(key)
+        if s is None:
+            s = torch.empty_strided(t.shape, t.stride(), dtype=t.dtype, device=t.device)
+            if s.dtype.is_floating_point:
+                s.zero_()
+            self._scratch[key] = s
+        return s
+
+    # ---------------------------------------------------------------- launch
+    def launch(self, key: Tuple, g: Sequence[int], chunk: int, run: Callable[[int, bool], None]) -> int:
+        """``run(cfg, scratch)`` performs the launch (into scratch outputs when ``scratch``).  Returns the
+        configuration used for the real launch (-1 = kernel heuristic)."""
+        cfg = self.cache.get(key)
+        if cfg is None:
+            cfg = self._tune(g, chunk, run) if self.enabled else -1
+            self.cache[key] = cfg
+        run(cfg, False)
+        return cfg
+
+    def _tune(self, g: Sequence[int], chunk: int, run: Callable[[int, bool], None]) -> int:
+        cands = self.candidates(g, chunk)
+        if len(cands) <= 1:
+            return cands[0] if cands else -1
+        best, best_t = -1, float("inf")
+        for cfg in cands:
+            run(cfg, True)  # warm-up (instruction cache, first-touch)
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(self.reps):
+                run(cfg, True)
+            e1.record()
+            e1.synchronize()
+            t = e0.elapsed_time(e1)
+            if t < best_t:
+                best, best_t = cfg, t
+        return best

@@ -70,7 +70,7 @@ def test_conv_fwd_stats_and_affine(case):
     from pytorchvideo_accelerate_amd.ops.conv import conv_m_tiles
     To, Ho, Wo = spec.out_dims(xa.T, xa.H, xa.W)
     M = xa.N * To * Ho * Wo
-    tiles = conv_m_tiles(M, spec.cout)
+    tiles = conv_m_tiles(M, spec.cout, spec)
     stats = torch.empty(tiles, 2, spec.cout, device=DEV)
     y = conv_fwd(xa, wf, spec, stats=stats, in_scale=sc, in_shift=sh, in_relu=True)
     assert rel_err(y.to_ncthw(), ref) < 1.5e-2
@@ -94,6 +94,49 @@ def test_conv_dgrad(case):
     # accumulate mode
     dx2 = conv_dgrad(dy, wd, spec, tuple(x.shape[2:]), out=dx.t.clone(), accum=True)
     assert rel_err(dx2.to_ncthw(), 2 * x.grad) < 1.5e-2
+
+
+# fast-pathway shapes at realistic row counts (M >= 32768): small-channel tiles, strided dgrad phases
+STREAM_CASES = [
+    (8, 8, (1, 3, 3), (1, 1, 1), (0, 1, 1), (2, 16, 40, 40)),      # fast res2 conv_b
+    (32, 8, (3, 1, 1), (1, 1, 1), (1, 0, 0), (2, 16, 32, 32)),     # fast res2 conv_a
+    (8, 32, (1, 1, 1), (1, 1, 1), (0, 0, 0), (2, 16, 32, 32)),     # fast res2 conv_c
+    (16, 16, (1, 3, 3), (1, 2, 2), (0, 1, 1), (2, 16, 64, 64)),    # fast res3 conv_b stride 2
+    (16, 64, (1, 1, 1), (1, 1, 1), (0, 0, 0), (2, 16, 32, 32)),    # fast res3 conv_c (N = 64)
+    (64, 16, (3, 1, 1), (1, 1, 1), (1, 0, 0), (2, 16, 32, 32)),    # K = 192 (KC = 32 variant)
+]
+
+
+@pytest.mark.parametrize("case", STREAM_CASES)
+def test_small_channel_fwd_stats_affine_dgrad(case):
+    from pytorchvideo_accelerate_amd.ops._ext import require
+    from pytorchvideo_accelerate_amd.ops.conv import conv_m_tiles
+    C = require()
+    x, w, spec = _mk(case, seed=21)
+    Cin = spec.cin
+    sc = torch.rand(Cin, device=DEV) + 0.5
+    sh = torch.randn(Cin, device=DEV) * 0.5
+    xa = Act.from_ncthw(x)
+    xt = torch.relu(x * sc.view(1, Cin, 1, 1, 1) + sh.view(1, Cin, 1, 1, 1))
+    ref = torch.nn.functional.conv3d(xt, w, None, spec.stride, spec.pad)
+    wf, wd = pack_weight(w, spec)
+    To, Ho, Wo = spec.out_dims(xa.T, xa.H, xa.W)
+    M = xa.N * To * Ho * Wo
+    assert M >= 32768
+    stats = torch.full((conv_m_tiles(M, spec.cout, spec), 2, spec.cout), float("nan"), device=DEV)
+    y = conv_fwd(xa, wf, spec, stats=stats, in_scale=sc, in_shift=sh, in_relu=True)
+    assert rel_err(y.to_ncthw(), ref) < 1.5e-2
+    yf = y.t.float()
+    torch.testing.assert_close(stats.sum(0)[0], yf.sum(0), rtol=1e-3, atol=1e-2 * yf.abs().sum(0).max().item() / M ** 0.5)
+    torch.testing.assert_close(stats.sum(0)[1], (yf * yf).sum(0), rtol=1e-3, atol=1e-3)
+    # dgrad (incl. stride-2 phases) and accumulate through the same kernel family
+    gy = torch.randn_like(ref).to(torch.bfloat16).float()
+    dx_ref = torch.nn.grad.conv3d_input(x.shape, w, gy, spec.stride, spec.pad)
+    dy = Act.from_ncthw(gy)
+    dx = conv_dgrad(dy, wd, spec, tuple(x.shape[2:]))
+    assert rel_err(dx.to_ncthw(), dx_ref) < 1e-2
+    dx2 = conv_dgrad(dy, wd, spec, tuple(x.shape[2:]), out=dx.t.clone(), accum=True)
+    assert rel_err(dx2.to_ncthw(), 2 * dx_ref) < 1.5e-2
 
 
 def _bits(mask):
