@@ -72,4 +72,5 @@ struct WgradParams {
   int splits, p_per_split;
   int slab;                 // 1: deterministic mode — split s stores into partial + s*Cout*K (no atomics)
   unsigned dybytes, xbytes; // buffer-resource extents
+  int variant;              // tile variant (0: 16x128, 1: 32x128, 2: 64x64, 3: 128x64); -1 = heuristic
 };

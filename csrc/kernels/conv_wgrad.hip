@@ -368,8 +368,8 @@ static int wgrad_variant(int Cout, int K) {
   return 3;                   // 128 x 64
 }
 
-void conv_wgrad_tile(int Cout, int K, int* bmw, int* bnw) {
-  switch (wgrad_variant(Cout, K)) {
+void conv_wgrad_tile(int Cout, int K, int variant, int* bmw, int* bnw) {
+  switch (variant >= 0 ? variant : wgrad_variant(Cout, K)) {
     case 0: *bmw = 16; *bnw = 128; break;
     case 1: *bmw = 32; *bnw = 128; break;
     case 2: *bmw = 64; *bnw = 64; break;
@@ -378,7 +378,7 @@ void conv_wgrad_tile(int Cout, int K, int* bmw, int* bnw) {
 }
 
 void conv_wgrad_launch(const WgradParams& p, int chunk, hipStream_t stream) {
-  const int v = wgrad_variant(p.Cout, p.K);
+  const int v = p.variant >= 0 ? (p.variant & 3) : wgrad_variant(p.Cout, p.K);
   if (chunk == 8) {
     switch (v) {
       case 0: launch_w<16, 128, 16, 32, 8>(p, stream); break;

@@ -22,7 +22,7 @@ int conv_igemm_m_tiles(int M, int N);
 int conv_igemm_m_tiles_k(int M, int N, int K, int Cg);
 void conv_igemm_set_bk(int bk);
 void conv_wgrad_launch(const WgradParams& p, int chunk, hipStream_t stream);
-void conv_wgrad_tile(int Cout, int K, int* bmw, int* bnw);
+void conv_wgrad_tile(int Cout, int K, int variant, int* bmw, int* bnw);
 void wgrad_reduce_launch(float* accbuf, float* grad, int splits, int Cout, int taps, int Cin, int Cin_real,
                          float scale, float beta, int slab, hipStream_t stream);
 void bn_finalize_launch(const float* part, int tiles, int C, int64_t count, const float* gamma, const float* beta,
@@ -175,15 +175,16 @@ int64_t conv_m_tiles(int64_t M, int64_t N, int64_t K, int64_t Cg) {
   return K > 0 ? conv_igemm_m_tiles_k((int)M, (int)N, (int)K, (int)Cg) : conv_igemm_m_tiles((int)M, (int)N);
 }
 
-std::vector<int64_t> wgrad_tile(int64_t Cout, int64_t K) {
+std::vector<int64_t> wgrad_tile(int64_t Cout, int64_t K, int64_t variant) {
   int a, b;
-  conv_wgrad_tile((int)Cout, (int)K, &a, &b);
+  conv_wgrad_tile((int)Cout, (int)K, (int)variant, &a, &b);
   return {a, b};
 }
 
 // geometry: [P, Cout, K, Cin, ldd, ldx, Ti, Hi, Wi, To, Ho, Wo, kt, kh, kw, st, sh, sw, pt, ph, pw, splits, pps]
 void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& partial, const OptT& scale,
-                const OptT& shift, int64_t affine, std::vector<int64_t> g, int64_t chunk, int64_t slab) {
+                const OptT& shift, int64_t affine, std::vector<int64_t> g, int64_t chunk, int64_t slab,
+                int64_t variant) {
   TORCH_CHECK(g.size() == 23, "wgrad geometry must have 23 entries");
   WgradParams p{};
   p.dy = bfp(dy); p.x = bfp(x); p.partial = f32(partial);
@@ -195,6 +196,7 @@ void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& par
   TORCH_CHECK(p.Cin % chunk == 0 && p.Cout % 8 == 0, "wgrad channel alignment");
   TORCH_CHECK(p.p_per_split % 32 == 0, "p_per_split must be a multiple of 32");
   p.slab = (int)slab;
+  p.variant = (int)variant;
   TORCH_CHECK(dy.numel() * 2 < 0xFFFFFF00ll && x.numel() * 2 < 0xFFFFFF00ll, "buffer extents must fit 32 bits");
   p.dybytes = (unsigned)(dy.numel() * 2);
   p.xbytes = (unsigned)(x.numel() * 2);
@@ -378,9 +380,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_m_tiles", &conv_m_tiles, py::arg("M"), py::arg("N"), py::arg("K") = 0, py::arg("Cg") = 0);
   m.def("conv_set_bk", [](int64_t bk) { conv_igemm_set_bk((int)bk); });
   m.def("conv_set_ut", [](int64_t mode) { conv_igemm_set_ut((int)mode); });
-  m.def("wgrad_tile", &wgrad_tile);
+  m.def("wgrad_tile", &wgrad_tile, py::arg("Cout"), py::arg("K"), py::arg("variant") = -1);
   m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("partial"), py::arg("scale"),
-        py::arg("shift"), py::arg("affine"), py::arg("g"), py::arg("chunk"), py::arg("slab") = 0);
+        py::arg("shift"), py::arg("affine"), py::arg("g"), py::arg("chunk"), py::arg("slab") = 0,
+        py::arg("variant") = -1);
   m.def("wgrad_reduce", &wgrad_reduce, py::arg("partial"), py::arg("grad"), py::arg("splits"), py::arg("Cout"),
         py::arg("taps"), py::arg("Cin"), py::arg("Cin_real"), py::arg("scale"), py::arg("beta"), py::arg("slab") = 0);
   m.def("bn_finalize", &bn_finalize);

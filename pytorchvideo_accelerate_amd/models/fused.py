@@ -163,22 +163,63 @@ class _ConvBN:
         eng, s, C = self.eng, self.spec, self.eng.C
         eng.mark(self.name + ".wgrad")
         K = s.taps * s.cin_pad
-        key = (self.name, "wsplit", dy.M)
-        sp = eng._splits.get(key)
-        if sp is None:
-            from ..ops.conv import wgrad_splits
-            sp = eng._splits[key] = wgrad_splits(dy.M, s.cout, K, target_blocks=256 if eng.deterministic else 1024)
-        splits, pps = sp
+        from ..ops.conv import wgrad_splits
+        aff = 0 if xf is None else (2 if xf.relu else 1)
+        sc_, sh_ = (None, None) if xf is None else (xf.scale, xf.shift)
         slab = 1 if eng.deterministic else 0
+
+        def geometry(cfg):
+            """(splits, rows per split, tile variant) of launch configuration ``cfg``."""
+            key = (self.name, "wsplit", dy.M, cfg)
+            sp = eng._splits.get(key)
+            if sp is None:
+                if cfg < 0:
+                    sp = wgrad_splits(dy.M, s.cout, K, target_blocks=256 if slab else 1024) + (-1,)
+                else:
+                    v, tb = cfg & 3, (512, 1024, 2048)[(cfg >> 2) & 3]
+                    sp = wgrad_splits(dy.M, s.cout, K, target_blocks=tb, variant=v) + (v,)
+                eng._splits[key] = sp
+            return sp
+
+        def launch(cfg, part):
+            splits, pps, v = geometry(cfg)
+            g = [dy.M, s.cout, K, s.cin_pad, dy.ld, x.ld, x.T, x.H, x.W, dy.T, dy.H, dy.W,
+                 *s.k, *s.stride, *s.pad, splits, pps]
+            C.conv_wgrad(dy.t, x.t, part, sc_, sh_, aff, g, s.chunk, slab, v)
+            return splits
+
+        tkey = ("w", dy.M, dy.ld, x.ld, x.T, x.H, x.W, s.cout, K, s.chunk, aff) + tuple(s.k) + tuple(s.stride)
+        cfg = eng.wtune.get(tkey)
+        if cfg is None:
+            cfg = -1
+            if eng.tuner.enabled and not slab:
+                # first use: time tile variant x split-K target on a scratch accumulator (atomic adds; the
+                # scratch content is irrelevant), keep the fastest
+                scratch = eng.scratch("wgrad_tune", s.cout * K)
+                best = None
+                for v in range(4):
+                    bmw = C.wgrad_tile(s.cout, K, v)[0]
+                    if bmw > max(16, s.cout) or bmw * 8 < s.cout:
+                        continue
+                    for tbi in range(3):
+                        c = 16 | v | (tbi << 2)
+                        launch(c, scratch)
+                        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                        e0.record()
+                        for _ in range(3):
+                            launch(c, scratch)
+                        e1.record()
+                        e1.synchronize()
+                        t = e0.elapsed_time(e1)
+                        if best is None or t < best[0]:
+                            best = (t, c)
+                cfg = best[1] if best else -1
+            eng.wtune[tkey] = cfg
         if slab:  # per-split slabs summed in a fixed order: bitwise reproducible weight gradients
-            part = eng.scratch("wgrad_slab", splits * s.cout * K)
+            part = eng.scratch("wgrad_slab", geometry(cfg)[0] * s.cout * K)
         else:     # fp32 atomics into one zeroed accumulator (kept zero by wgrad_reduce)
             part = eng.scratch("wgrad_acc", s.cout * K, zero=True)
-        aff = 0 if xf is None else (2 if xf.relu else 1)
-        g = [dy.M, s.cout, K, s.cin_pad, dy.ld, x.ld, x.T, x.H, x.W, dy.T, dy.H, dy.W,
-             *s.k, *s.stride, *s.pad, splits, pps]
-        C.conv_wgrad(dy.t, x.t, part, None if xf is None else xf.scale, None if xf is None else xf.shift, aff, g,
-                     s.chunk, slab)
+        splits = launch(cfg, part)
         C.wgrad_reduce(part, eng.flat.gview(self.conv.weight), splits, s.cout, s.taps, s.cin_pad, s.cin, 1.0,
                        eng.grad_beta, slab)
 
@@ -538,6 +579,7 @@ class FusedNet:
         self.prof: Optional[List] = None   # [(label, event)] when per-op profiling is enabled
         from ..ops.tune import ConvTuner
         self.tuner = ConvTuner(require(), enabled=not deterministic and torch.device(device).type == "cuda")
+        self.wtune: Dict = {}
         self._ws: Dict = {}
         self._splits: Dict = {}
         self._bnb: Dict = {}

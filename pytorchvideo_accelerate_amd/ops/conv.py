@@ -188,9 +188,10 @@ def conv_dgrad(dy: Act, wt_pack: torch.Tensor, spec: ConvSpec, in_dims: Triple, 
     return Act(out, dy.N, Ti, Hi, Wi)
 
 
-def wgrad_splits(P: int, Cout: int, K: int, target_blocks: int = 1024, min_rows: int = 1024) -> Tuple[int, int]:
+def wgrad_splits(P: int, Cout: int, K: int, target_blocks: int = 1024, min_rows: int = 1024,
+                 variant: int = -1) -> Tuple[int, int]:
     C = require()
-    bmw, bnw = C.wgrad_tile(Cout, K)
+    bmw, bnw = C.wgrad_tile(Cout, K, variant)
     tiles = ((Cout + bmw - 1) // bmw) * ((K + bnw - 1) // bnw)
     splits = max(1, min(target_blocks // max(tiles, 1), (P + min_rows - 1) // min_rows))
     pps = (P + splits - 1) // splits
