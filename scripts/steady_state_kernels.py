@@ -1,0 +1,57 @@
+"""Steady-state per-kernel summary from a rocprofv3 ``--kernel-trace`` CSV.
+
+The first steps of a run include first-use autotuning (ops/tune.py) and warm-up, which pollute
+``--stats``.  This keeps only the kernels of the last ``--steps`` training steps, using the fused SGD
+kernel (one launch per optimizer step) as the step delimiter, and prints per-kernel and per-family GPU
+time per step plus the wall span of those steps.
+
+    python scripts/steady_state_kernels.py gpurun_out/prof/x_kernel_trace.csv --steps 2 > profiles/.../kernels.txt
+"""
+import argparse
+import collections
+import csv
+import re
+
+
+def family(name: str) -> str:
+    m = re.search(r"(\w+_kernel)", name)
+    base = m.group(1) if m else name[:40]
+    t = re.search(r"<([^>]*)>", name)
+    return base, (base + ("<" + t.group(1) + ">" if t else ""))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--delim", default="sgd_momentum_kernel")
+    ap.add_argument("--top", type=int, default=40)
+    a = ap.parse_args()
+    rows = list(csv.DictReader(open(a.trace)))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    ends = [i for i, r in enumerate(rows) if a.delim in r["Kernel_Name"]]
+    assert len(ends) > a.steps, f"need > {a.steps} optimizer steps in the trace, found {len(ends)}"
+    lo, hi = ends[-a.steps - 1] + 1, ends[-1] + 1
+    sel = rows[lo:hi]
+    span = (int(sel[-1]["End_Timestamp"]) - int(sel[0]["Start_Timestamp"])) / 1e6 / a.steps
+    per = collections.defaultdict(lambda: [0.0, 0])
+    fam = collections.defaultdict(float)
+    for r in sel:
+        d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+        f, full = family(r["Kernel_Name"])
+        per[full][0] += d
+        per[full][1] += 1
+        fam[f] += d
+    busy = sum(v[0] for v in per.values()) / a.steps
+    print(f"# steady state over the last {a.steps} optimizer steps: wall span {span:.2f} ms/step, "
+          f"kernel busy {busy:.2f} ms/step ({100 * busy / span:.1f}% of span), {len(sel) // a.steps} launches/step")
+    print("\n# per kernel family (ms/step)")
+    for k, v in sorted(fam.items(), key=lambda kv: -kv[1]):
+        print(f"{v / a.steps:9.3f}  {100 * v / a.steps / busy:5.1f}%  {k}")
+    print(f"\n# top {a.top} kernel instantiations (ms/step, launches/step)")
+    for k, (t, n) in sorted(per.items(), key=lambda kv: -kv[1][0])[:a.top]:
+        print(f"{t / a.steps:9.3f}  {n // a.steps:4d}  {k[:120]}")
+
+
+if __name__ == "__main__":
+    main()
