@@ -665,8 +665,13 @@ static int pick_variant(int M, int N) {
 }
 
 // Launch configuration word: tile variant (bits 0-1: 128x128, 128x64, 256x32, 256x16), BK (bit 2: 32 / 64),
-// uniform-tap loader (bit 3), bit 4 set = explicit (else the built-in heuristic).  -1 = heuristic.
+// uniform-tap loader (bit 3), bit 4 set = explicit (else the built-in heuristic), bit 5 = the narrow
+// direct-to-register kernel of conv_direct.hip (bit 6: 2048 rows per workgroup, else 512).  -1 = heuristic.
+int conv_direct_rows(int cfg);
+void conv_direct_launch(const ConvParams& p, int cfg, hipStream_t s);
+
 int conv_cfg_bm(int cfg, int N) {
+  if (cfg >= 0 && (cfg & 16) && (cfg & 32)) return conv_direct_rows(cfg);
   const int v = (cfg >= 0 && (cfg & 16)) ? (cfg & 3) : pick_variant(0, N);
   return v <= 1 ? 128 : 256;
 }
@@ -688,6 +693,10 @@ int conv_igemm_ut_legal(const ConvParams& p, int chunk, int bk) { return conv_ut
 void conv_igemm_launch(const ConvParams& p, int chunk, hipStream_t stream, int cfg) {
   if ((p.eres || p.emask || p.epart) && chunk != 8) return;  // host binding rejects this combination
   int v, bk, ut_force;
+  if (cfg >= 0 && (cfg & 16) && (cfg & 32)) {  // narrow direct-to-register kernel (conv_direct.hip)
+    conv_direct_launch(p, cfg, stream);
+    return;
+  }
   if (cfg >= 0 && (cfg & 16)) {
     v = cfg & 3;
     bk = (cfg & 4) ? 64 : 32;

@@ -17,6 +17,7 @@ static_assert(offsetof(ConvParams, bws) - offsetof(ConvParams, M) == 38 * sizeof
 void conv_igemm_launch(const ConvParams& p, int chunk, hipStream_t stream, int cfg);
 int conv_cfg_bm(int cfg, int N);
 int conv_igemm_ut_legal(const ConvParams& p, int chunk, int bk);
+int conv_direct_legal(const ConvParams& p, int chunk);
 void conv_igemm_set_ut(int mode);
 int conv_igemm_m_tiles(int M, int N);
 int conv_igemm_m_tiles_k(int M, int N, int K, int Cg);
@@ -372,6 +373,12 @@ PYBIND11_MODULE(_C, m) {
     int* f = &q.M;
     for (int i = 0; i < 39 && i < (int)g.size(); ++i) f[i] = (int)g[i];
     return (int64_t)conv_igemm_ut_legal(q, (int)chunk, (int)bk);
+  });
+  m.def("conv_direct_legal", [](std::vector<int64_t> g, int64_t chunk) {
+    ConvParams q{};
+    int* f = &q.M;
+    for (int i = 0; i < 39 && i < (int)g.size(); ++i) f[i] = (int)g[i];
+    return (int64_t)conv_direct_legal(q, (int)chunk);
   });
   m.def("conv_igemm_epi", &conv_igemm_epi, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("accum"), py::arg("g"),
         py::arg("chunk"), py::arg("res"), py::arg("ldr"), py::arg("mask"), py::arg("y0"), py::arg("mean0"),

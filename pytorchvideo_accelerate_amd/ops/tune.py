@@ -2,7 +2,8 @@
 
 The gfx950 conv kernel (csrc/kernels/conv_igemm.hip) has several launch configurations per conv: output
 tile (128x128, 128x64, 256x32, 256x16), K depth per LDS stage (BK 32 / 64) and the uniform-tap loader
-on or off.  Which one wins depends on the layer (measured: the uniform-tap loader is 20-25 % faster on
+on or off; convs with <= 64 output channels can also run the direct-to-register kernel
+(csrc/kernels/conv_direct.hip, 512 or 2048 rows per workgroup; ``PVA_CONV_DIRECT=0`` excludes it).  Which one wins depends on the layer (measured: the uniform-tap loader is 20-25 % faster on
 3x3 convs with the consumer-side BN fold and 15-30 % slower on padded temporal convs; BK=64 wins only for
 deep K).  The first time a geometry is launched, :class:`ConvTuner` times every legal configuration on
 scratch outputs (same shapes and strides, so inputs and real outputs are untouched — including
@@ -14,6 +15,7 @@ Disabled by ``PVA_AUTOTUNE=0`` and in deterministic mode (the built-in heuristic
 from __future__ import annotations
 
 import os
+import sys
 from typing import Callable, Dict, List, Sequence, Tuple
 
 import torch
@@ -21,8 +23,19 @@ import torch
 EXPLICIT = 16          # cfg bit: explicit configuration (else the kernel's heuristic)
 BK64 = 4
 UT = 8
+DIRECT = 32           # narrow direct-to-register kernel (csrc/kernels/conv_direct.hip)
+DIRECT_2K = 64        #   with 2048 rows per workgroup (else 512)
 TILE_BN = (128, 64, 32, 16)   # variants 0..3
 TILE_BM = (128, 128, 256, 256)
+
+
+def describe(cfg: int) -> str:
+    """Human-readable configuration word (``PVA_TUNE_LOG=1`` prints every candidate's time)."""
+    if cfg < 0 or not cfg & EXPLICIT:
+        return "heuristic"
+    if cfg & DIRECT:
+        return "direct%d" % (2048 if cfg & DIRECT_2K else 512)
+    return "%dx%d/bk%d%s" % (TILE_BM[cfg & 3], TILE_BN[cfg & 3], 64 if cfg & BK64 else 32, "/ut" if cfg & UT else "")
 
 
 def cfg_word(variant: int, bk: int, ut: bool) -> int:
@@ -33,6 +46,8 @@ class ConvTuner:
     def __init__(self, C, enabled: bool = True, reps: int = 3):
         self.C = C
         self.enabled = enabled and os.environ.get("PVA_AUTOTUNE", "1") != "0"
+        self.direct = os.environ.get("PVA_CONV_DIRECT", "1") != "0"
+        self.log = os.environ.get("PVA_TUNE_LOG", "0") != "0"
         self.reps = reps
         self.cache: Dict[Tuple, int] = {}
         self._scratch: Dict[Tuple, torch.Tensor] = {}
@@ -55,6 +70,8 @@ class ConvTuner:
                     uts.append(True)
                 for ut in uts:
                     out.append(cfg_word(v, bk, ut))
+        if self.direct and self.C.conv_direct_legal(list(g), chunk):
+            out += [EXPLICIT | DIRECT, EXPLICIT | DIRECT | DIRECT_2K]
         return out
 
     def bm(self, cfg: int, N: int) -> int:
@@ -86,6 +103,7 @@ class ConvTuner:
         if len(cands) <= 1:
             return cands[0] if cands else -1
         best, best_t = -1, float("inf")
+        times = []
         for cfg in cands:
             run(cfg, True)  # warm-up (instruction cache, first-touch)
             e0 = torch.cuda.Event(enable_timing=True)
@@ -96,6 +114,11 @@ class ConvTuner:
             e1.record()
             e1.synchronize()
             t = e0.elapsed_time(e1)
+            times.append((cfg, t / self.reps))
             if t < best_t:
                 best, best_t = cfg, t
+        if self.log:
+            print("tune M=%d N=%d K=%d taps=%s: " % (g[0], g[1], g[2], tuple(g[28:31]))
+                  + " ".join("%s=%.1fus" % (describe(c), 1e3 * t) for c, t in times)
+                  + " -> " + describe(best), file=sys.stderr, flush=True)
         return best

@@ -61,7 +61,11 @@ def test_fused_step_matches_oracle(slowfast):
         out_ac = ac([x.to(DEV) for x in xs] if slowfast else xs[0].to(DEV))
     loss_ac = F.cross_entropy(out_ac.float(), labels)
     loss_ac.backward()
-    tol = max(2e-2, 2 * abs(loss_ac.item() - loss_ref.item()))
+    # One autocast run is a single sample of that noise: equally valid bf16 executions that differ only in
+    # launch configuration (i.e. fp32 summation order of the BN partial sums) land up to ~4 % apart at this
+    # size (scripts/debug_direct.py: 2.246 / 2.258 / 2.320 / 2.338 for four configuration mixes; random-init
+    # BN nets amplify bf16 rounding with depth), so the loss floor is 8 %.
+    tol = max(8e-2, 2 * abs(loss_ac.item() - loss_ref.item()))
     assert abs(loss.item() - loss_ref.item()) < tol * max(1.0, abs(loss_ref.item()))
     ref_params = dict(oracle.named_parameters())
     ac_params = dict(ac.named_parameters())
