@@ -6,7 +6,9 @@
 //   * k is ordered (tap, channel), so each 16-B (8 x bf16) or 8-B (4 x bf16, stems with RGB0 input)
 //     chunk of a tile row is one contiguous global load of one tap; padding taps load zeros.
 //   * A (gathered activations) and B (weights) are register-staged into a double-buffered LDS tile
-//     (BK = 32, one MFMA k-step) with an XOR slot swizzle that makes every ds_read_b128 fragment read
+//     (BK = 32 or 64) through a one-stage-ahead register ring (tile s+1 is written to LDS right after the
+//     barrier of step s, tile s+2 is issued at once: one barrier per k-step, every load gets a whole
+//     k-step of MFMA work to land; cdna_hip_programming.md T14), with an XOR slot swizzle that makes every ds_read_b128 fragment read
 //     conflict-free ((slot ^ ((row>>2)&1)<<1), brute-force checked against the b128 lane groups).
 //   * Optional per-channel affine(+ReLU) is applied to A while staging: this is how a consumer conv
 //     applies the producer's training-mode BatchNorm + ReLU without that activation ever being
@@ -28,6 +30,21 @@ namespace {
 // LDS bytes before the stats/affine area: the double-buffered k tiles, or (EPI) the fp32 output tile.
 __host__ __device__ constexpr int main_lds_bytes(int BM, int BN, int BK, int EPI) {
   return (EPI && BM * (BN * 4 + 16) > 2 * (BM + BN) * BK * 2) ? BM * (BN * 4 + 16) : 2 * (BM + BN) * BK * 2;
+}
+
+// 16-B LDS-DMA of one lane: buffer_load_dwordx4 ... lds into wave-uniform LDS address `lds` + 16 * lane
+// (the address_space(3) cast only exists in the device pass; the host pass only needs the kernel stub)
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds, int voff, int soff) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
+#endif
+}
+
+// the XOR applied to a row's 16-B slot index by lds_off (an involution: slot ^ swz ^ swz == slot)
+template <int BK>
+__device__ __forceinline__ int lds_swz(int row) {
+  if constexpr (BK == 32) return ((row >> 2) & 1) << 1;
+  else return row & 6;
 }
 
 template <int BK>
@@ -104,7 +121,9 @@ void conv_igemm_kernel(const ConvParams p) {
     for (int j = 0; j < TN; ++j) fb[kk][j] = BM * BK * 2 + lds_off<BK>(wn * WN + j * 16 + frow, fslot + 4 * kk);
   }
 
-  if constexpr (UT) {
+  if constexpr (UT & 1) {
+    // UT bit 1: padding reachable (bounds tests), bits 2-3: consumer-side affine mode — compile-time, so
+    // the k-loop is branch-free
     // ================= uniform-tap loader (Cg % BK == 0, CH == 8) =================
     // Every k-step of the block lies inside one tap, so the tap / channel cursor is wave-uniform (SGPRs).
     // Raw buffer loads: weights = per-slot VGPR row offset + SGPR (tap, channel) offset -> no VALU;
@@ -115,7 +134,10 @@ void conv_igemm_kernel(const ConvParams p) {
     const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, (int)p.wbytes, 0x00020000);
     constexpr unsigned OOB = 0xFFFFFFF0u;
     const int col = tid % CPR;
-    const bool check = p.check != 0;
+    constexpr bool check = (UT >> 1) & 1;
+    constexpr int uaff = (UT >> 2) & 3;
+    constexpr bool glds_ut = (UT >> 4) & 1;
+    static_assert(!glds_ut || uaff == 0, "LDS-DMA staging cannot transform the A operand");
     const int GHW = p.Gh * p.Gw, GTHW = p.Gt * GHW;
     // most negative tap offset (dgrad walks taps backwards): the no-check form adds taps as a >= 0 soffset
     const int tmin = p.dir < 0 ? -(((p.nt - 1) * p.Gh + (p.nh - 1)) * p.Gw + (p.nw - 1)) * p.ldx : 0;
@@ -134,7 +156,9 @@ void conv_igemm_kernel(const ConvParams p) {
         const int qt = r / RHW; r -= qt * RHW;
         const int qh = r / p.Rw; const int qw = r - qh * p.Rw;
         at = qt * p.ast + p.aot; ah = qh * p.ash + p.aoh; aw = qw * p.asw + p.aow;
-        off = (b * GTHW + (at * p.Gh + ah) * p.Gw + aw) * p.ldx + col * 8;
+        // LDS-DMA staging: the lane's LDS slot is `col`, so it loads the logical chunk that the XOR swizzle
+        // places there (lds_off: physical slot = logical ^ swz(row), an involution)
+        off = (b * GTHW + (at * p.Gh + ah) * p.Gw + aw) * p.ldx + (glds_ut ? col ^ lds_swz<BK>(row) : col) * 8;
       }
       unsigned msk = 0;
       if (check && rv) {
@@ -157,7 +181,8 @@ void conv_igemm_kernel(const ConvParams p) {
       const int idx = tid + s * NT;
       const int row = idx / CPR;
       const int n = n0 + row;
-      b_vo[s] = (idx < B_CHUNKS && n < p.Ngemm) ? (n * p.Kfull + col * 8) * 2 : 0;  // columns >= N: ignored
+      const int bcol = glds_ut ? col ^ lds_swz<BK>(row) : col;
+      b_vo[s] = (idx < B_CHUNKS && n < p.Ngemm) ? (n * p.Kfull + bcol * 8) * 2 : 0;  // columns >= N: ignored
       sb[s] = lds_off<BK>(row, col);
     }
     // uniform k cursor
@@ -201,9 +226,9 @@ void conv_igemm_kernel(const ConvParams p) {
       char* B = A + BM * BK * 2;
 #pragma unroll
       for (int s = 0; s < A_SLOTS; ++s) {
-        if (tid + s * NT >= A_CHUNKS) break;
+        if constexpr (A_CHUNKS % NT != 0) if (tid + s * NT >= A_CHUNKS) break;
         uint4 v = ra[s];
-        if (affine) {
+        if constexpr (uaff != 0) {
           // packed consumer-side BN(+ReLU): 8 unpacks, 8 FMAs, 4 cvt_pk_bf16_f32, 4 v_pk_max_i16
           const float* sc = aff + ra_c + col * 8;
           const f32x4_t s0 = *reinterpret_cast<const f32x4_t*>(sc), s1 = *reinterpret_cast<const f32x4_t*>(sc + 4);
@@ -216,26 +241,74 @@ void conv_igemm_kernel(const ConvParams p) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) f[e] = __builtin_fmaf(f[e], sc8[e], sh8[e]);
           v = pack8_fast(f);
-          if (affine == 2) v = relu_bf16x8(v);
-          if (check && !((ra_valid >> s) & 1u)) v = uint4{0, 0, 0, 0};  // zero padding of the activation
+          if constexpr (uaff == 2) v = relu_bf16x8(v);
+          if constexpr (check) if (!((ra_valid >> s) & 1u)) v = uint4{0, 0, 0, 0};  // zero padding of the activation
         }
         *reinterpret_cast<uint4*>(A + sa[s]) = v;
       }
 #pragma unroll
       for (int s = 0; s < B_SLOTS; ++s) {
-        if (tid + s * NT >= B_CHUNKS) break;
+        if constexpr (B_CHUNKS % NT != 0) if (tid + s * NT >= B_CHUNKS) break;
         *reinterpret_cast<uint4*>(B + sb[s]) = rb[s];
       }
     };
     const int nsteps = (p.nt * p.nh * p.nw * p.Cg) / BK;
     __syncthreads();  // affine table ready
-    load();
-    store_lds(0);
-    __syncthreads();
+    // LDS-DMA staging (UT bit 4, no input affine): buffer_load ... lds writes each wave's 64 x 16 B straight
+    // into LDS (lane-linear: the XOR swizzle moves to the source column), skipping the VGPR round trip and
+    // the ds_write_b128 pass (~79 B/clk/CU, the LDS bottleneck of register staging).  Two buffers: the DMA
+    // of tile s+1 is issued right after the barrier of step s and lands during its MFMAs.
+    auto issue_dma = [&](int buf) {
+      char* A = smem + buf * TILE_BYTES;
+      char* B = A + BM * BK * 2;
+      const int ta = tapA + kb;
+#pragma unroll
+      for (int s = 0; s < A_SLOTS; ++s) {
+        const int rs = __builtin_amdgcn_readfirstlane((s * NT + 64 * wid) / CPR);
+        if constexpr (check) {
+          const bool v = (tmask[s] >> t_) & 1u;
+          dma16(xr, A + rs * BK * 2, v ? a_vo[s] + ta * 2 : (int)OOB, 0);
+        } else {
+          dma16(xr, A + rs * BK * 2, a_vo[s], (ta - tmin) * 2);
+        }
+      }
+      const int wso = (tapW + kb) * 2;
+#pragma unroll
+      for (int s = 0; s < B_SLOTS; ++s) {
+        if (s * NT + 64 * wid >= B_CHUNKS) break;   // wave-uniform (B_CHUNKS is a multiple of 64)
+        const int rs = __builtin_amdgcn_readfirstlane((s * NT + 64 * wid) / CPR);
+        dma16(wr, B + rs * BK * 2, b_vo[s], wso);
+      }
+      kb += BK;
+      if (kb == p.Cg) {
+        kb = 0;
+        ++t_;
+        if (++kw_ == p.nw) { kw_ = 0; if (++kh_ == p.nh) { kh_ = 0; ++kt_; } }
+        retap();
+      }
+    };
+    if constexpr (glds_ut) {
+      issue_dma(0);
+    } else {
+      // register ring one stage ahead of LDS: tile s+1 is written right after the barrier that frees its
+      // buffer, and tile s+2 is re-issued immediately, so each load has a full k-step of MFMA to land
+      load();
+      store_lds(0);
+      if (nsteps > 1) load();
+    }
     for (int step = 0; step < nsteps; ++step) {
       const int cur = step & 1;
-      const bool has_next = step + 1 < nsteps;
-      if (has_next) load();
+      if constexpr (glds_ut) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA of tile `step` has landed
+        __syncthreads();                                    // ... and every wave's; buffer cur^1 is free
+        if (step + 1 < nsteps) issue_dma(cur ^ 1);
+      } else {
+        __syncthreads();
+        if (step + 1 < nsteps) {
+          store_lds(cur ^ 1);
+          if (step + 2 < nsteps) load();
+        }
+      }
       const char* A = smem + cur * TILE_BYTES;
 #pragma unroll
       for (int kk = 0; kk < BK / 32; ++kk) {
@@ -250,8 +323,6 @@ void conv_igemm_kernel(const ConvParams p) {
           for (int j = 0; j < TN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
       }
-      if (has_next) store_lds(cur ^ 1);
-      __syncthreads();
     }
   } else {
   // ---- per-slot row coordinates (fixed over the K loop) ----
@@ -350,7 +421,7 @@ void conv_igemm_kernel(const ConvParams p) {
       char* B = A + BM * BK * 2;
   #pragma unroll
       for (int s = 0; s < A_SLOTS; ++s) {
-        if (tid + s * NT >= A_CHUNKS) break;
+        if constexpr (A_CHUNKS % NT != 0) if (tid + s * NT >= A_CHUNKS) break;
         VT v = ra[s];
         if (affine && (ra_valid >> s & 1)) {
           float f[CH];
@@ -366,7 +437,7 @@ void conv_igemm_kernel(const ConvParams p) {
       }
   #pragma unroll
       for (int s = 0; s < B_SLOTS; ++s) {
-        if (tid + s * NT >= B_CHUNKS) break;
+        if constexpr (B_CHUNKS % NT != 0) if (tid + s * NT >= B_CHUNKS) break;
         *reinterpret_cast<VT*>(B + sb[s]) = rb[s];
       }
     };
@@ -376,12 +447,15 @@ void conv_igemm_kernel(const ConvParams p) {
     __syncthreads();  // affine table ready
     load();
     store_lds(0);
-    __syncthreads();
-  
-    for (int step = 0; step < nsteps; ++step) {
+    if (nsteps > 1) load();
+
+    for (int step = 0; step < nsteps; ++step) {   // same one-stage-ahead register ring as above
       const int cur = step & 1;
-      const bool has_next = step + 1 < nsteps;
-      if (has_next) load();
+      __syncthreads();
+      if (step + 1 < nsteps) {
+        store_lds(cur ^ 1);
+        if (step + 2 < nsteps) load();
+      }
       const char* A = smem + cur * TILE_BYTES;
   #pragma unroll
       for (int kk = 0; kk < BK / 32; ++kk) {
@@ -396,11 +470,9 @@ void conv_igemm_kernel(const ConvParams p) {
           for (int j = 0; j < TN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
       }
-      if (has_next) store_lds(cur ^ 1);
-      __syncthreads();
     }
-  
   }
+  if constexpr (EPI == 1) __syncthreads();   // the fp32 staging below overwrites the k tiles
 
   // ---- epilogue: D[n][m] fragment: lane holds channels n..n+3 of position m ----
   // EPI 0: direct fragment stores, cs = sum y, cq = sum y^2 (forward BN statistics)
@@ -617,7 +689,7 @@ inline bool conv_ut_legal(const ConvParams& p, int ch, int bk) {
 }
 
 template <int BM, int BN, int WM, int WN, int CH, int BK>
-void launch_cfg(const ConvParams& p, int ut_force, hipStream_t stream) {
+void launch_cfg(const ConvParams& p, int ut_force, hipStream_t stream, bool dma = false) {
   constexpr int NT = (BM / WM) * (BN / WN) * 64;
   const int m_tiles = (p.M + BM - 1) / BM, n_tiles = (p.Ngemm + BN - 1) / BN;
   const bool epi = p.eres || p.emask || p.epart;
@@ -633,12 +705,32 @@ void launch_cfg(const ConvParams& p, int ut_force, hipStream_t stream) {
   const bool ut_pays = !p.check || (p.nt == 1 && p.ash == 1 && p.asw == 1);
   const bool ut = ut_legal && (ut_force >= 0 ? ut_force == 1 : (g_ut_mode == 2 || (g_ut_mode == 1 && ut_pays)));
   if constexpr (CH == 8) {
-    if (epi) {
-      if (ut) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 1, 1>), grid, block, lds, stream, p);
+    if (ut && dma && !p.affine) {   // LDS-DMA staged uniform-tap loader (UT word bit 4)
+      if (epi) {
+        if (p.check) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 1, 19>), grid, block, lds, stream, p);
+        else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 1, 17>), grid, block, lds, stream, p);
+      } else {
+        if (p.check) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 0, 19>), grid, block, lds, stream, p);
+        else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 0, 17>), grid, block, lds, stream, p);
+      }
+      return;
+    }
+    if (epi) {   // dgrad epilogue: never an input affine
+      if (ut && p.check) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 1, 3>), grid, block, lds, stream, p);
+      else if (ut) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 1, 1>), grid, block, lds, stream, p);
       else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 1, 0>), grid, block, lds, stream, p);
+    } else if (ut) {
+      // UT word = 1 | check << 1 | affine << 2 (compile-time loader variants)
+      switch ((p.check ? 2 : 0) | (p.affine << 2)) {
+        case 0: hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 0, 1>), grid, block, lds, stream, p); break;
+        case 2: hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 0, 3>), grid, block, lds, stream, p); break;
+        case 4: hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 0, 5>), grid, block, lds, stream, p); break;
+        case 6: hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 0, 7>), grid, block, lds, stream, p); break;
+        case 8: hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 0, 9>), grid, block, lds, stream, p); break;
+        default: hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 0, 11>), grid, block, lds, stream, p); break;
+      }
     } else {
-      if (ut) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 0, 1>), grid, block, lds, stream, p);
-      else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 0, 0>), grid, block, lds, stream, p);
+      hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 0, 0>), grid, block, lds, stream, p);
     }
   } else {
     hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 0, 0>), grid, block, lds, stream, p);
@@ -646,12 +738,12 @@ void launch_cfg(const ConvParams& p, int ut_force, hipStream_t stream) {
 }
 
 template <int CH, int BK>
-void launch_variant(int v, const ConvParams& p, int ut_force, hipStream_t stream) {
+void launch_variant(int v, const ConvParams& p, int ut_force, hipStream_t stream, bool dma = false) {
   switch (v) {
-    case 0: launch_cfg<128, 128, 64, 64, CH, BK>(p, ut_force, stream); break;
-    case 1: launch_cfg<128, 64, 64, 32, CH, BK>(p, ut_force, stream); break;
-    case 2: launch_cfg<256, 32, 64, 32, CH, BK>(p, ut_force, stream); break;
-    default: launch_cfg<256, 16, 64, 16, CH, BK>(p, ut_force, stream); break;
+    case 0: launch_cfg<128, 128, 64, 64, CH, BK>(p, ut_force, stream, dma); break;
+    case 1: launch_cfg<128, 64, 64, 32, CH, BK>(p, ut_force, stream, dma); break;
+    case 2: launch_cfg<256, 32, 64, 32, CH, BK>(p, ut_force, stream, dma); break;
+    default: launch_cfg<256, 16, 64, 16, CH, BK>(p, ut_force, stream, dma); break;
   }
 }
 
@@ -666,7 +758,8 @@ static int pick_variant(int M, int N) {
 
 // Launch configuration word: tile variant (bits 0-1: 128x128, 128x64, 256x32, 256x16), BK (bit 2: 32 / 64),
 // uniform-tap loader (bit 3), bit 4 set = explicit (else the built-in heuristic), bit 5 = the narrow
-// direct-to-register kernel of conv_direct.hip (bit 6: 2048 rows per workgroup, else 512).  -1 = heuristic.
+// direct-to-register kernel of conv_direct.hip (bit 6: 2048 rows per workgroup, else 512), bit 7 = LDS-DMA
+// staging of the uniform-tap loader (launches without an input affine).  -1 = heuristic.
 int conv_direct_rows(int cfg);
 void conv_direct_launch(const ConvParams& p, int cfg, hipStream_t s);
 
@@ -693,6 +786,7 @@ int conv_igemm_ut_legal(const ConvParams& p, int chunk, int bk) { return conv_ut
 void conv_igemm_launch(const ConvParams& p, int chunk, hipStream_t stream, int cfg) {
   if ((p.eres || p.emask || p.epart) && chunk != 8) return;  // host binding rejects this combination
   int v, bk, ut_force;
+  bool dma = false;
   if (cfg >= 0 && (cfg & 16) && (cfg & 32)) {  // narrow direct-to-register kernel (conv_direct.hip)
     conv_direct_launch(p, cfg, stream);
     return;
@@ -701,6 +795,7 @@ void conv_igemm_launch(const ConvParams& p, int chunk, hipStream_t stream, int c
     v = cfg & 3;
     bk = (cfg & 4) ? 64 : 32;
     ut_force = (cfg >> 3) & 1;
+    dma = (cfg & 128) != 0;   // LDS-DMA staging (uniform-tap loader, no input affine)
   } else {
     v = pick_variant(p.M, p.Ngemm);
     const int K = p.nt * p.nh * p.nw * p.Cg;
@@ -708,7 +803,7 @@ void conv_igemm_launch(const ConvParams& p, int chunk, hipStream_t stream, int c
     ut_force = -1;
   }
   if (chunk == 8) {
-    if (bk == 64) launch_variant<8, 64>(v, p, ut_force, stream); else launch_variant<8, 32>(v, p, ut_force, stream);
+    if (bk == 64) launch_variant<8, 64>(v, p, ut_force, stream, dma); else launch_variant<8, 32>(v, p, ut_force, stream, dma);
   } else {
     if (bk == 64) launch_variant<4, 64>(v, p, ut_force, stream); else launch_variant<4, 32>(v, p, ut_force, stream);
   }

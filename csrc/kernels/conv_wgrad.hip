@@ -18,7 +18,7 @@
 
 namespace {
 
-constexpr int BP = 32;  // positions per reduction step (one MFMA k-step)
+// BP (template): positions per LDS stage = 32 (one MFMA k-step) or 64 (two k-steps per barrier pair)
 
 template <int COLS>
 __device__ __forceinline__ int img_off(int row, int colbyte) {
@@ -42,9 +42,10 @@ __device__ __forceinline__ s16x4_t tr_read(const char* base) {
 
 // DENSE: 1x1x1, stride 1, no padding — the im2col row of position p is x row p, so both operands stream
 // with raw buffer loads whose per-step advance is one SGPR offset (no per-lane address math).
-template <int BMW, int BNW, int WMW, int WNW, int CH, int DENSE>
+template <int BMW, int BNW, int WMW, int WNW, int CH, int DENSE, int BP>
 __global__ __launch_bounds__((BMW / WMW) * (BNW / WNW) * 64)
 void conv_wgrad_kernel(const WgradParams p) {
+  static_assert(BP == 32 || BP == 64, "positions per stage");
   constexpr int NWN = BNW / WNW;
   constexpr int NT = (BMW / WMW) * NWN * 64;
   constexpr int A_CPR = BMW / 8;            // 16-B chunks per dY row
@@ -212,12 +213,12 @@ void conv_wgrad_kernel(const WgradParams p) {
     char* B = A + A_BYTES;
 #pragma unroll
     for (int s = 0; s < A_SLOTS; ++s) {
-      if (tid + s * NT >= A_CHUNKS) break;
+      if constexpr (A_CHUNKS % NT != 0) if (tid + s * NT >= A_CHUNKS) break;
       *reinterpret_cast<uint4*>(A + sa[s]) = ra[s];
     }
 #pragma unroll
     for (int s = 0; s < B_SLOTS; ++s) {
-      if (tid + s * NT >= B_CHUNKS) break;
+      if constexpr (B_CHUNKS % NT != 0) if (tid + s * NT >= B_CHUNKS) break;
       VT v = rb[s];
       if (affine) {
         // recompute the producer's BN(+ReLU) on the fly: packed cvt + v_pk_max_i16 ReLU
@@ -247,12 +248,13 @@ void conv_wgrad_kernel(const WgradParams p) {
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   const int nsteps = (p_end - p_begin + BP - 1) / BP;
-  __syncthreads();
+  // one-stage-ahead register ring (as conv_igemm.hip): stage s+1 is written right after the barrier of
+  // step s and stage s+2 issued at once, so each load has a whole step of MFMA work to land
   if (nsteps > 0) {
     load();
     store_lds(0);
   }
-  __syncthreads();
+  if (nsteps > 1) load();
 
   // tr-read addressing: group g = lane>>4 covers p rows 8g..8g+7; lane i = lane&15 supplies row
   // (i>>2) of a 4-row block and columns 4*(i&3)..+3 of the 16-column block.  Offsets precomputed.
@@ -274,31 +276,35 @@ void conv_wgrad_kernel(const WgradParams p) {
   }
   for (int step = 0; step < nsteps; ++step) {
     const int cur = step & 1;
-    const bool has_next = step + 1 < nsteps;
-    if (has_next) load();
-    const char* A = smem + cur * TILE;
-    bf16x8_t af[TM], bfr[TN];
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      s16x4_t lo = tr_read(A + ta[i][0]);
-      s16x4_t hi = tr_read(A + ta[i][1]);
-      s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      af[i] = __builtin_bit_cast(bf16x8_t, v);
-    }
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      s16x4_t lo = tr_read(A + tb[j][0]);
-      s16x4_t hi = tr_read(A + tb[j][1]);
-      s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      bfr[j] = __builtin_bit_cast(bf16x8_t, v);
-    }
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    if (has_next) store_lds(cur ^ 1);
     __syncthreads();
+    if (step + 1 < nsteps) {
+      store_lds(cur ^ 1);
+      if (step + 2 < nsteps) load();
+    }
+    const char* A = smem + cur * TILE;
+#pragma unroll
+    for (int kk = 0; kk < BP / 32; ++kk) {   // rows 32*kk.. of the stage: same swizzle (row bits 0-3)
+      bf16x8_t af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        s16x4_t lo = tr_read(A + kk * 32 * BMW * 2 + ta[i][0]);
+        s16x4_t hi = tr_read(A + kk * 32 * BMW * 2 + ta[i][1]);
+        s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        af[i] = __builtin_bit_cast(bf16x8_t, v);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        s16x4_t lo = tr_read(A + kk * 32 * BNW * 2 + tb[j][0]);
+        s16x4_t hi = tr_read(A + kk * 32 * BNW * 2 + tb[j][1]);
+        s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        bfr[j] = __builtin_bit_cast(bf16x8_t, v);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
   }
 
   // D[n][k]: lane holds k = col (lane&15), n = 4*(lane>>4) + r.  With one slab the tile is stored;
@@ -323,7 +329,7 @@ void conv_wgrad_kernel(const WgradParams p) {
     }
 }
 
-template <int BMW, int BNW, int WMW, int WNW, int CH>
+template <int BMW, int BNW, int WMW, int WNW, int CH, int BP>
 void launch_w(const WgradParams& p, hipStream_t stream) {
   constexpr int NT = (BMW / WMW) * (BNW / WNW) * 64;
   dim3 grid((p.Cout + BMW - 1) / BMW, (p.K + BNW - 1) / BNW, p.splits);
@@ -332,11 +338,21 @@ void launch_w(const WgradParams& p, hipStream_t stream) {
                      p.pt == 0 && p.ph == 0 && p.pw == 0;
   if constexpr (CH == 8) {
     if (dense) {
-      hipLaunchKernelGGL((conv_wgrad_kernel<BMW, BNW, WMW, WNW, CH, 1>), grid, dim3(NT), lds, stream, p);
+      hipLaunchKernelGGL((conv_wgrad_kernel<BMW, BNW, WMW, WNW, CH, 1, BP>), grid, dim3(NT), lds, stream, p);
       return;
     }
   }
-  hipLaunchKernelGGL((conv_wgrad_kernel<BMW, BNW, WMW, WNW, CH, 0>), grid, dim3(NT), lds, stream, p);
+  hipLaunchKernelGGL((conv_wgrad_kernel<BMW, BNW, WMW, WNW, CH, 0, BP>), grid, dim3(NT), lds, stream, p);
+}
+
+template <int CH, int BP>
+void launch_w_variant(int v, const WgradParams& p, hipStream_t stream) {
+  switch (v) {
+    case 0: launch_w<16, 128, 16, 32, CH, BP>(p, stream); break;
+    case 1: launch_w<32, 128, 32, 32, CH, BP>(p, stream); break;
+    case 2: launch_w<64, 64, 32, 32, CH, BP>(p, stream); break;
+    default: launch_w<128, 64, 64, 32, CH, BP>(p, stream); break;
+  }
 }
 
 // dW accumulator [Cout][taps][Cin_pad] -> grad[Cout][Cin][taps] (PyTorch layout),
@@ -369,7 +385,7 @@ static int wgrad_variant(int Cout, int K) {
 }
 
 void conv_wgrad_tile(int Cout, int K, int variant, int* bmw, int* bnw) {
-  switch (variant >= 0 ? variant : wgrad_variant(Cout, K)) {
+  switch (variant >= 0 ? (variant & 3) : wgrad_variant(Cout, K)) {
     case 0: *bmw = 16; *bnw = 128; break;
     case 1: *bmw = 32; *bnw = 128; break;
     case 2: *bmw = 64; *bnw = 64; break;
@@ -377,22 +393,15 @@ void conv_wgrad_tile(int Cout, int K, int variant, int* bmw, int* bnw) {
   }
 }
 
+// p.variant: -1 = heuristic tile, 32-position stages; else bits 0-1 = tile variant, bit 2 = 64-position stages
+// (p_per_split must then be a multiple of 64)
 void conv_wgrad_launch(const WgradParams& p, int chunk, hipStream_t stream) {
   const int v = p.variant >= 0 ? (p.variant & 3) : wgrad_variant(p.Cout, p.K);
+  const bool bp64 = p.variant >= 0 && (p.variant & 4);
   if (chunk == 8) {
-    switch (v) {
-      case 0: launch_w<16, 128, 16, 32, 8>(p, stream); break;
-      case 1: launch_w<32, 128, 32, 32, 8>(p, stream); break;
-      case 2: launch_w<64, 64, 32, 32, 8>(p, stream); break;
-      default: launch_w<128, 64, 64, 32, 8>(p, stream); break;
-    }
+    if (bp64) launch_w_variant<8, 64>(v, p, stream); else launch_w_variant<8, 32>(v, p, stream);
   } else {
-    switch (v) {
-      case 0: launch_w<16, 128, 16, 32, 4>(p, stream); break;
-      case 1: launch_w<32, 128, 32, 32, 4>(p, stream); break;
-      case 2: launch_w<64, 64, 32, 32, 4>(p, stream); break;
-      default: launch_w<128, 64, 64, 32, 4>(p, stream); break;
-    }
+    if (bp64) launch_w_variant<4, 64>(v, p, stream); else launch_w_variant<4, 32>(v, p, stream);
   }
 }
 

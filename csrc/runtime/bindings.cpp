@@ -196,6 +196,7 @@ void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& par
   p.pt = g[18]; p.ph = g[19]; p.pw = g[20]; p.splits = g[21]; p.p_per_split = g[22];
   TORCH_CHECK(p.Cin % chunk == 0 && p.Cout % 8 == 0, "wgrad channel alignment");
   TORCH_CHECK(p.p_per_split % 32 == 0, "p_per_split must be a multiple of 32");
+  TORCH_CHECK(variant < 0 || !(variant & 4) || p.p_per_split % 64 == 0, "64-position stages need p_per_split % 64 == 0");
   p.slab = (int)slab;
   p.variant = (int)variant;
   TORCH_CHECK(dy.numel() * 2 < 0xFFFFFF00ll && x.numel() * 2 < 0xFFFFFF00ll, "buffer extents must fit 32 bits");

@@ -147,7 +147,7 @@ class _ConvBN:
             C.conv_igemm(x.t, self.wf, tuner.scratch_like(y) if scratch else y,
                          None if stats is None else (tuner.scratch_like(stats) if scratch else stats),
                          sc_, sh_, aff, 0, g, s.chunk, cfg)
-        cfg = tuner.launch(("f", s.chunk, aff, train) + tuple(g), g, s.chunk, run)
+        cfg = tuner.launch(("f", s.chunk, aff, train) + tuple(g), g, s.chunk, run, aff=aff)
         bn = self.bn
         if train:
             tiles = (M + tuner.bm(cfg, s.cout) - 1) // tuner.bm(cfg, s.cout)
@@ -175,9 +175,9 @@ class _ConvBN:
             if sp is None:
                 if cfg < 0:
                     sp = wgrad_splits(dy.M, s.cout, K, target_blocks=256 if slab else 1024) + (-1,)
-                else:
+                else:   # bits 0-1 tile variant, 2-3 split-K target, 5: 64-position stages
                     v, tb = cfg & 3, (512, 1024, 2048)[(cfg >> 2) & 3]
-                    sp = wgrad_splits(dy.M, s.cout, K, target_blocks=tb, variant=v) + (v,)
+                    sp = wgrad_splits(dy.M, s.cout, K, target_blocks=tb, variant=v) + (v | (4 if cfg & 32 else 0),)
                 eng._splits[key] = sp
             return sp
 
@@ -201,8 +201,8 @@ class _ConvBN:
                     bmw = C.wgrad_tile(s.cout, K, v)[0]
                     if bmw > max(16, s.cout) or bmw * 8 < s.cout:
                         continue
-                    for tbi in range(3):
-                        c = 16 | v | (tbi << 2)
+                    for tbi, bp in ((t, b) for t in range(3) for b in (0, 32)):
+                        c = 16 | v | (tbi << 2) | bp
                         launch(c, scratch)
                         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                         e0.record()

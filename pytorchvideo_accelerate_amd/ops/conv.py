@@ -195,7 +195,7 @@ def wgrad_splits(P: int, Cout: int, K: int, target_blocks: int = 1024, min_rows:
     tiles = ((Cout + bmw - 1) // bmw) * ((K + bnw - 1) // bnw)
     splits = max(1, min(target_blocks // max(tiles, 1), (P + min_rows - 1) // min_rows))
     pps = (P + splits - 1) // splits
-    pps = (pps + 31) // 32 * 32
+    pps = (pps + 63) // 64 * 64      # whole 32- or 64-position stages
     splits = (P + pps - 1) // pps
     return splits, pps
 
@@ -203,19 +203,22 @@ def wgrad_splits(P: int, Cout: int, K: int, target_blocks: int = 1024, min_rows:
 def conv_wgrad(dy: Act, x: Act, spec: ConvSpec, grad: torch.Tensor, workspace: Optional[torch.Tensor] = None,
                in_scale: Optional[torch.Tensor] = None, in_shift: Optional[torch.Tensor] = None,
                in_relu: bool = True, scale: float = 1.0, beta: float = 0.0,
-               splits_pps: Optional[Tuple[int, int]] = None) -> torch.Tensor:
-    """grad (fp32, [Cout, Cin, kt, kh, kw]) = beta*grad + scale * dW."""
+               splits_pps: Optional[Tuple[int, int]] = None, variant: int = -1) -> torch.Tensor:
+    """grad (fp32, [Cout, Cin, kt, kh, kw]) = beta*grad + scale * dW.
+
+    ``variant``: -1 = heuristic tile; else bits 0-1 = tile (16x128, 32x128, 64x64, 128x64), bit 2 = 64-position
+    LDS stages (two MFMA k-steps per barrier)."""
     C = require()
     P = dy.M
     K = spec.taps * spec.cin_pad
-    splits, pps = splits_pps or wgrad_splits(P, spec.cout, K)
+    splits, pps = splits_pps or wgrad_splits(P, spec.cout, K, variant=(variant & 3) if variant >= 0 else -1)
     need = spec.cout * K
     if workspace is None or workspace.numel() < need:
         workspace = torch.zeros(need, device=dy.t.device, dtype=torch.float32)  # kept zero by wgrad_reduce
     affine = 0 if in_scale is None else (2 if in_relu else 1)
     g = [P, spec.cout, K, spec.cin_pad, dy.ld, x.ld, x.T, x.H, x.W, dy.T, dy.H, dy.W,
          *spec.k, *spec.stride, *spec.pad, splits, pps]
-    C.conv_wgrad(dy.t, x.t, workspace, in_scale, in_shift, affine, g, spec.chunk)
+    C.conv_wgrad(dy.t, x.t, workspace, in_scale, in_shift, affine, g, spec.chunk, 0, variant)
     C.wgrad_reduce(workspace, grad, splits, spec.cout, spec.taps, spec.cin_pad, spec.cin, scale, beta)
     return grad
 

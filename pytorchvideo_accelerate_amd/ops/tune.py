@@ -25,6 +25,7 @@ BK64 = 4
 UT = 8
 DIRECT = 32           # narrow direct-to-register kernel (csrc/kernels/conv_direct.hip)
 DIRECT_2K = 64        #   with 2048 rows per workgroup (else 512)
+DMA = 128             # uniform-tap loader staged by LDS-DMA (buffer_load ... lds); launches without input affine
 TILE_BN = (128, 64, 32, 16)   # variants 0..3
 TILE_BM = (128, 128, 256, 256)
 
@@ -35,7 +36,8 @@ def describe(cfg: int) -> str:
         return "heuristic"
     if cfg & DIRECT:
         return "direct%d" % (2048 if cfg & DIRECT_2K else 512)
-    return "%dx%d/bk%d%s" % (TILE_BM[cfg & 3], TILE_BN[cfg & 3], 64 if cfg & BK64 else 32, "/ut" if cfg & UT else "")
+    return "%dx%d/bk%d%s%s" % (TILE_BM[cfg & 3], TILE_BN[cfg & 3], 64 if cfg & BK64 else 32, "/ut" if cfg & UT else "",
+                               "/dma" if cfg & DMA else "")
 
 
 def cfg_word(variant: int, bk: int, ut: bool) -> int:
@@ -47,13 +49,14 @@ class ConvTuner:
         self.C = C
         self.enabled = enabled and os.environ.get("PVA_AUTOTUNE", "1") != "0"
         self.direct = os.environ.get("PVA_CONV_DIRECT", "1") != "0"
+        self.dma = os.environ.get("PVA_CONV_DMA", "1") != "0"
         self.log = os.environ.get("PVA_TUNE_LOG", "0") != "0"
         self.reps = reps
         self.cache: Dict[Tuple, int] = {}
         self._scratch: Dict[Tuple, torch.Tensor] = {}
 
     # ---------------------------------------------------------------- candidates
-    def candidates(self, g: Sequence[int], chunk: int) -> List[int]:
+    def candidates(self, g: Sequence[int], chunk: int, aff: int = 0) -> List[int]:
         N, Cg = g[1], g[3]
         K = g[28] * g[29] * g[30] * Cg
         out = []
@@ -70,6 +73,8 @@ class ConvTuner:
                     uts.append(True)
                 for ut in uts:
                     out.append(cfg_word(v, bk, ut))
+                    if ut and aff == 0 and self.dma:
+                        out.append(cfg_word(v, bk, ut) | DMA)
         if self.direct and self.C.conv_direct_legal(list(g), chunk):
             out += [EXPLICIT | DIRECT, EXPLICIT | DIRECT | DIRECT_2K]
         return out
@@ -88,18 +93,19 @@ class ConvTuner:
         return s
 
     # ---------------------------------------------------------------- launch
-    def launch(self, key: Tuple, g: Sequence[int], chunk: int, run: Callable[[int, bool], None]) -> int:
+    def launch(self, key: Tuple, g: Sequence[int], chunk: int, run: Callable[[int, bool], None],
+               aff: int = 0) -> int:
         """``run(cfg, scratch)`` performs the launch (into scratch outputs when ``scratch``).  Returns the
         configuration used for the real launch (-1 = kernel heuristic)."""
         cfg = self.cache.get(key)
         if cfg is None:
-            cfg = self._tune(g, chunk, run) if self.enabled else -1
+            cfg = self._tune(g, chunk, run, aff) if self.enabled else -1
             self.cache[key] = cfg
         run(cfg, False)
         return cfg
 
-    def _tune(self, g: Sequence[int], chunk: int, run: Callable[[int, bool], None]) -> int:
-        cands = self.candidates(g, chunk)
+    def _tune(self, g: Sequence[int], chunk: int, run: Callable[[int, bool], None], aff: int = 0) -> int:
+        cands = self.candidates(g, chunk, aff)
         if len(cands) <= 1:
             return cands[0] if cands else -1
         best, best_t = -1, float("inf")

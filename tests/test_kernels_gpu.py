@@ -250,6 +250,20 @@ def test_conv_wgrad(case):
     assert rel_err(grad, 1.5 * w.grad) < 1e-2
 
 
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("case", [CASES[1], CASES[3], CASES[6], STEMS[1]])
+def test_conv_wgrad_tile_variants(case, variant):
+    """Every tile variant x {32, 64}-position LDS stages (bit 2) against PyTorch."""
+    x, w, spec = _mk(case, seed=13)
+    w.requires_grad_(True)
+    ref_y = torch.nn.functional.conv3d(x, w, None, spec.stride, spec.pad)
+    gy = torch.randn_like(ref_y).to(torch.bfloat16).float()
+    ref_y.backward(gy)
+    grad = torch.zeros_like(w)
+    conv_wgrad(Act.from_ncthw(gy), Act.from_ncthw(x, spec.cin_pad), spec, grad, variant=variant)
+    assert rel_err(grad, w.grad) < 1e-2
+
+
 def test_conv_wgrad_affine():
     case = CASES[2]
     x, w, spec = _mk(case, seed=4)
@@ -313,3 +327,88 @@ def test_stem_s2d_fwd_wgrad(kt, cout):
     C.stem_wgrad_convert(acc, grad, cout, kt, 0.0)
     assert rel_err(grad, wr.grad) < 1e-2
     assert acc.abs().max().item() == 0.0  # re-zeroed for the next use
+
+
+# LDS-DMA staged uniform-tap loader (ops/tune.DMA): every tile variant x BK, forward (no input affine),
+# strided dgrad phases and the backward-BN dgrad epilogue, against PyTorch
+DMA_CASES = [CASES[0], CASES[1], CASES[2], CASES[3], CASES[4], CASES[10]]
+
+
+def _dma_cfgs(g):
+    from pytorchvideo_accelerate_amd.ops._ext import require
+    from pytorchvideo_accelerate_amd.ops.tune import BK64, DMA, EXPLICIT, UT
+    C = require()
+    out = []
+    for v in range(4):
+        for bk in (32, 64):
+            if C.conv_ut_legal(list(g), 8, bk):
+                out.append(EXPLICIT | UT | DMA | v | (BK64 if bk == 64 else 0))
+    return out
+
+
+@pytest.mark.parametrize("case", DMA_CASES)
+def test_conv_dma_loader_fwd_dgrad(case):
+    from pytorchvideo_accelerate_amd.ops._ext import require
+    from pytorchvideo_accelerate_amd.ops.conv import conv_m_tiles, dgrad_phases, fwd_geometry
+    C = require()
+    x, w, spec = _mk(case, seed=41)
+    ref = torch.nn.functional.conv3d(x, w, None, spec.stride, spec.pad)
+    wf, wd = pack_weight(w, spec)
+    xa = Act.from_ncthw(x)
+    To, Ho, Wo = spec.out_dims(xa.T, xa.H, xa.W)
+    M = xa.N * To * Ho * Wo
+    g = fwd_geometry(spec, xa.N, xa.T, xa.H, xa.W, xa.ld, spec.cout)
+    cfgs = _dma_cfgs(g)
+    assert cfgs, "uniform-tap loader must be legal for this case"
+    for cfg in cfgs:
+        y = torch.empty(M, spec.cout, device=DEV, dtype=torch.bfloat16)
+        stats = torch.full(((M + 127) // 128, 2, spec.cout), float("nan"), device=DEV)
+        C.conv_igemm(xa.t, wf, y, stats, None, None, 0, 0, g, 8, cfg)
+        assert rel_err(Act(y, xa.N, To, Ho, Wo).to_ncthw(), ref) < 1e-2, cfg
+        tiles = (M + C.conv_cfg_bm(cfg, spec.cout) - 1) // C.conv_cfg_bm(cfg, spec.cout)
+        torch.testing.assert_close(stats[:tiles].sum(0)[0], y.float().sum(0), rtol=1e-3,
+                                   atol=1e-2 * y.float().abs().sum(0).max().item() / M ** 0.5)
+    gy = torch.randn_like(ref).to(torch.bfloat16).float()
+    dx_ref = torch.nn.grad.conv3d_input(x.shape, w, gy, spec.stride, spec.pad)
+    dy = Act.from_ncthw(gy)
+    N, Ci, T, H, W = x.shape
+    geo = dgrad_phases(spec, N, (T, H, W), (dy.T, dy.H, dy.W), dy.ld, Ci)
+    for cfg in _dma_cfgs(geo[0]):
+        out = torch.zeros(N * T * H * W, Ci, device=DEV, dtype=torch.bfloat16)
+        for gg in geo:
+            if gg[28] == 0:
+                continue
+            C.conv_igemm(dy.t, wd, out, None, None, None, 0, 0, gg, 8, cfg if C.conv_ut_legal(list(gg), 8, 64 if cfg & 4 else 32) else -1)
+        assert rel_err(Act(out, N, T, H, W).to_ncthw(), dx_ref) < 1e-2, cfg
+
+
+@pytest.mark.parametrize("case", [CASES[0], CASES[1]])
+def test_conv_dma_loader_bn_epilogue(case):
+    from pytorchvideo_accelerate_amd.ops._ext import require
+    from pytorchvideo_accelerate_amd.ops.conv import dgrad_phases
+    C = require()
+    x, w, spec = _mk(case, seed=42)
+    N, Ci, T, H, W = x.shape
+    ref_y = torch.nn.functional.conv3d(x, w, None, spec.stride, spec.pad)
+    gy = torch.randn_like(ref_y).to(torch.bfloat16).float()
+    M = N * T * H * W
+    dx_ref = torch.nn.grad.conv3d_input(x.shape, w, gy, spec.stride, spec.pad).permute(0, 2, 3, 4, 1).reshape(M, Ci)
+    gen = torch.Generator(device="cpu").manual_seed(43)
+    bf = lambda *s: torch.randn(*s, generator=gen).to(torch.bfloat16).to(DEV)
+    res, old, y0 = bf(M, Ci), bf(M, Ci), bf(M, Ci) * 2 + 0.5
+    mask = torch.rand(M, Ci, generator=gen).to(DEV) > 0.4
+    mean0, rstd0 = torch.randn(Ci, device=DEV) * 0.3, torch.rand(Ci, device=DEV) + 0.5
+    _, wd = pack_weight(w, spec)
+    dy = Act.from_ncthw(gy)
+    geo = dgrad_phases(spec, N, (T, H, W), (dy.T, dy.H, dy.W), dy.ld, Ci)
+    for cfg in _dma_cfgs(geo[0]):
+        out = old.clone()
+        part = torch.full(((M + 127) // 128, 3, Ci), float("nan"), device=DEV)
+        C.conv_igemm_epi(dy.t, wd, out, 1, geo[0], 8, res, Ci, _bits(mask), y0, mean0, rstd0, None, None, None, part,
+                         None, None, cfg)
+        v = (dx_ref + old.float() + res.float()) * mask
+        assert rel_err(out, v) < 1.5e-2, cfg
+        tiles = (M + C.conv_cfg_bm(cfg, Ci) - 1) // C.conv_cfg_bm(cfg, Ci)
+        q = out.float()
+        torch.testing.assert_close(part[:tiles].sum(0)[0], q.sum(0), rtol=1e-3,
+                                   atol=1e-2 * q.abs().sum(0).max().item() / M ** 0.5)
