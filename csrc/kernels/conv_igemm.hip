@@ -28,8 +28,27 @@ namespace {
 // groups of every ds_read_b128 fragment read hit 16 distinct slots of the 256-byte bank row
 // (brute-force checked against the gfx950 b128 lane groups for both row lengths).
 // LDS bytes before the stats/affine area: the double-buffered k tiles, or (EPI) the fp32 output tile.
-__host__ __device__ constexpr int main_lds_bytes(int BM, int BN, int BK, int EPI) {
-  return (EPI && BM * (BN * 4 + 16) > 2 * (BM + BN) * BK * 2) ? BM * (BN * 4 + 16) : 2 * (BM + BN) * BK * 2;
+// NS = k-tile buffers: 2 (register staging) or 3 (LDS-DMA ring, one tile in flight across each barrier)
+__host__ __device__ constexpr int main_lds_bytes(int BM, int BN, int BK, int EPI, int NS = 2) {
+  return (EPI && BM * (BN * 4 + 16) > NS * (BM + BN) * BK * 2) ? BM * (BN * 4 + 16) : NS * (BM + BN) * BK * 2;
+}
+
+__host__ __device__ constexpr int dma_stages(int BM, int BN, int BK, bool dma) {
+  return (dma && 3 * (BM + BN) * BK * 2 <= 96 * 1024) ? 3 : 2;
+}
+
+template <int N>
+__device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
+// s_waitcnt vmcnt(BASE + nb) for a wave-uniform runtime nb in [0, MAXB] (the immediate must be a constant)
+template <int BASE, int MAXB>
+__device__ __forceinline__ void vm_wait_dyn(int nb) {
+  if constexpr (MAXB <= 0) {
+    vm_wait<BASE>();
+  } else {
+    if (nb >= MAXB) vm_wait<BASE + MAXB>();
+    else vm_wait_dyn<BASE, MAXB - 1>(nb);
+  }
 }
 
 // 16-B LDS-DMA of one lane: buffer_load_dwordx4 ... lds into wave-uniform LDS address `lds` + 16 * lane
@@ -65,7 +84,9 @@ void conv_igemm_kernel(const ConvParams p) {
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int TILE_BYTES = (BM + BN) * BK * 2;
   constexpr int STG_PITCH = BN * 4 + 16;  // EPI staging row pitch (fp32 tile, padded)
-  constexpr int MAIN_BYTES = main_lds_bytes(BM, BN, BK, EPI);
+  // LDS-DMA loader: 3-buffer ring when it fits 96 KB (>= 1 more workgroup per CU), else 2 buffers
+  constexpr int NSTAGE = dma_stages(BM, BN, BK, (UT & 17) == 17);
+  constexpr int MAIN_BYTES = main_lds_bytes(BM, BN, BK, EPI, NSTAGE);
   static_assert(NT % CPR == 0, "thread count must be a multiple of chunks per row");
   using VT = typename std::conditional<CH == 8, uint4, uint2>::type;
 
@@ -287,8 +308,14 @@ void conv_igemm_kernel(const ConvParams p) {
         retap();
       }
     };
+    // DMA instructions of one tile issued by this wave (A slots always; B slots only for waves whose rows exist)
+    int nb_w = 0;
+#pragma unroll
+    for (int s = 0; s < B_SLOTS; ++s) nb_w += (s * NT + 64 * wid < B_CHUNKS) ? 1 : 0;
+    nb_w = __builtin_amdgcn_readfirstlane(nb_w);
     if constexpr (glds_ut) {
       issue_dma(0);
+      if (NSTAGE == 3 && nsteps > 1) issue_dma(1);
     } else {
       // register ring one stage ahead of LDS: tile s+1 is written right after the barrier that frees its
       // buffer, and tile s+2 is re-issued immediately, so each load has a full k-step of MFMA to land
@@ -298,18 +325,35 @@ void conv_igemm_kernel(const ConvParams p) {
     }
     for (int step = 0; step < nsteps; ++step) {
       const int cur = step & 1;
-      if constexpr (glds_ut) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA of tile `step` has landed
-        __syncthreads();                                    // ... and every wave's; buffer cur^1 is free
+      const char* A;
+      if constexpr (glds_ut && NSTAGE == 3) {
+        // 3-buffer ring: tile step+1 stays in flight across this barrier (counted vmcnt, raw s_barrier —
+        // __syncthreads would drain the pending LDS-DMA with vmcnt(0)); buffer (step+2)%3 held tile step-1,
+        // whose readers all passed this barrier
+        if (step + 1 < nsteps) {
+          vm_wait_dyn<A_SLOTS, B_SLOTS>(nb_w);   // leave this wave's A_SLOTS + nb_w DMAs of tile step+1
+        } else {
+          vm_wait<0>();
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (step + 2 < nsteps) issue_dma((step + 2) % 3);
+        A = smem + (step % 3) * TILE_BYTES;
+      } else if constexpr (glds_ut) {
+        // 2 buffers (large tiles): tile step landed -> barrier -> DMA of tile step+1 during this step's MFMAs
+        vm_wait<0>();
+        __syncthreads();
         if (step + 1 < nsteps) issue_dma(cur ^ 1);
+        A = smem + cur * TILE_BYTES;
       } else {
         __syncthreads();
         if (step + 1 < nsteps) {
           store_lds(cur ^ 1);
           if (step + 2 < nsteps) load();
         }
+        A = smem + cur * TILE_BYTES;
       }
-      const char* A = smem + cur * TILE_BYTES;
 #pragma unroll
       for (int kk = 0; kk < BK / 32; ++kk) {
         bf16x8_t af[TM], bfr[TN];
@@ -695,7 +739,9 @@ void launch_cfg(const ConvParams& p, int ut_force, hipStream_t stream, bool dma 
   const bool epi = p.eres || p.emask || p.epart;
   constexpr int NW = (BM / WM) * (BN / WN);
   const size_t red_bytes = epi ? (NW * 3 + 6) * BN * 4 : (BM / WM) * 2 * BN * 4;
-  const size_t lds = main_lds_bytes(BM, BN, BK, epi ? 1 : 0) + red_bytes + (p.affine ? 2 * p.Cg * 4 : 0);
+  const bool use_dma = CH == 8 && dma && !p.affine && conv_ut_legal(p, CH, BK) && ut_force != 0;
+  const size_t lds = main_lds_bytes(BM, BN, BK, epi ? 1 : 0, dma_stages(BM, BN, BK, use_dma)) + red_bytes +
+                     (p.affine ? 2 * p.Cg * 4 : 0);
   const dim3 grid(m_tiles * n_tiles), block(NT);
   // heuristic (ut_force < 0), measured with scripts/conv_bench.py --ut 0/1/2: the uniform-tap loader wins
   // without reachable padding and for spatial (1,k,k) unit-stride gathers (with the consumer-side BN fold
@@ -704,7 +750,27 @@ void launch_cfg(const ConvParams& p, int ut_force, hipStream_t stream, bool dma 
   const bool ut_legal = conv_ut_legal(p, CH, BK);
   const bool ut_pays = !p.check || (p.nt == 1 && p.ash == 1 && p.asw == 1);
   const bool ut = ut_legal && (ut_force >= 0 ? ut_force == 1 : (g_ut_mode == 2 || (g_ut_mode == 1 && ut_pays)));
-  if constexpr (CH == 8) {
+  // 256x256 tile: forward / plain dgrad only (the EPI 1 fp32 staging tile would not fit LDS)
+  constexpr bool BIG = BM * BN > 128 * 128;
+  if constexpr (BIG) {
+    if (epi) return;   // rejected by the host binding
+    if (ut && dma && !p.affine) {
+      if (p.check) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 0, 19>), grid, block, lds, stream, p);
+      else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 0, 17>), grid, block, lds, stream, p);
+    } else if (ut) {
+      switch ((p.check ? 2 : 0) | (p.affine << 2)) {
+        case 0: hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 0, 1>), grid, block, lds, stream, p); break;
+        case 2: hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 0, 3>), grid, block, lds, stream, p); break;
+        case 4: hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 0, 5>), grid, block, lds, stream, p); break;
+        case 6: hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 0, 7>), grid, block, lds, stream, p); break;
+        case 8: hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 0, 9>), grid, block, lds, stream, p); break;
+        default: hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 0, 11>), grid, block, lds, stream, p); break;
+      }
+    } else {
+      hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 0, 0>), grid, block, lds, stream, p);
+    }
+    return;
+  } else if constexpr (CH == 8) {
     if (ut && dma && !p.affine) {   // LDS-DMA staged uniform-tap loader (UT word bit 4)
       if (epi) {
         if (p.check) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 1, 19>), grid, block, lds, stream, p);
@@ -743,6 +809,9 @@ void launch_variant(int v, const ConvParams& p, int ut_force, hipStream_t stream
     case 0: launch_cfg<128, 128, 64, 64, CH, BK>(p, ut_force, stream, dma); break;
     case 1: launch_cfg<128, 64, 64, 32, CH, BK>(p, ut_force, stream, dma); break;
     case 2: launch_cfg<256, 32, 64, 32, CH, BK>(p, ut_force, stream, dma); break;
+    case 4:
+      if constexpr (CH == 8) launch_cfg<256, 256, 128, 64, CH, BK>(p, ut_force, stream, dma);
+      break;
     default: launch_cfg<256, 16, 64, 16, CH, BK>(p, ut_force, stream, dma); break;
   }
 }
@@ -759,12 +828,14 @@ static int pick_variant(int M, int N) {
 // Launch configuration word: tile variant (bits 0-1: 128x128, 128x64, 256x32, 256x16), BK (bit 2: 32 / 64),
 // uniform-tap loader (bit 3), bit 4 set = explicit (else the built-in heuristic), bit 5 = the narrow
 // direct-to-register kernel of conv_direct.hip (bit 6: 2048 rows per workgroup, else 512), bit 7 = LDS-DMA
-// staging of the uniform-tap loader (launches without an input affine).  -1 = heuristic.
+// staging of the uniform-tap loader (launches without an input affine), bit 8 = 256x256 tile of 8 waves
+// (overrides bits 0-1; forward / plain dgrad only).  -1 = heuristic.
 int conv_direct_rows(int cfg);
 void conv_direct_launch(const ConvParams& p, int cfg, hipStream_t s);
 
 int conv_cfg_bm(int cfg, int N) {
   if (cfg >= 0 && (cfg & 16) && (cfg & 32)) return conv_direct_rows(cfg);
+  if (cfg >= 0 && (cfg & 16) && (cfg & 256)) return 256;   // 256x256 tile
   const int v = (cfg >= 0 && (cfg & 16)) ? (cfg & 3) : pick_variant(0, N);
   return v <= 1 ? 128 : 256;
 }
@@ -792,7 +863,7 @@ void conv_igemm_launch(const ConvParams& p, int chunk, hipStream_t stream, int c
     return;
   }
   if (cfg >= 0 && (cfg & 16)) {
-    v = cfg & 3;
+    v = (cfg & 256) ? 4 : (cfg & 3);
     bk = (cfg & 4) ? 64 : 32;
     ut_force = (cfg >> 3) & 1;
     dma = (cfg & 128) != 0;   // LDS-DMA staging (uniform-tap loader, no input affine)

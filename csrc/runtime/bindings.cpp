@@ -148,6 +148,7 @@ void conv_igemm_epi(const at::Tensor& x, const at::Tensor& w, const at::Tensor& 
                     const OptT& y0, const OptT& mean0, const OptT& rstd0, const OptT& y1, const OptT& mean1,
                     const OptT& rstd1, const OptT& part, const OptT& msc, const OptT& msh, int64_t cfg) {
   ConvParams p = conv_params(x, w, y, accum, g, chunk);
+  TORCH_CHECK(cfg < 0 || !(cfg & 256), "the 256x256 tile has no backward-BN epilogue");
   p.eres = bfo(res); p.ldr = (int)ldr;
   TORCH_CHECK(!res.has_value() || ldr % 4 == 0, "residual row stride alignment");
   if (mask.has_value()) {

@@ -248,7 +248,7 @@ class _ConvBN:
                 C.conv_igemm_epi(dy.t, self.wd, tuner.scratch_like(out) if scratch else out, 0, g, 8, None, 0, None,
                                  y.t, u.mean, u.rstd, None, None, None,
                                  tuner.scratch_like(part) if scratch else part, u.scale, u.shift, cfg)
-            cfg = tuner.launch(("eb",) + tuple(g), g, 8, run)
+            cfg = tuner.launch(("eb",) + tuple(g), g, 8, run, epi=True)
             bm = tuner.bm(cfg, g[1])
             return part, (g[0] + bm - 1) // bm
         if res is not None or epi is not None:
@@ -270,7 +270,7 @@ class _ConvBN:
                                  None if part is None else (tuner.scratch_like(part) if scratch else part),
                                  None, None, cfg)
             cfg = tuner.launch(("er", accum, res is not None, epi is not None,
-                                epi is not None and one is not None) + tuple(g), g, 8, run)
+                                epi is not None and one is not None) + tuple(g), g, 8, run, epi=True)
             if epi is None:
                 return None
             bm = tuner.bm(cfg, g[1])

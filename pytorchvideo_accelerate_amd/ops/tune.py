@@ -26,6 +26,7 @@ UT = 8
 DIRECT = 32           # narrow direct-to-register kernel (csrc/kernels/conv_direct.hip)
 DIRECT_2K = 64        #   with 2048 rows per workgroup (else 512)
 DMA = 128             # uniform-tap loader staged by LDS-DMA (buffer_load ... lds); launches without input affine
+BIG = 256             # 256x256 tile of 8 waves (N >= 256; forward / plain dgrad, no backward-BN epilogue)
 TILE_BN = (128, 64, 32, 16)   # variants 0..3
 TILE_BM = (128, 128, 256, 256)
 
@@ -36,6 +37,8 @@ def describe(cfg: int) -> str:
         return "heuristic"
     if cfg & DIRECT:
         return "direct%d" % (2048 if cfg & DIRECT_2K else 512)
+    if cfg & BIG:
+        return "256x256/bk%d%s%s" % (64 if cfg & BK64 else 32, "/ut" if cfg & UT else "", "/dma" if cfg & DMA else "")
     return "%dx%d/bk%d%s%s" % (TILE_BM[cfg & 3], TILE_BN[cfg & 3], 64 if cfg & BK64 else 32, "/ut" if cfg & UT else "",
                                "/dma" if cfg & DMA else "")
 
@@ -56,7 +59,7 @@ class ConvTuner:
         self._scratch: Dict[Tuple, torch.Tensor] = {}
 
     # ---------------------------------------------------------------- candidates
-    def candidates(self, g: Sequence[int], chunk: int, aff: int = 0) -> List[int]:
+    def candidates(self, g: Sequence[int], chunk: int, aff: int = 0, epi: bool = False) -> List[int]:
         N, Cg = g[1], g[3]
         K = g[28] * g[29] * g[30] * Cg
         out = []
@@ -75,6 +78,13 @@ class ConvTuner:
                     out.append(cfg_word(v, bk, ut))
                     if ut and aff == 0 and self.dma:
                         out.append(cfg_word(v, bk, ut) | DMA)
+        if N >= 256 and not epi and chunk == 8:   # 256x256 tile (UT loader only: the generic one is VALU-bound)
+            for bk in (32, 64):
+                if self.C.conv_ut_legal(list(g), chunk, bk):
+                    w = EXPLICIT | BIG | UT | (BK64 if bk == 64 else 0)
+                    out.append(w)
+                    if aff == 0 and self.dma:
+                        out.append(w | DMA)
         if self.direct and self.C.conv_direct_legal(list(g), chunk):
             out += [EXPLICIT | DIRECT, EXPLICIT | DIRECT | DIRECT_2K]
         return out
@@ -94,18 +104,19 @@ class ConvTuner:
 
     # ---------------------------------------------------------------- launch
     def launch(self, key: Tuple, g: Sequence[int], chunk: int, run: Callable[[int, bool], None],
-               aff: int = 0) -> int:
+               aff: int = 0, epi: bool = False) -> int:
         """``run(cfg, scratch)`` performs the launch (into scratch outputs when ``scratch``).  Returns the
         configuration used for the real launch (-1 = kernel heuristic)."""
         cfg = self.cache.get(key)
         if cfg is None:
-            cfg = self._tune(g, chunk, run, aff) if self.enabled else -1
+            cfg = self._tune(g, chunk, run, aff, epi) if self.enabled else -1
             self.cache[key] = cfg
         run(cfg, False)
         return cfg
 
-    def _tune(self, g: Sequence[int], chunk: int, run: Callable[[int, bool], None], aff: int = 0) -> int:
-        cands = self.candidates(g, chunk, aff)
+    def _tune(self, g: Sequence[int], chunk: int, run: Callable[[int, bool], None], aff: int = 0,
+              epi: bool = False) -> int:
+        cands = self.candidates(g, chunk, aff, epi)
         if len(cands) <= 1:
             return cands[0] if cands else -1
         best, best_t = -1, float("inf")

@@ -412,3 +412,55 @@ def test_conv_dma_loader_bn_epilogue(case):
         q = out.float()
         torch.testing.assert_close(part[:tiles].sum(0)[0], q.sum(0), rtol=1e-3,
                                    atol=1e-2 * q.abs().sum(0).max().item() / M ** 0.5)
+
+
+@pytest.mark.parametrize("case", [CASES[0], CASES[1], CASES[4], CASES[10]])
+def test_conv_big_tile(case):
+    """256x256 tile of 8 waves (tune.BIG), register and LDS-DMA staging, BK 32/64: forward (+ BN partial sums,
+    + consumer affine for the register path) and plain dgrad phases."""
+    from pytorchvideo_accelerate_amd.ops._ext import require
+    from pytorchvideo_accelerate_amd.ops.conv import dgrad_phases, fwd_geometry
+    from pytorchvideo_accelerate_amd.ops.tune import BIG, BK64, DMA, EXPLICIT, UT
+    C = require()
+    x, w, spec = _mk(case, seed=44)
+    Ci = spec.cin
+    sc = torch.rand(Ci, device=DEV) + 0.5
+    sh = torch.randn(Ci, device=DEV) * 0.5
+    wf, wd = pack_weight(w, spec)
+    xa = Act.from_ncthw(x)
+    To, Ho, Wo = spec.out_dims(xa.T, xa.H, xa.W)
+    M = xa.N * To * Ho * Wo
+    g = fwd_geometry(spec, xa.N, xa.T, xa.H, xa.W, xa.ld, spec.cout)
+    xt = torch.relu(x * sc.view(1, Ci, 1, 1, 1) + sh.view(1, Ci, 1, 1, 1))
+    refs = {0: torch.nn.functional.conv3d(x, w, None, spec.stride, spec.pad),
+            2: torch.nn.functional.conv3d(xt, w, None, spec.stride, spec.pad)}
+    ran = 0
+    for bk in (32, 64):
+        if spec.cout < 256 or not C.conv_ut_legal(g, 8, bk):
+            continue
+        base = EXPLICIT | BIG | UT | (BK64 if bk == 64 else 0)
+        for cfg, aff in ((base, 0), (base | DMA, 0), (base, 2)):
+            y = torch.empty(M, spec.cout, device=DEV, dtype=torch.bfloat16)
+            stats = torch.full(((M + 255) // 256, 2, spec.cout), float("nan"), device=DEV)
+            C.conv_igemm(xa.t, wf, y, stats, sc if aff else None, sh if aff else None, aff, 0, g, 8, cfg)
+            assert rel_err(Act(y, xa.N, To, Ho, Wo).to_ncthw(), refs[aff]) < 1e-2, (cfg, aff)
+            yf = y.float()
+            torch.testing.assert_close(stats.sum(0)[0], yf.sum(0), rtol=1e-3,
+                                       atol=1e-2 * yf.abs().sum(0).max().item() / M ** 0.5)
+            ran += 1
+    gy = torch.randn_like(refs[0]).to(torch.bfloat16).float()
+    dx_ref = torch.nn.grad.conv3d_input(x.shape, w, gy, spec.stride, spec.pad)
+    dy = Act.from_ncthw(gy)
+    N, _, T, H, W = x.shape
+    geo = dgrad_phases(spec, N, (T, H, W), (dy.T, dy.H, dy.W), dy.ld, Ci)
+    for bk in (32, 64):
+        if Ci < 256 or not all(C.conv_ut_legal(list(gg), 8, bk) for gg in geo if gg[28]):
+            continue
+        for cfg in (EXPLICIT | BIG | UT | (BK64 if bk == 64 else 0), EXPLICIT | BIG | UT | DMA | (BK64 if bk == 64 else 0)):
+            out = torch.zeros(N * T * H * W, Ci, device=DEV, dtype=torch.bfloat16)
+            for gg in geo:
+                if gg[28]:
+                    C.conv_igemm(dy.t, wd, out, None, None, None, 0, 0, gg, 8, cfg)
+            assert rel_err(Act(out, N, T, H, W).to_ncthw(), dx_ref) < 1e-2, cfg
+            ran += 1
+    assert ran > 0
