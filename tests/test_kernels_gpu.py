@@ -292,13 +292,15 @@ def test_pack_weights_kernel_matches_host_pack():
             assert torch.equal(u.wd.view_as(wd), wd), u.name
 
 
-@pytest.mark.parametrize("kt,cout", [(5, 8), (1, 64)])
-def test_stem_s2d_fwd_wgrad(kt, cout):
+# (5, 8): frame-pair kernels (PVA_STEM_PAIR default) for even / odd T, and the one-frame kernels
+@pytest.mark.parametrize("kt,cout,T,pair", [(5, 8, 6, "1"), (5, 8, 5, "1"), (5, 8, 6, "0"), (1, 64, 6, "1")])
+def test_stem_s2d_fwd_wgrad(kt, cout, T, pair, monkeypatch):
     from pytorchvideo_accelerate_amd.models.fused import to_s2d
     from pytorchvideo_accelerate_amd.ops._ext import require
+    monkeypatch.setenv("PVA_STEM_PAIR", pair)
     C = require()
     g = torch.Generator(device="cpu").manual_seed(7)
-    N, T, H = 2, 6, 40
+    N, H = 2, 40
     x = torch.randn(N, 3, T, H, H, generator=g).to(DEV).to(torch.bfloat16).float()
     w = (torch.randn(cout, 3, kt, 7, 7, generator=g) * 0.05).to(DEV).to(torch.bfloat16).float()
     ref = torch.nn.functional.conv3d(x, w, None, (1, 2, 2), (kt // 2, 3, 3))
