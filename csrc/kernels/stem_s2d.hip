@@ -296,14 +296,48 @@ __device__ __forceinline__ bf16x8_t ld_frag(const uint16_t* p, bool ok) {
   return __builtin_bit_cast(bf16x8_t, u);
 }
 
+constexpr uint32_t OOB = 0x7ffffff0u;         // buffer offset past num_records: the load returns zeros
+constexpr int SLOT_BYTES = 448 * 16;           // frame slot: 418 chunks padded to 7 x 64 lanes
+
+// 16-B LDS-DMA of one lane: buffer_load_dwordx4 ... lds into wave-uniform LDS address `lds` + 16 * lane
+// (the address_space(3) cast only exists in the device pass)
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds, uint32_t voff) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, (int)voff, 0, 0, 0);
+#endif
+}
+
+// one input frame's s2d patch -> LDS slot by LDS-DMA; positions outside the frame / image read zeros
+// through out-of-range buffer offsets.  No VGPR staging, no ds_write: the copy overlaps the MFMA loop.
+__device__ __forceinline__ void dma_patch(__amdgpu_buffer_rsrc_t r, const StemParams& p, int ti, int hs0, int ws0,
+                                          char* slot) {
+  const int tid = threadIdx.x, w = tid >> 6;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    if (s == 1 && w == 3) break;  // chunks 448.. do not exist (wave-uniform)
+    const int idx = tid + s * 256;
+    const int pos = idx >> 1, half = idx & 1;
+    const int r_ = pos / PW, c_ = pos - r_ * PW;
+    const int hs = hs0 + r_ - 2, ws = ws0 + c_ - 2;
+    const bool ok = idx < PH * PW * 2 && ti >= 0 && ti < p.T && (unsigned)hs < (unsigned)p.Hs &&
+                    (unsigned)ws < (unsigned)p.Ws;
+    const uint32_t vo = ok ? (uint32_t)((((ti * p.Hs + hs) * p.Ws + ws) * 16 + half * 8) * 2) : OOB;
+    dma16(r, slot + (w * 64 + s * 256) * 16, vo);  // chunks 418..447 land in the slot padding
+  }
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t clip_rsrc(const uint16_t* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)bytes, 0x00020000);
+}
+
 template <int KT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void stem_fwd_pair_kernel(const StemParams p) {
   constexpr int TAPS = KT * 16;
-  constexpr int J = KT + 1;   // input frames per output-frame pair
-  constexpr int KS = 8;       // k-steps per input frame: 16 spatial taps x 16 channels / 32
-  constexpr int SLOTS = J;    // frame ring: window frame j of pair t0 lives in slot (t0 + j) % SLOTS
+  constexpr int J = KT + 1;     // input frames per output-frame pair
+  constexpr int KS = 8;         // k-steps per input frame: 16 spatial taps x 16 channels / 32
+  constexpr int SLOTS = J + 2;  // window frame j of pair t0 lives in slot (t0 + j) % SLOTS; +2 in flight
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* red = reinterpret_cast<float*>(smem + SLOTS * FRAME_BYTES);  // [4 waves][2][8]
+  float* red = reinterpret_cast<float*>(smem + SLOTS * SLOT_BYTES);  // [4 waves][2][8]
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
@@ -312,6 +346,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const int th = b % p.tiles_h;
   const int n = b / p.tiles_h;
   const int ho0 = th * TH, wo0 = tw * TW;
+  const __amdgpu_buffer_rsrc_t xr =
+      clip_rsrc(p.x + (int64_t)n * p.T * p.Hs * p.Ws * 16, (uint32_t)(p.T * p.Hs * p.Ws * 32));
+
+  for (int f = 0; f < J; ++f) dma_patch(xr, p, f - p.pt, ho0, wo0, smem + f * SLOT_BYTES);
 
   bf16x8_t wa[J][KS];
 #pragma unroll
@@ -322,28 +360,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     for (int ks = 0; ks < KS; ++ks)
       wa[j][ks] = ld_frag(p.w + (int64_t)(li & 7) * (TAPS * 16) + (ok ? dt : 0) * 256 + ks * 32 + 8 * g, ok);
   }
-
-  PatchRegs pr0, pr1;
-  for (int f = 0; f < J; ++f) {
-    load_patch(p, n, f - p.pt, ho0, wo0, pr0);
-    store_patch(smem + f * FRAME_BYTES, pr0);
-  }
-  __syncthreads();
+  __syncthreads();  // drains this wave's DMAs (vmcnt(0)) and publishes every wave's
 
   float cs[4] = {0.f, 0.f, 0.f, 0.f}, cq[4] = {0.f, 0.f, 0.f, 0.f};
   const int half = g & 1;
   const int co0 = 4 * (g & 1);  // D rows 4g..4g+3: channels co0.. of output frame t0 + (g >> 1)
   for (int t0 = 0; t0 < p.To; t0 += 2) {
-    const int tn = t0 - p.pt + J;  // first of the two frames the next pair adds to the window
-    const bool pf = t0 + 2 < p.To;
-    if (pf) {
-      load_patch(p, n, tn, ho0, wo0, pr0);
-      load_patch(p, n, tn + 1, ho0, wo0, pr1);
+    if (t0 + 2 < p.To) {  // the next pair's two new frames, into slots outside the current window
+      const int tn = t0 - p.pt + J;
+      dma_patch(xr, p, tn, ho0, wo0, smem + ((t0 + J) % SLOTS) * SLOT_BYTES);
+      dma_patch(xr, p, tn + 1, ho0, wo0, smem + ((t0 + J + 1) % SLOTS) * SLOT_BYTES);
     }
     f32x4_t acc[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
     for (int j = 0; j < J; ++j) {
-      const char* slot = smem + ((t0 + j) % SLOTS) * FRAME_BYTES;
+      const char* slot = smem + ((t0 + j) % SLOTS) * SLOT_BYTES;
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
         const int tap = 2 * ks + (g >> 1);
@@ -371,12 +402,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         for (int r = 0; r < 4; ++r) { cs[r] += f[r]; cq[r] += f[r] * f[r]; }
       }
     }
-    if (pf) {
-      __syncthreads();  // window frames 0 and 1 are dead: their slots take the prefetched frames
-      store_patch(smem + (t0 % SLOTS) * FRAME_BYTES, pr0);
-      store_patch(smem + ((t0 + 1) % SLOTS) * FRAME_BYTES, pr1);
-      __syncthreads();
-    }
+    __syncthreads();  // new frames landed (vmcnt(0) + barrier); window frames 0, 1 may be overwritten next
   }
   // BN partial sums: lanes g and g^2 hold the same channels (frames t0 / t0+1); fixed summation order
 #pragma unroll
@@ -403,9 +429,10 @@ template <int KT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void stem_wgrad_pair_kernel(const StemParams p) {
   constexpr int TAPS = KT * 16;
   constexpr int J = KT + 1;
-  constexpr int SLOTS = J;
+  constexpr int SLOTS = J + 2;
+  constexpr int DYB = TH * TW * 16 * 2;  // dY tile [128 pos][16]: frame t0 (0-7) | frame t0+1 (8-15)
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* dyt = smem + SLOTS * FRAME_BYTES;  // [128 pos][16]: dY of frame t0 (0-7) | frame t0+1 (8-15)
+  char* dyt = smem + SLOTS * SLOT_BYTES;  // two dY tile buffers (pair parity)
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
@@ -414,6 +441,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const int th = b % p.tiles_h;
   const int n = b / p.tiles_h;
   const int ho0 = th * TH, wo0 = tw * TW;
+  const __amdgpu_buffer_rsrc_t xr =
+      clip_rsrc(p.x + (int64_t)n * p.T * p.Hs * p.Ws * 16, (uint32_t)(p.T * p.Hs * p.Ws * 32));
+  const __amdgpu_buffer_rsrc_t yr =
+      clip_rsrc(p.dy + (int64_t)n * p.To * p.Ho * p.Wo * 8, (uint32_t)(p.To * p.Ho * p.Wo * 16));
+  // dY chunk of this lane: position tid >> 1 of the tile, frame t0 + (tid & 1); LDS offset tid * 16
+  const int dpos = tid >> 1, dfh = tid & 1;
+  const int dho = ho0 + dpos / TW, dwo = wo0 + dpos % TW;
+  const bool dok = dho < p.Ho && dwo < p.Wo;
+  auto dma_dy = [&](int t0, char* buf) {
+    const int to = t0 + dfh;
+    const uint32_t vo = dok && to < p.To ? (uint32_t)((((to * p.Ho + dho) * p.Wo + dwo) * 8) * 2) : OOB;
+    dma16(yr, buf + w * 64 * 16, vo);
+  };
 
   // wave w owns spatial taps (bh = w, bw = 0..3) of every window frame: both halves of a (co, dt) sum
   // end up in the same wave (rows 0-7 of acc[dt], rows 8-15 of acc[dt+1]) and are combined by a shuffle.
@@ -423,43 +463,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
     for (int s = 0; s < 4; ++s) acc[j][s] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  PatchRegs pr0, pr1;
-  for (int f = 0; f < J; ++f) {
-    load_patch(p, n, f - p.pt, ho0, wo0, pr0);
-    store_patch(smem + f * FRAME_BYTES, pr0);
-  }
+  for (int f = 0; f < J; ++f) dma_patch(xr, p, f - p.pt, ho0, wo0, smem + f * SLOT_BYTES);
+  dma_dy(0, dyt);
+  __syncthreads();
   const int rq = li >> 2, cb = (li & 3) * 8;
   for (int t0 = 0; t0 < p.To; t0 += 2) {
-    {
-      const int idx = tid;  // 128 positions x 2 frames = 256 16-byte chunks
-      const int pos = idx >> 1, fh = idx & 1;
-      const int ho = ho0 + pos / TW, wo = wo0 + pos % TW, to = t0 + fh;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (ho < p.Ho && wo < p.Wo && to < p.To)
-        v = *reinterpret_cast<const uint4*>(p.dy + ((((int64_t)n * p.To + to) * p.Ho + ho) * p.Wo + wo) * 8);
-      *reinterpret_cast<uint4*>(dyt + pos * 32 + fh * 16) = v;
+    const char* dcur = dyt + ((t0 >> 1) & 1) * DYB;
+    if (t0 + 2 < p.To) {
+      const int tn = t0 - p.pt + J;
+      dma_patch(xr, p, tn, ho0, wo0, smem + ((t0 + J) % SLOTS) * SLOT_BYTES);
+      dma_patch(xr, p, tn + 1, ho0, wo0, smem + ((t0 + J + 1) % SLOTS) * SLOT_BYTES);
+      dma_dy(t0 + 2, dyt + (((t0 >> 1) + 1) & 1) * DYB);
     }
-    const int tn = t0 - p.pt + J;
-    const bool pf = t0 + 2 < p.To;
-    if (pf) {
-      load_patch(p, n, tn, ho0, wo0, pr0);
-      load_patch(p, n, tn + 1, ho0, wo0, pr1);
-    }
-    __syncthreads();
 #pragma unroll
     for (int kstep = 0; kstep < TH * TW / 32; ++kstep) {
       const int hh = 2 * kstep + (g >> 1);
       const int wq = 8 * (g & 1) + rq;
       bf16x8_t a;
       {
-        const char* base = dyt + (hh * TW + wq) * 32 + cb;
+        const char* base = dcur + (hh * TW + wq) * 32 + cb;
         s16x4_t lo = trr(base), hi = trr(base + 4 * 32);
         s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         a = __builtin_bit_cast(bf16x8_t, v);
       }
 #pragma unroll
       for (int j = 0; j < J; ++j) {
-        const char* slot = smem + ((t0 + j) % SLOTS) * FRAME_BYTES;
+        const char* slot = smem + ((t0 + j) % SLOTS) * SLOT_BYTES;
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
           const char* base = slot + ((hh + w) * PW + (wq + s)) * POSB + cb;
@@ -469,11 +498,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         }
       }
     }
-    __syncthreads();
-    if (pf) {
-      store_patch(smem + (t0 % SLOTS) * FRAME_BYTES, pr0);
-      store_patch(smem + ((t0 + 1) % SLOTS) * FRAME_BYTES, pr1);
-    }
+    __syncthreads();  // next frames / dY tile landed; current window frames 0, 1 and dY buffer are free
   }
   // dW[co][dt][tap] = rows 0-7 of acc[dt] (lanes g < 2) + rows 8-15 of acc[dt + 1] (lanes g >= 2)
 #pragma unroll
@@ -541,13 +566,13 @@ void launch_wgrad(const StemParams& p, hipStream_t s) {
 
 template <int KT>
 void launch_fwd_pair(const StemParams& p, hipStream_t s) {
-  const size_t lds = (KT + 1) * FRAME_BYTES + 4 * 16 * 4;
+  const size_t lds = (KT + 3) * SLOT_BYTES + 4 * 16 * 4;
   hipLaunchKernelGGL((stem_fwd_pair_kernel<KT>), dim3(p.N * p.tiles_h * p.tiles_w), dim3(256), lds, s, p);
 }
 
 template <int KT>
 void launch_wgrad_pair(const StemParams& p, hipStream_t s) {
-  const size_t lds = (KT + 1) * FRAME_BYTES + TH * TW * 16 * 2;
+  const size_t lds = (KT + 3) * SLOT_BYTES + 2 * TH * TW * 16 * 2;
   hipLaunchKernelGGL((stem_wgrad_pair_kernel<KT>), dim3(p.N * p.tiles_h * p.tiles_w), dim3(256), lds, s, p);
 }
 
