@@ -8,8 +8,9 @@
 //     16 bf16 channels, so the conv becomes k(kt,4,4) stride 1 with 32-byte positions (weights for
 //     the tap positions outside the 7x7 window are zero);
 //   * a workgroup owns an 8x16 output tile of one clip and walks its frames: input frames live in an
-//     LDS ring of kt+1 slots (each frame is read from HBM exactly once per tile, the next frame is
-//     prefetched into registers while the current one computes); one barrier per frame;
+//     LDS ring (each frame is read from HBM exactly once per tile); the next frame (and, for wgrad, the
+//     next dY tile) is copied by LDS-DMA (buffer_load ... lds) while the current one computes, so no
+//     VGPRs or ds_writes are spent on staging; one barrier per frame;
 //   * forward: all weight fragments sit in VGPRs (A operand), input fragments are one ds_read_b128
 //     each (B operand), BN partial sums are produced in the epilogue;
 //   * wgrad: dY tile of the frame is staged in LDS, both MFMA operands are read with the gfx950
@@ -23,7 +24,6 @@ namespace {
 constexpr int TH = 8, TW = 16;              // output tile (positions = 128 = 4 waves x 2 rows)
 constexpr int PH = TH + 3, PW = TW + 3;     // s2d patch (kernel 4)
 constexpr int POSB = 32;                    // bytes per s2d position (16 bf16)
-constexpr int FRAME_BYTES = PH * PW * POSB; // 6688
 
 struct StemParams {
   const uint16_t* x;    // [N, T, Hs, Ws, 16] s2d input
@@ -37,264 +37,6 @@ struct StemParams {
   int pt;               // temporal padding (kt/2)
   int tiles_h, tiles_w;
 };
-
-// load one input frame's patch (zero outside) into registers: 418 16-B chunks over 256 threads
-struct PatchRegs { uint4 v[2]; };
-
-__device__ __forceinline__ void load_patch(const StemParams& p, int n, int ti, int hs0, int ws0, PatchRegs& r) {
-  const int tid = threadIdx.x;
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    const int idx = tid + s * 256;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (idx < PH * PW * 2 && ti >= 0 && ti < p.T) {
-      const int pos = idx >> 1, half = idx & 1;
-      const int r_ = pos / PW, c_ = pos - r_ * PW;
-      const int hs = hs0 + r_ - 2, ws = ws0 + c_ - 2;
-      if ((unsigned)hs < (unsigned)p.Hs && (unsigned)ws < (unsigned)p.Ws)
-        v = *reinterpret_cast<const uint4*>(p.x + ((((int64_t)n * p.T + ti) * p.Hs + hs) * p.Ws + ws) * 16 + half * 8);
-    }
-    r.v[s] = v;
-  }
-}
-
-__device__ __forceinline__ void store_patch(char* slot, const PatchRegs& r) {
-  const int tid = threadIdx.x;
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    const int idx = tid + s * 256;
-    if (idx < PH * PW * 2) *reinterpret_cast<uint4*>(slot + idx * 16) = r.v[s];
-  }
-}
-
-// ------------------------------------------------------------------------------------------------
-// forward
-// ------------------------------------------------------------------------------------------------
-template <int KT, int COT>
-__global__ __launch_bounds__(256) void stem_fwd_kernel(const StemParams p) {
-  constexpr int TAPS = KT * 16;
-  constexpr int KSTEPS = TAPS * 16 / 32;  // 2 taps per MFMA k-step
-  constexpr int SLOTS = KT + 1;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* red = reinterpret_cast<float*>(smem + SLOTS * FRAME_BYTES);  // [4 waves][2][COT*16]
-
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int g = lane >> 4, li = lane & 15;
-  int b = blockIdx.x;
-  const int tw = b % p.tiles_w; b /= p.tiles_w;
-  const int th = b % p.tiles_h;
-  const int n = b / p.tiles_h;
-  const int ho0 = th * TH, wo0 = tw * TW;
-
-  // weight fragments (A operand: lane holds W[co = 16*c + li][k = 32*ks + 8*g .. +8])
-  bf16x8_t wa[COT][KSTEPS];
-#pragma unroll
-  for (int c = 0; c < COT; ++c)
-#pragma unroll
-    for (int ks = 0; ks < KSTEPS; ++ks)
-      wa[c][ks] = *reinterpret_cast<const bf16x8_t*>(p.w + (int64_t)(16 * c + li) * (TAPS * 16) + ks * 32 + 8 * g);
-
-  // prologue: frames -pt .. -pt+KT-1
-  PatchRegs pr;
-  for (int f = 0; f < KT; ++f) {
-    const int ti = f - p.pt;
-    load_patch(p, n, ti, ho0, wo0, pr);
-    store_patch(smem + ((ti + p.pt) % SLOTS) * FRAME_BYTES, pr);
-  }
-  __syncthreads();
-
-  float cs[COT][4], cq[COT][4];
-#pragma unroll
-  for (int c = 0; c < COT; ++c)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) { cs[c][r] = 0.f; cq[c][r] = 0.f; }
-
-  const int ww = li;                 // position column inside the tile
-  const int half = g & 1;            // channel half of the lane's 8 k-values
-  for (int to = 0; to < p.To; ++to) {
-    const int tnext = to - p.pt + KT;  // frame needed first by the next output frame
-    const bool pf = to + 1 < p.To;
-    if (pf) load_patch(p, n, tnext, ho0, wo0, pr);
-    f32x4_t acc[2][COT];
-#pragma unroll
-    for (int q = 0; q < 2; ++q)
-#pragma unroll
-      for (int c = 0; c < COT; ++c) acc[q][c] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ks = 0; ks < KSTEPS; ++ks) {
-      const int tap = 2 * ks + (g >> 1);
-      const int dt = tap >> 4, bh = (tap >> 2) & 3, bw = tap & 3;
-      const char* slot = smem + ((to + dt) % SLOTS) * FRAME_BYTES;
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const int hh = 2 * w + q;
-        const bf16x8_t xb = *reinterpret_cast<const bf16x8_t*>(
-            slot + ((hh + bh) * PW + (ww + bw)) * POSB + half * 16);
-#pragma unroll
-        for (int c = 0; c < COT; ++c)
-          acc[q][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[c][ks], xb, acc[q][c], 0, 0, 0);
-      }
-    }
-    // epilogue: D[co][pos]: lane holds co = 16c + 4g + r for position (row 2w+q, col li)
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int ho = ho0 + 2 * w + q, wo = wo0 + li;
-      const bool valid = ho < p.Ho && wo < p.Wo;
-      const int64_t pos = (((int64_t)n * p.To + to) * p.Ho + ho) * p.Wo + wo;
-#pragma unroll
-      for (int c = 0; c < COT; ++c) {
-        const int co = 16 * c + 4 * g;
-        if (valid && co < p.Cout) {
-          float v[4] = {acc[q][c][0], acc[q][c][1], acc[q][c][2], acc[q][c][3]};
-          const uint2 pk = pack4(v);
-          *reinterpret_cast<uint2*>(p.y + pos * p.Cout + co) = pk;
-          float f[4];
-          unpack4(pk, f);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) { cs[c][r] += f[r]; cq[c][r] += f[r] * f[r]; }
-        }
-      }
-    }
-    if (pf) {
-      __syncthreads();  // everyone is done reading the slot about to be overwritten
-      store_patch(smem + ((tnext + p.pt) % SLOTS) * FRAME_BYTES, pr);
-      __syncthreads();
-    }
-  }
-  // BN partial sums of this workgroup: one slot per wave, summed in wave order (deterministic)
-  constexpr int CT = COT * 16;
-#pragma unroll
-  for (int c = 0; c < COT; ++c)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float s = sum16(cs[c][r]), q = sum16(cq[c][r]);
-      if (li == 0) {
-        red[w * 2 * CT + 16 * c + 4 * g + r] = s;
-        red[w * 2 * CT + CT + 16 * c + 4 * g + r] = q;
-      }
-    }
-  __syncthreads();
-  for (int i = tid; i < p.Cout; i += 256) {
-    float s = 0.f, q = 0.f;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) { s += red[k * 2 * CT + i]; q += red[k * 2 * CT + CT + i]; }
-    p.stats[(int64_t)blockIdx.x * 2 * p.Cout + i] = s;
-    p.stats[(int64_t)blockIdx.x * 2 * p.Cout + p.Cout + i] = q;
-  }
-}
-
-// ------------------------------------------------------------------------------------------------
-// weight gradient
-// ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ s16x4_t trr(const char* a) {
-  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(a));
-}
-
-template <int KT, int COT>
-__global__ __launch_bounds__(256) void stem_wgrad_kernel(const StemParams p) {
-  constexpr int TAPS = KT * 16;
-  constexpr int TPW = TAPS / 4;              // taps per wave
-  constexpr int SLOTS = KT + 1;
-  constexpr int DYB = TH * TW * COT * 16 * 2;  // dY tile bytes [128 pos][COT*16 co]
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* dyt = smem + SLOTS * FRAME_BYTES;
-
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int g = lane >> 4, li = lane & 15;
-  int b = blockIdx.x;
-  const int tw = b % p.tiles_w; b /= p.tiles_w;
-  const int th = b % p.tiles_h;
-  const int n = b / p.tiles_h;
-  const int ho0 = th * TH, wo0 = tw * TW;
-  const int COP = COT * 16;
-
-  f32x4_t acc[COT][TPW];
-#pragma unroll
-  for (int c = 0; c < COT; ++c)
-#pragma unroll
-    for (int t = 0; t < TPW; ++t) acc[c][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-  PatchRegs pr;
-  for (int f = 0; f < KT; ++f) {
-    const int ti = f - p.pt;
-    load_patch(p, n, ti, ho0, wo0, pr);
-    store_patch(smem + ((ti + p.pt) % SLOTS) * FRAME_BYTES, pr);
-  }
-  // tr-read lane roles: group g covers positions 8g..8g+7 of a 32-position k-step (rows of 16 w);
-  // lane supplies row (li >> 2) of a 4-row block and 4 columns at 8*(li & 3) bytes.
-  const int rq = li >> 2, cb = (li & 3) * 8;
-  for (int to = 0; to < p.To; ++to) {
-    // stage the dY tile of this frame: [pos = hh*16 + ww][COP] (zero for co >= Cout / invalid pos)
-    for (int idx = tid; idx < TH * TW * COP / 8; idx += 256) {
-      const int pos = idx / (COP / 8), ch = (idx % (COP / 8)) * 8;
-      const int ho = ho0 + pos / TW, wo = wo0 + pos % TW;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (ho < p.Ho && wo < p.Wo && ch < p.Cout)
-        v = *reinterpret_cast<const uint4*>(p.dy + ((((int64_t)n * p.To + to) * p.Ho + ho) * p.Wo + wo) * p.Cout + ch);
-      *reinterpret_cast<uint4*>(dyt + pos * COP * 2 + ch * 2) = v;
-    }
-    const int tnext = to - p.pt + KT;
-    const bool pf = to + 1 < p.To;
-    if (pf) load_patch(p, n, tnext, ho0, wo0, pr);
-    __syncthreads();
-#pragma unroll
-    for (int kstep = 0; kstep < TH * TW / 32; ++kstep) {
-      // positions of this k-step: rows 2*kstep, 2*kstep+1; group g -> row 2*kstep + (g >> 1), w 8*(g&1)..+7
-      const int hh = 2 * kstep + (g >> 1);
-      const int wq = 8 * (g & 1) + rq;          // position column of the lane's tr-read row (first block)
-      bf16x8_t a[COT];
-#pragma unroll
-      for (int c = 0; c < COT; ++c) {
-        const char* base = dyt + (hh * TW + wq) * COP * 2 + c * 32 + cb;
-        s16x4_t lo = trr(base), hi = trr(base + 4 * COP * 2);
-        s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        a[c] = __builtin_bit_cast(bf16x8_t, v);
-      }
-#pragma unroll
-      for (int t = 0; t < TPW; ++t) {
-        const int tap = w * TPW + t;
-        const int dt = tap >> 4, bh = (tap >> 2) & 3, bw = tap & 3;
-        const char* slot = smem + ((to + dt) % SLOTS) * FRAME_BYTES;
-        const char* base = slot + ((hh + bh) * PW + (wq + bw)) * POSB + cb;
-        s16x4_t lo = trr(base), hi = trr(base + 4 * POSB);
-        s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        const bf16x8_t xb = __builtin_bit_cast(bf16x8_t, v);
-#pragma unroll
-        for (int c = 0; c < COT; ++c)
-          acc[c][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[c], xb, acc[c][t], 0, 0, 0);
-      }
-    }
-    __syncthreads();
-    if (pf) {
-      store_patch(smem + ((tnext + p.pt) % SLOTS) * FRAME_BYTES, pr);
-    }
-  }
-  // D[co][k]: lane holds channel k = li of tap, co = 16c + 4g + r
-#pragma unroll
-  for (int c = 0; c < COT; ++c)
-#pragma unroll
-    for (int t = 0; t < TPW; ++t) {
-      const int tap = w * TPW + t;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int co = 16 * c + 4 * g + r;
-        if (co < p.Cout) atomicAdd(p.dw + (int64_t)co * TAPS * 16 + tap * 16 + li, acc[c][t][r]);
-      }
-    }
-}
-
-// ------------------------------------------------------------------------------------------------
-// Cout == 8 temporal stem (fast pathway, k(KT,7,7)): two output frames per MFMA.
-// With 8 output channels half of a 16-row MFMA tile is idle.  Here rows 0-7 carry output frame t and
-// rows 8-15 frame t+1: for input frame j of the pair's window (j = f - t + pt = 0..KT) frame t uses tap
-// j and frame t+1 tap j-1, so the A fragment of window frame j is [W[:, j]; W[:, j-1]] and one MFMA
-// serves both frames — KT+1 input frames per output pair instead of 2*KT (40 % fewer MFMAs at KT = 5).
-// The wgrad kernel mirrors it with the dY tiles of the two frames stacked as 16 "channels".
-// ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ bf16x8_t ld_frag(const uint16_t* p, bool ok) {
-  const uint4 u = ok ? *reinterpret_cast<const uint4*>(p) : make_uint4(0, 0, 0, 0);
-  return __builtin_bit_cast(bf16x8_t, u);
-}
 
 constexpr uint32_t OOB = 0x7ffffff0u;         // buffer offset past num_records: the load returns zeros
 constexpr int SLOT_BYTES = 448 * 16;           // frame slot: 418 chunks padded to 7 x 64 lanes
@@ -330,8 +72,232 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t clip_rsrc(const uint16_t* base
   return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)bytes, 0x00020000);
 }
 
+// ------------------------------------------------------------------------------------------------
+// forward
+// ------------------------------------------------------------------------------------------------
+template <int KT, int COT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void stem_fwd_kernel(const StemParams p) {
+  constexpr int TAPS = KT * 16;
+  constexpr int KSTEPS = TAPS * 16 / 32;  // 2 taps per MFMA k-step
+  constexpr int SLOTS = KT + 1;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* red = reinterpret_cast<float*>(smem + SLOTS * SLOT_BYTES);  // [4 waves][2][COT*16]
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  int b = blockIdx.x;
+  const int tw = b % p.tiles_w; b /= p.tiles_w;
+  const int th = b % p.tiles_h;
+  const int n = b / p.tiles_h;
+  const int ho0 = th * TH, wo0 = tw * TW;
+
+  const __amdgpu_buffer_rsrc_t xr =
+      clip_rsrc(p.x + (int64_t)n * p.T * p.Hs * p.Ws * 16, (uint32_t)(p.T * p.Hs * p.Ws * 32));
+  // weight fragments (A operand: lane holds W[co = 16*c + li][k = 32*ks + 8*g .. +8])
+  bf16x8_t wa[COT][KSTEPS];
+#pragma unroll
+  for (int c = 0; c < COT; ++c)
+#pragma unroll
+    for (int ks = 0; ks < KSTEPS; ++ks)
+      wa[c][ks] = *reinterpret_cast<const bf16x8_t*>(p.w + (int64_t)(16 * c + li) * (TAPS * 16) + ks * 32 + 8 * g);
+
+  // prologue: frames -pt .. -pt+KT-1 into slots 0..KT-1 (frame ti lives in slot (ti + pt) % SLOTS)
+  for (int f = 0; f < KT; ++f) dma_patch(xr, p, f - p.pt, ho0, wo0, smem + f * SLOT_BYTES);
+  __syncthreads();
+
+  float cs[COT][4], cq[COT][4];
+#pragma unroll
+  for (int c = 0; c < COT; ++c)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { cs[c][r] = 0.f; cq[c][r] = 0.f; }
+
+  const int ww = li;                 // position column inside the tile
+  const int half = g & 1;            // channel half of the lane's 8 k-values
+  for (int to = 0; to < p.To; ++to) {
+    if (to + 1 < p.To)  // frame needed first by the next output frame, into the slot outside the window
+      dma_patch(xr, p, to - p.pt + KT, ho0, wo0, smem + ((to + KT) % SLOTS) * SLOT_BYTES);
+    f32x4_t acc[2][COT];
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int c = 0; c < COT; ++c) acc[q][c] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KSTEPS; ++ks) {
+      const int tap = 2 * ks + (g >> 1);
+      const int dt = tap >> 4, bh = (tap >> 2) & 3, bw = tap & 3;
+      const char* slot = smem + ((to + dt) % SLOTS) * SLOT_BYTES;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int hh = 2 * w + q;
+        const bf16x8_t xb = *reinterpret_cast<const bf16x8_t*>(
+            slot + ((hh + bh) * PW + (ww + bw)) * POSB + half * 16);
+#pragma unroll
+        for (int c = 0; c < COT; ++c)
+          acc[q][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[c][ks], xb, acc[q][c], 0, 0, 0);
+      }
+    }
+    // epilogue: D[co][pos]: lane holds co = 16c + 4g + r for position (row 2w+q, col li)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int ho = ho0 + 2 * w + q, wo = wo0 + li;
+      const bool valid = ho < p.Ho && wo < p.Wo;
+      const int64_t pos = (((int64_t)n * p.To + to) * p.Ho + ho) * p.Wo + wo;
+#pragma unroll
+      for (int c = 0; c < COT; ++c) {
+        const int co = 16 * c + 4 * g;
+        if (valid && co < p.Cout) {
+          float v[4] = {acc[q][c][0], acc[q][c][1], acc[q][c][2], acc[q][c][3]};
+          const uint2 pk = pack4(v);
+          *reinterpret_cast<uint2*>(p.y + pos * p.Cout + co) = pk;
+          float f[4];
+          unpack4(pk, f);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) { cs[c][r] += f[r]; cq[c][r] += f[r] * f[r]; }
+        }
+      }
+    }
+    __syncthreads();  // next frame landed (vmcnt(0) + barrier); window frame 0's slot is free
+  }
+  // BN partial sums of this workgroup: one slot per wave, summed in wave order (deterministic)
+  constexpr int CT = COT * 16;
+#pragma unroll
+  for (int c = 0; c < COT; ++c)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float s = sum16(cs[c][r]), q = sum16(cq[c][r]);
+      if (li == 0) {
+        red[w * 2 * CT + 16 * c + 4 * g + r] = s;
+        red[w * 2 * CT + CT + 16 * c + 4 * g + r] = q;
+      }
+    }
+  __syncthreads();
+  for (int i = tid; i < p.Cout; i += 256) {
+    float s = 0.f, q = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { s += red[k * 2 * CT + i]; q += red[k * 2 * CT + CT + i]; }
+    p.stats[(int64_t)blockIdx.x * 2 * p.Cout + i] = s;
+    p.stats[(int64_t)blockIdx.x * 2 * p.Cout + p.Cout + i] = q;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// weight gradient
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ s16x4_t trr(const char* a) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(a));
+}
+
+template <int KT, int COT>
+__global__ __launch_bounds__(256) void stem_wgrad_kernel(const StemParams p) {
+  constexpr int TAPS = KT * 16;
+  constexpr int TPW = TAPS / 4;              // taps per wave
+  constexpr int SLOTS = KT + 1;
+  constexpr int COP = COT * 16;
+  constexpr int DYB = TH * TW * COP * 2;     // dY tile bytes [128 pos][COP co]
+  constexpr int DYC = TH * TW * COP / 8 / 256;  // 16-B dY chunks per thread
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* dyt = smem + SLOTS * SLOT_BYTES;     // two dY tile buffers (frame parity)
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  int b = blockIdx.x;
+  const int tw = b % p.tiles_w; b /= p.tiles_w;
+  const int th = b % p.tiles_h;
+  const int n = b / p.tiles_h;
+  const int ho0 = th * TH, wo0 = tw * TW;
+  const __amdgpu_buffer_rsrc_t xr =
+      clip_rsrc(p.x + (int64_t)n * p.T * p.Hs * p.Ws * 16, (uint32_t)(p.T * p.Hs * p.Ws * 32));
+  const __amdgpu_buffer_rsrc_t yr = clip_rsrc(p.dy + (int64_t)n * p.To * p.Ho * p.Wo * p.Cout,
+                                              (uint32_t)(p.To * p.Ho * p.Wo * p.Cout * 2));
+  // dY tile of frame `to` -> buf by LDS-DMA: chunk idx = pos * (COP / 8) + ch / 8 at LDS offset idx * 16
+  auto dma_dy = [&](int to, char* buf) {
+#pragma unroll
+    for (int k = 0; k < DYC; ++k) {
+      const int idx = tid + k * 256;
+      const int pos = idx / (COP / 8), ch = (idx % (COP / 8)) * 8;
+      const int ho = ho0 + pos / TW, wo = wo0 + pos % TW;
+      const bool ok = ho < p.Ho && wo < p.Wo && ch < p.Cout;
+      const uint32_t vo = ok ? (uint32_t)((((to * p.Ho + ho) * p.Wo + wo) * p.Cout + ch) * 2) : OOB;
+      dma16(yr, buf + (k * 256 + w * 64) * 16, vo);
+    }
+  };
+
+  f32x4_t acc[COT][TPW];
+#pragma unroll
+  for (int c = 0; c < COT; ++c)
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) acc[c][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  for (int f = 0; f < KT; ++f) dma_patch(xr, p, f - p.pt, ho0, wo0, smem + f * SLOT_BYTES);
+  dma_dy(0, dyt);
+  __syncthreads();
+  // tr-read lane roles: group g covers positions 8g..8g+7 of a 32-position k-step (rows of 16 w);
+  // lane supplies row (li >> 2) of a 4-row block and 4 columns at 8*(li & 3) bytes.
+  const int rq = li >> 2, cb = (li & 3) * 8;
+  for (int to = 0; to < p.To; ++to) {
+    const char* dcur = dyt + (to & 1) * DYB;
+    if (to + 1 < p.To) {  // next frame's input (slot outside the window) and dY tile (other buffer)
+      dma_patch(xr, p, to - p.pt + KT, ho0, wo0, smem + ((to + KT) % SLOTS) * SLOT_BYTES);
+      dma_dy(to + 1, dyt + ((to + 1) & 1) * DYB);
+    }
+#pragma unroll
+    for (int kstep = 0; kstep < TH * TW / 32; ++kstep) {
+      // positions of this k-step: rows 2*kstep, 2*kstep+1; group g -> row 2*kstep + (g >> 1), w 8*(g&1)..+7
+      const int hh = 2 * kstep + (g >> 1);
+      const int wq = 8 * (g & 1) + rq;          // position column of the lane's tr-read row (first block)
+      bf16x8_t a[COT];
+#pragma unroll
+      for (int c = 0; c < COT; ++c) {
+        const char* base = dcur + (hh * TW + wq) * COP * 2 + c * 32 + cb;
+        s16x4_t lo = trr(base), hi = trr(base + 4 * COP * 2);
+        s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        a[c] = __builtin_bit_cast(bf16x8_t, v);
+      }
+#pragma unroll
+      for (int t = 0; t < TPW; ++t) {
+        const int tap = w * TPW + t;
+        const int dt = tap >> 4, bh = (tap >> 2) & 3, bw = tap & 3;
+        const char* slot = smem + ((to + dt) % SLOTS) * SLOT_BYTES;
+        const char* base = slot + ((hh + bh) * PW + (wq + bw)) * POSB + cb;
+        s16x4_t lo = trr(base), hi = trr(base + 4 * POSB);
+        s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        const bf16x8_t xb = __builtin_bit_cast(bf16x8_t, v);
+#pragma unroll
+        for (int c = 0; c < COT; ++c)
+          acc[c][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[c], xb, acc[c][t], 0, 0, 0);
+      }
+    }
+    __syncthreads();  // next frame + dY tile landed; the window's first slot and this dY buffer are free
+  }
+  // D[co][k]: lane holds channel k = li of tap, co = 16c + 4g + r
+#pragma unroll
+  for (int c = 0; c < COT; ++c)
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+      const int tap = w * TPW + t;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = 16 * c + 4 * g + r;
+        if (co < p.Cout) atomicAdd(p.dw + (int64_t)co * TAPS * 16 + tap * 16 + li, acc[c][t][r]);
+      }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Cout == 8 temporal stem (fast pathway, k(KT,7,7)): two output frames per MFMA.
+// With 8 output channels half of a 16-row MFMA tile is idle.  Here rows 0-7 carry output frame t and
+// rows 8-15 frame t+1: for input frame j of the pair's window (j = f - t + pt = 0..KT) frame t uses tap
+// j and frame t+1 tap j-1, so the A fragment of window frame j is [W[:, j]; W[:, j-1]] and one MFMA
+// serves both frames — KT+1 input frames per output pair instead of 2*KT (40 % fewer MFMAs at KT = 5).
+// The wgrad kernel mirrors it with the dY tiles of the two frames stacked as 16 "channels".
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ bf16x8_t ld_frag(const uint16_t* p, bool ok) {
+  const uint4 u = ok ? *reinterpret_cast<const uint4*>(p) : make_uint4(0, 0, 0, 0);
+  return __builtin_bit_cast(bf16x8_t, u);
+}
+
 template <int KT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void stem_fwd_pair_kernel(const StemParams p) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void stem_fwd_pair_kernel(const StemParams p) {
   constexpr int TAPS = KT * 16;
   constexpr int J = KT + 1;     // input frames per output-frame pair
   constexpr int KS = 8;         // k-steps per input frame: 16 spatial taps x 16 channels / 32
@@ -426,7 +392,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 }
 
 template <int KT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void stem_wgrad_pair_kernel(const StemParams p) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void stem_wgrad_pair_kernel(const StemParams p) {
   constexpr int TAPS = KT * 16;
   constexpr int J = KT + 1;
   constexpr int SLOTS = J + 2;
@@ -554,13 +520,13 @@ __global__ void stem_pack_kernel(const float* __restrict__ w, uint16_t* __restri
 
 template <int KT, int COT>
 void launch_fwd(const StemParams& p, hipStream_t s) {
-  const size_t lds = (KT + 1) * FRAME_BYTES + 4 * 2 * COT * 16 * 4;
+  const size_t lds = (KT + 1) * SLOT_BYTES + 4 * 2 * COT * 16 * 4;
   hipLaunchKernelGGL((stem_fwd_kernel<KT, COT>), dim3(p.N * p.tiles_h * p.tiles_w), dim3(256), lds, s, p);
 }
 
 template <int KT, int COT>
 void launch_wgrad(const StemParams& p, hipStream_t s) {
-  const size_t lds = (KT + 1) * FRAME_BYTES + TH * TW * COT * 16 * 2;
+  const size_t lds = (KT + 1) * SLOT_BYTES + 2 * TH * TW * COT * 16 * 2;
   hipLaunchKernelGGL((stem_wgrad_kernel<KT, COT>), dim3(p.N * p.tiles_h * p.tiles_w), dim3(256), lds, s, p);
 }
 
