@@ -711,7 +711,11 @@ void conv_igemm_kernel(const ConvParams p) {
           red[wm * 2 * BN + BN + nl] = q;
         }
       }
-    __syncthreads();
+    // raw barrier: __syncthreads would first drain every output store of the tile (vmcnt(0)) and expose
+    // the write-acknowledge latency on every workgroup; only the LDS slots must be visible here
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
     for (int i = tid; i < BN; i += NT) {
       const int n = n0 + i;
       if (n < p.Ngemm) {

@@ -136,6 +136,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void s
           acc[q][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[c][ks], xb, acc[q][c], 0, 0, 0);
       }
     }
+    __syncthreads();  // next frame landed; window frame 0's slot is free.  Stores after the barrier.
     // epilogue: D[co][pos]: lane holds co = 16c + 4g + r for position (row 2w+q, col li)
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
@@ -156,7 +157,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void s
         }
       }
     }
-    __syncthreads();  // next frame landed (vmcnt(0) + barrier); window frame 0's slot is free
   }
   // BN partial sums of this workgroup: one slot per wave, summed in wave order (deterministic)
   constexpr int CT = COT * 16;
@@ -353,6 +353,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void s
         }
       }
     }
+    // barrier first (next frames landed; window frames 0, 1 free), then this pair's stores: their write
+    // latency hides behind the next pair's MFMAs instead of stalling at a barrier
+    __syncthreads();
     const int to = t0 + (g >> 1);
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
@@ -368,7 +371,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void s
         for (int r = 0; r < 4; ++r) { cs[r] += f[r]; cq[r] += f[r] * f[r]; }
       }
     }
-    __syncthreads();  // new frames landed (vmcnt(0) + barrier); window frames 0, 1 may be overwritten next
   }
   // BN partial sums: lanes g and g^2 hold the same channels (frames t0 / t0+1); fixed summation order
 #pragma unroll

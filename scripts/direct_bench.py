@@ -18,6 +18,8 @@ SHAPES = {
     "f.res2.conv_c": (8, 32, (1, 1, 1), (1, 1, 1), (0, 0, 0), (32, 56, 56)),
     "f.res3.conv_b": (16, 16, (1, 3, 3), (1, 1, 1), (0, 1, 1), (32, 28, 28)),
     "s.res2.conv_a0": (80, 64, (1, 1, 1), (1, 1, 1), (0, 0, 0), (8, 56, 56)),
+    "s.res2.conv_c": (64, 256, (1, 1, 1), (1, 1, 1), (0, 0, 0), (8, 56, 56)),
+    "s.res3.conv_c": (128, 512, (1, 1, 1), (1, 1, 1), (0, 0, 0), (8, 28, 28)),
 }
 
 
@@ -28,6 +30,8 @@ def main():
     ap.add_argument("--cfg", default="direct2048")
     ap.add_argument("--affine", type=int, default=1)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--nostats", action="store_true")
+    ap.add_argument("--nostore", action="store_true", help="debug builds only: accum=2 skips the output store")
     a = ap.parse_args()
     from pytorchvideo_accelerate_amd.ops._ext import require
     C = require()
@@ -50,8 +54,8 @@ def main():
     cfg = int(a.cfg) if cfg is None else cfg
 
     def run():
-        C.conv_igemm(xa.t, wf, y, stats, sc if a.affine else None, sh if a.affine else None, 2 if a.affine else 0,
-                     0, g, 8, cfg)
+        C.conv_igemm(xa.t, wf, y, None if a.nostats else stats, sc if a.affine else None, sh if a.affine else None, 2 if a.affine else 0,
+                     2 if a.nostore else 0, g, 8, cfg)
     for _ in range(3):
         run()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
