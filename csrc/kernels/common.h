@@ -23,9 +23,18 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
   return __builtin_bit_cast(bf16_t, b);
 }
 
-__device__ __forceinline__ uint32_t pack2(float a, float b) {
-  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+typedef __attribute__((ext_vector_type(2))) float f32x2_t;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+typedef __attribute__((ext_vector_type(2))) short s16x2_t;
+
+// 2 x f32 -> packed bf16 pair in ONE v_cvt_pk_bf16_f32 (RNE, NaN-preserving).  Two scalar __bf16 casts
+// OR-ed together cost 2 cvt + 4 mask/shift/or VALU ops per pair (measured in the ISA): the packing sits
+// in every epilogue and elementwise kernel, so it matters.
+__device__ __forceinline__ uint32_t cvt_pk_bf16(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){a, b}, bf16x2_t));
 }
+
+__device__ __forceinline__ uint32_t pack2(float a, float b) { return cvt_pk_bf16(a, b); }
 
 __device__ __forceinline__ void unpack8(const uint4& v, float* f) {
   f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
@@ -38,14 +47,6 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
   return make_uint4(pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7]));
 }
 
-typedef __attribute__((ext_vector_type(2))) float f32x2_t;
-typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
-typedef __attribute__((ext_vector_type(2))) short s16x2_t;
-
-// 2 x f32 -> packed bf16 pair in ONE v_cvt_pk_bf16_f32 (RNE, NaN-preserving)
-__device__ __forceinline__ uint32_t cvt_pk_bf16(float a, float b) {
-  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){a, b}, bf16x2_t));
-}
 
 __device__ __forceinline__ uint4 pack8_fast(const float* f) {
   return make_uint4(cvt_pk_bf16(f[0], f[1]), cvt_pk_bf16(f[2], f[3]), cvt_pk_bf16(f[4], f[5]), cvt_pk_bf16(f[6], f[7]));
