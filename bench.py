@@ -1,19 +1,31 @@
 """Headline benchmark: SlowFast-R50 32x2x224 bf16 training throughput (clips/s, whole job).
 
-    python bench.py --gpus N --steps K --warmup W          # N>1: launched by torch.distributed.run
+    python bench.py --gpus N --steps K --warmup W
+
+``--gpus N > 1`` without a torchrun environment: this process starts
+``python -m torch.distributed.run --nproc-per-node N`` as a CHILD (before touching the GPU), waits for it
+and exits with its status; each rank then runs one GPU (RCCL over xGMI).  Under torchrun/``accelerate
+launch`` (``WORLD_SIZE`` set) it runs as one rank directly.
 
 One training step = on-device video preprocessing of synthetic decoded uint8 clips (temporal subsample,
 random short-side scale, random crop, flip, normalise, PackPathway) → fused SlowFast forward/backward
 on the gfx950 kernels → bucketed RCCL gradient all-reduce overlapped with backward → fused SGD +
 weight re-pack.  Weights are random-init (no network); data is synthetic uint8 frames of the Kinetics
-clip shape (64 source frames = 2.13 s at 30 fps, 256x340).  Timing: W untimed warmup steps, then K
-steps bracketed by barrier + device synchronize, max over ranks; rank 0 prints one JSON line.
+clip shape (64 source frames = 2.13 s at 30 fps, 256x340).  Timing: W untimed warmup steps (plus one
+untimed autotuning pass, in which the ranks agree on kernel configurations), then K steps bracketed by
+barrier + device synchronize, max over ranks; rank 0 prints one JSON line.
+
+``--plumbing``: CPU/gloo rehearsal of the same launch + gradient-sync path on the reference PyTorch
+modules (tiny crop, no dropout) — what the CPU test suite drives (tests/test_bench_launch_cpu.py).
+Reference launch being benchmarked: ``run_slowfast_r50.sh:1`` / ``run.py:196-198`` (accelerate DDP).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -28,7 +40,7 @@ METRIC = "clips/sec (whole node) SlowFast-R50 32x2x224 at 1/2/4/8 MI355X; step-t
 STOCK_CLIPS_PER_S_1GPU = 75.35
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -44,85 +56,184 @@ def parse():
     ap.add_argument("--src-h", type=int, default=256)
     ap.add_argument("--src-w", type=int, default=340)
     ap.add_argument("--bucket-mb", type=float, default=32.0)
+    ap.add_argument("--first-bucket-mb", type=float, default=4.0)
+    ap.add_argument("--grad-dtype", choices=("fp32", "bf16"), default="fp32",
+                    help="all-reduce payload dtype (bf16 = DDP bf16_compress_hook analogue)")
     ap.add_argument("--lr", type=float, default=0.1)
     ap.add_argument("--grad-accum", type=int, default=1,
                     help="micro-batches of --batch clips per optimizer step (gradients all-reduced once, on the last)")
-    return ap.parse_args()
+    ap.add_argument("--plumbing", action="store_true", help="CPU/gloo rehearsal on the PyTorch modules")
+    ap.add_argument("--dump", default=None, help="(plumbing) write rank-0 first-step gradients + final params here")
+    return ap.parse_args(argv)
 
 
-def main():
-    a = parse()
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def self_launch(a, argv) -> int:
+    """Run this script as ``a.gpus`` torchrun ranks in a child process; returns its exit status.
+
+    Called before anything initialises the GPU (``torch.cuda.device_count`` does not), and never via
+    exec: the child is a separate process and this one only waits for it."""
+    if not a.plumbing:
+        ndev = torch.cuda.device_count()
+        if ndev < a.gpus:
+            print(f"bench.py: --gpus {a.gpus} requested but only {ndev} GPU(s) visible", file=sys.stderr)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "4")
+    return subprocess.call(cmd, env=env)
+
+
+# ---------------------------------------------------------------------------------------------- plumbing
+def plumbing_model(a):
+    from pytorchvideo_accelerate_amd.models import reference as R
+    torch.manual_seed(1234)
+    s = a.crop // 32
+    return R.create_slowfast(a.depth, a.classes, alpha=a.alpha, dropout_rate=0.0,
+                             head_pool_kernel_sizes=((a.frames // a.alpha, s, s), (a.frames, s, s)))
+
+
+def plumbing_batch(a, rank: int, i: int):
+    g = torch.Generator().manual_seed(1000 + 7919 * rank + i)
+    fast = torch.randn(a.batch, 3, a.frames, a.crop, a.crop, generator=g)
+    idx = torch.linspace(0, a.frames - 1, a.frames // a.alpha).long()
+    return [fast.index_select(2, idx).contiguous(), fast], torch.randint(0, a.classes, (a.batch,), generator=g)
+
+
+# ---------------------------------------------------------------------------------------------- main
+def run(a):
     from pytorchvideo_accelerate_amd.parallel.dist import DistState
     from pytorchvideo_accelerate_amd.parallel.ddp import GradSync
-    from pytorchvideo_accelerate_amd.models import reference as R
-    from pytorchvideo_accelerate_amd.models.fused import FusedNet
     from pytorchvideo_accelerate_amd.ops.optim import FusedSGD
-    from pytorchvideo_accelerate_amd.data.transforms import GpuClipBatch, sample_params
 
-    st = DistState.from_env()
+    st = DistState.from_env(cpu=a.plumbing)
     dev = st.device
-    assert dev.type == "cuda", "bench.py needs a GPU"
-    torch.manual_seed(1234)
-    model = R.create_slowfast(a.depth, a.classes)
-    eng = FusedNet(model, dev)
-    st.broadcast_tensors([eng.flat.data] + [b for b in model.buffers()])
-    eng.pack()
-    opt = FusedSGD(eng.flat, lr=a.lr, momentum=0.9, weight_decay=1e-4, after_step=eng.pack)
-    bounds = sorted(set(eng.flat.span(p)[1] for p in eng.flat.params))
-    sync = GradSync(eng.flat.grad, st, a.bucket_mb, boundaries=bounds)
-    eng.grad_hook = sync.progress
-
+    gdt = torch.bfloat16 if a.grad_dtype == "bf16" else None
     B = a.batch
-    gen = torch.Generator().manual_seed(1000 + st.rank)
-    frames = torch.empty(B, a.src_frames, a.src_h, a.src_w, 3, dtype=torch.uint8, device=dev)
-    eng.C.synth_frames(frames, 7 + st.rank)
-    prep = GpuClipBatch(dev, a.frames, a.crop, a.alpha, s2d=eng.input_s2d)
-    labels_all = torch.randint(0, a.classes, (64, B), generator=gen).to(dev)
+    dump = {}
+    if a.plumbing:
+        from pytorchvideo_accelerate_amd.engine.backends import TorchBackend
+        be = TorchBackend(plumbing_model(a), st, "no", a.bucket_mb)
+        be.sync = GradSync(be.flat.grad, st, a.bucket_mb, first_mb=a.first_bucket_mb, grad_dtype=gdt)
+        st.broadcast_tensors([be.flat.data] + list(be.model.buffers()))
+        be.train()
+        opt = FusedSGD(be.flat, lr=a.lr, momentum=0.9, weight_decay=1e-4)
+        sync = be.sync
 
-    def step(i):
-        params = [sample_params(a.src_frames, a.src_h, a.src_w, a.frames, a.crop, True, generator=gen)
-                  for _ in range(B)]
-        xs = prep(frames, params)
-        opt.zero_grad()
-        for j in range(a.grad_accum):
-            if j:
-                xs = prep(frames, params)
-            last = j == a.grad_accum - 1
-            sync.begin(last)
-            loss, _ = eng.forward_backward(xs, labels_all[(i * a.grad_accum + j) % 64], loss_scale=1.0 / a.grad_accum)
-            sync.finish()
-        opt.step()
-        return loss
+        def step(i, tune=False):
+            opt.zero_grad()
+            for j in range(a.grad_accum):
+                xs, y = plumbing_batch(a, st.rank, i * a.grad_accum + j)
+                loss, _ = be.train_step(xs, y, loss_scale=1.0 / a.grad_accum, sync=j == a.grad_accum - 1)
+            if i == 0 and a.dump:
+                dump["grad"] = be.flat.grad.clone()
+            opt.step()
+            return loss
+    else:
+        from pytorchvideo_accelerate_amd.models import reference as R
+        from pytorchvideo_accelerate_amd.models.fused import FusedNet
+        from pytorchvideo_accelerate_amd.data.transforms import GpuClipBatch, sample_params
+        assert dev.type == "cuda", "bench.py needs a GPU (or --plumbing)"
+        torch.manual_seed(1234)
+        model = R.create_slowfast(a.depth, a.classes)
+        eng = FusedNet(model, dev)
+        if st.world_size > 1:
+            eng.tuner.agree = st.agree_times
+        st.broadcast_tensors([eng.flat.data] + [b for b in model.buffers()])
+        eng.pack()
+        opt = FusedSGD(eng.flat, lr=a.lr, momentum=0.9, weight_decay=1e-4, after_step=eng.pack)
+        bounds = sorted(set(eng.flat.span(p)[1] for p in eng.flat.params))
+        sync = GradSync(eng.flat.grad, st, a.bucket_mb, boundaries=bounds, first_mb=a.first_bucket_mb,
+                        grad_dtype=gdt, timing=st.world_size > 1)
+        eng.grad_hook = sync.progress
+        gen = torch.Generator().manual_seed(1000 + st.rank)
+        frames = torch.empty(B, a.src_frames, a.src_h, a.src_w, 3, dtype=torch.uint8, device=dev)
+        eng.C.synth_frames(frames, 7 + st.rank)
+        prep = GpuClipBatch(dev, a.frames, a.crop, a.alpha, s2d=eng.input_s2d)
+        labels_all = torch.randint(0, a.classes, (64, B), generator=gen).to(dev)
 
-    # The conv autotuner (ops/tune.py) times its candidates on the first execution of each geometry; that
-    # one-time cost belongs outside the timed region even when --warmup 0 is requested.
+        def step(i, tune=False):
+            params = [sample_params(a.src_frames, a.src_h, a.src_w, a.frames, a.crop, True, generator=gen)
+                      for _ in range(B)]
+            xs = prep(frames, params)
+            if tune:
+                # untimed autotuning pass: every conv geometry is tuned (ranks agree on the choice) with
+                # no gradient all-reduce in flight and no optimizer step (weights stay rank-identical)
+                sync.begin(False)
+                eng.forward_backward(xs, labels_all[0], accumulate=False)
+                return None
+            opt.zero_grad()
+            for j in range(a.grad_accum):
+                if j:
+                    xs = prep(frames, params)
+                last = j == a.grad_accum - 1
+                sync.begin(last)
+                loss, _ = eng.forward_backward(xs, labels_all[(i * a.grad_accum + j) % 64],
+                                               loss_scale=1.0 / a.grad_accum)
+                sync.finish()
+            opt.step()
+            return loss
+
+    if not a.plumbing:
+        step(0, tune=True)
     for i in range(max(a.warmup, 1)):
         step(i)
-    torch.cuda.synchronize()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
     st.barrier()
-    torch.cuda.synchronize()
-    torch.cuda.reset_peak_memory_stats(dev)
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+        torch.cuda.reset_peak_memory_stats(dev)
+    sync.stats(reset=True)
     times = []
     t0 = time.perf_counter()
     for i in range(a.steps):
-        ev0 = torch.cuda.Event(enable_timing=True)
-        ev1 = torch.cuda.Event(enable_timing=True)
-        ev0.record()
-        loss = step(a.warmup + i)
-        ev1.record()
-        times.append((ev0, ev1))
-    torch.cuda.synchronize()
+        if dev.type == "cuda":
+            ev0 = torch.cuda.Event(enable_timing=True)
+            ev1 = torch.cuda.Event(enable_timing=True)
+            ev0.record()
+            loss = step(a.warmup + i)
+            ev1.record()
+            times.append((ev0, ev1))
+        else:
+            s0 = time.perf_counter()
+            loss = step(a.warmup + i)
+            times.append((time.perf_counter() - s0) * 1e3)
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
     st.barrier()
-    torch.cuda.synchronize()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    step_ms = sorted(e0.elapsed_time(e1) for e0, e1 in times)
-    p50 = step_ms[len(step_ms) // 2]
-    el = torch.tensor([elapsed], device=dev)
+    step_ms = sorted(e0.elapsed_time(e1) for e0, e1 in times) if dev.type == "cuda" else sorted(times)
+    p50 = step_ms[len(step_ms) // 2] if step_ms else 0.0
+    comm = sync.stats()
+    el = torch.tensor([elapsed], device=dev if st.backend == "nccl" else "cpu")
     st.all_reduce_(el, "max")
     elapsed = float(el.item())
-    ms_per_step = elapsed * 1000.0 / a.steps
-    clips = B * a.grad_accum * st.world_size * a.steps / elapsed
+    ms_per_step = elapsed * 1000.0 / max(a.steps, 1)
+    clips = B * a.grad_accum * st.world_size * a.steps / elapsed if a.steps else 0.0
+    if a.dump:
+        dump["params"] = opt.flat.data.clone()
+        gathered = [torch.zeros_like(dump["params"]) for _ in range(st.world_size)]
+        if st.world_size > 1:
+            import torch.distributed as dist
+            dist.all_gather(gathered, dump["params"])
+        else:
+            gathered = [dump["params"]]
+        if st.is_main_process:
+            torch.save({"grad": dump["grad"].cpu(), "params": [g.cpu() for g in gathered],
+                        "world_size": st.world_size}, a.dump)
     if st.is_main_process:
+        headline = (a.depth, a.frames, a.crop, a.alpha) == (50, 32, 224, 4) and not a.plumbing
         print(json.dumps({
             "metric": METRIC,
             "value": round(clips, 2),
@@ -135,16 +246,32 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             # the stock baseline is measured on the headline config only
-            "vs_baseline": (round(clips / (STOCK_CLIPS_PER_S_1GPU * st.world_size), 3)
-                            if (a.depth, a.frames, a.crop, a.alpha) == (50, 32, 224, 4) else None),
-            "dtype": "bf16",
-            "data": "synthetic uint8 decoded clips (64x256x340), on-device preprocessing; random-init weights",
-            "config": {"model": f"SlowFast-R{a.depth} {a.frames}x2x{a.crop}", "global_batch": B * a.grad_accum * st.world_size,
-                       "per_gpu_batch": B, "grad_accum": a.grad_accum, "seq_len": a.frames, "parallelism": f"dp{st.world_size}",
-                       "classes": a.classes, "final_loss": round(float(loss), 4),
-                       "peak_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2**30, 1)},
+            "vs_baseline": round(clips / (STOCK_CLIPS_PER_S_1GPU * st.world_size), 3) if headline else None,
+            "dtype": "fp32" if a.plumbing else "bf16",
+            "data": ("synthetic normal clips, CPU plumbing run" if a.plumbing else
+                     "synthetic uint8 decoded clips (64x256x340), on-device preprocessing; random-init weights"),
+            "config": {"model": f"SlowFast-R{a.depth} {a.frames}x2x{a.crop}",
+                       "global_batch": B * a.grad_accum * st.world_size,
+                       "per_gpu_batch": B, "grad_accum": a.grad_accum, "seq_len": a.frames,
+                       "parallelism": f"dp{st.world_size}", "backend": st.backend or "none",
+                       "grad_dtype": a.grad_dtype, "classes": a.classes,
+                       "final_loss": round(float(loss), 4) if loss is not None else None,
+                       "peak_mem_gb": (round(torch.cuda.max_memory_allocated(dev) / 2**30, 1)
+                                       if dev.type == "cuda" else None),
+                       **comm},
         }), flush=True)
     st.destroy()
+
+
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
+    a = parse(argv)
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(self_launch(a, argv))
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    if ws != a.gpus:
+        print(f"bench.py: WORLD_SIZE={ws} but --gpus {a.gpus}", file=sys.stderr)
+    run(a)
 
 
 if __name__ == "__main__":

@@ -95,6 +95,8 @@ class FusedBackend:
         self.state = state
         self.device = state.device
         self.net = FusedNet(model, self.device)
+        if state.world_size > 1:   # identical autotuner choices on every rank
+            self.net.tuner.agree = state.agree_times
         self.model = model
         self.flat = self.net.flat
         bounds = sorted(set(self.flat.span(p)[1] for p in self.flat.params))

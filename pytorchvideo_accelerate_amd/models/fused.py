@@ -196,7 +196,7 @@ class _ConvBN:
                 # first use: time tile variant x split-K target on a scratch accumulator (atomic adds; the
                 # scratch content is irrelevant), keep the fastest
                 scratch = eng.scratch("wgrad_tune", s.cout * K)
-                best = None
+                cands, times = [], []
                 for v in range(4):
                     bmw = C.wgrad_tile(s.cout, K, v)[0]
                     if bmw > max(16, s.cout) or bmw * 8 < s.cout:
@@ -210,10 +210,11 @@ class _ConvBN:
                             launch(c, scratch)
                         e1.record()
                         e1.synchronize()
-                        t = e0.elapsed_time(e1)
-                        if best is None or t < best[0]:
-                            best = (t, c)
-                cfg = best[1] if best else -1
+                        cands.append(c)
+                        times.append(e0.elapsed_time(e1))
+                if eng.tuner.agree is not None:   # same choice on every data-parallel rank
+                    times = eng.tuner.agree(times)
+                cfg = cands[min(range(len(cands)), key=times.__getitem__)] if cands else -1
             eng.wtune[tkey] = cfg
         if slab:  # per-split slabs summed in a fixed order: bitwise reproducible weight gradients
             part = eng.scratch("wgrad_slab", geometry(cfg)[0] * s.cout * K)

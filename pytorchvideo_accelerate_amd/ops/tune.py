@@ -16,7 +16,7 @@ from __future__ import annotations
 
 import os
 import sys
-from typing import Callable, Dict, List, Sequence, Tuple
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import torch
 
@@ -57,6 +57,9 @@ class ConvTuner:
         self.reps = reps
         self.cache: Dict[Tuple, int] = {}
         self._scratch: Dict[Tuple, torch.Tensor] = {}
+        # multi-rank consensus: ``agree(times) -> times`` (e.g. ``DistState.agree_times``, the per-candidate
+        # max over ranks) so that every data-parallel rank picks the same configuration
+        self.agree: Optional[Callable[[List[float]], List[float]]] = None
 
     # ---------------------------------------------------------------- candidates
     def candidates(self, g: Sequence[int], chunk: int, aff: int = 0, epi: bool = False) -> List[int]:
@@ -119,7 +122,6 @@ class ConvTuner:
         cands = self.candidates(g, chunk, aff, epi)
         if len(cands) <= 1:
             return cands[0] if cands else -1
-        best, best_t = -1, float("inf")
         times = []
         for cfg in cands:
             run(cfg, True)  # warm-up (instruction cache, first-touch)
@@ -130,10 +132,10 @@ class ConvTuner:
                 run(cfg, True)
             e1.record()
             e1.synchronize()
-            t = e0.elapsed_time(e1)
-            times.append((cfg, t / self.reps))
-            if t < best_t:
-                best, best_t = cfg, t
+            times.append((cfg, e0.elapsed_time(e1) / self.reps))
+        if self.agree is not None:
+            times = list(zip(cands, self.agree([t for _, t in times])))
+        best, best_t = min(times, key=lambda ct: ct[1])
         if self.log:
             print("tune M=%d N=%d K=%d taps=%s: " % (g[0], g[1], g[2], tuple(g[28:31]))
                   + " ".join("%s=%.1fus" % (describe(c), 1e3 * t) for c, t in times)

@@ -48,15 +48,22 @@ class DistState:
             st.device = torch.device("cuda", lr % max(ndev, 1))
             torch.cuda.set_device(st.device)
         if ws > 1:
-            st.backend = "nccl" if use_gpu else "gloo"
+            # PVA_DIST_BACKEND=gloo on a GPU: several ranks may share one device (1-GPU rehearsal of the
+            # multi-rank path; RCCL refuses duplicate devices).  Default on GPU: nccl (= RCCL on ROCm).
+            st.backend = os.environ.get("PVA_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
             st.distributed_type = "MULTI_GPU" if use_gpu else "MULTI_CPU"
             if not dist.is_initialized():
                 os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
                 os.environ.setdefault("MASTER_PORT", "29500")
                 import datetime
                 kw = {}
-                if use_gpu:
+                if use_gpu and st.backend == "nccl":
                     kw["device_id"] = st.device
+                    # collectives on a high-priority HIP stream: bucket all-reduces overlapping the
+                    # backward pass get scheduled ahead of the compute stream's queued kernels
+                    opts = dist.ProcessGroupNCCL.Options()
+                    opts.is_high_priority_stream = True
+                    kw["pg_options"] = opts
                 timeout = datetime.timedelta(seconds=timeout_s)
                 if os.environ.get("TORCHELASTIC_USE_AGENT_STORE") == "True":
                     # under the torchrun agent: join its TCPStore with a per-attempt prefix so an elastic
@@ -75,6 +82,17 @@ class DistState:
                 dist.barrier(device_ids=[self.device.index])
             else:
                 dist.barrier()
+
+    def agree_times(self, times: List[float]) -> List[float]:
+        """Autotuner consensus: every rank times the same candidate list; all pick the argmin of the
+        per-candidate MAX over ranks (the slowest rank bounds a data-parallel step), so every rank runs
+        identical kernels."""
+        if not (self.initialized and self.world_size > 1) or not times:
+            return times
+        dev = self.device if self.backend == "nccl" else torch.device("cpu")
+        t = torch.tensor(times, dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return t.cpu().tolist()
 
     def all_reduce_(self, t: torch.Tensor, op: str = "avg") -> torch.Tensor:
         if not (self.initialized and self.world_size > 1):

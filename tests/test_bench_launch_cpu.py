@@ -1,0 +1,58 @@
+"""bench.py's multi-rank self-launch path (``--gpus N`` → child torchrun → N ranks), rehearsed on CPU/gloo
+with ``--plumbing``: the JSON line reports the whole job, every rank ends with identical weights and the
+all-reduced gradient equals the mean of the per-rank gradients (DDP semantics, per-rank BN statistics)."""
+import json
+import os
+import subprocess
+import sys
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+sys.path.insert(0, REPO)
+
+ARGS = ["--plumbing", "--steps", "1", "--warmup", "1", "--batch", "2", "--frames", "8", "--crop", "64",
+        "--classes", "5", "--bucket-mb", "8", "--first-bucket-mb", "1"]
+
+
+def _run(extra, tmp_path):
+    env = dict(os.environ, OMP_NUM_THREADS="2", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py")] + ARGS + extra, capture_output=True,
+                       text=True, timeout=900, cwd=str(tmp_path), env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+def test_bench_self_launch_two_ranks(tmp_path):
+    dump = str(tmp_path / "dump.pt")
+    res = _run(["--gpus", "2", "--dump", dump], tmp_path)
+    assert res["n_gpus"] == 2 and res["config"]["parallelism"] == "dp2"
+    assert res["config"]["global_batch"] == 4 and res["value"] > 0 and res["steps"] == 1
+    d = torch.load(dump, weights_only=True)
+    assert d["world_size"] == 2
+    torch.testing.assert_close(d["params"][0], d["params"][1], rtol=0, atol=0)
+
+    import bench
+    from pytorchvideo_accelerate_amd.engine.backends import TorchBackend
+    from pytorchvideo_accelerate_amd.parallel.dist import DistState
+
+    a = bench.parse(ARGS)
+    be = TorchBackend(bench.plumbing_model(a), DistState(), "no")
+    be.train()
+    for r in range(2):   # mean over ranks of per-rank gradients (each rank its own BN batch statistics)
+        xs, y = bench.plumbing_batch(a, r, 0)
+        be.train_step(xs, y, loss_scale=0.5)
+    ref = be.flat.grad
+    got = d["grad"]
+    assert got.shape == ref.shape
+    err = (got - ref).norm() / ref.norm()
+    assert err < 1e-5, float(err)
+
+
+def test_bench_single_rank_plumbing(tmp_path):
+    res = _run(["--gpus", "1"], tmp_path)
+    assert res["n_gpus"] == 1 and res["config"]["parallelism"] == "dp1"
