@@ -35,6 +35,7 @@ from ..models import reference as R
 from ..utils.misc import set_seed
 from ..utils.metrics import Accuracy
 from ..utils.profiling import StepTimer
+from ..utils.progress import progress_bar
 from .accelerator import Accelerator
 
 
@@ -211,7 +212,12 @@ def training_function(args: Namespace) -> dict:
     val_metric = Accuracy(acc.device, acc.state)
     output_dir = None
     show = acc.is_main_process and not getattr(args, "quiet", False)
+    # reference run.py:233: one bar over every epoch's steps, main process only
+    bar = progress_bar(args.num_epochs * steps_per_epoch, disable=not show)
+    if global_step:
+        bar.update(min(global_step, args.num_epochs * steps_per_epoch))
     for epoch in range(starting_epoch, args.num_epochs):
+        bar.set_description_str("Epoch: %s" % epoch)
         train_ds.set_epoch(epoch)
         backend.train()
         total_loss = torch.zeros((), device=acc.device)
@@ -246,6 +252,7 @@ def training_function(args: Namespace) -> dict:
                     scheduler.step()
                     optimizer.zero_grad()
             timer.end_step(batch["label"].shape[0] * acc.num_processes)
+            bar.update(1)
             global_step += 1
             acc.step = global_step
             clips += batch["label"].shape[0] * acc.num_processes
@@ -258,8 +265,7 @@ def training_function(args: Namespace) -> dict:
                     acc.log({"train_loss_step": step_loss.item(), "lr": optimizer.param_groups[0]["lr"], **perf},
                             step=global_step)
             if show and (step + 1) % max(args.log_every, 1) == 0:
-                print(f"epoch {epoch} step {step + 1}/{steps_per_epoch} loss {step_loss.item():.4f} "
-                      f"lr {optimizer.param_groups[0]['lr']:.5f}", flush=True)
+                bar.set_postfix_str(f"loss {step_loss.item():.4f} lr {optimizer.param_groups[0]['lr']:.5f}")
             if isinstance(checkpointing_steps, int) and global_step % checkpointing_steps == 0:
                 output_dir = os.path.join(args.output_dir or ".", f"step_{global_step}")
                 acc.save_state(output_dir)
@@ -275,6 +281,7 @@ def training_function(args: Namespace) -> dict:
             train_ds.set_epoch(epoch)
 
         # ---------------- evaluation
+        bar.set_description_str("Val Epoch: %s" % epoch)
         acc.sync_buffers()
         backend.eval()
         val_metric.reset()
@@ -295,6 +302,7 @@ def training_function(args: Namespace) -> dict:
             output_dir = os.path.join(args.output_dir or ".", f"epoch_{epoch}")
             acc.save_state(output_dir)
 
+    bar.close()
     if args.with_tracking:
         acc.end_training()
     final_dir = output_dir or os.path.join(args.output_dir or ".", "final")

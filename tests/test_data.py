@@ -185,3 +185,22 @@ def test_native_clip_reader(tmp_path):
     C.read_clips(dst, [(p, v.data_offset, fb, [0, 5, 11], 0), (p, v.data_offset, fb, [2, 2, 3], 3 * fb)], 4)
     out = dst.numpy().reshape(6, 5, 6, 3)
     assert np.array_equal(out[:3], arr[[0, 5, 11]]) and np.array_equal(out[3:], arr[[2, 2, 3]])
+
+
+def test_prepare_synthetic_raw_frame_tree_trains(tmp_path):
+    """data/prepare.py writes the documented .npy + .json layout; the Kinetics index reads it back."""
+    from pytorchvideo_accelerate_amd.data import prepare
+    from pytorchvideo_accelerate_amd.data.kinetics import LabeledVideoPaths
+    from pytorchvideo_accelerate_amd.data.video import RawFramesVideo
+    n = prepare.synthetic(str(tmp_path), classes=3, videos=2, frames=20, height=32, width=40, fps=25.0)
+    assert n == 3 * 2 + 3 * 1
+    rep = prepare.check(str(tmp_path))
+    assert rep["bad"] == [] and rep["train"] == {"videos": 6, "classes": 3}
+    lp = LabeledVideoPaths.from_directory(str(tmp_path / "train"))
+    assert lp.num_labels == 3 and lp.num_videos == 6
+    v = RawFramesVideo(str(tmp_path / "train" / "class_001" / "vid_0001.npy"))
+    assert v.fps == 25.0 and (v.num_frames, v.height, v.width) == (20, 32, 40)
+    clip = v.get_clip(0, 0.5)        # frames with i/25 in [0, 0.5): 0..12
+    assert clip.shape == (13, 32, 40, 3)
+    small = prepare._resize_short_side(clip, 16)
+    assert small.shape == (13, 16, 20, 3) and small.dtype == np.uint8

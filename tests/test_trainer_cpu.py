@@ -31,3 +31,23 @@ def test_step_checkpoints_and_resume(tmp_path):
 def test_slow_r50_epoch_checkpoint_and_final(tmp_path):
     h = run.main(**_args(tmp_path, num_epochs=1, limit_train_batches=0, freeze_backbone=True))
     assert h["final_dir"].endswith("final") and os.path.exists(os.path.join(h["final_dir"], "model.safetensors"))
+
+
+def test_progress_bar_on_main_process(tmp_path, capsys):
+    """reference run.py:233-288: tqdm over num_epochs * len(train_loader), "Epoch: e" / "Val Epoch: e"."""
+    run.main(**_args(tmp_path, num_epochs=1, limit_train_batches=-1, quiet=False))
+    err = capsys.readouterr().err
+    assert "Epoch: 0" in err and "Val Epoch: 0" in err
+    assert "4/4" in err   # 8 videos / batch 2 = 4 steps, all updated
+
+
+def test_progress_fallback_bar():
+    import io
+    from pytorchvideo_accelerate_amd.utils.progress import _FallbackBar
+    f = io.StringIO()
+    b = _FallbackBar(3, file=f, mininterval=0.0)
+    b.set_description_str("Epoch: 0")
+    for _ in range(3):
+        b.update(1)
+    b.close()
+    assert "Epoch: 0" in f.getvalue() and "3/3" in f.getvalue()
