@@ -71,6 +71,15 @@ void stem_wgrad_convert_launch(float* acc, float* grad, int Cout, int kt, float 
 void stem_pack_launch(const float* w, uint16_t* out, int Cout, int kt, hipStream_t s);
 void synth_frames_launch(uint8_t* out, int64_t n, uint32_t seed, hipStream_t s);
 
+void head_forward_launch(const float* feat, int N, int P, int C, const float* W, const float* b, int K, float p_drop,
+                         uint64_t seed, float* xm, float* logits, hipStream_t s);
+void head_ce_launch(const float* logits, const int64_t* labels, int N, int K, float gscale, float* dlogits,
+                    float* row_loss, int* row_correct, float* loss, int64_t* counts, int acc_counts, hipStream_t s);
+void head_backward_launch(const float* dlogits, const float* xm, const float* W, int N, int P, int C, int K,
+                          float p_drop, uint64_t seed, float* dW, float* db, float beta, float* dfeat, float* dlT,
+                          float* xmT, float* WT, hipStream_t s);
+void head_dropout_mask_launch(int64_t total, float p_drop, uint64_t seed, uint8_t* out, hipStream_t s);
+
 void register_clip_reader(pybind11::module& m);
 
 namespace {
@@ -358,6 +367,53 @@ void stem_wgrad(const at::Tensor& x, const at::Tensor& dy, const at::Tensor& acc
                   cur_stream());
 }
 
+// ---- classification head (csrc/kernels/head.hip) ----
+// feat [N][P][C] fp32, W [K][C] fp32, b [K] (nullable); xm [N][C], logits [N][K] outputs
+void head_forward(const at::Tensor& feat, const at::Tensor& W, const OptT& b, double p_drop, int64_t seed,
+                  const at::Tensor& xm, const at::Tensor& logits) {
+  TORCH_CHECK(feat.dim() == 3 && feat.is_contiguous(), "feat must be [N][P][C] contiguous");
+  const int N = feat.size(0), P = feat.size(1), C = feat.size(2), K = W.size(0);
+  TORCH_CHECK(W.dim() == 2 && W.size(1) == C && W.is_contiguous(), "W must be [K][C]");
+  TORCH_CHECK(xm.numel() >= (int64_t)N * C && logits.numel() >= (int64_t)N * K, "head outputs too small");
+  TORCH_CHECK(p_drop >= 0.0 && p_drop < 1.0, "dropout probability must be in [0, 1)");
+  if (N == 0) return;
+  head_forward_launch(f32(feat), N, P, C, f32(W), f32o(b), K, (float)p_drop, (uint64_t)seed, f32(xm), f32(logits),
+                      cur_stream());
+}
+
+// cross-entropy: loss [1] (mean over rows), dlogits (nullable) = (softmax - onehot) * gscale, counts int64 [2]
+// (correct, rows; accumulated when acc_counts); rows scratch fp32 [N] + int32 [N]
+void head_ce(const at::Tensor& logits, const OptT& labels, double gscale, const OptT& dlogits, const OptT& loss,
+             const OptT& counts, int64_t acc_counts, const at::Tensor& row_loss, const at::Tensor& row_correct) {
+  const int N = logits.size(0), K = logits.size(1);
+  TORCH_CHECK(!labels.has_value() || (labels->scalar_type() == at::kLong && labels->numel() == N), "labels int64 [N]");
+  TORCH_CHECK(!counts.has_value() || (counts->scalar_type() == at::kLong && counts->numel() >= 2), "counts int64 [2]");
+  TORCH_CHECK(row_correct.scalar_type() == at::kInt && row_correct.numel() >= N && row_loss.numel() >= N, "row scratch");
+  if (N == 0) return;
+  head_ce_launch(f32(logits), labels.has_value() ? labels->data_ptr<int64_t>() : nullptr, N, K, (float)gscale,
+                 f32o(dlogits), f32(row_loss), row_correct.data_ptr<int>(), f32o(loss),
+                 counts.has_value() ? counts->data_ptr<int64_t>() : nullptr, (int)acc_counts, cur_stream());
+}
+
+void head_backward(const at::Tensor& dlogits, const at::Tensor& xm, const at::Tensor& W, int64_t P, double p_drop,
+                   int64_t seed, const at::Tensor& dW, const OptT& db, double beta, const OptT& dfeat,
+                   const at::Tensor& scratch) {
+  const int N = dlogits.size(0), K = dlogits.size(1), C = W.size(1);
+  TORCH_CHECK(xm.numel() >= (int64_t)N * C && dW.numel() == (int64_t)K * C, "head backward shapes");
+  TORCH_CHECK(!dfeat.has_value() || dfeat->numel() >= (int64_t)N * P * C, "dfeat too small");
+  TORCH_CHECK(scratch.numel() >= (int64_t)K * N + (int64_t)C * N + (int64_t)C * K, "head scratch too small");
+  if (N == 0) return;
+  float* sc = f32(scratch);
+  head_backward_launch(f32(dlogits), f32(xm), f32(W), N, (int)P, C, K, (float)p_drop, (uint64_t)seed, f32(dW),
+                       f32o(db), (float)beta, f32o(dfeat), sc, sc + (int64_t)K * N, sc + (int64_t)K * N + (int64_t)C * N,
+                       cur_stream());
+}
+
+void head_dropout_mask(const at::Tensor& out, double p_drop, int64_t seed) {
+  TORCH_CHECK(out.scalar_type() == at::kByte, "mask must be uint8");
+  head_dropout_mask_launch(out.numel(), (float)p_drop, (uint64_t)seed, out.data_ptr<uint8_t>(), cur_stream());
+}
+
 void synth_frames(const at::Tensor& out, int64_t seed) {
   synth_frames_launch(out.data_ptr<uint8_t>(), out.numel(), (uint32_t)seed, cur_stream());
 }
@@ -414,6 +470,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("synth_frames", &synth_frames);
   m.def("stem_tiles", [](int64_t Ho, int64_t Wo, int64_t N) { return stem_tiles((int)Ho, (int)Wo, (int)N); });
   m.def("stem_supported", [](int64_t Cout, int64_t kt) { return stem_s2d_supported((int)Cout, (int)kt); });
+  m.def("head_forward", &head_forward);
+  m.def("head_ce", &head_ce);
+  m.def("head_backward", &head_backward);
+  m.def("head_dropout_mask", &head_dropout_mask);
   m.def("stem_fwd", &stem_fwd);
   m.def("stem_wgrad", &stem_wgrad);
   m.def("stem_wgrad_convert", [](const at::Tensor& acc, const at::Tensor& grad, int64_t Cout, int64_t kt, double beta) {

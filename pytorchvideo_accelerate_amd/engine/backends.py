@@ -127,6 +127,10 @@ class FusedBackend:
     def eval_step(self, video):
         return self.net.forward_eval(video)
 
+    def eval_counts(self, logits, labels):
+        """(correct, total) of one eval batch on the HIP argmax/count kernel."""
+        return self.net.eval_counts(logits, labels)
+
     def after_optimizer_step(self):
         self.net.pack()
 

@@ -287,7 +287,10 @@ def training_function(args: Namespace) -> dict:
         val_metric.reset()
         for step, batch in enumerate(val_loader):
             logits = backend.eval_step(batch["video"])
-            val_metric.update(logits, batch["label"])
+            if hasattr(backend, "eval_counts"):    # fused path: argmax + count on device
+                val_metric.update_counts(backend.eval_counts(logits, batch["label"]))
+            else:
+                val_metric.update(logits, batch["label"])
             if step == args.limit_val_batches:
                 break
         val_acc = val_metric.compute().item()

@@ -20,8 +20,8 @@ gfx950 kernels (``ops/conv.py`` + ``csrc/kernels``).  Design (SURVEY.md §7.1/§
   (``parallel/ddp.py``) and the single-launch fused SGD (``ops/optim.py``) operate on.  bf16 packed
   weights (forward ``[Cout][taps][Cin]`` and dgrad ``[Cin][taps][Cout]`` layouts) are refreshed by one
   multi-tensor kernel after each optimizer step.
-* The tiny classification head (dropout → linear → position mean → CE) runs in PyTorch fp32 on the
-  pooled features (≈0.01 % of FLOPs).
+* The classification head (dropout → linear → position mean → softmax-CE, forward and backward) runs on
+  the fp32-MFMA head kernels (``csrc/kernels/head.hip``), writing dW/db straight into the flat gradient.
 
 Semantics follow the pytorchvideo modules in ``models/reference.py`` (reference ``run.py:105-118``);
 ``tests/test_fused_gpu.py`` pins loss / gradient / running-stat parity against that oracle.
@@ -776,19 +776,45 @@ class FusedNet:
             coff += o.C
         return feat, ks
 
-    def _head(self, feat: torch.Tensor, train: bool) -> torch.Tensor:
+    # ------------------------------------------------------------------ head (csrc/kernels/head.hip)
+    def _head_forward(self, feat: torch.Tensor, train: bool, tag: str):
+        """Dropout -> Linear per position -> position mean (K17-K19) on the HIP head kernels.
+        Returns (logits [N, K] fp32, xm [N, C] = dropped position-mean features, p_drop, seed)."""
         h = self.head
-        x = feat
-        if train and h.dropout is not None:
-            x = F.dropout(x, h.dropout.p, training=True)
-        logits = F.linear(x, h.proj.weight, h.proj.bias)  # [N, P, K]
-        return logits.mean(1)
+        W, b = h.proj.weight, h.proj.bias
+        p = float(h.dropout.p) if (train and h.dropout is not None) else 0.0
+        # per-step Philox key from torch's CPU generator (reproducible under set_seed; no device sync)
+        seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if p > 0 else 0
+        N = feat.shape[0]
+        xm = self.ws(("head_xm", tag), (N, feat.shape[2]), torch.float32)
+        logits = torch.empty(N, W.shape[0], device=self.device, dtype=torch.float32)
+        self.mark("head.fwd")
+        self.C.head_forward(feat, self.flat.view(W), None if b is None else self.flat.view(b), p, seed, xm, logits)
+        return logits, xm, p, seed
 
     @torch.no_grad()
     def forward_eval(self, xs: List[Act]) -> torch.Tensor:
         outs = self._forward_backbone(xs, train=False)
         feat, _ = self._pool_features(outs, "e")
-        return self._head(feat, train=False)
+        logits, _, _, _ = self._head_forward(feat, False, "e")
+        return logits
+
+    @torch.no_grad()
+    def eval_counts(self, logits: torch.Tensor, labels: torch.Tensor,
+                    counts: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Top-1 (correct, total) int64 counters of ``logits`` vs ``labels`` (argmax, first maximum on ties;
+        reference run.py:297), accumulated into ``counts`` when given (HIP head_ce kernel, no host sync)."""
+        N, K = logits.shape
+        if counts is None:
+            counts = torch.zeros(2, device=self.device, dtype=torch.long)
+            acc = 0
+        else:
+            acc = 1
+        rl = self.ws(("head_rl",), (max(N, 1),), torch.float32)
+        rc = self.ws(("head_rc",), (max(N, 1),), torch.int32)
+        self.C.head_ce(logits.contiguous(), labels.to(self.device, torch.long).contiguous(), 0.0, None, None, counts,
+                       acc, rl, rc)
+        return counts
 
     def forward_backward(self, xs: List[Act], labels: torch.Tensor, loss_scale: float = 1.0,
                          accumulate: Optional[bool] = None) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -802,25 +828,29 @@ class FusedNet:
         with torch.no_grad():
             outs = self._forward_backbone(xs, train=True)
             feat, ks = self._pool_features(outs, "t")
-        h = self.head
-        self.mark("head.fwdbwd")
-        feat_t = feat.detach().requires_grad_(True)
-        with torch.enable_grad():
-            logits = self._head(feat_t, train=True)
-            loss = F.cross_entropy(logits.float(), labels)
-            params = [h.proj.weight, h.proj.bias]
-            gfeat, gw, gb = torch.autograd.grad(loss * loss_scale, [feat_t] + params)
-        with torch.no_grad():
-            for p, g in ((h.proj.weight, gw), (h.proj.bias, gb)):
-                gv = self.flat.gview(p)
-                if accumulate:
-                    gv.add_(g)
-                else:
-                    gv.copy_(g)
+            logits, xm, p, seed = self._head_forward(feat, True, "t")
+            N, K = logits.shape
+            Ct = feat.shape[2]
+            labels = labels.to(self.device, torch.long).contiguous()
+            loss = torch.empty(1, device=self.device, dtype=torch.float32)
+            dlogits = self.ws(("head_dl",), (N, K), torch.float32)
+            rl = self.ws(("head_rl",), (max(N, 1),), torch.float32)
+            rc = self.ws(("head_rc",), (max(N, 1),), torch.int32)
+            self.mark("head.ce")
+            # softmax cross-entropy (mean over the batch, reference run.py:254) and its gradient
+            self.C.head_ce(logits, labels, float(loss_scale) / max(N, 1), dlogits, loss, None, 0, rl, rc)
+            h = self.head
+            W, b = h.proj.weight, h.proj.bias
+            train_backbone = any(q.requires_grad for q in self.units[0].conv.parameters())  # else frozen backbone
+            gfeat = self.ws(("gfeat",), tuple(feat.shape), torch.float32) if train_backbone else None
+            scratch = self.scratch("head_bwd", K * N + Ct * N + Ct * K)
+            self.mark("head.bwd")
+            self.C.head_backward(dlogits, xm, self.flat.view(W), feat.shape[1], p, seed, self.flat.gview(W),
+                                 None if b is None else self.flat.gview(b), self.grad_beta, gfeat, scratch)
             self._progress(self._head_hi)
-            if any(p.requires_grad for p in self.units[0].conv.parameters()):  # else frozen backbone
-                self._backward_backbone(outs, gfeat.contiguous(), ks)
-        return loss.detach(), logits.detach()
+            if train_backbone:
+                self._backward_backbone(outs, gfeat, ks)
+        return loss[0], logits
 
     def _backward_backbone(self, outs: List[Act], gfeat: torch.Tensor, ks):
         C = self.C

@@ -31,6 +31,12 @@ class Accuracy:
         self.correct += (p == t).sum()
         self.total += t.numel()
 
+    def update_counts(self, counts: torch.Tensor):
+        """Add device-side (correct, total) int64 counters (e.g. from the fused head's argmax kernel)."""
+        c = counts.to(self.device)
+        self.correct += c[0]
+        self.total += c[1]
+
     def forward(self, preds: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
         """Update and return this batch's (local) accuracy, like ``torchmetrics.Metric.forward``."""
         p = self._preds(preds).to(self.device)
