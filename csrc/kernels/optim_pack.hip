@@ -14,9 +14,23 @@
 
 namespace {
 
+// GradScaler pre-pass: flag = 1 if any g*gscale is inf/nan (torch _amp_foreach_non_finite_check_and_unscale_)
+__global__ void nonfinite_check_kernel(const float* __restrict__ g, int64_t n, float gscale, int* __restrict__ flag) {
+  bool bad = false;
+  const int64_t n4 = n >> 2;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    const float4 v = reinterpret_cast<const float4*>(g)[i];
+    bad |= !isfinite(v.x * gscale) || !isfinite(v.y * gscale) || !isfinite(v.z * gscale) || !isfinite(v.w * gscale);
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (n & 3)) bad |= !isfinite(g[(n4 << 2) + threadIdx.x] * gscale);
+  if (__any(bad) && (threadIdx.x & 63) == 0) *flag = 1;   // benign race: every writer stores 1
+}
+
 __global__ void sgd_momentum_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ buf,
                                     int64_t n, const float* __restrict__ lr_ptr, float momentum, float wd,
-                                    float gscale, int first, int* __restrict__ found_inf) {
+                                    float gscale, int first, int* __restrict__ found_inf,
+                                    const int* __restrict__ skip_flag) {
+  if (skip_flag && *skip_flag) return;   // overflowed fp16-scaled step: parameters and momentum untouched
   const float lr = *lr_ptr;
   const int64_t n4 = n >> 2;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
@@ -156,12 +170,19 @@ __global__ void synth_frames_kernel(uint8_t* __restrict__ out, int64_t n, uint32
 }  // namespace
 
 void sgd_momentum_launch(float* p, const float* g, float* buf, int64_t n, const float* lr, float momentum, float wd,
-                         float gscale, int first, int* found_inf, hipStream_t s) {
+                         float gscale, int first, int* found_inf, const int* skip_flag, hipStream_t s) {
   int64_t blocks = ((n >> 2) + 255) / 256;
   if (blocks > 4096) blocks = 4096;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(sgd_momentum_kernel, dim3((int)blocks), dim3(256), 0, s, p, g, buf, n, lr, momentum, wd, gscale,
-                     first, found_inf);
+                     first, found_inf, skip_flag);
+}
+
+void nonfinite_check_launch(const float* g, int64_t n, float gscale, int* flag, hipStream_t s) {
+  int64_t blocks = ((n >> 2) + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(nonfinite_check_kernel, dim3((int)blocks), dim3(256), 0, s, g, n, gscale, flag);
 }
 
 void pack_weights_launch(const float* master, uint16_t* fwd, uint16_t* dgr, const void* descs, int ntensors,

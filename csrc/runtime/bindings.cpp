@@ -57,7 +57,8 @@ void avgpool_fwd_launch(const uint16_t* x, int N, int T, int H, int W, int C, in
 void avgpool_bwd_launch(const float* dout, int ldo, int coff, int N, int T, int H, int W, int C, int kt, int kh,
                         int kw, uint16_t* dx, hipStream_t s);
 void sgd_momentum_launch(float* p, const float* g, float* buf, int64_t n, const float* lr, float momentum, float wd,
-                         float gscale, int first, int* found_inf, hipStream_t s);
+                         float gscale, int first, int* found_inf, const int* skip_flag, hipStream_t s);
+void nonfinite_check_launch(const float* g, int64_t n, float gscale, int* flag, hipStream_t s);
 void pack_weights_launch(const float* master, uint16_t* fwd, uint16_t* dgr, const void* descs, int ntensors,
                          hipStream_t s);
 int pack_desc_size();
@@ -320,12 +321,21 @@ void avgpool_bwd(const at::Tensor& dout, int64_t ldo, int64_t coff, std::vector<
                      (int)dims[4], (int)k[0], (int)k[1], (int)k[2], bfpm(dx), cur_stream());
 }
 
+// found_inf: raised on non-finite gradients; skip_if: when given, the step is a no-op if *skip_if != 0
+// (fp16 GradScaler: nonfinite_check fills the flag first, then the update reads it on the device)
 void sgd_momentum(const at::Tensor& p, const at::Tensor& g, const at::Tensor& buf, const at::Tensor& lr,
-                  double momentum, double wd, double gscale, int64_t first, const OptT& found_inf) {
+                  double momentum, double wd, double gscale, int64_t first, const OptT& found_inf,
+                  const OptT& skip_if) {
   TORCH_CHECK(p.numel() == g.numel() && p.numel() == buf.numel(), "sgd buffers must match");
   int* fi = found_inf.has_value() ? found_inf->data_ptr<int>() : nullptr;
+  const int* sk = skip_if.has_value() ? skip_if->data_ptr<int>() : nullptr;
   sgd_momentum_launch(f32(p), f32(g), f32(buf), p.numel(), f32(lr), (float)momentum, (float)wd, (float)gscale,
-                      (int)first, fi, cur_stream());
+                      (int)first, fi, sk, cur_stream());
+}
+
+void nonfinite_check(const at::Tensor& g, double gscale, const at::Tensor& flag) {
+  TORCH_CHECK(flag.scalar_type() == at::kInt, "flag must be int32");
+  nonfinite_check_launch(f32(g), g.numel(), (float)gscale, flag.data_ptr<int>(), cur_stream());
 }
 
 void pack_weights(const at::Tensor& master, const at::Tensor& fwd, const at::Tensor& dgr, const at::Tensor& descs,
@@ -463,7 +473,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("stem_pool_bwd", &stem_pool_bwd);
   m.def("avgpool_fwd", &avgpool_fwd);
   m.def("avgpool_bwd", &avgpool_bwd);
-  m.def("sgd_momentum", &sgd_momentum);
+  m.def("sgd_momentum", &sgd_momentum, py::arg("p"), py::arg("g"), py::arg("buf"), py::arg("lr"),
+        py::arg("momentum"), py::arg("wd"), py::arg("gscale"), py::arg("first"), py::arg("found_inf"),
+        py::arg("skip_if") = py::none());
+  m.def("nonfinite_check", &nonfinite_check);
   m.def("pack_weights", &pack_weights);
   m.def("pack_desc_size", &pack_desc_size);
   m.def("video_preprocess", &video_preprocess);

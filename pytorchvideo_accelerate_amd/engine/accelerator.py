@@ -60,10 +60,15 @@ class Accelerator:
         self.trackers = Trackers(log_with, logging_dir, self.state.is_main_process)
         self.logging_dir = logging_dir
         self.bucket_mb = bucket_mb
-        # fused gfx950 kernels whenever a GPU runs a reduced-precision step (bf16; fp16 requests run the
-        # same bf16 kernels — bf16 has fp32 range so no loss scaling is needed); fp32 -> PyTorch path
+        # On a GPU the fused gfx950 kernels always run (bf16 MFMA compute, fp32 master weights and
+        # optimizer; fp16 adds the dynamic loss-scale state machine).  The PyTorch/MIOpen module path is
+        # an explicit debugging / oracle opt-in (kernels="torch"), never a silent fallback; on CPU it is
+        # the only path.
         if kernels == "auto":
-            kernels = "fused" if (self.device.type == "cuda" and mixed_precision in ("bf16", "fp16")) else "torch"
+            kernels = "fused" if self.device.type == "cuda" else "torch"
+            if kernels == "fused" and mixed_precision == "no" and self.state.is_main_process:
+                print("note: --mixed_precision no on the fused MI355X path computes convolutions in bf16 with fp32 "
+                      "master weights/optimizer; pass --kernels torch for fp32 PyTorch execution", flush=True)
         self.kernels = kernels
         self._models: List[Any] = []
         self._optimizers: List[Any] = []
@@ -99,7 +104,7 @@ class Accelerator:
     def prepare_model(self, model: torch.nn.Module):
         from .backends import FusedBackend, TorchBackend
         if self.kernels == "fused":
-            be = FusedBackend(model, self.state, self.bucket_mb)
+            be = FusedBackend(model, self.state, self.bucket_mb, mixed_precision=self.mixed_precision)
         else:
             be = TorchBackend(model, self.state, self.mixed_precision, self.bucket_mb)
         # rank-0 parameters + BN buffers everywhere (DDP construction broadcast)

@@ -90,8 +90,10 @@ class TorchBackend:
 class FusedBackend:
     name = "fused"
 
-    def __init__(self, model: torch.nn.Module, state: DistState, bucket_mb: float = 32.0):
+    def __init__(self, model: torch.nn.Module, state: DistState, bucket_mb: float = 32.0,
+                 mixed_precision: str = "bf16"):
         from ..models.fused import FusedNet
+        from ..ops.optim import FusedGradScaler
         self.state = state
         self.device = state.device
         self.net = FusedNet(model, self.device)
@@ -102,7 +104,8 @@ class FusedBackend:
         bounds = sorted(set(self.flat.span(p)[1] for p in self.flat.params))
         self.sync = GradSync(self.flat.grad, state, bucket_mb, boundaries=bounds)
         self.net.grad_hook = self.sync.progress
-        self.scaler = None
+        # fp16 requests get the dynamic loss-scale state machine (compute stays bf16 MFMA)
+        self.scaler = FusedGradScaler() if mixed_precision == "fp16" else None
         self._training = True
         self.timer = None   # utils.profiling.StepTimer (optional)
 
@@ -118,6 +121,8 @@ class FusedBackend:
         t = self.timer
         with (t.phase("fwd_bwd") if t else contextlib.nullcontext()):
             self.sync.begin(sync)
+            if self.scaler is not None:
+                loss_scale = loss_scale * self.scaler.get_scale()
             loss, logits = self.net.forward_backward(video, labels.to(self.device), loss_scale)
         with (t.phase("comm") if t else contextlib.nullcontext()):
             self.sync.finish()

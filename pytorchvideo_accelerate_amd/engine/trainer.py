@@ -311,5 +311,6 @@ def training_function(args: Namespace) -> dict:
     final_dir = output_dir or os.path.join(args.output_dir or ".", "final")
     acc.save_state(final_dir)
     history["final_dir"] = final_dir
+    history["backend"] = backend.name
     history["global_step"] = global_step
     return history

@@ -44,22 +44,39 @@ class FusedSGD(torch.optim.SGD):
         self.lr_t.fill_(float(self.param_groups[0]["lr"]))
 
     @torch.no_grad()
-    def step(self, closure=None, grad_scale: float = 1.0):
+    def step(self, closure=None, grad_scale: float = 1.0, check_finite: bool = False):
+        """One SGD step on ``grad * grad_scale``.  ``check_finite`` (fp16 loss scaling): a non-finite
+        gradient turns the whole step into a no-op (parameters and momentum untouched) and sets
+        ``step_was_skipped`` (one device->host read of the flag)."""
         g = self.param_groups[0]
         lo, hi = self.span if self.span is not None else (0, self.flat.numel)
         data, grad, buf = self.flat.data[lo:hi], self.flat.grad[lo:hi], self.buf[lo:hi]
+        skipped = False
         if self._C is None:  # CPU path: plain torch math on the flat buffers
             lr, m, wd = g["lr"], g["momentum"], g["weight_decay"]
-            d = grad * grad_scale + wd * data
-            if self._first:
-                buf.copy_(d)
+            if check_finite and not bool(torch.isfinite(grad * grad_scale).all()):
+                skipped = True
             else:
-                buf.mul_(m).add_(d)
-            data.add_(buf, alpha=-lr)
+                d = grad * grad_scale + wd * data
+                if self._first:
+                    buf.copy_(d)
+                else:
+                    buf.mul_(m).add_(d)
+                data.add_(buf, alpha=-lr)
         else:
             self.set_lr_tensor()
-            self._C.sgd_momentum(data, grad, buf, self.lr_t, g["momentum"],
-                                 g["weight_decay"], grad_scale, 1 if self._first else 0, None)
+            if check_finite:
+                self.found_inf.zero_()
+                self._C.nonfinite_check(grad, grad_scale, self.found_inf)
+                self._C.sgd_momentum(data, grad, buf, self.lr_t, g["momentum"], g["weight_decay"], grad_scale,
+                                     1 if self._first else 0, None, self.found_inf)
+                skipped = bool(self.found_inf.item())
+            else:
+                self._C.sgd_momentum(data, grad, buf, self.lr_t, g["momentum"],
+                                     g["weight_decay"], grad_scale, 1 if self._first else 0, None)
+        self.step_was_skipped = skipped
+        if skipped:
+            return None
         if self._first:
             self._bind_state()
             self._first = False
@@ -85,3 +102,63 @@ class FusedSGD(torch.optim.SGD):
         if any_buf:
             self._bind_state()
             self._first = False
+
+
+class FusedGradScaler:
+    """Dynamic loss scaling for ``--mixed_precision fp16`` on the fused path (reference recipe,
+    ``run_slowfast_r50.sh:7``; accelerate/torch ``GradScaler`` semantics):
+
+    * the backward pass computes gradients of ``loss * scale`` (the executor folds ``scale`` into the
+      head's dlogits, so no extra pass);
+    * ``step(optimizer)`` unscales inside the fused SGD kernel (``grad_scale = 1/scale``) after a
+      device-side non-finite check; an overflowing step is skipped entirely (``optimizer.step_was_skipped``,
+      which also skips the LR scheduler step, accelerate ``scheduler.py:66-68``);
+    * ``update()``: ×``backoff_factor`` after an overflow, ×``growth_factor`` after ``growth_interval``
+      consecutive clean steps (torch defaults 2**16, 2.0, 0.5, 2000).
+
+    ``state_dict`` has torch ``GradScaler``'s keys, so ``scaler.pt`` checkpoints interoperate.
+    Compute stays bf16 (MFMA) with fp32 master weights — the loss-scale state machine is what fp16
+    training semantics need; bf16 needs no scaling for range, so overflow skips are rare."""
+
+    def __init__(self, init_scale: float = 2.0 ** 16, growth_factor: float = 2.0, backoff_factor: float = 0.5,
+                 growth_interval: int = 2000, enabled: bool = True):
+        self._scale = float(init_scale)
+        self._growth_factor = float(growth_factor)
+        self._backoff_factor = float(backoff_factor)
+        self._growth_interval = int(growth_interval)
+        self._growth_tracker = 0
+        self._enabled = enabled
+        self._found_inf = False
+
+    def is_enabled(self) -> bool:
+        return self._enabled
+
+    def get_scale(self) -> float:
+        return self._scale if self._enabled else 1.0
+
+    def step(self, optimizer: FusedSGD):
+        optimizer.step(grad_scale=1.0 / self.get_scale(), check_finite=self._enabled)
+        self._found_inf = bool(optimizer.step_was_skipped)
+
+    def update(self):
+        if not self._enabled:
+            return
+        if self._found_inf:
+            self._scale *= self._backoff_factor
+            self._growth_tracker = 0
+        else:
+            self._growth_tracker += 1
+            if self._growth_tracker == self._growth_interval:
+                self._scale *= self._growth_factor
+                self._growth_tracker = 0
+
+    def state_dict(self):
+        return {"scale": self._scale, "growth_factor": self._growth_factor, "backoff_factor": self._backoff_factor,
+                "growth_interval": self._growth_interval, "_growth_tracker": self._growth_tracker}
+
+    def load_state_dict(self, sd):
+        self._scale = float(sd["scale"])
+        self._growth_factor = float(sd.get("growth_factor", self._growth_factor))
+        self._backoff_factor = float(sd.get("backoff_factor", self._backoff_factor))
+        self._growth_interval = int(sd.get("growth_interval", self._growth_interval))
+        self._growth_tracker = int(sd.get("_growth_tracker", 0))

@@ -71,6 +71,25 @@ def test_run_py_fused_gpu(tmp_path):
     assert h2["global_step"] == 6
 
 
+@pytest.mark.parametrize("mp", ["fp16", "no"])
+def test_run_py_fused_fp16_and_default_precision(tmp_path, mp):
+    """fp16 = fused kernels + dynamic loss scaling (scaler.pt saved/restored); "no" (the reference default)
+    also runs the fused kernels on the GPU (PyTorch/MIOpen only with an explicit --kernels torch)."""
+    import run
+    kw = dict(synthetic=True, synthetic_videos=8, synthetic_classes=4, is_slowfast=True, num_frames=8, crop_size=64,
+              batch_size=4, num_workers=0, limit_val_batches=0, mixed_precision=mp, checkpointing_steps="epoch",
+              output_dir=str(tmp_path / "o"), gradient_accumulation_steps=2, lr=0.01, quiet=True,
+              logging_dir=str(tmp_path / "l"))
+    h = run.main(num_epochs=1, **kw)
+    assert h["global_step"] == 2 and h["backend"] == "fused"
+    assert (tmp_path / "o" / "epoch_0" / "scaler.pt").exists() == (mp == "fp16")
+    if mp == "fp16":
+        sd = torch.load(tmp_path / "o" / "epoch_0" / "scaler.pt", weights_only=True)
+        assert sd["scale"] == 2.0 ** 16 and sd["_growth_tracker"] == 1   # one clean optimizer step
+        h2 = run.main(num_epochs=2, resume_from_checkpoint=str(tmp_path / "o" / "epoch_0"), **kw)
+        assert h2["global_step"] == 4
+
+
 def test_graft_smoke():
     import __graft_entry__ as g
     g.smoke()
