@@ -1,0 +1,112 @@
+"""Full-geometry numerical gate: the fused executor with the autotuner ON at the real
+SlowFast shapes, one training step vs the fp32 PyTorch oracle, judged against the bf16-autocast noise floor
+of the same oracle; plus a fixed-batch run at the bench clip shape whose loss must fall.
+
+Reference semantics: run.py:253-261 (forward, CE, backward, SGD step)."""
+import copy
+import os
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")   # the fp32 oracle runs on MIOpen: skip exhaustive search
+
+from pytorchvideo_accelerate_amd.models import reference as R  # noqa: E402
+from pytorchvideo_accelerate_amd.models.fused import FusedNet  # noqa: E402
+from pytorchvideo_accelerate_amd.ops.optim import FusedSGD  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda")
+
+
+def _clip(N, T, S, alpha, seed):
+    g = torch.Generator().manual_seed(seed)
+    fast = torch.randn(N, 3, T, S, S, generator=g).to(torch.bfloat16).float()
+    idx = torch.linspace(0, T - 1, T // alpha).long()
+    return [fast[:, :, idx].contiguous(), fast]
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12)).item()
+
+
+def _step_vs_oracle(model, xs, labels):
+    init = copy.deepcopy(model)
+    oracle = copy.deepcopy(model).to(DEV).train()
+    loss_ref = F.cross_entropy(oracle([x.to(DEV) for x in xs]), labels)
+    loss_ref.backward()
+    ac = copy.deepcopy(init).to(DEV).train()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        out_ac = ac([x.to(DEV) for x in xs])
+    loss_ac = F.cross_entropy(out_ac.float(), labels)
+    loss_ac.backward()
+    eng = FusedNet(model, DEV)
+    assert eng.tuner.enabled
+    loss, _ = eng.forward_backward(eng.prepare_inputs(xs), labels)
+    torch.cuda.synchronize()
+    ref = dict(oracle.named_parameters())
+    acp = dict(ac.named_parameters())
+    fe, ae = [], []
+    for n, p in model.named_parameters():
+        fe.append(_rel(p.grad, ref[n].grad))
+        ae.append(_rel(acp[n].grad, ref[n].grad))
+    fe.sort()
+    ae.sort()
+    print(f"loss fused {float(loss):.4f} fp32 {float(loss_ref):.4f} autocast {float(loss_ac):.4f}; median grad rel-L2 "
+          f"fused {fe[len(fe) // 2]:.4f} autocast {ae[len(ae) // 2]:.4f}")
+    return float(loss), float(loss_ref.detach()), float(loss_ac.detach()), fe, ae
+
+
+def _check(loss, loss_ref, loss_ac, fe, ae):
+    tol = max(0.05, 2 * abs(loss_ac - loss_ref))
+    assert abs(loss - loss_ref) < tol * max(1.0, abs(loss_ref)), (loss, loss_ref, loss_ac)
+    med_f, med_a = fe[len(fe) // 2], ae[len(ae) // 2]
+    p90_f, p90_a = fe[int(0.9 * len(fe))], ae[int(0.9 * len(ae))]
+    # per-parameter gradient rel-L2 within 2x of bf16 autocast (median and 90th percentile)
+    assert med_f <= 2 * med_a + 0.01, (med_f, med_a)
+    assert p90_f <= 2 * p90_a + 0.02, (p90_f, p90_a)
+
+
+def test_slowfast_r50_32x2x224_step_vs_fp32_oracle():
+    torch.manual_seed(0)
+    model = R.create_slowfast(50, 400, dropout_rate=0.0)
+    xs = _clip(2, 32, 224, 4, seed=11)
+    labels = torch.tensor([3, 250], device=DEV)
+    _check(*_step_vs_oracle(model, xs, labels))
+
+
+def test_slowfast_r101_32x2x256_step_vs_fp32_oracle():
+    torch.manual_seed(0)
+    # 256 crop: (8,8,8)/(32,8,8) final maps -> PoolConcat (1,2,2) overlapping windows
+    model = R.slowfast_r101(400, dropout_rate=0.0)
+    xs = _clip(1, 32, 256, 4, seed=12)
+    labels = torch.tensor([77], device=DEV)
+    _check(*_step_vs_oracle(model, xs, labels))
+
+
+def test_fixed_batch_loss_decreases_at_bench_shape():
+    """40 fused SGD steps on one fixed batch of 32x2x224 clips (bench preprocessing, B=16): the loss must fall
+    well below its start (memorisation), i.e. forward, backward and the optimizer agree at full geometry.
+    (bench.py's final_loss > ln(400) comes from fresh random labels every step at lr 0.1: nothing to learn.)"""
+    from pytorchvideo_accelerate_amd.data.transforms import GpuClipBatch, sample_params
+    torch.manual_seed(0)
+    model = R.create_slowfast(50, 400)
+    eng = FusedNet(model, DEV)
+    opt = FusedSGD(eng.flat, lr=0.02, momentum=0.9, weight_decay=1e-4, after_step=eng.pack)
+    B = 16
+    frames = torch.empty(B, 64, 256, 340, 3, dtype=torch.uint8, device=DEV)
+    eng.C.synth_frames(frames, 5)
+    prep = GpuClipBatch(DEV, 32, 224, 4, s2d=eng.input_s2d)
+    g = torch.Generator().manual_seed(0)
+    params = [sample_params(64, 256, 340, 32, 224, True, generator=g) for _ in range(B)]
+    labels = torch.randint(0, 400, (B,), generator=g).to(DEV)
+    losses = []
+    for _ in range(40):
+        xs = prep(frames, params)
+        opt.zero_grad()
+        loss, _ = eng.forward_backward(xs, labels)
+        opt.step()
+        losses.append(float(loss))
+    assert all(torch.isfinite(torch.tensor(losses)))
+    assert min(losses[-5:]) < 0.5 * losses[0], losses
