@@ -345,13 +345,20 @@ void launch_w(const WgradParams& p, hipStream_t stream) {
   hipLaunchKernelGGL((conv_wgrad_kernel<BMW, BNW, WMW, WNW, CH, 0, BP>), grid, dim3(NT), lds, stream, p);
 }
 
+// tiles 0-3: narrow outputs (fast pathway, small Cout); 4-7: 64x64 / 128x64 per wave (TM x TN = 16 or 32
+// MFMAs per 32-position k-step against 16 / 24 transposed LDS reads) for the compute-bound slow-pathway
+// weight gradients (Cout >= 128, K = taps x Cin >= 576)
 template <int CH, int BP>
 void launch_w_variant(int v, const WgradParams& p, hipStream_t stream) {
   switch (v) {
     case 0: launch_w<16, 128, 16, 32, CH, BP>(p, stream); break;
     case 1: launch_w<32, 128, 32, 32, CH, BP>(p, stream); break;
     case 2: launch_w<64, 64, 32, 32, CH, BP>(p, stream); break;
-    default: launch_w<128, 64, 64, 32, CH, BP>(p, stream); break;
+    case 3: launch_w<128, 64, 64, 32, CH, BP>(p, stream); break;
+    case 4: launch_w<128, 128, 64, 64, CH, BP>(p, stream); break;
+    case 5: launch_w<256, 128, 64, 64, CH, BP>(p, stream); break;
+    case 6: launch_w<128, 256, 64, 64, CH, BP>(p, stream); break;
+    default: launch_w<256, 256, 128, 64, CH, BP>(p, stream); break;
   }
 }
 
@@ -384,19 +391,25 @@ static int wgrad_variant(int Cout, int K) {
   return 3;                   // 128 x 64
 }
 
+static int wgrad_tile_index(int variant) { return (variant & 3) | ((variant >> 3) & 1) << 2; }
+
 void conv_wgrad_tile(int Cout, int K, int variant, int* bmw, int* bnw) {
-  switch (variant >= 0 ? (variant & 3) : wgrad_variant(Cout, K)) {
+  switch (variant >= 0 ? wgrad_tile_index(variant) : wgrad_variant(Cout, K)) {
     case 0: *bmw = 16; *bnw = 128; break;
     case 1: *bmw = 32; *bnw = 128; break;
     case 2: *bmw = 64; *bnw = 64; break;
-    default: *bmw = 128; *bnw = 64; break;
+    case 3: *bmw = 128; *bnw = 64; break;
+    case 4: *bmw = 128; *bnw = 128; break;
+    case 5: *bmw = 256; *bnw = 128; break;
+    case 6: *bmw = 128; *bnw = 256; break;
+    default: *bmw = 256; *bnw = 256; break;
   }
 }
 
-// p.variant: -1 = heuristic tile, 32-position stages; else bits 0-1 = tile variant, bit 2 = 64-position stages
-// (p_per_split must then be a multiple of 64)
+// p.variant: -1 = heuristic tile, 32-position stages; else bits 0-1 (+ bit 3 for tiles 4-7) = tile variant,
+// bit 2 = 64-position stages (p_per_split must then be a multiple of 64)
 void conv_wgrad_launch(const WgradParams& p, int chunk, hipStream_t stream) {
-  const int v = p.variant >= 0 ? (p.variant & 3) : wgrad_variant(p.Cout, p.K);
+  const int v = p.variant >= 0 ? wgrad_tile_index(p.variant) : wgrad_variant(p.Cout, p.K);
   const bool bp64 = p.variant >= 0 && (p.variant & 4);
   if (chunk == 8) {
     if (bp64) launch_w_variant<8, 64>(v, p, stream); else launch_w_variant<8, 32>(v, p, stream);

@@ -169,14 +169,15 @@ class _ConvBN:
         slab = 1 if eng.deterministic else 0
 
         def geometry(cfg):
-            """(splits, rows per split, tile variant) of launch configuration ``cfg``."""
+            """(splits, rows per split, kernel variant word) of launch configuration ``cfg``."""
             key = (self.name, "wsplit", dy.M, cfg)
             sp = eng._splits.get(key)
             if sp is None:
                 if cfg < 0:
                     sp = wgrad_splits(dy.M, s.cout, K, target_blocks=256 if slab else 1024) + (-1,)
-                else:   # bits 0-1 tile variant, 2-3 split-K target, 5: 64-position stages
-                    v, tb = cfg & 3, (512, 1024, 2048)[(cfg >> 2) & 3]
+                else:   # bits 0-1 (+ bit 6: tiles 4-7) tile variant, 2-3 split-K target, 5: 64-position stages
+                    v = (cfg & 3) | (8 if cfg & 64 else 0)
+                    tb = (512, 1024, 2048)[(cfg >> 2) & 3]
                     sp = wgrad_splits(dy.M, s.cout, K, target_blocks=tb, variant=v) + (v | (4 if cfg & 32 else 0),)
                 eng._splits[key] = sp
             return sp
@@ -197,12 +198,13 @@ class _ConvBN:
                 # scratch content is irrelevant), keep the fastest
                 scratch = eng.scratch("wgrad_tune", s.cout * K)
                 cands, times = [], []
-                for v in range(4):
-                    bmw = C.wgrad_tile(s.cout, K, v)[0]
-                    if bmw > max(16, s.cout) or bmw * 8 < s.cout:
+                for v in range(8):
+                    vw = (v & 3) | (8 if v >= 4 else 0)
+                    bmw, bnw = C.wgrad_tile(s.cout, K, vw)
+                    if bmw > max(16, s.cout) or bmw * 8 < s.cout or (v >= 4 and bnw > 2 * K):
                         continue
                     for tbi, bp in ((t, b) for t in range(3) for b in (0, 32)):
-                        c = 16 | v | (tbi << 2) | bp
+                        c = 16 | (v & 3) | (64 if v >= 4 else 0) | (tbi << 2) | bp
                         launch(c, scratch)
                         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                         e0.record()
@@ -215,6 +217,11 @@ class _ConvBN:
                 if eng.tuner.agree is not None:   # same choice on every data-parallel rank
                     times = eng.tuner.agree(times)
                 cfg = cands[min(range(len(cands)), key=times.__getitem__)] if cands else -1
+                if eng.tuner.log:
+                    import sys
+                    print("wtune %s P=%d Cout=%d K=%d: " % (self.name, dy.M, s.cout, K)
+                          + " ".join("%d=%.1fus" % (c, 1e3 * t / 3) for c, t in zip(cands, times))
+                          + " -> %d" % cfg, file=sys.stderr, flush=True)
             eng.wtune[tkey] = cfg
         if slab:  # per-split slabs summed in a fixed order: bitwise reproducible weight gradients
             part = eng.scratch("wgrad_slab", geometry(cfg)[0] * s.cout * K)

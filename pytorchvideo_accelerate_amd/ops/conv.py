@@ -206,12 +206,12 @@ def conv_wgrad(dy: Act, x: Act, spec: ConvSpec, grad: torch.Tensor, workspace: O
                splits_pps: Optional[Tuple[int, int]] = None, variant: int = -1) -> torch.Tensor:
     """grad (fp32, [Cout, Cin, kt, kh, kw]) = beta*grad + scale * dW.
 
-    ``variant``: -1 = heuristic tile; else bits 0-1 = tile (16x128, 32x128, 64x64, 128x64), bit 2 = 64-position
-    LDS stages (two MFMA k-steps per barrier)."""
+    ``variant``: -1 = heuristic tile; else bits 0-1 (+ bit 3 -> tiles 4-7) = tile (16x128, 32x128, 64x64, 128x64,
+    128x128, 256x128, 128x256, 256x256), bit 2 = 64-position LDS stages (two MFMA k-steps per barrier)."""
     C = require()
     P = dy.M
     K = spec.taps * spec.cin_pad
-    splits, pps = splits_pps or wgrad_splits(P, spec.cout, K, variant=(variant & 3) if variant >= 0 else -1)
+    splits, pps = splits_pps or wgrad_splits(P, spec.cout, K, variant=(variant & 11) if variant >= 0 else -1)
     need = spec.cout * K
     if workspace is None or workspace.numel() < need:
         workspace = torch.zeros(need, device=dy.t.device, dtype=torch.float32)  # kept zero by wgrad_reduce

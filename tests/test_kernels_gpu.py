@@ -250,10 +250,10 @@ def test_conv_wgrad(case):
     assert rel_err(grad, 1.5 * w.grad) < 1e-2
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15])
 @pytest.mark.parametrize("case", [CASES[1], CASES[3], CASES[6], STEMS[1]])
 def test_conv_wgrad_tile_variants(case, variant):
-    """Every tile variant x {32, 64}-position LDS stages (bit 2) against PyTorch."""
+    """Every tile variant (bits 0-1 + bit 3) x {32, 64}-position LDS stages (bit 2) against PyTorch."""
     x, w, spec = _mk(case, seed=13)
     w.requires_grad_(True)
     ref_y = torch.nn.functional.conv3d(x, w, None, spec.stride, spec.pad)
