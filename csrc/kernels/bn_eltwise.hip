@@ -161,7 +161,7 @@ __global__ void bn_bwd_reduce_kernel(const uint16_t* __restrict__ g, int ldg, in
   if (lr < rpi) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      m0[e] = mean0[c + e]; r0[e] = rstd0[c + e];
+      m0[e] = y0 ? mean0[c + e] : 0.f; r0[e] = y0 ? rstd0[c + e] : 0.f;
       m1[e] = y1 ? mean1[c + e] : 0.f; r1[e] = y1 ? rstd1[c + e] : 0.f;
       MS[e] = mask_mode == 2 ? ms[c + e] : 0.f; MH[e] = mask_mode == 2 ? mh[c + e] : 0.f;
     }
@@ -170,7 +170,7 @@ __global__ void bn_bwd_reduce_kernel(const uint16_t* __restrict__ g, int ldg, in
     for (int64_t m = mbeg + lr; m < mend; m += rpi) {
       float dz[8], a[8];
       unpack8(*reinterpret_cast<const uint4*>(g + m * ldg + c), dz);
-      unpack8(*reinterpret_cast<const uint4*>(y0 + m * C + c), a);
+      unpack8(y0 ? *reinterpret_cast<const uint4*>(y0 + m * C + c) : uint4{0, 0, 0, 0}, a);
       if (mask_mode == 1) {
         float o[8];
         unpack8(*reinterpret_cast<const uint4*>(mo + m * ldm + c), o);
@@ -269,14 +269,14 @@ __global__ void bn_bwd_apply_kernel(const uint16_t* __restrict__ g, int ldg, int
   float A0[8], B0[8], C0[8], A1[8], B1[8], C1[8], MS[8], MH[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    A0[e] = coef0[c + e]; B0[e] = coef0[C + c + e]; C0[e] = coef0[2 * C + c + e];
+    A0[e] = y0 ? coef0[c + e] : 0.f; B0[e] = y0 ? coef0[C + c + e] : 0.f; C0[e] = y0 ? coef0[2 * C + c + e] : 0.f;
     A1[e] = y1 ? coef1[c + e] : 0.f; B1[e] = y1 ? coef1[C + c + e] : 0.f; C1[e] = y1 ? coef1[2 * C + c + e] : 0.f;
     MS[e] = mask_mode == 2 ? ms[c + e] : 0.f; MH[e] = mask_mode == 2 ? mh[c + e] : 0.f;
   }
   for (int64_t m = (int64_t)blockIdx.x * rpi + lr; m < M; m += (int64_t)gridDim.x * rpi) {
     float dz[8], a[8];
     unpack8(*reinterpret_cast<const uint4*>(g + m * ldg + c), dz);
-    unpack8(*reinterpret_cast<const uint4*>(y0 + m * C + c), a);
+    unpack8(y0 ? *reinterpret_cast<const uint4*>(y0 + m * C + c) : uint4{0, 0, 0, 0}, a);
     if (mask_mode == 1) {
       float o[8];
       unpack8(*reinterpret_cast<const uint4*>(mo + m * ldm + c), o);
@@ -291,9 +291,11 @@ __global__ void bn_bwd_apply_kernel(const uint16_t* __restrict__ g, int ldg, int
       for (int e = 0; e < 8; ++e) dz[e] = (a[e] * MS[e] + MH[e]) > 0.f ? dz[e] : 0.f;
     }
     float o[8];
+    if (y0) {   // y0 == nullptr: only dz (identity shortcut) / dy1 are produced
 #pragma unroll
-    for (int e = 0; e < 8; ++e) o[e] = A0[e] * dz[e] + B0[e] * a[e] + C0[e];
-    *reinterpret_cast<uint4*>(dy0 + m * C + c) = pack8(o);
+      for (int e = 0; e < 8; ++e) o[e] = A0[e] * dz[e] + B0[e] * a[e] + C0[e];
+      *reinterpret_cast<uint4*>(dy0 + m * C + c) = pack8(o);
+    }
     if (y1) {
       unpack8(*reinterpret_cast<const uint4*>(y1 + m * C + c), a);
 #pragma unroll

@@ -1,0 +1,260 @@
+// BatchNorm folding for the 1x1 conv_c of a bottleneck unit (gfx950), so its raw output yc is never
+// materialised (removes the res_out and BN-apply passes over the widest tensors).
+//
+// With a = act_b(yb) [M][c] (the conv_c input), Wc [C][c] (bf16 weights as the conv uses them), the Gram
+// matrix Ga = a^T a [c][c] and column sums s = 1^T a [c] (both from the wgrad kernel in Gram mode):
+//   forward statistics of yc = a Wc^T:  mean_n = (Wc s)_n / M,  E[yc_n^2] = (Wc Ga Wc^T)_nn / M
+//   (bnfold_fwd_stats_kernel; T = Wc Ga is kept for the backward).
+// Backward, from dz [M][C] (the ReLU-masked residual gradient), G = dz^T a [C][c] and dbeta = 1^T dz:
+//   sum_m dz yc = rowdot(Wc, G),  dgamma = rstd (rowdot - mean dbeta)
+//   dyc = A dz + B (yc - mean) + D   with A = g r, B = -g r^2 dgamma / M, D = -g r dbeta / M
+//   dWc      = A o G + B o (T - mean s^T) + D s^T                          (bnfold_bwd_grad_kernel)
+//   d act_b  = (dz - mean dz) W1 + (a - abar) W2,   W1 = diag(A) Wc,  W2 = Wc^T diag(B) Wc (symmetric):
+//              a W2 - abar W2 (1x1 conv + bias) followed by the dgrad of dz with W1 - mean(dz) W1
+//              (accumulating, bias epilogue); each mean term uses the bf16 weights of its MFMA so the
+//              cancellation happens in fp32 before rounding (bnfold_bias_kernel).
+// All reductions are fixed-order (deterministic); the fp32-MFMA tiles use v_mfma_f32_16x16x4_f32.
+#include "common.h"
+
+namespace {
+
+typedef __attribute__((ext_vector_type(4))) float f4;
+
+// 4 consecutive row elements as fp32 from a bf16 or fp32 row (k multiple of 4, 8-B / 16-B aligned rows)
+__device__ __forceinline__ f4 ld4(const uint16_t* row, int k) {
+  const uint2 v = *reinterpret_cast<const uint2*>(row + k);
+  return f4{__uint_as_float(v.x << 16), __uint_as_float(v.x & 0xffff0000u), __uint_as_float(v.y << 16),
+            __uint_as_float(v.y & 0xffff0000u)};
+}
+__device__ __forceinline__ f4 ld4(const float* row, int k) { return *reinterpret_cast<const f4*>(row + k); }
+
+// out[i][j] = sum_k A[i][k] * sc[k] * B[j][k]   (16x16 tile; the 4 waves split k in 16-wide chunks)
+// rows must be 4-element aligned and K % 4 == 0 (channel counts here are multiples of 8)
+template <typename TA, typename TB>
+__device__ __forceinline__ f32x4_t tile16(const TA* A, int lda, int Mr, const TB* B, int ldb, int Nr, int K,
+                                          const float* sc, int i0, int j0, int wave, int lane) {
+  f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+  const int r = lane & 15, q = lane >> 4;
+  const bool ai = i0 + r < Mr, bj = j0 + r < Nr;
+  const TA* ap = A + (int64_t)(ai ? i0 + r : 0) * lda;
+  const TB* bp = B + (int64_t)(bj ? j0 + r : 0) * ldb;
+  for (int k0 = wave * 16; k0 < K; k0 += 64) {
+    const int k = k0 + 4 * q;
+    f4 a = {0.f, 0.f, 0.f, 0.f}, b = {0.f, 0.f, 0.f, 0.f};
+    if (k < K) {
+      if (ai) a = ld4(ap, k);
+      if (bj) b = ld4(bp, k);
+      if (sc) a *= ld4(sc, k);
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t], b[t], acc, 0, 0, 0);
+  }
+  return acc;
+}
+
+__device__ __forceinline__ f32x4_t reduce4(f32x4_t acc, float* red, int wave, int lane) {
+  __syncthreads();
+  *reinterpret_cast<f32x4_t*>(red + (wave * 64 + lane) * 4) = acc;
+  __syncthreads();
+  f32x4_t t = *reinterpret_cast<const f32x4_t*>(red + lane * 4);
+#pragma unroll
+  for (int w = 1; w < 4; ++w) t += *reinterpret_cast<const f32x4_t*>(red + (w * 64 + lane) * 4);
+  return t;   // every wave gets the total
+}
+
+// sum of colsum slabs [splits][c] -> s [c]
+__device__ __forceinline__ float slab_sum(const float* slabs, int splits, int c, int j) {
+  float t = 0.f;
+  for (int k = 0; k < splits; ++k) t += slabs[(int64_t)k * c + j];
+  return t;
+}
+
+// one block per 16 output channels n: T[n][:] = Wc[n] Ga, q_n = Wc[n] . T[n], mean_n = Wc[n] . s / M;
+// then the training-mode BN finalize (running stats with unbiased variance, consumer affine)
+__global__ __launch_bounds__(256) void bnfold_fwd_stats_kernel(
+    const uint16_t* __restrict__ Wf, const float* __restrict__ Ga, const float* __restrict__ sslab, int splits,
+    int C, int c, int64_t count, float* __restrict__ T, float* __restrict__ s_out, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float* __restrict__ run_mean, float* __restrict__ run_var,
+    int64_t* __restrict__ nbt, float momentum, float eps, float* __restrict__ save_mean,
+    float* __restrict__ save_rstd, float* __restrict__ scale, float* __restrict__ shift) {
+  __shared__ __attribute__((aligned(16))) float red[4 * 64 * 4];
+  __shared__ float s_sh[2048];
+  __shared__ double qsum[16];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int i0 = blockIdx.x * 16;
+  for (int j = threadIdx.x; j < c; j += 256) {
+    const float v = slab_sum(sslab, splits, c, j);
+    s_sh[j] = v;
+    if (blockIdx.x == 0) s_out[j] = v;
+  }
+  if (threadIdx.x < 16) qsum[threadIdx.x] = 0.0;
+  __syncthreads();
+  for (int j0 = 0; j0 < c; j0 += 16) {
+    const f32x4_t t = reduce4(tile16(Wf, c, C, Ga, c, c, c, (const float*)nullptr, i0, j0, wave, lane), red, wave,
+                              lane);
+    if (wave == 0) {
+      const int j = j0 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = i0 + 4 * (lane >> 4) + r;
+        float w = 0.f;
+        if (n < C && j < c) {
+          T[(int64_t)n * c + j] = t[r];
+          w = bf2f(Wf[(int64_t)n * c + j]) * t[r];
+        }
+        w = sum16(w);
+        if ((lane & 15) == 0) qsum[4 * (lane >> 4) + r] += (double)w;
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 16) {
+    const int n = i0 + threadIdx.x;
+    if (n < C) {
+      double mu = 0.0;
+      for (int j = 0; j < c; ++j) mu += (double)bf2f(Wf[(int64_t)n * c + j]) * (double)s_sh[j];
+      mu /= (double)count;
+      double var = qsum[threadIdx.x] / (double)count - mu * mu;
+      if (var < 0) var = 0;
+      const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+      save_mean[n] = (float)mu;
+      save_rstd[n] = rstd;
+      const float g = gamma[n], b = beta[n];
+      scale[n] = g * rstd;
+      shift[n] = b - (float)mu * g * rstd;
+      if (run_mean) {
+        const double unb = count > 1 ? var * (double)count / (double)(count - 1) : var;
+        run_mean[n] = (1.f - momentum) * run_mean[n] + momentum * (float)mu;
+        run_var[n] = (1.f - momentum) * run_var[n] + momentum * (float)unb;
+      }
+      if (n == 0 && nbt) nbt[0] += 1;
+    }
+  }
+}
+
+// per output channel n (block): dbeta = sum of the epilogue partials, sdzy = Wc[n] . G[n],
+// dgamma = rstd (sdzy - mean dbeta) -> grad buffers (beta-accumulate) and coef [A | B | D] [3][C]
+__global__ __launch_bounds__(256) void bnfold_bwd_coef_kernel(
+    const float* __restrict__ part, int tiles, const uint16_t* __restrict__ Wf, const float* __restrict__ G, int C,
+    int c, int64_t count, const float* __restrict__ gamma, const float* __restrict__ mean,
+    const float* __restrict__ rstd, float* __restrict__ dgamma, float* __restrict__ dbeta, float beta_acc,
+    float* __restrict__ coef) {
+  const int n = blockIdx.x;
+  __shared__ double ra[256], rb[256];
+  double sdz = 0.0, sy = 0.0;
+  for (int t = threadIdx.x; t < tiles; t += 256) sdz += part[(int64_t)t * 3 * C + n];
+  for (int j = threadIdx.x; j < c; j += 256) sy += (double)bf2f(Wf[(int64_t)n * c + j]) * G[(int64_t)n * c + j];
+  ra[threadIdx.x] = sdz; rb[threadIdx.x] = sy;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) { ra[threadIdx.x] += ra[threadIdx.x + o]; rb[threadIdx.x] += rb[threadIdx.x + o]; }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const double db = ra[0];
+    const double r = rstd[n], mu = mean[n];
+    const double dg = r * (rb[0] - mu * db);
+    if (dgamma) {
+      dgamma[n] = (beta_acc == 0.f ? 0.f : beta_acc * dgamma[n]) + (float)dg;
+      dbeta[n] = (beta_acc == 0.f ? 0.f : beta_acc * dbeta[n]) + (float)db;
+    }
+    const double g = gamma[n], inv = 1.0 / (double)count;
+    coef[n] = (float)(g * r);                       // A
+    coef[C + n] = (float)(-g * r * r * dg * inv);   // B
+    coef[2 * C + n] = (float)(-g * r * db * inv);   // D
+    coef[3 * C + n] = (float)(db * inv);            // mean(dz)
+  }
+}
+
+// elementwise over [C][c]: dWc = A G + B (T - mean s) + D s  -> grad (PyTorch [C][c][1][1][1], beta-accumulate);
+// W1t[j][n] = bf16(A_n Wc[n][j])  (the dgrad pack layout [Cin = c][Cout = C]) through a 32x32 LDS transpose
+__global__ __launch_bounds__(256) void bnfold_bwd_grad_kernel(
+    const float* __restrict__ G, const float* __restrict__ T, const float* __restrict__ s, const float* __restrict__ mean,
+    const float* __restrict__ coef, const uint16_t* __restrict__ Wf, int C, int c, float* __restrict__ grad,
+    float beta, uint16_t* __restrict__ W1t) {
+  __shared__ uint16_t tile[32][33];
+  const int j0 = blockIdx.x * 32, n0 = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int y = ty; y < 32; y += 8) {
+    const int n = n0 + y, j = j0 + tx;
+    uint16_t w1 = 0;
+    if (n < C && j < c) {
+      const int64_t o = (int64_t)n * c + j;
+      const float A = coef[n], B = coef[C + n], D = coef[2 * C + n];
+      const float v = A * G[o] + B * (T[o] - mean[n] * s[j]) + D * s[j];
+      grad[o] = (beta == 0.f ? 0.f : beta * grad[o]) + v;
+      w1 = f2bf(A * bf2f(Wf[o]));
+    }
+    tile[y][tx] = w1;
+  }
+  __syncthreads();
+  for (int y = ty; y < 32; y += 8) {
+    const int j = j0 + y, n = n0 + tx;
+    if (j < c && n < C) W1t[(int64_t)j * C + n] = tile[tx][y];
+  }
+}
+
+// W2[i][j] = sum_n Wd[i][n] B_n Wd[j][n]  (Wd = the dgrad pack [c][C] = Wc^T) -> bf16 forward pack [c][c];
+// grid (c/16, c/16)
+__global__ __launch_bounds__(256) void bnfold_w2_kernel(const uint16_t* __restrict__ Wd, const float* __restrict__ coef,
+                                                       int C, int c, uint16_t* __restrict__ W2) {
+  __shared__ __attribute__((aligned(16))) float red[4 * 64 * 4];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int i0 = blockIdx.y * 16, j0 = blockIdx.x * 16;
+  const f32x4_t t = reduce4(tile16(Wd, C, c, Wd, C, c, C, coef + C, i0, j0, wave, lane), red, wave, lane);
+  if (wave == 0) {
+    const int j = j0 + (lane & 15);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = i0 + 4 * (lane >> 4) + r;
+      if (i < c && j < c) W2[(int64_t)i * c + j] = f2bf(t[r]);
+    }
+  }
+}
+
+// The two large mean terms of d act_b are cancelled with the SAME bf16-rounded weights the MFMAs use, in fp32
+// before any rounding (dz carries the broadcast mean of the pooled-head gradient, which the BN backward
+// removes: dz W1 and its mean correction are each far larger than their sum):
+//   biasA[j] = -sum_n mean(dz_n) W1b[n][j]   (epilogue of the dz W1 dgrad)
+//   biasB[j] = -sum_i abar_i W2b[j][i]       (epilogue of the act_b W2 conv; abar = s / M)
+__global__ __launch_bounds__(256) void bnfold_bias_kernel(const uint16_t* __restrict__ W1t,
+                                                         const uint16_t* __restrict__ W2b, const float* __restrict__ coef,
+                                                         const float* __restrict__ s, int C, int c, int64_t count,
+                                                         float* __restrict__ bias) {
+  const int j = blockIdx.x;
+  __shared__ double r0[256], r1[256];
+  double a = 0.0, b = 0.0;
+  const double inv = 1.0 / (double)count;
+  for (int n = threadIdx.x; n < C; n += 256) a -= (double)coef[3 * C + n] * bf2f(W1t[(int64_t)j * C + n]);
+  for (int i = threadIdx.x; i < c; i += 256) b -= (double)s[i] * inv * bf2f(W2b[(int64_t)j * c + i]);
+  r0[threadIdx.x] = a;
+  r1[threadIdx.x] = b;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) { r0[threadIdx.x] += r0[threadIdx.x + o]; r1[threadIdx.x] += r1[threadIdx.x + o]; }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) { bias[j] = (float)r0[0]; bias[c + j] = (float)r1[0]; }
+}
+
+}  // namespace
+
+void bnfold_fwd_stats_launch(const uint16_t* Wf, const float* Ga, const float* sslab, int splits, int C, int c,
+                             int64_t count, float* T, float* s_out, const float* gamma, const float* beta, float* rm,
+                             float* rv, int64_t* nbt, float momentum, float eps, float* smean, float* srstd,
+                             float* scale, float* shift, hipStream_t st) {
+  hipLaunchKernelGGL(bnfold_fwd_stats_kernel, dim3((C + 15) / 16), dim3(256), 0, st, Wf, Ga, sslab, splits, C, c,
+                     count, T, s_out, gamma, beta, rm, rv, nbt, momentum, eps, smean, srstd, scale, shift);
+}
+
+void bnfold_bwd_launch(const float* part, int tiles, const uint16_t* Wf, const uint16_t* Wd, const float* G,
+                       const float* T, const float* s, int C, int c, int64_t count, const float* gamma,
+                       const float* mean, const float* rstd, float* dgamma, float* dbeta, float* dW, float beta_acc,
+                       float* coef, uint16_t* W1t, uint16_t* W2, float* bias, hipStream_t st) {
+  hipLaunchKernelGGL(bnfold_bwd_coef_kernel, dim3(C), dim3(256), 0, st, part, tiles, Wf, G, C, c, count, gamma, mean,
+                     rstd, dgamma, dbeta, beta_acc, coef);
+  hipLaunchKernelGGL(bnfold_bwd_grad_kernel, dim3((c + 31) / 32, (C + 31) / 32), dim3(256), 0, st, G, T, s, mean, coef,
+                     Wf, C, c, dW, beta_acc, W1t);
+  hipLaunchKernelGGL(bnfold_w2_kernel, dim3((c + 15) / 16, (c + 15) / 16), dim3(256), 0, st, Wd, coef, C, c, W2);
+  hipLaunchKernelGGL(bnfold_bias_kernel, dim3(c), dim3(256), 0, st, W1t, W2, coef, s, C, c, count, bias);
+}

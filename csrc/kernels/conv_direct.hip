@@ -230,7 +230,7 @@ __global__ __launch_bounds__(DNT) void conv_direct_kernel(const ConvParams p, in
           if (p.emask) bits = (p.emask[(int64_t)ps * (p.Ngemm >> 3) + (n >> 3)] >> (n & 7)) & 0xfu;
           float y0[4] = {0.f, 0.f, 0.f, 0.f}, y1[4] = {0.f, 0.f, 0.f, 0.f};
           if (do_bstats) {
-            unpack4(*reinterpret_cast<const uint2*>(p.ey0 + (int64_t)ps * p.Ngemm + n), y0);
+            if (p.ey0) unpack4(*reinterpret_cast<const uint2*>(p.ey0 + (int64_t)ps * p.Ngemm + n), y0);
             if (dual) unpack4(*reinterpret_cast<const uint2*>(p.ey1 + (int64_t)ps * p.Ngemm + n), y1);
             if (masky) {
               const f32x4_t ms = *reinterpret_cast<const f32x4_t*>(mk + n);
@@ -295,7 +295,8 @@ __global__ __launch_bounds__(DNT) void conv_direct_kernel(const ConvParams p, in
       for (int w = 0; w < 4; ++w) t[k] += red[(w * 3 + k) * NBW + i];
     }
     if (EPI == 1) {
-      const float m0 = p.emean0[i], r0 = p.erstd0[i];
+      // no y0 (BN-folded conv_c: its raw output does not exist): only the sums of v and v*xhat1
+      const float m0 = p.ey0 ? p.emean0[i] : 0.f, r0 = p.ey0 ? p.erstd0[i] : 0.f;
       t[1] = (t[1] - m0 * t[0]) * r0;
       t[2] = dual ? (t[2] - p.emean1[i] * t[0]) * p.erstd1[i] : 0.f;
       for (int k = 0; k < nq; ++k) p.epart[((int64_t)blockIdx.x * 3 + k) * p.Ngemm + i] = t[k];

@@ -113,9 +113,9 @@ void conv_igemm_kernel(const ConvParams p) {
   if (do_bstats) {  // this tile's BN constants, read once here so the epilogue never waits on them
     for (int i = tid; i < BN; i += NT) {
       const int n = n0 + i;
-      const bool ok = n < p.Ngemm, d = ok && p.ey1 != nullptr;
-      bnp[i] = ok ? p.emean0[n] : 0.f;
-      bnp[BN + i] = ok ? p.erstd0[n] : 0.f;
+      const bool ok = n < p.Ngemm, d = ok && p.ey1 != nullptr, d0 = ok && p.ey0 != nullptr;
+      bnp[i] = d0 ? p.emean0[n] : 0.f;
+      bnp[BN + i] = d0 ? p.erstd0[n] : 0.f;
       bnp[2 * BN + i] = d ? p.emean1[n] : 0.f;
       bnp[3 * BN + i] = d ? p.erstd1[n] : 0.f;
       bnp[4 * BN + i] = (ok && p.emsc) ? p.emsc[n] : 0.f;
@@ -544,8 +544,44 @@ void conv_igemm_kernel(const ConvParams p) {
       for (int j = 0; j < TN; ++j) {
         const int n = n0 + wn * WN + j * 16 + 4 * fslot;
         float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        if (p.fres) {
+          // residual-unit output from known BN statistics: out = relu(v*osc + osh + r), ReLU bits
+          const bool ok = m < p.M && n < p.Ngemm;
+          unsigned bits = 0;
+          if (ok) {
+            const f32x4_t sc = *reinterpret_cast<const f32x4_t*>(p.fsc + n);
+            const f32x4_t sh = *reinterpret_cast<const f32x4_t*>(p.fsh + n);
+            float r[4];
+            unpack4(*reinterpret_cast<const uint2*>(p.eres + pos * p.ldr + n), r);
+            if (p.rsc) {
+              const f32x4_t rs = *reinterpret_cast<const f32x4_t*>(p.rsc + n);
+              const f32x4_t rh = *reinterpret_cast<const f32x4_t*>(p.rsh + n);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) r[e] = r[e] * rs[e] + rh[e];
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e] * sc[e] + sh[e] + r[e], 0.f);
+            const uint2 pk = pack4(v);
+            *reinterpret_cast<uint2*>(p.y + pos * p.ldy + n) = pk;
+            const uint32_t w2[2] = {pk.x, pk.y};
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {   // bit = stored bf16 > 0 (res_out's convention)
+              bits |= ((w2[e] & 0x7fffu) != 0 && !(w2[e] & 0x8000u)) ? 1u << (2 * e) : 0u;
+              bits |= ((w2[e] & 0x7fff0000u) != 0 && !(w2[e] & 0x80000000u)) ? 1u << (2 * e + 1) : 0u;
+            }
+          }
+          // channels 8k..8k+7 of a row live in lanes l (fslot even) and l ^ 16: one mask byte per pair
+          const unsigned other = __shfl_xor(bits, 16, 64);
+          if (ok && !(fslot & 1)) p.emask_out[pos * (p.Ngemm >> 3) + (n >> 3)] = (uint8_t)(bits | (other << 4));
+          continue;
+        }
         if (m < p.M && n < p.Ngemm) {
           uint16_t* dst = p.y + pos * p.ldy + n;
+          if (p.ebias) {   // per-column bias, added in fp32 before the bf16 rounding
+            const f32x4_t b = *reinterpret_cast<const f32x4_t*>(p.ebias + n);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] += b[r];
+          }
           if (p.accum) {
             float o[4];
             unpack4(*reinterpret_cast<const uint2*>(dst), o);
@@ -613,7 +649,7 @@ void conv_igemm_kernel(const ConvParams p) {
           if (p.eres) lr[u] = *reinterpret_cast<const uint4*>(p.eres + ps * p.ldr + n);
           if (p.emask) bits[u] = p.emask[ps * (p.Ngemm >> 3) + (n >> 3)];
           if (do_bstats) {
-            l0[u] = *reinterpret_cast<const uint4*>(p.ey0 + ps * p.Ngemm + n);
+            if (p.ey0) l0[u] = *reinterpret_cast<const uint4*>(p.ey0 + ps * p.Ngemm + n);
             if (dual) l1[u] = *reinterpret_cast<const uint4*>(p.ey1 + ps * p.Ngemm + n);
           }
         }
@@ -635,6 +671,12 @@ void conv_igemm_kernel(const ConvParams p) {
           for (int e = 0; e < 8; ++e)
             if (!(a[e] * bnp[4 * BN + cg * 8 + e] + bnp[5 * BN + cg * 8 + e] > 0.f)) bits[u] &= ~(1u << e);
         }
+        if (p.ebias) {
+          const f32x4_t b0 = *reinterpret_cast<const f32x4_t*>(p.ebias + n);
+          const f32x4_t b1 = *reinterpret_cast<const f32x4_t*>(p.ebias + n + 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) { rs[e] += b0[e]; rs[e + 4] += b1[e]; }
+        }
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const float t = v[e] + o[e] + rs[e];
@@ -645,7 +687,7 @@ void conv_igemm_kernel(const ConvParams p) {
         if (do_bstats) {
           float q[8], a[8];
           unpack8(pk, q);
-          unpack8(l0[u], a);
+          unpack8(l0[u], a);   // zeros when there is no y0 (then s0 stays 0: bnp mean0/rstd0 are 0 too)
 #pragma unroll
           for (int e = 0; e < 8; ++e) { sv[e] += q[e]; s0[e] += q[e] * a[e]; }
           if (dual) {
@@ -740,7 +782,7 @@ template <int BM, int BN, int WM, int WN, int CH, int BK>
 void launch_cfg(const ConvParams& p, int ut_force, hipStream_t stream, bool dma = false) {
   constexpr int NT = (BM / WM) * (BN / WN) * 64;
   const int m_tiles = (p.M + BM - 1) / BM, n_tiles = (p.Ngemm + BN - 1) / BN;
-  const bool epi = p.eres || p.emask || p.epart;
+  const bool epi = !p.fres && (p.eres || p.emask || p.epart);   // EPI 1 (the fres epilogue is EPI 0)
   constexpr int NW = (BM / WM) * (BN / WN);
   const size_t red_bytes = epi ? (NW * 3 + 6) * BN * 4 : (BM / WM) * 2 * BN * 4;
   const bool use_dma = CH == 8 && dma && !p.affine && conv_ut_legal(p, CH, BK) && ut_force != 0;
@@ -836,8 +878,14 @@ static int pick_variant(int M, int N) {
 // (overrides bits 0-1; forward / plain dgrad only).  -1 = heuristic.
 int conv_direct_rows(int cfg);
 void conv_direct_launch(const ConvParams& p, int cfg, hipStream_t s);
+// bit 9 = the streaming pointwise kernel of conv_pw.hip (dense 1x1x1 GEMMs; bits 0-1: 1024 << v rows per
+// workgroup)
+int conv_pw_rows(int cfg);
+int conv_pw_legal(const ConvParams& p, int chunk);
+void conv_pw_launch(const ConvParams& p, int cfg, hipStream_t st);
 
 int conv_cfg_bm(int cfg, int N) {
+  if (cfg >= 0 && (cfg & 16) && (cfg & 512)) return conv_pw_rows(cfg);
   if (cfg >= 0 && (cfg & 16) && (cfg & 32)) return conv_direct_rows(cfg);
   if (cfg >= 0 && (cfg & 16) && (cfg & 256)) return 256;   // 256x256 tile
   const int v = (cfg >= 0 && (cfg & 16)) ? (cfg & 3) : pick_variant(0, N);
@@ -859,9 +907,14 @@ void conv_igemm_set_bk(int bk) { g_bk_override = bk; }
 int conv_igemm_ut_legal(const ConvParams& p, int chunk, int bk) { return conv_ut_legal(p, chunk, bk) ? 1 : 0; }
 
 void conv_igemm_launch(const ConvParams& p, int chunk, hipStream_t stream, int cfg) {
-  if ((p.eres || p.emask || p.epart) && chunk != 8) return;  // host binding rejects this combination
+  if ((p.eres || p.emask || p.epart || p.fres) && chunk != 8) return;  // host binding rejects this combination
   int v, bk, ut_force;
   bool dma = false;
+  if (cfg >= 0 && (cfg & 16) && (cfg & 512)) {   // streaming pointwise kernel (legality checked by the bindings)
+    conv_pw_launch(p, cfg, stream);
+    return;
+  }
+  if ((p.fres || p.ebias) && cfg >= 0 && (cfg & 32)) cfg = -1;   // the direct kernel has no fres / bias epilogue
   if (cfg >= 0 && (cfg & 16) && (cfg & 32)) {  // narrow direct-to-register kernel (conv_direct.hip)
     conv_direct_launch(p, cfg, stream);
     return;

@@ -52,6 +52,17 @@ struct ConvParams {
   const float* emsc;        // optional ReLU mask from the BN input itself: v *= (y0*emsc + emsh > 0)
   const float* emsh;        //   (mask mode 2: the gradient of a BN whose ReLU output feeds this conv)
   unsigned xbytes, wbytes;  // buffer-resource extents of x and w (uniform-tap loader)
+  const float* ebias;       // EPI 1: optional per-column bias added before the ReLU mask
+  // Forward residual-unit epilogue (fres = 1; EPI 0): the conv's own BatchNorm is applied from known
+  // statistics and the unit output is written directly:
+  //   out = relu(acc * fsc + fsh + r)   with r = eres row (identity shortcut) or r = eres * rsc + rsh
+  //   (branch1 BN), ReLU bits of the stored bf16 into emask_out [rows][Ngemm/8]; no raw output, no stats.
+  int fres;
+  const float* fsc;
+  const float* fsh;
+  const float* rsc;
+  const float* rsh;
+  uint8_t* emask_out;
 };
 
 // Weight gradient: dW[n = cout][k = (tap, cin)] = sum_p dY[p][cout] * im2col(X)[p][k]
@@ -72,5 +83,10 @@ struct WgradParams {
   int splits, p_per_split;
   int slab;                 // 1: deterministic mode — split s stores into partial + s*Cout*K (no atomics)
   unsigned dybytes, xbytes; // buffer-resource extents
-  int variant;              // tile variant (0: 16x128, 1: 32x128, 2: 64x64, 3: 128x64); -1 = heuristic
+  int variant;              // tile variant (0: 16x128, 1: 32x128, 2: 64x64, 3: 128x64, ...); -1 = heuristic
+  // Gram mode (BatchNorm folding of a following 1x1 conv): the SAME affine(+relu) is applied to dy too,
+  // i.e. partial = act(x)^T act(x); colsum (optional, [splits][Cout]) receives sum_p act(dy)[p][n] from the
+  // k-tile-0 blocks of each split
+  int dy_affine;
+  float* colsum;
 };

@@ -79,6 +79,17 @@ void conv_wgrad_kernel(const WgradParams p) {
   const int a_col = tid % A_CPR;
   const int a_n = n0 + a_col * 8;
   const bool a_col_ok = a_n < p.Cout;
+  // Gram mode: dY is the same BN-ReLU input as x (affine on both operands) + column sums
+  const bool dy_aff = p.dy_affine != 0;
+  float dsc[8], dsh[8], csum[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    dsc[e] = (dy_aff && a_col_ok) ? p.in_scale[a_n + e] : 0.f;
+    dsh[e] = (dy_aff && a_col_ok) ? p.in_shift[a_n + e] : 0.f;
+    csum[e] = 0.f;
+  }
+  const bool do_csum = dy_aff && p.colsum != nullptr && blockIdx.y == 0;
+  unsigned ra_valid = ~0u;
   int a_vo[A_SLOTS], a_row[A_SLOTS], sa[A_SLOTS];
 #pragma unroll
   for (int s = 0; s < A_SLOTS; ++s) {
@@ -158,6 +169,11 @@ void conv_wgrad_kernel(const WgradParams p) {
   auto load = [&]() {
     const int pd = pcur - p_begin;  // uniform step offset (positions)
     rb_valid = 0;
+    if (dy_aff) {   // rows past this split (or P): act(0) != 0, so both Gram operands are zeroed there
+      ra_valid = 0;
+#pragma unroll
+      for (int s = 0; s < A_SLOTS; ++s) ra_valid |= (pcur + a_row[s] < p_end ? 1u : 0u) << s;
+    }
     if constexpr (DENSE && CH == 8) {
 #pragma unroll
       for (int s = 0; s < A_SLOTS; ++s) {
@@ -179,7 +195,11 @@ void conv_wgrad_kernel(const WgradParams p) {
               xr, v ? b_vo[s] + pd * p.ldx * 2 : (int)OOB, 0, 0));
         }
       }
-      rb_valid = ~0u;
+      rb_valid = dy_aff ? 0u : ~0u;
+      if (dy_aff) {
+#pragma unroll
+        for (int s = 0; s < B_SLOTS; ++s) rb_valid |= (pcur + b_row[s] < p_end ? 1u : 0u) << s;
+      }
       pcur += BP;
       return;
     }
@@ -214,7 +234,26 @@ void conv_wgrad_kernel(const WgradParams p) {
 #pragma unroll
     for (int s = 0; s < A_SLOTS; ++s) {
       if constexpr (A_CHUNKS % NT != 0) if (tid + s * NT >= A_CHUNKS) break;
-      *reinterpret_cast<uint4*>(A + sa[s]) = ra[s];
+      uint4 v = ra[s];
+      if (dy_aff) {
+        float f[8];
+        unpack8(v, f);
+        const bool ok = (ra_valid >> s) & 1u;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float z = __builtin_fmaf(f[e], dsc[e], dsh[e]);
+          z = affine == 2 ? fmaxf(z, 0.f) : z;
+          f[e] = ok ? z : 0.f;
+        }
+        v = pack8_fast(f);
+        if (do_csum) {   // sum of the bf16 operand values actually multiplied
+          float q[8];
+          unpack8(v, q);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) csum[e] += q[e];
+        }
+      }
+      *reinterpret_cast<uint4*>(A + sa[s]) = v;
     }
 #pragma unroll
     for (int s = 0; s < B_SLOTS; ++s) {
@@ -229,7 +268,7 @@ void conv_wgrad_kernel(const WgradParams p) {
         if constexpr (CH == 8) {
           v = pack8_fast(f);
           if (affine == 2) v = relu_bf16x8(v);
-          if (!DENSE && !((rb_valid >> s) & 1u)) v = uint4{0, 0, 0, 0};   // zero padding stays zero
+          if ((!DENSE || dy_aff) && !((rb_valid >> s) & 1u)) v = uint4{0, 0, 0, 0};   // padding stays zero
         } else {
           if (affine == 2)
             for (int e = 0; e < CH; ++e) f[e] = fmaxf(f[e], 0.f);
@@ -307,6 +346,27 @@ void conv_wgrad_kernel(const WgradParams p) {
     }
   }
 
+  if (do_csum) {
+    // threads with the same A column (tid % A_CPR) hold partial sums of the same 8 channels: reduce within
+    // the wave, then across waves through the (now idle) LDS in a fixed order -> colsum[split][n]
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);
+    constexpr int NWAVE = NT / 64;
+    static_assert(A_CPR <= 64, "column groups per wave");
+#pragma unroll
+    for (int e = 0; e < 8; ++e) csum[e] = wave_sum_stride(csum[e], A_CPR);
+    if (lane < A_CPR) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) red[wid * BMW + a_col * 8 + e] = csum[e];
+    }
+    __syncthreads();
+    for (int c = tid; c < BMW; c += NT) {
+      float t = 0.f;
+      for (int w = 0; w < NWAVE; ++w) t += red[w * BMW + c];
+      if (n0 + c < p.Cout) p.colsum[(int64_t)split * p.Cout + n0 + c] = t;
+    }
+  }
+
   // D[n][k]: lane holds k = col (lane&15), n = 4*(lane>>4) + r.  With one slab the tile is stored;
   // with several, slabs accumulate into one zero-initialised fp32 buffer with no-return
   // global_atomic_add_f32 (each wave-instruction = 4 rows x 64 contiguous bytes).
@@ -327,6 +387,185 @@ void conv_wgrad_kernel(const WgradParams p) {
         }
       }
     }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Narrow weight gradient (Cout <= 16 * MT, K = taps x Cin <= 16 * NTN, Cin % 8 == 0): the fast-pathway
+// convs, whose block tiles above spend their time in per-stage barriers.  Every WAVE is an independent
+// worker over its own contiguous position range with a private LDS slice, so there is no workgroup barrier
+// at all: lane l stages row l of a 64-position chunk — its dY row (A image) and its im2col row, one 16-B
+// chunk per (tap, 8 channels) (B image) — and the wave reads the two 32-row halves back with
+// ds_read_b64_tr_b16 for 2 x MT x NTN MFMAs.  LDS ops of one wave execute in order, so the reads see the
+// writes and the next chunk's writes never overtake them.  The next chunk's global loads are issued before
+// the current chunk's MFMAs.  Tiles are added into the zeroed fp32 accumulator with no-return atomics.
+// Gram mode (dy_affine) applies the x affine to dY too and writes per-wave column sums (slab row = wave).
+template <int MT, int NTN>
+__global__ __launch_bounds__(256) void wgrad_narrow_kernel(const WgradParams p) {
+  constexpr int KP = 16 * NTN, MP = 16 * MT;
+  constexpr int KC = KP / 8, MC = MP / 8;          // 16-B chunks per im2col / dY row (upper bounds)
+  constexpr int A_IMG = 64 * MP * 2, B_IMG = 64 * KP * 2;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int gw = blockIdx.x * 4 + wave;
+  if (gw >= p.splits) return;   // grid rounded up to whole workgroups; no workgroup barriers follow
+  char* A = smem + wave * (A_IMG + B_IMG);
+  char* B = A + A_IMG;
+  const int p_begin = gw * p.p_per_split;
+  const int p_end = min(p.P, p_begin + p.p_per_split);
+  const int kchunks = p.K / 8, mchunks = (p.Cout + 7) / 8;
+  const int affine = p.affine;
+  const bool dy_aff = p.dy_affine != 0;
+  f32x4_t acc[MT][NTN];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NTN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float csum[MP];
+#pragma unroll
+  for (int e = 0; e < MP; ++e) csum[e] = 0.f;
+  const int OHW = p.Ho * p.Wo, OTHW = p.To * OHW;
+  const bool check = p.pt | p.ph | p.pw;
+  // transposed-read addressing (as conv_wgrad_kernel): group g = lane>>4 covers rows 8g..8g+7 of a
+  // 32-row half; lane i = lane&15 supplies row (i>>2) of a 4-row block, columns 4*(i&3)..+3
+  const int g = lane >> 4, li = lane & 15;
+  const int tr_row = 8 * g + (li >> 2);
+  const int tr_colb = (li & 3) * 8;
+  uint4 ra[MC], rb[KC];
+  auto act8 = [&](uint4 v, const float* sc, const float* sh) {
+    float f[8];
+    unpack8(v, f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float z = __builtin_fmaf(f[e], sc[e], sh[e]);
+      f[e] = affine == 2 ? fmaxf(z, 0.f) : z;
+    }
+    return pack8_fast(f);
+  };
+  auto load = [&](int pbase) {
+    const int pp = pbase + lane;
+#pragma unroll
+    for (int mc = 0; mc < MC; ++mc) ra[mc] = uint4{0, 0, 0, 0};
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) rb[kc] = uint4{0, 0, 0, 0};
+    if (pp >= p_end) return;   // rows past the range stay zero in both images (also in Gram mode)
+    const uint16_t* dyr = p.dy + (int64_t)pp * p.ldd;
+#pragma unroll
+    for (int mc = 0; mc < MC; ++mc)
+      if (mc < mchunks) ra[mc] = *reinterpret_cast<const uint4*>(dyr + mc * 8);
+    int q = pp;
+    const int b = q / OTHW; q -= b * OTHW;
+    const int t = q / OHW; q -= t * OHW;
+    const int h = q / p.Wo, w = q - (q / p.Wo) * p.Wo;
+    const int bt = t * p.st - p.pt, bh = h * p.sh - p.ph, bw = w * p.sw - p.pw;
+    const int64_t base = (((int64_t)b * p.Ti + bt) * p.Hi + bh) * p.Wi + bw;
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) {
+      if (kc < kchunks) {
+        const int k = kc * 8;
+        const int tap = k / p.Cin, c0 = k - tap * p.Cin;
+        const int dt = tap / (p.kh * p.kw), r = tap - dt * p.kh * p.kw;
+        const int dh = r / p.kw, dw = r - (r / p.kw) * p.kw;
+        bool v = true;
+        if (check)
+          v = (unsigned)(bt + dt) < (unsigned)p.Ti && (unsigned)(bh + dh) < (unsigned)p.Hi &&
+              (unsigned)(bw + dw) < (unsigned)p.Wi;
+        if (v) {
+          const int64_t off = (base + ((int64_t)dt * p.Hi + dh) * p.Wi + dw) * p.ldx + c0;
+          rb[kc] = *reinterpret_cast<const uint4*>(p.x + off);
+          if (affine) rb[kc] = act8(rb[kc], p.in_scale + c0, p.in_shift + c0);   // padding stays zero
+        }
+      }
+    }
+    if (dy_aff) {   // Gram mode: dY is the same activation (Cout = Cin channels)
+#pragma unroll
+      for (int mc = 0; mc < MC; ++mc)
+        if (mc < mchunks) ra[mc] = act8(ra[mc], p.in_scale + mc * 8, p.in_shift + mc * 8);
+    }
+  };
+  const int niter = (p_end - p_begin + 63) / 64;
+  if (niter > 0) load(p_begin);
+  for (int it = 0; it < niter; ++it) {
+    // stage this chunk (row = lane) into the wave's private images
+#pragma unroll
+    for (int mc = 0; mc < MC; ++mc) *reinterpret_cast<uint4*>(A + img_off<MP>(lane, mc * 16)) = ra[mc];
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) *reinterpret_cast<uint4*>(B + img_off<KP>(lane, kc * 16)) = rb[kc];
+    if (dy_aff && p.colsum) {
+#pragma unroll
+      for (int mc = 0; mc < MC; ++mc) {
+        float f[8];
+        unpack8(ra[mc], f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) csum[mc * 8 + e] += f[e];
+      }
+    }
+    if (it + 1 < niter) load(p_begin + (it + 1) * 64);   // next chunk's loads fly under the MFMAs
+#pragma unroll
+    for (int hlf = 0; hlf < 2; ++hlf) {
+      const int rb0 = hlf * 32;
+      bf16x8_t af[MT];
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        const s16x4_t lo = tr_read(A + img_off<MP>(rb0 + tr_row, i * 32 + tr_colb));
+        const s16x4_t hi = tr_read(A + img_off<MP>(rb0 + tr_row + 4, i * 32 + tr_colb));
+        af[i] = __builtin_bit_cast(bf16x8_t, (s16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
+      }
+#pragma unroll
+      for (int j = 0; j < NTN; ++j) {
+        const s16x4_t blo = tr_read(B + img_off<KP>(rb0 + tr_row, j * 32 + tr_colb));
+        const s16x4_t bhi = tr_read(B + img_off<KP>(rb0 + tr_row + 4, j * 32 + tr_colb));
+        const bf16x8_t bf = __builtin_bit_cast(bf16x8_t,
+                                               (s16x8_t){blo[0], blo[1], blo[2], blo[3], bhi[0], bhi[1], bhi[2], bhi[3]});
+#pragma unroll
+        for (int i = 0; i < MT; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf, acc[i][j], 0, 0, 0);
+      }
+    }
+  }
+  // D[n][k]: lane holds k = j*16 + (lane&15), n = i*16 + 4*(lane>>4) + r
+  if (niter > 0) {
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NTN; ++j) {
+        const int k = j * 16 + li;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int n = i * 16 + 4 * g + r;
+          if (n < p.Cout && k < p.K) atomicAdd(p.partial + (int64_t)n * p.K + k, acc[i][j][r]);
+        }
+      }
+  }
+  if (dy_aff && p.colsum) {
+#pragma unroll
+    for (int e = 0; e < MP; ++e) csum[e] = wave_sum(csum[e]);
+    if (lane < p.Cout) {
+      float v = 0.f;
+#pragma unroll
+      for (int e = 0; e < MP; ++e) v = lane == e ? csum[e] : v;
+      p.colsum[(int64_t)gw * p.Cout + lane] = v;
+    }
+  }
+}
+
+template <int MT, int NTN>
+void launch_narrow(const WgradParams& p, hipStream_t stream) {
+  const int blocks = (p.splits + 3) / 4;
+  const size_t lds = 4 * (64 * 16 * MT * 2 + 64 * 16 * NTN * 2);
+  hipLaunchKernelGGL((wgrad_narrow_kernel<MT, NTN>), dim3(blocks), dim3(256), lds, stream, p);
+}
+
+template <int MT>
+void launch_narrow_k(const WgradParams& p, hipStream_t stream) {
+  switch ((p.K + 15) / 16) {
+    case 1: launch_narrow<MT, 1>(p, stream); break;
+    case 2: launch_narrow<MT, 2>(p, stream); break;
+    case 3: launch_narrow<MT, 3>(p, stream); break;
+    case 4: launch_narrow<MT, 4>(p, stream); break;
+    case 5: launch_narrow<MT, 5>(p, stream); break;
+    case 6: launch_narrow<MT, 6>(p, stream); break;
+    case 7: launch_narrow<MT, 7>(p, stream); break;
+    default: launch_narrow<MT, 8>(p, stream); break;
+  }
 }
 
 template <int BMW, int BNW, int WMW, int WNW, int CH, int BP>
@@ -408,7 +647,14 @@ void conv_wgrad_tile(int Cout, int K, int variant, int* bmw, int* bnw) {
 
 // p.variant: -1 = heuristic tile, 32-position stages; else bits 0-1 (+ bit 3 for tiles 4-7) = tile variant,
 // bit 2 = 64-position stages (p_per_split must then be a multiple of 64)
+// narrow kernel legality: Cout <= 32, Cin % 8 == 0, K <= 128
+int wgrad_narrow_legal(int Cout, int Cin, int K) { return (Cout <= 32 && Cin % 8 == 0 && K <= 128) ? 1 : 0; }
+
 void conv_wgrad_launch(const WgradParams& p, int chunk, hipStream_t stream) {
+  if (p.variant >= 0 && (p.variant & 16)) {   // narrow per-wave kernel: p.splits = waves, p_per_split = rows/wave
+    if (p.Cout <= 16) launch_narrow_k<1>(p, stream); else launch_narrow_k<2>(p, stream);
+    return;
+  }
   const int v = p.variant >= 0 ? wgrad_tile_index(p.variant) : wgrad_variant(p.Cout, p.K);
   const bool bp64 = p.variant >= 0 && (p.variant & 4);
   if (chunk == 8) {

@@ -18,12 +18,14 @@ void conv_igemm_launch(const ConvParams& p, int chunk, hipStream_t stream, int c
 int conv_cfg_bm(int cfg, int N);
 int conv_igemm_ut_legal(const ConvParams& p, int chunk, int bk);
 int conv_direct_legal(const ConvParams& p, int chunk);
+int conv_pw_legal(const ConvParams& p, int chunk);
 void conv_igemm_set_ut(int mode);
 int conv_igemm_m_tiles(int M, int N);
 int conv_igemm_m_tiles_k(int M, int N, int K, int Cg);
 void conv_igemm_set_bk(int bk);
 void conv_wgrad_launch(const WgradParams& p, int chunk, hipStream_t stream);
 void conv_wgrad_tile(int Cout, int K, int variant, int* bmw, int* bnw);
+int wgrad_narrow_legal(int Cout, int Cin, int K);
 void wgrad_reduce_launch(float* accbuf, float* grad, int splits, int Cout, int taps, int Cin, int Cin_real,
                          float scale, float beta, int slab, hipStream_t stream);
 void bn_finalize_launch(const float* part, int tiles, int C, int64_t count, const float* gamma, const float* beta,
@@ -72,6 +74,14 @@ void stem_wgrad_convert_launch(float* acc, float* grad, int Cout, int kt, float 
 void stem_pack_launch(const float* w, uint16_t* out, int Cout, int kt, hipStream_t s);
 void synth_frames_launch(uint8_t* out, int64_t n, uint32_t seed, hipStream_t s);
 
+void bnfold_fwd_stats_launch(const uint16_t* Wf, const float* Ga, const float* sslab, int splits, int C, int c,
+                             int64_t count, float* T, float* s_out, const float* gamma, const float* beta, float* rm,
+                             float* rv, int64_t* nbt, float momentum, float eps, float* smean, float* srstd,
+                             float* scale, float* shift, hipStream_t st);
+void bnfold_bwd_launch(const float* part, int tiles, const uint16_t* Wf, const uint16_t* Wd, const float* G,
+                       const float* T, const float* s, int C, int c, int64_t count, const float* gamma,
+                       const float* mean, const float* rstd, float* dgamma, float* dbeta, float* dW, float beta_acc,
+                       float* coef, uint16_t* W1t, uint16_t* W2, float* bias, hipStream_t st);
 void head_forward_launch(const float* feat, int N, int P, int C, const float* W, const float* b, int K, float p_drop,
                          uint64_t seed, float* xm, float* logits, hipStream_t s);
 void head_ce_launch(const float* logits, const int64_t* labels, int N, int K, float gscale, float* dlogits,
@@ -139,14 +149,54 @@ static ConvParams conv_params(const at::Tensor& x, const at::Tensor& w, const at
   return p;
 }
 
+// the streaming pointwise kernel (cfg bit 9) must only get geometries it supports: its slab count and row
+// mapping differ from the tile kernels', so a silent fallback would corrupt the caller's partial sums
+static void check_pw(const ConvParams& p, int64_t chunk, int64_t cfg) {
+  if (cfg < 0 || !(cfg & 16) || !(cfg & 512)) return;
+  TORCH_CHECK(conv_pw_legal(p, (int)chunk), "pointwise conv kernel selected for an unsupported geometry");
+  TORCH_CHECK(!p.eres || p.ldr % 8 == 0, "pointwise conv kernel: residual row stride must be a multiple of 8");
+  TORCH_CHECK(!p.emask || p.Ngemm % 8 == 0, "pointwise conv kernel: mask layout");
+}
+
 void conv_igemm(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, const OptT& stats,
                 const OptT& scale, const OptT& shift, int64_t affine, int64_t accum, std::vector<int64_t> g,
-                int64_t chunk, int64_t cfg) {
+                int64_t chunk, int64_t cfg, const OptT& bias) {
   ConvParams p = conv_params(x, w, y, accum, g, chunk);
+  p.ebias = f32o(bias);
+  TORCH_CHECK(!bias.has_value() || bias->numel() >= p.Ngemm, "bias too small");
   p.stats = f32o(stats);
   p.in_scale = f32o(scale); p.in_shift = f32o(shift);
   p.affine = (int)affine;
   TORCH_CHECK(!affine || (scale.has_value() && shift.has_value()), "affine needs scale/shift");
+  check_pw(p, chunk, cfg);
+  if (p.M == 0) return;
+  conv_igemm_launch(p, (int)chunk, cur_stream(), (int)cfg);
+}
+
+// forward conv whose epilogue applies its own BatchNorm from known statistics and writes the residual-unit
+// output: out = relu(acc * fsc + fsh + r), r = res (identity) or res * rsc + rsh (branch1 BN); ReLU bits
+// into mask [rows][Ngemm/8]
+void conv_igemm_fres(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, const OptT& scale,
+                     const OptT& shift, int64_t affine, std::vector<int64_t> g, int64_t chunk, int64_t cfg,
+                     const at::Tensor& osc, const at::Tensor& osh, const at::Tensor& res, int64_t ldr,
+                     const OptT& rsc, const OptT& rsh, const at::Tensor& mask) {
+  ConvParams p = conv_params(x, w, y, 0, g, chunk);
+  TORCH_CHECK(chunk == 8, "fres epilogue needs 16-B chunks");
+  p.in_scale = f32o(scale); p.in_shift = f32o(shift);
+  p.affine = (int)affine;
+  TORCH_CHECK(!affine || (scale.has_value() && shift.has_value()), "affine needs scale/shift");
+  p.fres = 1;
+  p.fsc = f32(osc); p.fsh = f32(osh);
+  TORCH_CHECK(osc.numel() >= p.Ngemm && osh.numel() >= p.Ngemm, "output affine too small");
+  p.eres = bfp(res); p.ldr = (int)ldr;
+  TORCH_CHECK(ldr % 4 == 0, "residual row stride alignment");
+  TORCH_CHECK(rsc.has_value() == rsh.has_value(), "residual affine needs scale and shift");
+  p.rsc = f32o(rsc); p.rsh = f32o(rsh);
+  TORCH_CHECK(mask.scalar_type() == at::kByte && p.Ngemm % 8 == 0 && mask.numel() >= (int64_t)p.M * (p.Ngemm / 8),
+              "mask must be uint8 bits [rows][C/8]");
+  p.emask_out = mask.data_ptr<uint8_t>();
+  TORCH_CHECK(p.ost == 1 && p.osh == 1 && p.osw == 1, "fres epilogue: dense output rows");
+  check_pw(p, chunk, cfg);
   if (p.M == 0) return;
   conv_igemm_launch(p, (int)chunk, cur_stream(), (int)cfg);
 }
@@ -156,8 +206,12 @@ void conv_igemm(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, c
 void conv_igemm_epi(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, int64_t accum,
                     std::vector<int64_t> g, int64_t chunk, const OptT& res, int64_t ldr, const OptT& mask,
                     const OptT& y0, const OptT& mean0, const OptT& rstd0, const OptT& y1, const OptT& mean1,
-                    const OptT& rstd1, const OptT& part, const OptT& msc, const OptT& msh, int64_t cfg) {
+                    const OptT& rstd1, const OptT& part, const OptT& msc, const OptT& msh, int64_t cfg,
+                    const OptT& bias) {
   ConvParams p = conv_params(x, w, y, accum, g, chunk);
+  p.ebias = f32o(bias);
+  TORCH_CHECK(!bias.has_value() || bias->numel() >= p.Ngemm, "bias too small");
+  TORCH_CHECK(!bias.has_value() || cfg < 0 || !(cfg & 32), "the direct kernel has no bias epilogue");
   TORCH_CHECK(cfg < 0 || !(cfg & 256), "the 256x256 tile has no backward-BN epilogue");
   p.eres = bfo(res); p.ldr = (int)ldr;
   TORCH_CHECK(!res.has_value() || ldr % 4 == 0, "residual row stride alignment");
@@ -166,17 +220,19 @@ void conv_igemm_epi(const at::Tensor& x, const at::Tensor& w, const at::Tensor& 
     p.emask = mask->data_ptr<uint8_t>();
   }
   if (part.has_value()) {
-    TORCH_CHECK(y0.has_value() && mean0.has_value() && rstd0.has_value(), "BN epilogue needs y0/mean0/rstd0");
+    TORCH_CHECK(!y0.has_value() || (mean0.has_value() && rstd0.has_value()), "BN epilogue needs mean0/rstd0 with y0");
+    TORCH_CHECK(!(msc.has_value() && !y0.has_value()), "mask affine reads y0");
     TORCH_CHECK(!y1.has_value() || (mean1.has_value() && rstd1.has_value()), "BN epilogue needs mean1/rstd1");
-    TORCH_CHECK(y0->size(-1) == p.Ngemm, "BN epilogue inputs must be dense [rows][Ngemm]");
-    p.ey0 = bfp(*y0); p.ey1 = bfo(y1);
-    p.emean0 = f32(*mean0); p.erstd0 = f32(*rstd0); p.emean1 = f32o(mean1); p.erstd1 = f32o(rstd1);
+    TORCH_CHECK(!y0.has_value() || y0->size(-1) == p.Ngemm, "BN epilogue inputs must be dense [rows][Ngemm]");
+    p.ey0 = bfo(y0); p.ey1 = bfo(y1);
+    p.emean0 = f32o(mean0); p.erstd0 = f32o(rstd0); p.emean1 = f32o(mean1); p.erstd1 = f32o(rstd1);
     p.epart = f32(*part);
     TORCH_CHECK(msc.has_value() == msh.has_value(), "mask affine needs scale and shift");
     p.emsc = f32o(msc); p.emsh = f32o(msh);
     const int bm = conv_cfg_bm((int)cfg, p.Ngemm);
     TORCH_CHECK(part->numel() >= (int64_t)((p.M + bm - 1) / bm) * 3 * p.Ngemm, "partials too small");
   }
+  check_pw(p, chunk, cfg);
   if (p.M == 0) return;
   conv_igemm_launch(p, (int)chunk, cur_stream(), (int)cfg);
 }
@@ -196,7 +252,7 @@ std::vector<int64_t> wgrad_tile(int64_t Cout, int64_t K, int64_t variant) {
 // geometry: [P, Cout, K, Cin, ldd, ldx, Ti, Hi, Wi, To, Ho, Wo, kt, kh, kw, st, sh, sw, pt, ph, pw, splits, pps]
 void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& partial, const OptT& scale,
                 const OptT& shift, int64_t affine, std::vector<int64_t> g, int64_t chunk, int64_t slab,
-                int64_t variant) {
+                int64_t variant, int64_t dy_affine, const OptT& colsum) {
   TORCH_CHECK(g.size() == 23, "wgrad geometry must have 23 entries");
   WgradParams p{};
   p.dy = bfp(dy); p.x = bfp(x); p.partial = f32(partial);
@@ -210,6 +266,17 @@ void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& par
   TORCH_CHECK(variant < 0 || !(variant & 4) || p.p_per_split % 64 == 0, "64-position stages need p_per_split % 64 == 0");
   p.slab = (int)slab;
   p.variant = (int)variant;
+  p.dy_affine = (int)dy_affine;
+  p.colsum = f32o(colsum);
+  TORCH_CHECK(!dy_affine || (affine && p.ldd >= p.Cout && chunk == 8 && p.kt * p.kh * p.kw == 1),
+              "Gram mode: 1x1 conv input with an affine, dy = x");
+  TORCH_CHECK(!colsum.has_value() || colsum->numel() >= (int64_t)p.splits * p.Cout, "colsum slab too small");
+  if (variant >= 0 && (variant & 16)) {
+    TORCH_CHECK(wgrad_narrow_legal(p.Cout, p.Cin, p.K) && chunk == 8 && !slab, "narrow wgrad not legal here");
+    TORCH_CHECK(p.p_per_split % 64 == 0 && (int64_t)p.splits * p.p_per_split >= p.P, "narrow wgrad: split cover");
+    TORCH_CHECK(p.ldd % 8 == 0 && p.ldx % 8 == 0, "narrow wgrad: 16-B rows");
+    TORCH_CHECK(!dy_affine || (p.Cout == p.Cin && p.K == p.Cin), "narrow Gram: square 1x1");
+  }
   TORCH_CHECK(dy.numel() * 2 < 0xFFFFFF00ll && x.numel() * 2 < 0xFFFFFF00ll, "buffer extents must fit 32 bits");
   p.dybytes = (unsigned)(dy.numel() * 2);
   p.xbytes = (unsigned)(x.numel() * 2);
@@ -270,13 +337,16 @@ std::vector<int64_t> bn_bwd_blocks(int64_t M, int64_t C) {
   return {b, rpb};
 }
 
+// y0 (+mean0/rstd0) optional: without it only sum(dz) (and the y1 terms) are reduced
 void bn_bwd_reduce(const at::Tensor& g, int64_t ldg, int64_t mask_mode, const OptT& mo, int64_t ldm, const OptT& ms,
-                   const OptT& mh, const at::Tensor& y0, const at::Tensor& mean0, const at::Tensor& rstd0,
+                   const OptT& mh, const OptT& y0, const OptT& mean0, const OptT& rstd0,
                    const OptT& y1, const OptT& mean1, const OptT& rstd1, int64_t M, int64_t C, int64_t blocks,
                    int64_t rpb, const at::Tensor& part) {
   TORCH_CHECK(C % 8 == 0 && C <= 2048, "bn_bwd_reduce channel constraint");
-  bn_bwd_reduce_launch(bfp(g), (int)ldg, (int)mask_mode, mask_ptr(mask_mode, mo), (int)ldm, f32o(ms), f32o(mh), bfp(y0), f32(mean0),
-                       f32(rstd0), bfo(y1), f32o(mean1), f32o(rstd1), M, (int)C, (int)blocks, (int)rpb, f32(part),
+  TORCH_CHECK(!y0.has_value() || (mean0.has_value() && rstd0.has_value()), "y0 needs mean0/rstd0");
+  TORCH_CHECK(mask_mode != 2 || y0.has_value(), "mask mode 2 reads y0");
+  bn_bwd_reduce_launch(bfp(g), (int)ldg, (int)mask_mode, mask_ptr(mask_mode, mo), (int)ldm, f32o(ms), f32o(mh), bfo(y0), f32o(mean0),
+                       f32o(rstd0), bfo(y1), f32o(mean1), f32o(rstd1), M, (int)C, (int)blocks, (int)rpb, f32(part),
                        cur_stream());
 }
 
@@ -287,12 +357,15 @@ void bn_bwd_finalize(const at::Tensor& part, int64_t blocks, int64_t C, int64_t 
                          f32o(dgamma), f32o(dbeta), (float)beta_acc, f32(coef), cur_stream());
 }
 
+// y0/coef0/dy0 optional (all or none): without them only dy1 and/or dz (dzout) are produced
 void bn_bwd_apply(const at::Tensor& g, int64_t ldg, int64_t mask_mode, const OptT& mo, int64_t ldm, const OptT& ms,
-                  const OptT& mh, const at::Tensor& y0, const at::Tensor& coef0, const at::Tensor& dy0,
+                  const OptT& mh, const OptT& y0, const OptT& coef0, const OptT& dy0,
                   const OptT& y1, const OptT& coef1, const OptT& dy1, const OptT& dzout, int64_t lddz,
                   int64_t dz_accum, int64_t M, int64_t C) {
-  bn_bwd_apply_launch(bfp(g), (int)ldg, (int)mask_mode, mask_ptr(mask_mode, mo), (int)ldm, f32o(ms), f32o(mh), bfp(y0), f32(coef0),
-                      bfpm(dy0), bfo(y1), f32o(coef1), bfom(dy1), bfom(dzout), (int)lddz, (int)dz_accum, M, (int)C,
+  TORCH_CHECK(y0.has_value() == coef0.has_value() && y0.has_value() == dy0.has_value(), "y0/coef0/dy0 go together");
+  TORCH_CHECK(mask_mode != 2 || y0.has_value(), "mask mode 2 reads y0");
+  bn_bwd_apply_launch(bfp(g), (int)ldg, (int)mask_mode, mask_ptr(mask_mode, mo), (int)ldm, f32o(ms), f32o(mh), bfo(y0), f32o(coef0),
+                      bfom(dy0), bfo(y1), f32o(coef1), bfom(dy1), bfom(dzout), (int)lddz, (int)dz_accum, M, (int)C,
                       cur_stream());
 }
 
@@ -419,6 +492,34 @@ void head_backward(const at::Tensor& dlogits, const at::Tensor& xm, const at::Te
                        cur_stream());
 }
 
+// ---- BatchNorm folding of conv_c (csrc/kernels/bn_fold.hip) ----
+void bnfold_fwd_stats(const at::Tensor& Wf, const at::Tensor& Ga, const at::Tensor& sslab, int64_t splits, int64_t C,
+                      int64_t c, int64_t count, const at::Tensor& T, const at::Tensor& s_out, const at::Tensor& gamma,
+                      const at::Tensor& beta, const OptT& rm, const OptT& rv, const OptT& nbt, double momentum,
+                      double eps, const at::Tensor& smean, const at::Tensor& srstd, const at::Tensor& scale,
+                      const at::Tensor& shift) {
+  TORCH_CHECK(c % 8 == 0 && c <= 2048 && Wf.numel() >= C * c && Ga.numel() >= c * c && T.numel() >= C * c,
+              "bnfold_fwd_stats shapes");
+  TORCH_CHECK(sslab.numel() >= splits * c && s_out.numel() >= c, "bnfold colsum shapes");
+  int64_t* nb = nbt.has_value() ? nbt->data_ptr<int64_t>() : nullptr;
+  bnfold_fwd_stats_launch(bfp(Wf), f32(Ga), f32(sslab), (int)splits, (int)C, (int)c, count, f32(T), f32(s_out),
+                          f32(gamma), f32(beta), f32o(rm), f32o(rv), nb, (float)momentum, (float)eps, f32(smean),
+                          f32(srstd), f32(scale), f32(shift), cur_stream());
+}
+
+void bnfold_bwd(const at::Tensor& part, int64_t tiles, const at::Tensor& Wf, const at::Tensor& Wd, const at::Tensor& G,
+                const at::Tensor& T, const at::Tensor& s, int64_t C, int64_t c, int64_t count, const at::Tensor& gamma,
+                const at::Tensor& mean, const at::Tensor& rstd, const OptT& dgamma, const OptT& dbeta,
+                const at::Tensor& dW, double beta_acc, const at::Tensor& coef, const at::Tensor& W1t,
+                const at::Tensor& W2, const at::Tensor& bias) {
+  TORCH_CHECK(c % 8 == 0 && Wf.numel() >= C * c && Wd.numel() >= C * c && G.numel() >= C * c && T.numel() >= C * c &&
+              dW.numel() == C * c && coef.numel() >= 4 * C && W1t.numel() >= C * c && W2.numel() >= c * c &&
+              bias.numel() >= 2 * c && part.numel() >= tiles * 3 * C, "bnfold_bwd shapes");
+  bnfold_bwd_launch(f32(part), (int)tiles, bfp(Wf), bfp(Wd), f32(G), f32(T), f32(s), (int)C, (int)c, count,
+                    f32(gamma), f32(mean), f32(rstd), f32o(dgamma), f32o(dbeta), f32(dW), (float)beta_acc, f32(coef),
+                    bfpm(W1t), bfpm(W2), f32(bias), cur_stream());
+}
+
 void head_dropout_mask(const at::Tensor& out, double p_drop, int64_t seed) {
   TORCH_CHECK(out.scalar_type() == at::kByte, "mask must be uint8");
   head_dropout_mask_launch(out.numel(), (float)p_drop, (uint64_t)seed, out.data_ptr<uint8_t>(), cur_stream());
@@ -433,7 +534,11 @@ void synth_frames(const at::Tensor& out, int64_t seed) {
 PYBIND11_MODULE(_C, m) {
   m.doc() = "gfx950 HIP kernels for pytorchvideo_accelerate_amd";
   m.def("conv_igemm", &conv_igemm, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("stats"), py::arg("scale"),
-        py::arg("shift"), py::arg("affine"), py::arg("accum"), py::arg("g"), py::arg("chunk"), py::arg("cfg") = -1);
+        py::arg("shift"), py::arg("affine"), py::arg("accum"), py::arg("g"), py::arg("chunk"), py::arg("cfg") = -1,
+        py::arg("bias") = py::none());
+  m.def("conv_igemm_fres", &conv_igemm_fres);
+  m.def("bnfold_fwd_stats", &bnfold_fwd_stats);
+  m.def("bnfold_bwd", &bnfold_bwd);
   // launch-config helpers for the autotuner
   m.def("conv_cfg_bm", [](int64_t cfg, int64_t N) { return (int64_t)conv_cfg_bm((int)cfg, (int)N); });
   m.def("conv_ut_legal", [](std::vector<int64_t> g, int64_t chunk, int64_t bk) {
@@ -441,6 +546,19 @@ PYBIND11_MODULE(_C, m) {
     int* f = &q.M;
     for (int i = 0; i < 39 && i < (int)g.size(); ++i) f[i] = (int)g[i];
     return (int64_t)conv_igemm_ut_legal(q, (int)chunk, (int)bk);
+  });
+  m.def("conv_pw_legal", [](std::vector<int64_t> g, int64_t chunk) {
+    ConvParams q{};
+    int* f = &q.M;
+    for (int i = 0; i < 39 && i < (int)g.size(); ++i) f[i] = (int)g[i];
+    auto dim_ok = [](int R, int as, int ao, int dir, int n, int G) {
+      const int lo = ao + (dir < 0 ? -(n - 1) : 0);
+      const int hi = (R - 1) * as + ao + (dir > 0 ? (n - 1) : 0);
+      return n == 0 || (lo >= 0 && hi < G);
+    };
+    q.check = (dim_ok(q.Rt, q.ast, q.aot, q.dir, q.nt, q.Gt) && dim_ok(q.Rh, q.ash, q.aoh, q.dir, q.nh, q.Gh) &&
+               dim_ok(q.Rw, q.asw, q.aow, q.dir, q.nw, q.Gw)) ? 0 : 1;
+    return (int64_t)conv_pw_legal(q, (int)chunk);
   });
   m.def("conv_direct_legal", [](std::vector<int64_t> g, int64_t chunk) {
     ConvParams q{};
@@ -451,14 +569,17 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_igemm_epi", &conv_igemm_epi, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("accum"), py::arg("g"),
         py::arg("chunk"), py::arg("res"), py::arg("ldr"), py::arg("mask"), py::arg("y0"), py::arg("mean0"),
         py::arg("rstd0"), py::arg("y1"), py::arg("mean1"), py::arg("rstd1"), py::arg("part"),
-        py::arg("msc") = py::none(), py::arg("msh") = py::none(), py::arg("cfg") = -1);
+        py::arg("msc") = py::none(), py::arg("msh") = py::none(), py::arg("cfg") = -1, py::arg("bias") = py::none());
   m.def("conv_m_tiles", &conv_m_tiles, py::arg("M"), py::arg("N"), py::arg("K") = 0, py::arg("Cg") = 0);
   m.def("conv_set_bk", [](int64_t bk) { conv_igemm_set_bk((int)bk); });
   m.def("conv_set_ut", [](int64_t mode) { conv_igemm_set_ut((int)mode); });
   m.def("wgrad_tile", &wgrad_tile, py::arg("Cout"), py::arg("K"), py::arg("variant") = -1);
+  m.def("wgrad_narrow_legal", [](int64_t Cout, int64_t Cin, int64_t K) {
+    return (bool)wgrad_narrow_legal((int)Cout, (int)Cin, (int)K);
+  });
   m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("partial"), py::arg("scale"),
         py::arg("shift"), py::arg("affine"), py::arg("g"), py::arg("chunk"), py::arg("slab") = 0,
-        py::arg("variant") = -1);
+        py::arg("variant") = -1, py::arg("dy_affine") = 0, py::arg("colsum") = py::none());
   m.def("wgrad_reduce", &wgrad_reduce, py::arg("partial"), py::arg("grad"), py::arg("splits"), py::arg("Cout"),
         py::arg("taps"), py::arg("Cin"), py::arg("Cin_real"), py::arg("scale"), py::arg("beta"), py::arg("slab") = 0);
   m.def("bn_finalize", &bn_finalize);

@@ -112,7 +112,7 @@ class _ConvBN:
         self.rstd = torch.ones(C, device=dev)
         self.scale = torch.ones(C, device=dev)
         self.shift = torch.zeros(C, device=dev)
-        self.coef = torch.zeros(3 * C, device=dev)
+        self.coef = torch.zeros(4 * C, device=dev)   # BN-backward coefficients (+ mean(dz) for BN folding)
         self._geo = {}
         self.wf = None  # bf16 forward pack view [Cout, taps*Cin_pad]
         self.wd = None  # bf16 dgrad pack view [Cin, taps*Cout]
@@ -159,22 +159,34 @@ class _ConvBN:
         return Act(y, x.N, To, Ho, Wo)
 
     # ---- backward pieces ----
-    def wgrad(self, dy: Act, x: Act, xf: Optional[_Xf]):
-        eng, s, C = self.eng, self.spec, self.eng.C
-        eng.mark(self.name + ".wgrad")
+    def wgrad(self, dy: Act, x: Act, xf: Optional[_Xf], spec: Optional[ConvSpec] = None,
+              dest: Optional[torch.Tensor] = None, beta: Optional[float] = None, gram: bool = False,
+              colsum: Optional[torch.Tensor] = None):
+        """Weight gradient dy^T im2col(x) (x through ``xf`` when given) into ``dest`` (default: this conv's
+        slot of the flat gradient, accumulated with the executor's ``grad_beta``).  ``gram``: Gram mode of the
+        BN folding — dy is x itself, both through ``xf`` (``spec`` = the c->c 1x1 shape), per-split column
+        sums into ``colsum`` [splits][c]; returns the number of splits."""
+        eng, C = self.eng, self.eng.C
+        s = spec or self.spec
+        eng.mark(self.name + (".gram" if gram else ".wgrad"))
         K = s.taps * s.cin_pad
         from ..ops.conv import wgrad_splits
         aff = 0 if xf is None else (2 if xf.relu else 1)
         sc_, sh_ = (None, None) if xf is None else (xf.scale, xf.shift)
         slab = 1 if eng.deterministic else 0
+        dya = 1 if gram else 0
 
         def geometry(cfg):
             """(splits, rows per split, kernel variant word) of launch configuration ``cfg``."""
-            key = (self.name, "wsplit", dy.M, cfg)
+            key = (self.name, "wsplit", dy.M, cfg, gram)
             sp = eng._splits.get(key)
             if sp is None:
                 if cfg < 0:
                     sp = wgrad_splits(dy.M, s.cout, K, target_blocks=256 if slab else 1024) + (-1,)
+                elif cfg & 128:   # narrow per-wave kernel: bits 2-3 = wave count target, 64 rows per chunk
+                    nw = (1024, 2048, 4096)[(cfg >> 2) & 3]
+                    pps = ((dy.M + nw - 1) // nw + 63) // 64 * 64
+                    sp = ((dy.M + pps - 1) // pps, pps, 16)
                 else:   # bits 0-1 (+ bit 6: tiles 4-7) tile variant, 2-3 split-K target, 5: 64-position stages
                     v = (cfg & 3) | (8 if cfg & 64 else 0)
                     tb = (512, 1024, 2048)[(cfg >> 2) & 3]
@@ -182,14 +194,15 @@ class _ConvBN:
                 eng._splits[key] = sp
             return sp
 
-        def launch(cfg, part):
+        def launch(cfg, part, cs=None):
             splits, pps, v = geometry(cfg)
             g = [dy.M, s.cout, K, s.cin_pad, dy.ld, x.ld, x.T, x.H, x.W, dy.T, dy.H, dy.W,
                  *s.k, *s.stride, *s.pad, splits, pps]
-            C.conv_wgrad(dy.t, x.t, part, sc_, sh_, aff, g, s.chunk, slab, v)
+            C.conv_wgrad(dy.t, x.t, part, sc_, sh_, aff, g, s.chunk, slab, v, dya,
+                         None if cs is None else cs[:splits * s.cout])
             return splits
 
-        tkey = ("w", dy.M, dy.ld, x.ld, x.T, x.H, x.W, s.cout, K, s.chunk, aff) + tuple(s.k) + tuple(s.stride)
+        tkey = ("w", dy.M, dy.ld, x.ld, x.T, x.H, x.W, s.cout, K, s.chunk, aff, gram) + tuple(s.k) + tuple(s.stride)
         cfg = eng.wtune.get(tkey)
         if cfg is None:
             cfg = -1
@@ -197,6 +210,7 @@ class _ConvBN:
                 # first use: time tile variant x split-K target on a scratch accumulator (atomic adds; the
                 # scratch content is irrelevant), keep the fastest
                 scratch = eng.scratch("wgrad_tune", s.cout * K)
+                cs_scr = eng.scratch("wgrad_tune_cs", 4096 * s.cout) if gram else None
                 cands, times = [], []
                 for v in range(8):
                     vw = (v & 3) | (8 if v >= 4 else 0)
@@ -205,21 +219,26 @@ class _ConvBN:
                         continue
                     for tbi, bp in ((t, b) for t in range(3) for b in (0, 32)):
                         c = 16 | (v & 3) | (64 if v >= 4 else 0) | (tbi << 2) | bp
-                        launch(c, scratch)
-                        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                        e0.record()
-                        for _ in range(3):
-                            launch(c, scratch)
-                        e1.record()
-                        e1.synchronize()
+                        if gram and geometry(c)[0] > 4096:
+                            continue
                         cands.append(c)
-                        times.append(e0.elapsed_time(e1))
+                if C.wgrad_narrow_legal(s.cout, s.cin_pad, K) and s.chunk == 8:
+                    cands += [16 | 128 | (tbi << 2) for tbi in range(3)]
+                for c in cands:
+                    launch(c, scratch, cs_scr)
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    for _ in range(3):
+                        launch(c, scratch, cs_scr)
+                    e1.record()
+                    e1.synchronize()
+                    times.append(e0.elapsed_time(e1))
                 if eng.tuner.agree is not None:   # same choice on every data-parallel rank
                     times = eng.tuner.agree(times)
                 cfg = cands[min(range(len(cands)), key=times.__getitem__)] if cands else -1
                 if eng.tuner.log:
                     import sys
-                    print("wtune %s P=%d Cout=%d K=%d: " % (self.name, dy.M, s.cout, K)
+                    print("wtune %s%s P=%d Cout=%d K=%d: " % (self.name, ".gram" if gram else "", dy.M, s.cout, K)
                           + " ".join("%d=%.1fus" % (c, 1e3 * t / 3) for c, t in zip(cands, times))
                           + " -> %d" % cfg, file=sys.stderr, flush=True)
             eng.wtune[tkey] = cfg
@@ -227,12 +246,92 @@ class _ConvBN:
             part = eng.scratch("wgrad_slab", geometry(cfg)[0] * s.cout * K)
         else:     # fp32 atomics into one zeroed accumulator (kept zero by wgrad_reduce)
             part = eng.scratch("wgrad_acc", s.cout * K, zero=True)
-        splits = launch(cfg, part)
-        C.wgrad_reduce(part, eng.flat.gview(self.conv.weight), splits, s.cout, s.taps, s.cin_pad, s.cin, 1.0,
-                       eng.grad_beta, slab)
+        if gram:
+            assert colsum is not None and colsum.numel() >= geometry(cfg)[0] * s.cout, "colsum slab too small"
+        splits = launch(cfg, part, colsum)
+        C.wgrad_reduce(part, eng.flat.gview(self.conv.weight) if dest is None else dest, splits, s.cout, s.taps,
+                       s.cin_pad, s.cin, 1.0, eng.grad_beta if beta is None else beta, slab)
+        return splits
+
+    # ---- BatchNorm folding of a 1x1 conv_c (csrc/kernels/bn_fold.hip) ----
+    def fold_forward(self, yb: Act, bxf: _Xf, train: bool):
+        """BN statistics of this conv's output computed from the Gram matrix of its input act_b(yb) — the raw
+        output is never materialised.  Keeps T = Wc Ga and the column sums for the backward."""
+        eng, C, s = self.eng, self.eng.C, self.spec
+        bn = self.bn
+        if not train:
+            C.bn_eval_affine(bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, self.scale, self.shift)
+            return
+        c, Co = s.cin, s.cout
+        if not hasattr(self, "gspec"):
+            self.gspec = ConvSpec(c, c, (1, 1, 1), (1, 1, 1), (0, 0, 0))
+        Ga = eng.scratch("fold_gram", c * c)
+        slab = eng.scratch("fold_colsum", 4096 * c)
+        splits = self.wgrad(yb, yb, bxf, spec=self.gspec, dest=Ga, beta=0.0, gram=True, colsum=slab)
+        self.T = eng.ws((self.name, "foldT"), (Co, c), torch.float32)
+        self.s = eng.ws((self.name, "folds"), (c,), torch.float32)
+        eng.mark(self.name + ".foldstats")
+        C.bnfold_fwd_stats(self.wf, Ga, slab, splits, Co, c, yb.M, self.T, self.s, bn.weight, bn.bias,
+                           bn.running_mean, bn.running_var, bn.num_batches_tracked,
+                           bn.momentum if bn.momentum is not None else 0.1, bn.eps, self.mean, self.rstd,
+                           self.scale, self.shift)
+
+    def fold_output(self, yb: Act, bxf: _Xf, out: torch.Tensor, res: Act, rxf: Optional[_Xf],
+                    mask: torch.Tensor, tag: str) -> Act:
+        """out = relu(BN(conv(act_b(yb))) + r), r = res (identity) or BN_1(res) (``rxf``); ReLU bits -> mask."""
+        eng, C, s = self.eng, self.eng.C, self.spec
+        eng.mark(self.name + ".fwdres")
+        key = ("fg", yb.N, yb.T, yb.H, yb.W, yb.ld)
+        g = self._geo.get(key)
+        if g is None:
+            g = self._geo[key] = fwd_geometry(s, yb.N, yb.T, yb.H, yb.W, yb.ld, out.stride(0))
+        g = list(g)
+        g[5] = out.stride(0)
+        tuner = eng.tuner
+
+        def run(cfg, scratch):
+            C.conv_igemm_fres(yb.t, self.wf, tuner.scratch_like(out) if scratch else out, bxf.scale, bxf.shift,
+                              2 if bxf.relu else 1, g, s.chunk, cfg, self.scale, self.shift, res.t, res.ld,
+                              None if rxf is None else rxf.scale, None if rxf is None else rxf.shift,
+                              tuner.scratch_like(mask) if scratch else mask)
+        tuner.launch(("fres", rxf is not None) + tuple(g), g, s.chunk, run, aff=2, epi=False, direct=False)
+        return Act(out, yb.N, yb.T, yb.H, yb.W)
+
+    def fold_backward(self, dz: Act, part, tiles: int, yb: Act, b: "_ConvBN", dab: torch.Tensor):
+        """BN_c + conv_c backward from dz without yc: G = dz^T act_b(yb) (wgrad kernel), coefficients, dWc,
+        dgamma/dbeta (bnfold_bwd), then d act_b = act_b(yb) W2 + bias (1x1 conv) followed by the dgrad of dz with
+        W1 = diag(A) Wc accumulated on top, whose epilogue applies b's ReLU mask and reduces b's BN-backward
+        sums.  Returns (partials, tiles) for ``b.bn_backward(pre=...)``."""
+        eng, C, s = self.eng, self.eng.C, self.spec
+        c, Co = s.cin, s.cout
+        bxf = b.xf()
+        G = eng.scratch("fold_G", Co * c)
+        self.wgrad(dz, yb, bxf, dest=G, beta=0.0)
+        if getattr(self, "W1t", None) is None:
+            self.W1t = torch.empty(c, Co, device=eng.device, dtype=torch.bfloat16)
+            self.W2 = torch.empty(c, c, device=eng.device, dtype=torch.bfloat16)
+            self.fbias = torch.empty(2 * c, device=eng.device, dtype=torch.float32)   # [biasA | biasB]
+        fg = eng.flat
+        eng.mark(self.name + ".foldbwd")
+        C.bnfold_bwd(part, tiles, self.wf, self.wd, G, self.T, self.s, Co, c, dz.M, self.bn.weight, self.mean,
+                     self.rstd, fg.gview(self.bn.weight), fg.gview(self.bn.bias), fg.gview(self.conv.weight),
+                     eng.grad_beta, self.coef, self.W1t, self.W2, self.fbias)
+        # (act_b(yb) - abar) W2 + c0 : a c->c 1x1 conv with the consumer-side BN_b fold and a bias epilogue
+        if not hasattr(self, "gspec"):
+            self.gspec = ConvSpec(c, c, (1, 1, 1), (1, 1, 1), (0, 0, 0))
+        eng.mark(self.name + ".foldw2")
+        g2 = fwd_geometry(self.gspec, yb.N, yb.T, yb.H, yb.W, yb.ld, c)
+        tuner = eng.tuner
+
+        def run(cfg, scratch):
+            C.conv_igemm(yb.t, self.W2, tuner.scratch_like(dab) if scratch else dab, None, bxf.scale, bxf.shift,
+                         2 if bxf.relu else 1, 0, g2, 8, cfg, self.fbias[c:])
+        tuner.launch(("fw2",) + tuple(g2), g2, 8, run, aff=2, direct=False)
+        return self.dgrad(dz, (yb.T, yb.H, yb.W), dab, True, bn=(b, yb), wd=self.W1t, bias=self.fbias[:c])
 
     def dgrad(self, dy: Act, in_dims, out: torch.Tensor, accum: bool, res: Optional[Act] = None,
-              epi: Optional["_ResBlock"] = None, bn: Optional[Tuple["_ConvBN", Act]] = None):
+              epi: Optional["_ResBlock"] = None, bn: Optional[Tuple["_ConvBN", Act]] = None,
+              wd: Optional[torch.Tensor] = None, bias: Optional[torch.Tensor] = None):
         """grad wrt the conv input into ``out`` (``accum``: added).  With ``res`` / ``epi`` the single-phase
         launch also adds the residual gradient ``res``, applies the ReLU mask of residual unit ``epi``'s
         output and emits the partial sums of ``epi``'s conv_c (+branch1) BN backward; returns
@@ -241,22 +340,25 @@ class _ConvBN:
         returns (partials, tiles) for ``unit.bn_backward(pre=...)``, or None when not fusable."""
         s, C = self.spec, self.eng.C
         self.eng.mark(self.name + ".dgrad")
+        wd = self.wd if wd is None else wd   # (BN folding passes diag(A)-scaled weights)
         Ti, Hi, Wi = in_dims
         key = ("dg", dy.N, tuple(in_dims), dy.ld, out.stride(0))
         geo = self._geo.get(key)
         if geo is None:
             geo = self._geo[key] = dgrad_phases(s, dy.N, tuple(in_dims), (dy.T, dy.H, dy.W), dy.ld, out.stride(0))
         tuner = self.eng.tuner
-        if bn is not None and res is None and epi is None and len(geo) == 1 and not accum:
+        if bn is not None and res is None and epi is None and len(geo) == 1:
             u, y = bn
             g = geo[0]
             part = self.eng.scratch("bnepi", ((g[0] + 127) // 128) * 3 * g[1])
+            # accum: the scratch launches of the autotuner add onto garbage — harmless, outputs are discarded
 
             def run(cfg, scratch):
-                C.conv_igemm_epi(dy.t, self.wd, tuner.scratch_like(out) if scratch else out, 0, g, 8, None, 0, None,
-                                 y.t, u.mean, u.rstd, None, None, None,
-                                 tuner.scratch_like(part) if scratch else part, u.scale, u.shift, cfg)
-            cfg = tuner.launch(("eb",) + tuple(g), g, 8, run, epi=True)
+                C.conv_igemm_epi(dy.t, wd, tuner.scratch_like(out) if scratch else out, 1 if accum else 0, g, 8, None,
+                                 0, None, y.t, u.mean, u.rstd, None, None, None,
+                                 tuner.scratch_like(part) if scratch else part, u.scale, u.shift, cfg, bias)
+            cfg = tuner.launch(("eb", accum, bias is not None) + tuple(g), g, 8, run, epi=True,
+                               direct=bias is None)
             bm = tuner.bm(cfg, g[1])
             return part, (g[0] + bm - 1) // bm
         if res is not None or epi is not None:
@@ -267,11 +369,13 @@ class _ConvBN:
                 part = self.eng.scratch("bnepi", ((g[0] + 127) // 128) * 3 * g[1])
                 c, one = epi.c, epi.one
 
+            yc = None if (epi is None or epi.yc is None) else epi.yc   # folded conv_c: no raw output
+
             def run(cfg, scratch):
-                C.conv_igemm_epi(dy.t, self.wd, tuner.scratch_like(out) if scratch else out, 1 if accum else 0, g, 8,
+                C.conv_igemm_epi(dy.t, wd, tuner.scratch_like(out) if scratch else out, 1 if accum else 0, g, 8,
                                  None if res is None else res.t, 0 if res is None else res.ld,
-                                 None if epi is None else epi.mask, None if epi is None else epi.yc.t,
-                                 None if epi is None else c.mean, None if epi is None else c.rstd,
+                                 None if epi is None else epi.mask, None if yc is None else yc.t,
+                                 None if yc is None else c.mean, None if yc is None else c.rstd,
                                  None if epi is None or one is None else epi.y1.t,
                                  None if epi is None or one is None else one.mean,
                                  None if epi is None or one is None else one.rstd,
@@ -288,7 +392,7 @@ class _ConvBN:
                 continue
 
             def run(cfg, scratch, g=g):
-                C.conv_igemm(dy.t, self.wd, tuner.scratch_like(out) if scratch else out, None, None, None, 0,
+                C.conv_igemm(dy.t, wd, tuner.scratch_like(out) if scratch else out, None, None, None, 0,
                              1 if accum else 0, g, 8, cfg)
             tuner.launch(("d", accum) + tuple(g), g, 8, run)
         return None
@@ -433,6 +537,10 @@ class _ResBlock:
         self.c = _ConvBN(eng, b2.conv_c, b2.norm_c, name + ".c")
         self.one = _ConvBN(eng, blk.branch1_conv, blk.branch1_norm, name + ".1") if blk.branch1_conv is not None else None
         self.units = [u for u in (self.a, self.b, self.c, self.one) if u is not None]
+        sc = self.c.spec
+        # BN folding of the 1x1 conv_c: its raw output (the widest tensor of the unit) is never written
+        self.fold = (eng.bn_fold and tuple(sc.k) == (1, 1, 1) and tuple(sc.stride) == (1, 1, 1) and sc.cin % 8 == 0
+                     and sc.cout % 8 == 0 and sc.cin >= eng.fold_min_c)
 
     def out_channels(self):
         return self.c.C
@@ -444,6 +552,17 @@ class _ResBlock:
         C = self.eng.C
         ya = self.a.fwd(x, None, train, tag)
         yb = self.b.fwd(ya, self.a.xf(), train, tag)
+        if self.fold:
+            # conv_c statistics from the Gram matrix of act_b(yb), then ONE launch writes the unit output
+            # relu(BN_c(conv_c) + shortcut) and its ReLU bits (no yc, no res_out pass)
+            y1 = self.one.fwd(x, None, train, tag) if self.one is not None else None
+            self.c.fold_forward(yb, self.b.xf(), train)
+            mask = self.eng.ws((self.name, "mask", tag), (yb.M, self.c.C // 8), torch.uint8)
+            res, rxf = (x, None) if y1 is None else (y1, self.one.xf(relu=False))
+            o = self.c.fold_output(yb, self.b.xf(), out, res, rxf, mask, tag)
+            self.mask = mask if train else None
+            self.x, self.ya, self.yb, self.yc, self.y1, self.out = x, ya, yb, None, y1, o
+            return o
         yc = self.c.fwd(yb, self.b.xf(), train, tag)
         y1 = self.one.fwd(x, None, train, tag) if self.one is not None else None
         M = yc.M
@@ -469,6 +588,8 @@ class _ResBlock:
         x, ya, yb, yc, y1 = self.x, self.ya, self.yb, self.yc, self.y1
         dxa = Act(dx, x.N, x.T, x.H, x.W)
         res = None
+        if self.fold:
+            return self._bwd_fold(dout, dx, dx_accum, pre, prev)
         if pre is not None:
             dyc, dy1 = self.c.bn_backward(dout, yc, 0, None, None, other=self.one, other_y=y1, pre=pre)
             if self.one is None:
@@ -493,6 +614,73 @@ class _ResBlock:
         if self.one is not None:
             self.one.wgrad(dy1, x, None)
             self.one.dgrad(dy1, (x.T, x.H, x.W), dx, dx_accum)
+            acc = True
+        else:
+            acc = dx_accum if pre is not None else True
+        if prev is not None and not self._epi_ok(prev):
+            prev = None
+        if res is None and prev is None:
+            self.a.dgrad(dya, (x.T, x.H, x.W), dx, acc)
+            return None
+        return self.a.dgrad(dya, (x.T, x.H, x.W), dx, acc, res=res, epi=prev)
+
+    def _bwd_fold(self, dout: Act, dx: torch.Tensor, dx_accum: bool, pre, prev: Optional["_ResBlock"]):
+        """Backward of a unit whose conv_c BN is folded (see ``_ConvBN.fold_backward``)."""
+        eng, C = self.eng, self.eng.C
+        x, ya, yb, y1, one = self.x, self.ya, self.yb, self.y1, self.one
+        dxa = Act(dx, x.N, x.T, x.H, x.W)
+        M, Cc = yb.M, self.c.C
+        fg = eng.flat
+        res = None
+        dy1 = eng.ws((one.name, "dy"), (M, Cc), torch.bfloat16) if one is not None else None
+        if pre is not None:
+            # dout is already the masked dz; its partial sums came from the next unit's dgrad epilogue
+            part, tiles = pre
+            dz = dout
+            if one is None:
+                res = dout          # identity shortcut: added by conv_a's dgrad below
+        else:
+            # dz = dout * ReLU bits, with sum(dz) (+ the branch1 BN's sum(dz xhat1)) reduced in one pass
+            blocks, rpb = eng._bn_blocks(M, Cc)
+            eng.mark(self.c.name + ".bnred")
+            part = eng.scratch("bnpart", blocks * 3 * Cc)
+            C.bn_bwd_reduce(dout.t, dout.ld, 3, self.mask, Cc // 8, None, None, None, None, None,
+                            None if one is None else y1.t, None if one is None else one.mean,
+                            None if one is None else one.rstd, M, Cc, blocks, rpb, part)
+            tiles = blocks
+            if one is None:
+                assert not dx_accum, "identity unit with an accumulating input gradient"
+                dz = dxa            # dz lands in dx; conv_a's dgrad accumulates on top of it
+            else:
+                dz = Act(eng.ws((self.name, "dz"), (M, Cc), torch.bfloat16), x.N, yb.T, yb.H, yb.W)
+        if one is not None:
+            # branch1 BN backward from the same sums: dy1 = A1 dz + B1 y1 + C1 (and dz itself when not yet stored)
+            C.bn_bwd_finalize(part, tiles, Cc, M, 1, one.bn.weight, one.mean, one.rstd, fg.gview(one.bn.weight),
+                              fg.gview(one.bn.bias), eng.grad_beta, one.coef)
+            eng.mark(one.name + ".bnapply")
+            if pre is not None:
+                C.bn_bwd_apply(dz.t, dz.ld, 0, None, 0, None, None, None, None, None, y1.t, one.coef, dy1, None, 0,
+                               0, M, Cc)
+            else:
+                C.bn_bwd_apply(dout.t, dout.ld, 3, self.mask, Cc // 8, None, None, None, None, None, y1.t, one.coef,
+                               dy1, dz.t, dz.ld, 0, M, Cc)
+        elif pre is None:
+            eng.mark(self.c.name + ".dz")
+            C.bn_bwd_apply(dout.t, dout.ld, 3, self.mask, Cc // 8, None, None, None, None, None, None, None, None,
+                           dxa.t, dxa.ld, 0, M, Cc)
+        dab = eng.ws((self.name, "dab"), (yb.M, self.b.C), torch.bfloat16)
+        pb = self.c.fold_backward(dz, part, tiles, yb, self.b, dab)
+        dyb, _ = self.b.bn_backward(Act(dab, yb.N, yb.T, yb.H, yb.W), yb, 0, None, None, pre=pb)
+        self.b.wgrad(dyb, ya, self.a.xf())
+        daa = eng.ws((self.name, "daa"), (ya.M, self.a.C), torch.bfloat16)
+        pa = self.b.dgrad(dyb, (ya.T, ya.H, ya.W), daa, False, bn=(self.a, ya))
+        dya, _ = self.a.bn_backward(Act(daa, ya.N, ya.T, ya.H, ya.W), ya, 0 if pa else 2, None,
+                                    None if pa else self.a.xf(), pre=pa)
+        self.a.wgrad(dya, x, None)
+        if one is not None:
+            d1 = Act(dy1, x.N, yb.T, yb.H, yb.W)
+            one.wgrad(d1, x, None)
+            one.dgrad(d1, (x.T, x.H, x.W), dx, dx_accum)
             acc = True
         else:
             acc = dx_accum if pre is not None else True
@@ -593,6 +781,11 @@ class FusedNet:
         self._bnb: Dict = {}
         self._scratch: Dict[str, torch.Tensor] = {}
         self.grad_beta = 0.0
+        import os
+        # BN folding of the 1x1 conv_c (never materialise its output); units whose conv_c input has at least
+        # fold_min_c channels (default: the slow pathway, where the Gram matrices run at MFMA speed)
+        self.bn_fold = os.environ.get("PVA_BN_FOLD", "1") != "0"
+        self.fold_min_c = int(os.environ.get("PVA_BN_FOLD_MIN_C", "64"))
         blocks = list(model.blocks)
         self.slowfast = isinstance(blocks[0], R.MultiPathWayWithFuse)
         self.stages: List[Tuple[List, Optional[_Fuse]]] = []

@@ -211,6 +211,11 @@ def conv_wgrad(dy: Act, x: Act, spec: ConvSpec, grad: torch.Tensor, workspace: O
     C = require()
     P = dy.M
     K = spec.taps * spec.cin_pad
+    if splits_pps is None and variant >= 0 and variant & 16:   # narrow per-wave kernel (Cout <= 32, K <= 128)
+        nw = 2048
+        pps = ((P + nw - 1) // nw + 63) // 64 * 64
+        splits_pps = ((P + pps - 1) // pps, pps)
+        variant = 16
     splits, pps = splits_pps or wgrad_splits(P, spec.cout, K, variant=(variant & 11) if variant >= 0 else -1)
     need = spec.cout * K
     if workspace is None or workspace.numel() < need:

@@ -3,7 +3,8 @@
 The gfx950 conv kernel (csrc/kernels/conv_igemm.hip) has several launch configurations per conv: output
 tile (128x128, 128x64, 256x32, 256x16), K depth per LDS stage (BK 32 / 64) and the uniform-tap loader
 on or off; convs with <= 64 output channels can also run the direct-to-register kernel
-(csrc/kernels/conv_direct.hip, 512 or 2048 rows per workgroup; ``PVA_CONV_DIRECT=0`` excludes it).  Which one wins depends on the layer (measured: the uniform-tap loader is 20-25 % faster on
+(csrc/kernels/conv_direct.hip, 512 or 2048 rows per workgroup; ``PVA_CONV_DIRECT=0`` excludes it), and dense
+1x1x1 convs the streaming pointwise kernel (csrc/kernels/conv_pw.hip; ``PVA_CONV_PW=0`` excludes it).  Which one wins depends on the layer (measured: the uniform-tap loader is 20-25 % faster on
 3x3 convs with the consumer-side BN fold and 15-30 % slower on padded temporal convs; BK=64 wins only for
 deep K).  The first time a geometry is launched, :class:`ConvTuner` times every legal configuration on
 scratch outputs (same shapes and strides, so inputs and real outputs are untouched — including
@@ -27,6 +28,8 @@ DIRECT = 32           # narrow direct-to-register kernel (csrc/kernels/conv_dire
 DIRECT_2K = 64        #   with 2048 rows per workgroup (else 512)
 DMA = 128             # uniform-tap loader staged by LDS-DMA (buffer_load ... lds); launches without input affine
 BIG = 256             # 256x256 tile of 8 waves (N >= 256; forward / plain dgrad, no backward-BN epilogue)
+PW = 512              # streaming pointwise kernel (csrc/kernels/conv_pw.hip): dense 1x1x1 GEMMs, K <= 256,
+PW_ROWS = (1024, 2048, 4096)   # N % 32 == 0, weights in LDS; bits 0-1 select the rows per workgroup
 TILE_BN = (128, 64, 32, 16)   # variants 0..3
 TILE_BM = (128, 128, 256, 256)
 
@@ -35,6 +38,8 @@ def describe(cfg: int) -> str:
     """Human-readable configuration word (``PVA_TUNE_LOG=1`` prints every candidate's time)."""
     if cfg < 0 or not cfg & EXPLICIT:
         return "heuristic"
+    if cfg & PW:
+        return "pw%d" % PW_ROWS[cfg & 3]
     if cfg & DIRECT:
         return "direct%d" % (2048 if cfg & DIRECT_2K else 512)
     if cfg & BIG:
@@ -53,6 +58,7 @@ class ConvTuner:
         self.enabled = enabled and os.environ.get("PVA_AUTOTUNE", "1") != "0"
         self.direct = os.environ.get("PVA_CONV_DIRECT", "1") != "0"
         self.dma = os.environ.get("PVA_CONV_DMA", "1") != "0"
+        self.pw = os.environ.get("PVA_CONV_PW", "1") != "0"
         self.log = os.environ.get("PVA_TUNE_LOG", "0") != "0"
         self.reps = reps
         self.cache: Dict[Tuple, int] = {}
@@ -62,7 +68,8 @@ class ConvTuner:
         self.agree: Optional[Callable[[List[float]], List[float]]] = None
 
     # ---------------------------------------------------------------- candidates
-    def candidates(self, g: Sequence[int], chunk: int, aff: int = 0, epi: bool = False) -> List[int]:
+    def candidates(self, g: Sequence[int], chunk: int, aff: int = 0, epi: bool = False,
+                   direct: bool = True) -> List[int]:
         N, Cg = g[1], g[3]
         K = g[28] * g[29] * g[30] * Cg
         out = []
@@ -88,8 +95,10 @@ class ConvTuner:
                     out.append(w)
                     if aff == 0 and self.dma:
                         out.append(w | DMA)
-        if self.direct and self.C.conv_direct_legal(list(g), chunk):
+        if direct and self.direct and self.C.conv_direct_legal(list(g), chunk):
             out += [EXPLICIT | DIRECT, EXPLICIT | DIRECT | DIRECT_2K]
+        if self.pw and self.C.conv_pw_legal(list(g), chunk):
+            out += [EXPLICIT | PW | v for v in range(len(PW_ROWS))]
         return out
 
     def bm(self, cfg: int, N: int) -> int:
@@ -107,19 +116,20 @@ class ConvTuner:
 
     # ---------------------------------------------------------------- launch
     def launch(self, key: Tuple, g: Sequence[int], chunk: int, run: Callable[[int, bool], None],
-               aff: int = 0, epi: bool = False) -> int:
+               aff: int = 0, epi: bool = False, direct: bool = True) -> int:
         """``run(cfg, scratch)`` performs the launch (into scratch outputs when ``scratch``).  Returns the
-        configuration used for the real launch (-1 = kernel heuristic)."""
+        configuration used for the real launch (-1 = kernel heuristic).  ``direct=False``: the launch needs an
+        epilogue the direct kernel lacks (fused residual output, bias)."""
         cfg = self.cache.get(key)
         if cfg is None:
-            cfg = self._tune(g, chunk, run, aff, epi) if self.enabled else -1
+            cfg = self._tune(g, chunk, run, aff, epi, direct) if self.enabled else -1
             self.cache[key] = cfg
         run(cfg, False)
         return cfg
 
     def _tune(self, g: Sequence[int], chunk: int, run: Callable[[int, bool], None], aff: int = 0,
-              epi: bool = False) -> int:
-        cands = self.candidates(g, chunk, aff, epi)
+              epi: bool = False, direct: bool = True) -> int:
+        cands = self.candidates(g, chunk, aff, epi, direct)
         if len(cands) <= 1:
             return cands[0] if cands else -1
         times = []

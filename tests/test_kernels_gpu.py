@@ -264,6 +264,32 @@ def test_conv_wgrad_tile_variants(case, variant):
     assert rel_err(grad, w.grad) < 1e-2
 
 
+@pytest.mark.parametrize("case", [CASES[5], CASES[6], CASES[8],
+                                  (8, 8, (1, 3, 3), (1, 1, 1), (0, 1, 1), (2, 8, 15, 13)),
+                                  (16, 16, (3, 1, 1), (1, 1, 1), (1, 0, 0), (3, 5, 7, 9)),
+                                  (8, 16, (1, 1, 1), (1, 2, 2), (0, 0, 0), (2, 4, 14, 14)),
+                                  (16, 32, (1, 1, 1), (1, 1, 1), (0, 0, 0), (2, 4, 9, 11)),
+                                  (8, 24, (3, 1, 1), (1, 1, 1), (1, 0, 0), (2, 4, 7, 7)),
+                                  (32, 32, (1, 1, 1), (1, 1, 1), (0, 0, 0), (2, 3, 10, 10))])
+@pytest.mark.parametrize("affine", [False, True])
+def test_conv_wgrad_narrow(case, affine):
+    """Barrier-free per-wave wgrad kernel (Cout <= 32, K <= 128): padding, strides, odd sizes, BN-ReLU recompute."""
+    x, w, spec = _mk(case, seed=21)
+    C = spec.cin
+    sc = torch.rand(C, device=DEV) + 0.5
+    sh = torch.randn(C, device=DEV) * 0.5
+    xt = torch.relu(x * sc.view(1, C, 1, 1, 1) + sh.view(1, C, 1, 1, 1)) if affine else x
+    xt = xt.to(torch.bfloat16).float()
+    w.requires_grad_(True)
+    ref_y = torch.nn.functional.conv3d(xt, w, None, spec.stride, spec.pad)
+    gy = torch.randn_like(ref_y).to(torch.bfloat16).float()
+    ref_y.backward(gy)
+    grad = torch.zeros_like(w)
+    conv_wgrad(Act.from_ncthw(gy), Act.from_ncthw(x), spec, grad, in_scale=sc if affine else None,
+               in_shift=sh if affine else None, variant=16)
+    assert rel_err(grad, w.grad) < 1.5e-2
+
+
 def test_conv_wgrad_affine():
     case = CASES[2]
     x, w, spec = _mk(case, seed=4)
