@@ -29,8 +29,13 @@ namespace {
 // (brute-force checked against the gfx950 b128 lane groups for both row lengths).
 // LDS bytes before the stats/affine area: the double-buffered k tiles, or (EPI) the fp32 output tile.
 // NS = k-tile buffers: 2 (register staging) or 3 (LDS-DMA ring, one tile in flight across each barrier)
+// EPI 1 stages the fp32 output tile through LDS in slices of epi_rows rows (64 for the 256x256 tile, whose
+// whole fp32 tile would not fit)
+__host__ __device__ constexpr int epi_rows(int BM, int BN) { return BM * BN > 128 * 128 ? 64 : BM; }
+
 __host__ __device__ constexpr int main_lds_bytes(int BM, int BN, int BK, int EPI, int NS = 2) {
-  return (EPI && BM * (BN * 4 + 16) > NS * (BM + BN) * BK * 2) ? BM * (BN * 4 + 16) : NS * (BM + BN) * BK * 2;
+  return (EPI && epi_rows(BM, BN) * (BN * 4 + 16) > NS * (BM + BN) * BK * 2) ? epi_rows(BM, BN) * (BN * 4 + 16)
+                                                                             : NS * (BM + BN) * BK * 2;
 }
 
 __host__ __device__ constexpr int dma_stages(int BM, int BN, int BK, bool dma) {
@@ -598,21 +603,16 @@ void conv_igemm_kernel(const ConvParams p) {
           }
         }
       }
-    } else {
-      // stage the fp32 fragment in LDS (k tiles are dead: the main loop ended with a barrier)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int row = wm * WM + i * 16 + frow, col = wn * WN + j * 16 + 4 * fslot;
-        *reinterpret_cast<f32x4_t*>(smem + row * STG_PITCH + col * 4) = acc[i][j];
-      }
     }
   }
   if constexpr (EPI == 1) {
     // row-contiguous pass: each thread owns 8 consecutive channels (16-B global accesses) of every
-    // RPP-th tile row: + old y, + residual, ReLU bits, store, backward-BN partial sums.
+    // RPP-th tile row: + old y, + residual, ReLU bits, store, backward-BN partial sums.  The fp32 tile is
+    // staged through LDS (the k tiles are dead: the main loop ended with a barrier) in slices of SR rows.
     constexpr int CPRW = BN / 8, RPP = NT / CPRW;
+    constexpr int SR = epi_rows(BM, BN);
     static_assert(NT % CPRW == 0, "rows per pass");
-    __syncthreads();
+    static_assert(SR % 16 == 0 && SR % RPP == 0, "staging slices hold whole fragments and row passes");
     const int cg = tid % CPRW, r0 = tid / CPRW;
     const int n = n0 + cg * 8;
     // sv = sum v, s0 = sum v*y0, s1 = sum v*y1 ; rebased to sum v*xhat at the end of the tile
@@ -622,8 +622,24 @@ void conv_igemm_kernel(const ConvParams p) {
     const bool nok = n < p.Ngemm;
     const bool dual = p.ey1 != nullptr;
     const bool masky = do_bstats && p.emsc != nullptr;
-    constexpr int RB = 4;  // rows whose loads are issued together (latency hiding)
-    for (int base = r0; base < BM && nok; base += RB * RPP) {
+    // rows whose loads are issued together (latency hiding); 2 for the 256x256 tile, whose 128 accumulator
+    // registers per lane leave no room for more
+    constexpr int RB = BM * BN > 128 * 128 ? 2 : 4;
+#pragma unroll   // compile-time slices: accumulators of staged slices are dead afterwards
+    for (int r_lo = 0; r_lo < BM; r_lo += SR) {
+    if (r_lo > 0) __syncthreads();   // the previous slice has been read
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int row = wm * WM + i * 16 + frow;
+      if (row < r_lo || row >= r_lo + SR) continue;   // uniform per fragment (16-row granularity)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = wn * WN + j * 16 + 4 * fslot;
+        *reinterpret_cast<f32x4_t*>(smem + (row - r_lo) * STG_PITCH + col * 4) = acc[i][j];
+      }
+    }
+    __syncthreads();
+    for (int base = r_lo + r0; base < r_lo + SR && nok; base += RB * RPP) {
       uint4 lo[RB], lr[RB], l0[RB], l1[RB];
       unsigned bits[RB];
       int pos[RB];
@@ -632,7 +648,7 @@ void conv_igemm_kernel(const ConvParams p) {
       for (int u = 0; u < RB; ++u) {
         const int rr = base + u * RPP;
         const int m = m0 + rr;
-        ok[u] = rr < BM && m < p.M;
+        ok[u] = rr < r_lo + SR && m < p.M;
         int ps = m;
         if (!dense_rows && ok[u]) {
           const int b = m / RTHW;
@@ -657,7 +673,7 @@ void conv_igemm_kernel(const ConvParams p) {
 #pragma unroll
       for (int u = 0; u < RB; ++u) {
         if (!ok[u]) continue;
-        const int rr = base + u * RPP;
+        const int rr = base + u * RPP - r_lo;
         const f32x4_t va = *reinterpret_cast<const f32x4_t*>(smem + rr * STG_PITCH + cg * 32);
         const f32x4_t vb = *reinterpret_cast<const f32x4_t*>(smem + rr * STG_PITCH + cg * 32 + 16);
         float v[8] = {va[0], va[1], va[2], va[3], vb[0], vb[1], vb[2], vb[3]};
@@ -698,6 +714,7 @@ void conv_igemm_kernel(const ConvParams p) {
         }
       }
     }
+    }   // staging slices
     if (do_bstats && nok) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -796,10 +813,22 @@ void launch_cfg(const ConvParams& p, int ut_force, hipStream_t stream, bool dma 
   const bool ut_legal = conv_ut_legal(p, CH, BK);
   const bool ut_pays = !p.check || (p.nt == 1 && p.ash == 1 && p.asw == 1);
   const bool ut = ut_legal && (ut_force >= 0 ? ut_force == 1 : (g_ut_mode == 2 || (g_ut_mode == 1 && ut_pays)));
-  // 256x256 tile: forward / plain dgrad only (the EPI 1 fp32 staging tile would not fit LDS)
+  // 256x256 tile (8 waves): the EPI 1 epilogue stages its fp32 tile in 64-row slices
   constexpr bool BIG = BM * BN > 128 * 128;
   if constexpr (BIG) {
-    if (epi) return;   // rejected by the host binding
+    if (epi) {   // dgrad epilogue: never an input affine; the tuner only proposes the uniform-tap loader here
+      if (ut && dma) {
+        if (p.check) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 1, 19>), grid, block, lds, stream, p);
+        else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 1, 17>), grid, block, lds, stream, p);
+      } else if (ut && p.check) {
+        hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 1, 3>), grid, block, lds, stream, p);
+      } else if (ut) {
+        hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 1, 1>), grid, block, lds, stream, p);
+      } else {
+        hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 1, 0>), grid, block, lds, stream, p);
+      }
+      return;
+    }
     if (ut && dma && !p.affine) {
       if (p.check) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 0, 19>), grid, block, lds, stream, p);
       else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 0, 17>), grid, block, lds, stream, p);

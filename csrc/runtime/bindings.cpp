@@ -212,7 +212,6 @@ void conv_igemm_epi(const at::Tensor& x, const at::Tensor& w, const at::Tensor& 
   p.ebias = f32o(bias);
   TORCH_CHECK(!bias.has_value() || bias->numel() >= p.Ngemm, "bias too small");
   TORCH_CHECK(!bias.has_value() || cfg < 0 || !(cfg & 32), "the direct kernel has no bias epilogue");
-  TORCH_CHECK(cfg < 0 || !(cfg & 256), "the 256x256 tile has no backward-BN epilogue");
   p.eres = bfo(res); p.ldr = (int)ldr;
   TORCH_CHECK(!res.has_value() || ldr % 4 == 0, "residual row stride alignment");
   if (mask.has_value()) {

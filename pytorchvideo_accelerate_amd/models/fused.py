@@ -785,7 +785,7 @@ class FusedNet:
         # BN folding of the 1x1 conv_c (never materialise its output); units whose conv_c input has at least
         # fold_min_c channels (default: the slow pathway, where the Gram matrices run at MFMA speed)
         self.bn_fold = os.environ.get("PVA_BN_FOLD", "1") != "0"
-        self.fold_min_c = int(os.environ.get("PVA_BN_FOLD_MIN_C", "64"))
+        self.fold_min_c = int(os.environ.get("PVA_BN_FOLD_MIN_C", "32"))
         blocks = list(model.blocks)
         self.slowfast = isinstance(blocks[0], R.MultiPathWayWithFuse)
         self.stages: List[Tuple[List, Optional[_Fuse]]] = []

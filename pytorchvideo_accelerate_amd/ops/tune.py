@@ -27,7 +27,7 @@ UT = 8
 DIRECT = 32           # narrow direct-to-register kernel (csrc/kernels/conv_direct.hip)
 DIRECT_2K = 64        #   with 2048 rows per workgroup (else 512)
 DMA = 128             # uniform-tap loader staged by LDS-DMA (buffer_load ... lds); launches without input affine
-BIG = 256             # 256x256 tile of 8 waves (N >= 256; forward / plain dgrad, no backward-BN epilogue)
+BIG = 256             # 256x256 tile of 8 waves (N >= 256; the backward-BN epilogue in 64-row slices)
 PW = 512              # streaming pointwise kernel (csrc/kernels/conv_pw.hip): dense 1x1x1 GEMMs, K <= 256,
 PW_ROWS = (1024, 2048, 4096)   # N % 32 == 0, weights in LDS; bits 0-1 select the rows per workgroup
 TILE_BN = (128, 64, 32, 16)   # variants 0..3
@@ -88,7 +88,7 @@ class ConvTuner:
                     out.append(cfg_word(v, bk, ut))
                     if ut and aff == 0 and self.dma:
                         out.append(cfg_word(v, bk, ut) | DMA)
-        if N >= 256 and not epi and chunk == 8:   # 256x256 tile (UT loader only: the generic one is VALU-bound)
+        if N >= 256 and chunk == 8:   # 256x256 tile (UT loader only: the generic one is VALU-bound)
             for bk in (32, 64):
                 if self.C.conv_ut_legal(list(g), chunk, bk):
                     w = EXPLICIT | BIG | UT | (BK64 if bk == 64 else 0)

@@ -492,3 +492,49 @@ def test_conv_big_tile(case):
             assert rel_err(Act(out, N, T, H, W).to_ncthw(), dx_ref) < 1e-2, cfg
             ran += 1
     assert ran > 0
+
+
+@pytest.mark.parametrize("case", [CASES[1], CASES[10]])
+def test_conv_big_tile_bn_epilogue(case):
+    """256x256 tile with the backward-BN dgrad epilogue staged in 64-row slices: residual, ReLU bits, accumulate,
+    partial sums of v, v*xhat0, v*xhat1 (register and LDS-DMA loaders, BK 32/64)."""
+    from pytorchvideo_accelerate_amd.ops._ext import require
+    from pytorchvideo_accelerate_amd.ops.conv import dgrad_phases
+    from pytorchvideo_accelerate_amd.ops.tune import BIG, BK64, DMA, EXPLICIT, UT
+    C = require()
+    x, w, spec = _mk(case, seed=45)
+    N, Ci, T, H, W = x.shape
+    ref_y = torch.nn.functional.conv3d(x, w, None, spec.stride, spec.pad)
+    gy = torch.randn_like(ref_y).to(torch.bfloat16).float()
+    M = N * T * H * W
+    dx_ref = torch.nn.grad.conv3d_input(x.shape, w, gy, spec.stride, spec.pad).permute(0, 2, 3, 4, 1).reshape(M, Ci)
+    gen = torch.Generator(device="cpu").manual_seed(46)
+    bf = lambda *s: torch.randn(*s, generator=gen).to(torch.bfloat16).to(DEV)
+    res, old, y0, y1 = bf(M, Ci), bf(M, Ci), bf(M, Ci) * 2 + 0.5, bf(M, Ci)
+    mask = torch.rand(M, Ci, generator=gen).to(DEV) > 0.4
+    mean0, rstd0 = torch.randn(Ci, device=DEV) * 0.3, torch.rand(Ci, device=DEV) + 0.5
+    mean1, rstd1 = torch.randn(Ci, device=DEV) * 0.3, torch.rand(Ci, device=DEV) + 0.5
+    _, wd = pack_weight(w, spec)
+    dy = Act.from_ncthw(gy)
+    geo = dgrad_phases(spec, N, (T, H, W), (dy.T, dy.H, dy.W), dy.ld, Ci)
+    assert len(geo) == 1
+    ran = 0
+    for bk in (32, 64):
+        if not C.conv_ut_legal(list(geo[0]), 8, bk):
+            continue
+        base = EXPLICIT | BIG | UT | (BK64 if bk == 64 else 0)
+        for cfg in (base, base | DMA):
+            out = old.clone()
+            part = torch.full(((M + 255) // 256, 3, Ci), float("nan"), device=DEV)
+            C.conv_igemm_epi(dy.t, wd, out, 1, geo[0], 8, res, Ci, _bits(mask), y0, mean0, rstd0, y1, mean1, rstd1,
+                             part, None, None, cfg)
+            v = (dx_ref + old.float() + res.float()) * mask
+            assert rel_err(out, v) < 1.5e-2, cfg
+            q = out.float()
+            s = part.sum(0)
+            tol = 2e-2 * (q.abs() * (y0.float() - mean0).abs() * rstd0).sum(0).max().item() / M ** 0.5
+            torch.testing.assert_close(s[0], q.sum(0), rtol=1e-3, atol=1e-2 * q.abs().sum(0).max().item() / M ** 0.5)
+            torch.testing.assert_close(s[1], (q * (y0.float() - mean0) * rstd0).sum(0), rtol=1e-3, atol=tol)
+            torch.testing.assert_close(s[2], (q * (y1.float() - mean1) * rstd1).sum(0), rtol=1e-3, atol=tol)
+            ran += 1
+    assert ran > 0
