@@ -4,7 +4,7 @@
 // With a = act_b(yb) [M][c] (the conv_c input), Wc [C][c] (bf16 weights as the conv uses them), the Gram
 // matrix Ga = a^T a [c][c] and column sums s = 1^T a [c] (both from the wgrad kernel in Gram mode):
 //   forward statistics of yc = a Wc^T:  mean_n = (Wc s)_n / M,  E[yc_n^2] = (Wc Ga Wc^T)_nn / M
-//   (bnfold_fwd_stats_kernel; T = Wc Ga is kept for the backward).
+//   (colsum reduce, T = Wc Ga tiles, per-channel finalize; T is kept for the backward).
 // Backward, from dz [M][C] (the ReLU-masked residual gradient), G = dz^T a [C][c] and dbeta = 1^T dz:
 //   sum_m dz yc = rowdot(Wc, G),  dgamma = rstd (rowdot - mean dbeta)
 //   dyc = A dz + B (yc - mean) + D   with A = g r, B = -g r^2 dgamma / M, D = -g r dbeta / M
@@ -62,73 +62,82 @@ __device__ __forceinline__ f32x4_t reduce4(f32x4_t acc, float* red, int wave, in
   return t;   // every wave gets the total
 }
 
-// sum of colsum slabs [splits][c] -> s [c]
-__device__ __forceinline__ float slab_sum(const float* slabs, int splits, int c, int j) {
+// s[j] = sum over the colsum slabs [splits][c]: 16 columns per block, 16 threads per column striding the
+// slabs, then a fixed-order 16-way combine (deterministic)
+__global__ __launch_bounds__(256) void bnfold_colsum_kernel(const float* __restrict__ sslab, int splits, int c,
+                                                            float* __restrict__ s_out) {
+  __shared__ float part[16][17];
+  const int jl = threadIdx.x & 15, kl = threadIdx.x >> 4;
+  const int j = blockIdx.x * 16 + jl;
   float t = 0.f;
-  for (int k = 0; k < splits; ++k) t += slabs[(int64_t)k * c + j];
-  return t;
+  if (j < c)
+    for (int k = kl; k < splits; k += 16) t += sslab[(int64_t)k * c + j];
+  part[kl][jl] = t;
+  __syncthreads();
+  if (kl == 0 && j < c) {
+    float v = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v += part[q][jl];
+    s_out[j] = v;
+  }
 }
 
-// one block per 16 output channels n: T[n][:] = Wc[n] Ga, q_n = Wc[n] . T[n], mean_n = Wc[n] . s / M;
-// then the training-mode BN finalize (running stats with unbiased variance, consumer affine)
-__global__ __launch_bounds__(256) void bnfold_fwd_stats_kernel(
-    const uint16_t* __restrict__ Wf, const float* __restrict__ Ga, const float* __restrict__ sslab, int splits,
-    int C, int c, int64_t count, float* __restrict__ T, float* __restrict__ s_out, const float* __restrict__ gamma,
-    const float* __restrict__ beta, float* __restrict__ run_mean, float* __restrict__ run_var,
-    int64_t* __restrict__ nbt, float momentum, float eps, float* __restrict__ save_mean,
-    float* __restrict__ save_rstd, float* __restrict__ scale, float* __restrict__ shift) {
+// T = Wc Ga, one 16x16 tile per block (the 4 waves split k), grid (c/16, C/16)
+__global__ __launch_bounds__(256) void bnfold_t_kernel(const uint16_t* __restrict__ Wf, const float* __restrict__ Ga,
+                                                       int C, int c, float* __restrict__ T) {
   __shared__ __attribute__((aligned(16))) float red[4 * 64 * 4];
-  __shared__ float s_sh[2048];
-  __shared__ double qsum[16];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int i0 = blockIdx.x * 16;
-  for (int j = threadIdx.x; j < c; j += 256) {
-    const float v = slab_sum(sslab, splits, c, j);
-    s_sh[j] = v;
-    if (blockIdx.x == 0) s_out[j] = v;
-  }
-  if (threadIdx.x < 16) qsum[threadIdx.x] = 0.0;
-  __syncthreads();
-  for (int j0 = 0; j0 < c; j0 += 16) {
-    const f32x4_t t = reduce4(tile16(Wf, c, C, Ga, c, c, c, (const float*)nullptr, i0, j0, wave, lane), red, wave,
-                              lane);
-    if (wave == 0) {
-      const int j = j0 + (lane & 15);
+  const int j0 = blockIdx.x * 16, i0 = blockIdx.y * 16;
+  // Ga is symmetric: row j of Ga = column j, so the B operand reads rows (contiguous)
+  const f32x4_t t = reduce4(tile16(Wf, c, C, Ga, c, c, c, (const float*)nullptr, i0, j0, wave, lane), red, wave,
+                            lane);
+  if (wave == 0) {
+    const int j = j0 + (lane & 15);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int n = i0 + 4 * (lane >> 4) + r;
-        float w = 0.f;
-        if (n < C && j < c) {
-          T[(int64_t)n * c + j] = t[r];
-          w = bf2f(Wf[(int64_t)n * c + j]) * t[r];
-        }
-        w = sum16(w);
-        if ((lane & 15) == 0) qsum[4 * (lane >> 4) + r] += (double)w;
-      }
+    for (int r = 0; r < 4; ++r) {
+      const int n = i0 + 4 * (lane >> 4) + r;
+      if (n < C && j < c) T[(int64_t)n * c + j] = t[r];
     }
   }
-  __syncthreads();
-  if (threadIdx.x < 16) {
-    const int n = i0 + threadIdx.x;
-    if (n < C) {
-      double mu = 0.0;
-      for (int j = 0; j < c; ++j) mu += (double)bf2f(Wf[(int64_t)n * c + j]) * (double)s_sh[j];
-      mu /= (double)count;
-      double var = qsum[threadIdx.x] / (double)count - mu * mu;
-      if (var < 0) var = 0;
-      const float rstd = (float)(1.0 / sqrt(var + (double)eps));
-      save_mean[n] = (float)mu;
-      save_rstd[n] = rstd;
-      const float g = gamma[n], b = beta[n];
-      scale[n] = g * rstd;
-      shift[n] = b - (float)mu * g * rstd;
-      if (run_mean) {
-        const double unb = count > 1 ? var * (double)count / (double)(count - 1) : var;
-        run_mean[n] = (1.f - momentum) * run_mean[n] + momentum * (float)mu;
-        run_var[n] = (1.f - momentum) * run_var[n] + momentum * (float)unb;
-      }
-      if (n == 0 && nbt) nbt[0] += 1;
+}
+
+// one wave per output channel n: mean_n = Wc[n] . s / M, E[yc^2] = Wc[n] . T[n] / M (double accumulation),
+// then the training-mode BN finalize (running stats with unbiased variance, consumer affine)
+__global__ __launch_bounds__(256) void bnfold_finalize_kernel(
+    const uint16_t* __restrict__ Wf, const float* __restrict__ T, const float* __restrict__ s, int C, int c,
+    int64_t count, const float* __restrict__ gamma, const float* __restrict__ beta, float* __restrict__ run_mean,
+    float* __restrict__ run_var, int64_t* __restrict__ nbt, float momentum, float eps, float* __restrict__ save_mean,
+    float* __restrict__ save_rstd, float* __restrict__ scale, float* __restrict__ shift) {
+  const int lane = threadIdx.x & 63;
+  const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (n >= C) return;   // wave-uniform; no barriers below
+  double mu = 0.0, q = 0.0;
+  for (int j = lane; j < c; j += 64) {
+    const double w = (double)bf2f(Wf[(int64_t)n * c + j]);
+    mu += w * (double)s[j];
+    q += w * (double)T[(int64_t)n * c + j];
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    mu += __shfl_xor(mu, o, 64);
+    q += __shfl_xor(q, o, 64);
+  }
+  if (lane == 0) {
+    mu /= (double)count;
+    double var = q / (double)count - mu * mu;
+    if (var < 0) var = 0;
+    const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+    save_mean[n] = (float)mu;
+    save_rstd[n] = rstd;
+    const float g = gamma[n], b = beta[n];
+    scale[n] = g * rstd;
+    shift[n] = b - (float)mu * g * rstd;
+    if (run_mean) {
+      const double unb = count > 1 ? var * (double)count / (double)(count - 1) : var;
+      run_mean[n] = (1.f - momentum) * run_mean[n] + momentum * (float)mu;
+      run_var[n] = (1.f - momentum) * run_var[n] + momentum * (float)unb;
     }
+    if (n == 0 && nbt) nbt[0] += 1;
   }
 }
 
@@ -243,8 +252,10 @@ void bnfold_fwd_stats_launch(const uint16_t* Wf, const float* Ga, const float* s
                              int64_t count, float* T, float* s_out, const float* gamma, const float* beta, float* rm,
                              float* rv, int64_t* nbt, float momentum, float eps, float* smean, float* srstd,
                              float* scale, float* shift, hipStream_t st) {
-  hipLaunchKernelGGL(bnfold_fwd_stats_kernel, dim3((C + 15) / 16), dim3(256), 0, st, Wf, Ga, sslab, splits, C, c,
-                     count, T, s_out, gamma, beta, rm, rv, nbt, momentum, eps, smean, srstd, scale, shift);
+  hipLaunchKernelGGL(bnfold_colsum_kernel, dim3((c + 15) / 16), dim3(256), 0, st, sslab, splits, c, s_out);
+  hipLaunchKernelGGL(bnfold_t_kernel, dim3((c + 15) / 16, (C + 15) / 16), dim3(256), 0, st, Wf, Ga, C, c, T);
+  hipLaunchKernelGGL(bnfold_finalize_kernel, dim3((C + 3) / 4), dim3(256), 0, st, Wf, T, s_out, C, c, count, gamma,
+                     beta, rm, rv, nbt, momentum, eps, smean, srstd, scale, shift);
 }
 
 void bnfold_bwd_launch(const float* part, int tiles, const uint16_t* Wf, const uint16_t* Wd, const float* G,

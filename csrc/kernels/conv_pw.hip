@@ -5,8 +5,9 @@
 // load -> MFMA -> epilogue latency chain with little to overlap it, and these memory-bound layers (the
 // bottleneck's conv_a / conv_c / branch1 and their dgrads, the BN-folded residual output) ran at
 // 2.3-3.6 TB/s (profiles/r2_layers).  Here:
-//   * the whole packed weight matrix lives in LDS, pre-arranged in MFMA fragment order (each 1-KB fragment
-//     is read by a wave as one contiguous, conflict-free ds_read_b128), filled once per workgroup;
+//   * the packed weights live in LDS, pre-arranged in MFMA fragment order (each 1-KB fragment is read by
+//     a wave as one contiguous, conflict-free ds_read_b128), filled once per workgroup; convs whose weights
+//     exceed the LDS budget are split into output-channel groups (one workgroup per group and row range);
 //   * each wave streams 16*TM-row tiles: the tile's activations are loaded ONCE into registers (the
 //     producer's BatchNorm + ReLU applied on the way) and reused for every 32-channel output chunk;
 //   * each chunk's epilogue operands (residual, old output, BN inputs, mask bits) are issued one or two
@@ -24,12 +25,13 @@
 // output (conv_igemm's fres), 2 the backward-BN epilogue of the dgrads (conv_igemm's EPI 1).
 #include "common.h"
 #include "conv_params.h"
+#include <algorithm>
 
 namespace {
 
 constexpr int PW_WAVES = 8;
 constexpr int PW_THREADS = PW_WAVES * 64;
-constexpr int PW_W_LDS = 128 * 1024;   // weight image budget (bytes)
+constexpr int PW_W_LDS = 96 * 1024;    // weight image budget per output-channel group (bytes)
 
 // Butterfly reduce-scatter over the 16 lanes sharing lane >> 4: v[L] in; lane rho ends up holding the
 // 16-lane total of element rho (L = 16) or of element rho >> 1 (L = 8) in v[0].
@@ -63,17 +65,25 @@ struct Pre {
 };
 
 template <int KS, int TM, int EP, int AFF>
-__global__ __launch_bounds__(PW_THREADS) void conv_pw_kernel(const ConvParams p, int rpb) {
+__global__ __launch_bounds__(PW_THREADS) void conv_pw_kernel(const ConvParams p, int rpb, int gch) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NST = EP == 2 ? 3 : 2;
   constexpr int MT = 16 * TM;
   constexpr int PD = EP == 2 ? 2 : 3;   // prefetch ring depth (chunks)
   const int N = p.Ngemm, K = p.Cg;
-  const int nch = N >> 5;
+  // output-channel group of this workgroup (weights of wide convs do not fit LDS at once: the row range
+  // is walked once per group of gch 32-channel chunks; the XCD remap puts the groups of one row range on
+  // the same XCD, so its activations are re-read from that L2)
+  const int ngrp = ((N >> 5) + gch - 1) / gch;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int grp = L % ngrp, rblk = L / ngrp;
+  const int cbase = grp * gch;                              // first chunk of the group
+  const int nch = min(gch, (N >> 5) - cbase);               // chunks in this group
+  const int NG = nch * 32, nb0 = cbase * 32;                // group channels, first channel
   const int wimg = nch * 2 * KS * 1024;
-  float* st_lds = reinterpret_cast<float*>(smem + wimg);   // [NST][N] workgroup statistics
-  float* cst = st_lds + NST * N;                            // [4][N] per-channel epilogue constants
-  float* affs = cst + 4 * N;                                // [2][K] input affine
+  float* st_lds = reinterpret_cast<float*>(smem + wimg);   // [NST][NG] workgroup statistics
+  float* cst = st_lds + NST * NG;                           // [4][NG] per-channel epilogue constants
+  float* affs = cst + 4 * NG;                               // [2][K] input affine
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int rho = lane & 15, g = lane >> 4;
 
@@ -85,7 +95,7 @@ __global__ __launch_bounds__(PW_THREADS) void conv_pw_kernel(const ConvParams p,
     const int s = f % KS, ch = f / KS;
     const int h = ch & 1, c = ch >> 1;
     const int r = l & 15;
-    const int n = 32 * c + 8 * (r >> 2) + 4 * h + (r & 3);
+    const int n = nb0 + 32 * c + 8 * (r >> 2) + 4 * h + (r & 3);
     const int k0 = 32 * s + 8 * (l >> 4);
     uint4 v = uint4{0, 0, 0, 0};
     if (k0 < K) v = *reinterpret_cast<const uint4*>(p.w + (int64_t)n * p.Kfull + k0);
@@ -93,22 +103,23 @@ __global__ __launch_bounds__(PW_THREADS) void conv_pw_kernel(const ConvParams p,
   }
   const bool do_stats = (EP == 0 && p.stats != nullptr) || (EP == 2 && p.epart != nullptr);
   if (do_stats)
-    for (int i = tid; i < NST * N; i += PW_THREADS) st_lds[i] = 0.f;
+    for (int i = tid; i < NST * NG; i += PW_THREADS) st_lds[i] = 0.f;
   if (AFF)
     for (int i = tid; i < K; i += PW_THREADS) { affs[i] = p.in_scale[i]; affs[K + i] = p.in_shift[i]; }
   // EP 1: fsc fsh rsc rsh ; EP 0 / 2: bias (0 when absent), mask-affine scale and shift
-  for (int i = tid; i < N; i += PW_THREADS) {
+  for (int i = tid; i < NG; i += PW_THREADS) {
+    const int n = nb0 + i;
     if (EP == 1) {
-      cst[i] = p.fsc[i]; cst[N + i] = p.fsh[i];
-      cst[2 * N + i] = p.rsc ? p.rsc[i] : 1.f; cst[3 * N + i] = p.rsh ? p.rsh[i] : 0.f;
+      cst[i] = p.fsc[n]; cst[NG + i] = p.fsh[n];
+      cst[2 * NG + i] = p.rsc ? p.rsc[n] : 1.f; cst[3 * NG + i] = p.rsh ? p.rsh[n] : 0.f;
     } else {
-      cst[i] = p.ebias ? p.ebias[i] : 0.f;
-      if (EP == 2 && p.emsc) { cst[N + i] = p.emsc[i]; cst[2 * N + i] = p.emsh[i]; }
+      cst[i] = p.ebias ? p.ebias[n] : 0.f;
+      if (EP == 2 && p.emsc) { cst[NG + i] = p.emsc[n]; cst[2 * NG + i] = p.emsh[n]; }
     }
   }
   __syncthreads();
 
-  const int row0 = blockIdx.x * rpb;
+  const int row0 = rblk * rpb;
   const int row_end = min(p.M, row0 + rpb);
   const int mrow = N >> 3;   // mask bytes per row
   const bool dual = EP == 2 && p.ey1 != nullptr;
@@ -146,7 +157,7 @@ __global__ __launch_bounds__(PW_THREADS) void conv_pw_kernel(const ConvParams p,
     // loads stay in flight behind the MFMAs and stores of the current one
     Pre<TM> P[PD];
     auto prefetch = [&](int c, Pre<TM>& Q) {
-      const int n = 32 * c + 8 * g;
+      const int n = nb0 + 32 * c + 8 * g;
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int m = m0 + 16 * i + rho;
@@ -167,7 +178,8 @@ __global__ __launch_bounds__(PW_THREADS) void conv_pw_kernel(const ConvParams p,
       if (d < nch) prefetch(d, P[d]);
 #pragma unroll 1
     for (int c = 0; c < nch; ++c) {
-      const int n = 32 * c + 8 * g;   // this lane's 8 output channels
+      const int nl = 32 * c + 8 * g;   // this lane's 8 output channels (group-local)
+      const int n = nb0 + nl;
       if (c + PD - 1 < nch) prefetch(c + PD - 1, P[PD - 1]);
       // ---- MFMAs: D = W X^T, lane gets channels n..n+3 (half 0) and n+4..n+7 (half 1) of its position
       f32x4_t acc[TM][2];
@@ -193,10 +205,10 @@ __global__ __launch_bounds__(PW_THREADS) void conv_pw_kernel(const ConvParams p,
       float cb[8], c2[8], c3[8], c4[8];   // per-channel constants of this lane's 8 channels (from LDS)
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        cb[e] = cst[n + e];
-        c2[e] = EP == 1 ? cst[N + n + e] : 0.f;
-        c3[e] = EP == 1 ? cst[2 * N + n + e] : (masky ? cst[N + n + e] : 0.f);
-        c4[e] = EP == 1 ? cst[3 * N + n + e] : (masky ? cst[2 * N + n + e] : 0.f);
+        cb[e] = cst[nl + e];
+        c2[e] = EP == 1 ? cst[NG + nl + e] : 0.f;
+        c3[e] = EP == 1 ? cst[2 * NG + nl + e] : (masky ? cst[NG + nl + e] : 0.f);
+        c4[e] = EP == 1 ? cst[3 * NG + nl + e] : (masky ? cst[2 * NG + nl + e] : 0.f);
       }
       float s_a[8], s_b[8], s_c[8];
 #pragma unroll
@@ -270,10 +282,10 @@ __global__ __launch_bounds__(PW_THREADS) void conv_pw_kernel(const ConvParams p,
 #pragma unroll
         for (int e = 0; e < 8; ++e) { t[e] = s_a[e]; t[8 + e] = s_b[e]; }
         rs16<16>(t, lane);
-        atomicAdd(st_lds + (rho >> 3) * N + n + (rho & 7), t[0]);
+        atomicAdd(st_lds + (rho >> 3) * NG + nl + (rho & 7), t[0]);
         if (EP == 2 && dual) {   // third statistic: lanes 2e and 2e + 1 end with channel e
           rs16<8>(s_c, lane);
-          if (!(rho & 1)) atomicAdd(st_lds + 2 * N + n + (rho >> 1), s_c[0]);
+          if (!(rho & 1)) atomicAdd(st_lds + 2 * NG + nl + (rho >> 1), s_c[0]);
         }
       }
 #pragma unroll
@@ -282,30 +294,31 @@ __global__ __launch_bounds__(PW_THREADS) void conv_pw_kernel(const ConvParams p,
   }
   if (!do_stats) return;
   __syncthreads();
-  for (int i = tid; i < NST * N; i += PW_THREADS) {
-    const int k = i / N, n = i - k * N;
+  for (int i = tid; i < NST * NG; i += PW_THREADS) {
+    const int k = i / NG, nl = i - k * NG, n = nb0 + nl;
     float v = st_lds[i];
     if (EP == 2 && k > 0) {   // sum v * xhat = rstd (sum v y - mean sum v)
       const float* mean = k == 1 ? p.emean0 : p.emean1;
       const float* rstd = k == 1 ? p.erstd0 : p.erstd1;
       const bool have = k == 1 ? p.ey0 != nullptr : p.ey1 != nullptr;
-      v = have ? (v - mean[n] * st_lds[n]) * rstd[n] : 0.f;
+      v = have ? (v - mean[n] * st_lds[nl]) * rstd[n] : 0.f;
     }
-    if (EP == 2) p.epart[((int64_t)blockIdx.x * 3 + k) * N + n] = v;
-    else p.stats[((int64_t)blockIdx.x * 2 + k) * N + n] = v;
+    if (EP == 2) p.epart[((int64_t)rblk * 3 + k) * N + n] = v;
+    else p.stats[((int64_t)rblk * 2 + k) * N + n] = v;
   }
 }
 
 template <int KS, int TM, int EP>
-void launch_ep(const ConvParams& p, int rpb, size_t lds, hipStream_t st) {
-  const dim3 grid((p.M + rpb - 1) / rpb), block(PW_THREADS);
+void launch_ep(const ConvParams& p, int rpb, int gch, size_t lds, hipStream_t st) {
+  const int ngrp = ((p.Ngemm >> 5) + gch - 1) / gch;
+  const dim3 grid(((p.M + rpb - 1) / rpb) * ngrp), block(PW_THREADS);
   if constexpr (EP == 2) {
-    hipLaunchKernelGGL((conv_pw_kernel<KS, TM, 2, 0>), grid, block, lds, st, p, rpb);
+    hipLaunchKernelGGL((conv_pw_kernel<KS, TM, 2, 0>), grid, block, lds, st, p, rpb, gch);
   } else {
     switch (p.affine) {
-      case 0: hipLaunchKernelGGL((conv_pw_kernel<KS, TM, EP, 0>), grid, block, lds, st, p, rpb); break;
-      case 1: hipLaunchKernelGGL((conv_pw_kernel<KS, TM, EP, 1>), grid, block, lds, st, p, rpb); break;
-      default: hipLaunchKernelGGL((conv_pw_kernel<KS, TM, EP, 2>), grid, block, lds, st, p, rpb); break;
+      case 0: hipLaunchKernelGGL((conv_pw_kernel<KS, TM, EP, 0>), grid, block, lds, st, p, rpb, gch); break;
+      case 1: hipLaunchKernelGGL((conv_pw_kernel<KS, TM, EP, 1>), grid, block, lds, st, p, rpb, gch); break;
+      default: hipLaunchKernelGGL((conv_pw_kernel<KS, TM, EP, 2>), grid, block, lds, st, p, rpb, gch); break;
     }
   }
 }
@@ -313,11 +326,11 @@ void launch_ep(const ConvParams& p, int rpb, size_t lds, hipStream_t st) {
 // forward epilogues: 64-row tiles (32 at K > 128); the backward-BN epilogue carries 4 operand rows per
 // position through a 2-deep ring: 32-row tiles (16 at K > 128) keep it in registers
 template <int KS>
-void launch_ks(const ConvParams& p, int ep, int rpb, size_t lds, hipStream_t st) {
+void launch_ks(const ConvParams& p, int ep, int rpb, int gch, size_t lds, hipStream_t st) {
   constexpr int TMF = KS <= 4 ? 4 : 2;
-  if (ep == 2) launch_ep<KS, (KS <= 4 ? 2 : 1), 2>(p, rpb, lds, st);
-  else if (ep == 1) launch_ep<KS, TMF, 1>(p, rpb, lds, st);
-  else launch_ep<KS, TMF, 0>(p, rpb, lds, st);
+  if (ep == 2) launch_ep<KS, (KS <= 4 ? 2 : 1), 2>(p, rpb, gch, lds, st);
+  else if (ep == 1) launch_ep<KS, TMF, 1>(p, rpb, gch, lds, st);
+  else launch_ep<KS, TMF, 0>(p, rpb, gch, lds, st);
 }
 
 inline int pw_ks(int K) {
@@ -340,22 +353,25 @@ int conv_pw_legal(const ConvParams& p, int chunk) {
   if (p.Ot != p.Rt || p.Oh != p.Rh || p.Ow != p.Rw) return 0;
   if (p.Kfull != p.Cg || p.Cg % 8 != 0 || p.Cg > 256 || p.Ngemm % 32 != 0) return 0;
   if (p.ldx % 8 != 0 || p.ldy % 8 != 0) return 0;
-  if ((p.Ngemm / 32) * 2 * pw_ks(p.Cg) * 1024 > PW_W_LDS) return 0;
   return 1;
 }
+
+// 32-channel chunks per output-channel group: the weight image of a group fits PW_W_LDS
+static int pw_group_chunks(int N, int ks) { return std::min(N / 32, PW_W_LDS / (2 * ks * 1024)); }
 
 void conv_pw_launch(const ConvParams& p, int cfg, hipStream_t st) {
   const bool ep2 = !p.fres && (p.eres || p.emask || p.epart);
   const int ep = p.fres ? 1 : (ep2 ? 2 : 0);
   const int ks = pw_ks(p.Cg);
   const int nst = ep == 2 ? 3 : 2;
-  const size_t lds = (size_t)(p.Ngemm / 32) * 2 * ks * 1024 + (size_t)(nst + 4) * p.Ngemm * 4 +
-                     (p.affine ? 2 * (size_t)p.Cg * 4 : 0);
+  const int gch = pw_group_chunks(p.Ngemm, ks);
+  const int NG = gch * 32;
+  const size_t lds = (size_t)gch * 2 * ks * 1024 + (size_t)(nst + 4) * NG * 4 + (p.affine ? 2 * (size_t)p.Cg * 4 : 0);
   const int rpb = conv_pw_rows(cfg);
   switch (ks) {
-    case 1: launch_ks<1>(p, ep, rpb, lds, st); break;
-    case 2: launch_ks<2>(p, ep, rpb, lds, st); break;
-    case 4: launch_ks<4>(p, ep, rpb, lds, st); break;
-    default: launch_ks<8>(p, ep, rpb, lds, st); break;
+    case 1: launch_ks<1>(p, ep, rpb, gch, lds, st); break;
+    case 2: launch_ks<2>(p, ep, rpb, gch, lds, st); break;
+    case 4: launch_ks<4>(p, ep, rpb, gch, lds, st); break;
+    default: launch_ks<8>(p, ep, rpb, gch, lds, st); break;
   }
 }

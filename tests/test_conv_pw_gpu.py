@@ -35,7 +35,7 @@ def _bits(mask):
 # (M as (N, T, H, W), Cin, Cout, extra input / output row padding)
 FWD = [((2, 3, 7, 9), 64, 256, 0, 0), ((1, 4, 10, 10), 128, 512, 16, 8), ((3, 1, 11, 13), 8, 32, 8, 0),
        ((2, 2, 9, 9), 80, 256, 0, 16), ((1, 2, 15, 15), 256, 64, 0, 0), ((1, 1, 33, 31), 200, 96, 8, 0),
-       ((2, 4, 8, 8), 32, 128, 0, 0)]
+       ((2, 4, 8, 8), 32, 128, 0, 0), ((1, 2, 7, 9), 256, 1024, 0, 0), ((1, 3, 5, 7), 64, 2048, 0, 0)]
 
 
 @pytest.mark.parametrize("case", FWD)
@@ -80,7 +80,8 @@ def test_pw_forward(case, aff):
 
 
 @pytest.mark.parametrize("identity", [True, False])
-@pytest.mark.parametrize("shape", [((2, 2, 8, 8), 64, 256), ((1, 3, 9, 11), 128, 512), ((2, 1, 7, 7), 16, 64)])
+@pytest.mark.parametrize("shape", [((2, 2, 8, 8), 64, 256), ((1, 3, 9, 11), 128, 512), ((2, 1, 7, 7), 16, 64),
+                                   ((1, 2, 7, 9), 256, 1024)])
 def test_pw_fres(identity, shape):
     C = _C()
     (N, T, H, W), c, Co = shape
@@ -115,7 +116,7 @@ def test_pw_fres(identity, shape):
 
 
 @pytest.mark.parametrize("shape", [((2, 3, 7, 9), 256, 64), ((1, 2, 10, 10), 64, 256), ((2, 2, 9, 7), 512, 128),
-                                   ((1, 1, 13, 13), 32, 24)])
+                                   ((1, 1, 13, 13), 32, 24), ((1, 2, 7, 9), 1024, 256)])
 @pytest.mark.parametrize("mode", ["res_mask_dual_accum", "bnmask_bias", "plain"])
 def test_pw_dgrad_epilogue(shape, mode):
     """dx = dy W for a 1x1 conv Ci -> Co (K = Co, N = Ci) with the backward-BN epilogue."""
@@ -178,8 +179,10 @@ def test_pw_legality():
     assert not C.conv_pw_legal(list(fwd_geometry(spec3, 1, 2, 8, 8, 64, 64)), 8)
     s2 = ConvSpec(64, 256, (1, 1, 1), (1, 2, 2), (0, 0, 0))
     assert not C.conv_pw_legal(list(fwd_geometry(s2, 1, 2, 8, 8, 64, 256)), 8)
-    big = ConvSpec(256, 1024, (1, 1, 1))   # 512 KB of weights: does not fit LDS
-    assert not C.conv_pw_legal(list(fwd_geometry(big, 1, 2, 8, 8, 256, 1024)), 8)
+    big = ConvSpec(256, 1024, (1, 1, 1))   # 512 KB of weights: output-channel groups
+    assert C.conv_pw_legal(list(fwd_geometry(big, 1, 2, 8, 8, 256, 1024)), 8)
+    deep = ConvSpec(512, 256, (1, 1, 1))   # K > 256
+    assert not C.conv_pw_legal(list(fwd_geometry(deep, 1, 2, 8, 8, 512, 256)), 8)
     n16 = ConvSpec(64, 16, (1, 1, 1))      # N % 32 != 0
     assert not C.conv_pw_legal(list(fwd_geometry(n16, 1, 2, 8, 8, 64, 16)), 8)
     ok = ConvSpec(64, 256, (1, 1, 1))
