@@ -31,7 +31,7 @@ namespace {
 
 constexpr int PW_WAVES = 8;
 constexpr int PW_THREADS = PW_WAVES * 64;
-constexpr int PW_W_LDS = 96 * 1024;    // weight image budget per output-channel group (bytes)
+constexpr int PW_LDS = 156 * 1024;     // LDS budget of a workgroup (weights, statistics, constants)
 
 // Butterfly reduce-scatter over the 16 lanes sharing lane >> 4: v[L] in; lane rho ends up holding the
 // 16-lane total of element rho (L = 16) or of element rho >> 1 (L = 8) in v[0].
@@ -356,17 +356,25 @@ int conv_pw_legal(const ConvParams& p, int chunk) {
   return 1;
 }
 
-// 32-channel chunks per output-channel group: the weight image of a group fits PW_W_LDS
-static int pw_group_chunks(int N, int ks) { return std::min(N / 32, PW_W_LDS / (2 * ks * 1024)); }
+// 32-channel chunks per output-channel group: the largest group whose weight image, statistics and epilogue
+// constants fit the LDS budget, then balanced over the groups (equal work per workgroup)
+static int pw_group_chunks(int N, int ks, int nst, int aff_bytes) {
+  const int nch = N / 32;
+  const int per_chunk = 2 * ks * 1024 + (nst + 4) * 32 * 4;
+  const int gmax = std::max(1, (PW_LDS - aff_bytes) / per_chunk);
+  const int ngrp = (nch + gmax - 1) / gmax;
+  return (nch + ngrp - 1) / ngrp;
+}
 
 void conv_pw_launch(const ConvParams& p, int cfg, hipStream_t st) {
   const bool ep2 = !p.fres && (p.eres || p.emask || p.epart);
   const int ep = p.fres ? 1 : (ep2 ? 2 : 0);
   const int ks = pw_ks(p.Cg);
   const int nst = ep == 2 ? 3 : 2;
-  const int gch = pw_group_chunks(p.Ngemm, ks);
+  const int aff_bytes = p.affine ? 2 * p.Cg * 4 : 0;
+  const int gch = pw_group_chunks(p.Ngemm, ks, nst, aff_bytes);
   const int NG = gch * 32;
-  const size_t lds = (size_t)gch * 2 * ks * 1024 + (size_t)(nst + 4) * NG * 4 + (p.affine ? 2 * (size_t)p.Cg * 4 : 0);
+  const size_t lds = (size_t)gch * 2 * ks * 1024 + (size_t)(nst + 4) * NG * 4 + aff_bytes;
   const int rpb = conv_pw_rows(cfg);
   switch (ks) {
     case 1: launch_ks<1>(p, ep, rpb, gch, lds, st); break;
