@@ -9,6 +9,7 @@ instantiation and reported with derived ratios:
   wait    = SQ_WAIT_ANY / SQ_WAVE_CYCLES  (parked on s_waitcnt / barrier)
   lds_cf  = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE
   GB      = 2 * FETCH_SIZE (gfx950 FETCH_SIZE reports half of wide streaming reads) and WRITE_SIZE
+  l2hit   = TCC_HIT_sum / (TCC_HIT_sum + TCC_MISS_sum)   (when that pass was collected)
 
     python scripts/pmc_step_summary.py gpurun_out/pmc_step > profiles/.../pmc_step.txt
 """
@@ -62,7 +63,7 @@ def main():
     tot = sum(dur.values())
     print(f"# one optimizer step, {sum(cnt.values())} dispatches, {tot / 1e3:.2f} ms kernel time (profiled: serialized)")
     print(f"{'kernel':70s} {'n':>4s} {'ms':>7s} {'%':>5s} {'mfma%':>6s} {'valu/mf':>7s} {'wait':>5s} {'instw':>5s} "
-          f"{'lds_cf':>6s} {'rdGB':>7s} {'wrGB':>7s} {'TB/s':>6s}")
+          f"{'lds_cf':>6s} {'rdGB':>7s} {'wrGB':>7s} {'TB/s':>6s} {'l2hit':>6s}")
     for k, t in sorted(dur.items(), key=lambda kv: -kv[1]):
         v = allc.get(k, {})
         g = lambda n: v.get(n, float("nan"))
@@ -74,7 +75,8 @@ def main():
               f"{100 * g('SQ_VALU_MFMA_BUSY_CYCLES') / max(g('GRBM_GUI_ACTIVE') * 4 * 32, 1):6.1f} "
               f"{g('SQ_INSTS_VALU') / max(g('SQ_INSTS_MFMA'), 1):7.2f} {g('SQ_WAIT_ANY') / wc:5.2f} "
               f"{g('SQ_WAIT_INST_ANY') / wc:5.2f} {g('SQ_LDS_BANK_CONFLICT') / max(g('SQ_LDS_IDX_ACTIVE'), 1):6.3f} "
-              f"{rd:7.3f} {wr:7.3f} {tbs:6.2f}")
+              f"{rd:7.3f} {wr:7.3f} {tbs:6.2f} "
+              f"{100 * g('TCC_HIT_sum') / max(g('TCC_HIT_sum') + g('TCC_MISS_sum'), 1):6.1f}")
 
 
 if __name__ == "__main__":
