@@ -650,7 +650,14 @@ void conv_wgrad_tile(int Cout, int K, int variant, int* bmw, int* bnw) {
 // narrow kernel legality: Cout <= 32, Cin % 8 == 0, K <= 128
 int wgrad_narrow_legal(int Cout, int Cin, int K) { return (Cout <= 32 && Cin % 8 == 0 && K <= 128) ? 1 : 0; }
 
+int wgrad_halo_legal(const WgradParams& p);
+void wgrad_halo_launch(const WgradParams& p, hipStream_t s);
+
 void conv_wgrad_launch(const WgradParams& p, int chunk, hipStream_t stream) {
+  if (p.variant >= 0 && (p.variant & 32)) {   // halo-staged kernel (wgrad_halo.hip); legality checked by the binding
+    wgrad_halo_launch(p, stream);
+    return;
+  }
   if (p.variant >= 0 && (p.variant & 16)) {   // narrow per-wave kernel: p.splits = waves, p_per_split = rows/wave
     if (p.Cout <= 16) launch_narrow_k<1>(p, stream); else launch_narrow_k<2>(p, stream);
     return;

@@ -26,6 +26,7 @@ void conv_igemm_set_bk(int bk);
 void conv_wgrad_launch(const WgradParams& p, int chunk, hipStream_t stream);
 void conv_wgrad_tile(int Cout, int K, int variant, int* bmw, int* bnw);
 int wgrad_narrow_legal(int Cout, int Cin, int K);
+int wgrad_halo_legal(const WgradParams& p);
 void wgrad_reduce_launch(float* accbuf, float* grad, int splits, int Cout, int taps, int Cin, int Cin_real,
                          float scale, float beta, int slab, hipStream_t stream);
 void bn_finalize_launch(const float* part, int tiles, int C, int64_t count, const float* gamma, const float* beta,
@@ -261,7 +262,8 @@ void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& par
   p.kt = g[12]; p.kh = g[13]; p.kw = g[14]; p.st = g[15]; p.sh = g[16]; p.sw = g[17];
   p.pt = g[18]; p.ph = g[19]; p.pw = g[20]; p.splits = g[21]; p.p_per_split = g[22];
   TORCH_CHECK(p.Cin % chunk == 0 && p.Cout % 8 == 0, "wgrad channel alignment");
-  TORCH_CHECK(p.p_per_split % 32 == 0, "p_per_split must be a multiple of 32");
+  const bool halo = variant >= 0 && (variant & 32);   // p_per_split = boxes per workgroup
+  TORCH_CHECK(halo || p.p_per_split % 32 == 0, "p_per_split must be a multiple of 32");
   TORCH_CHECK(variant < 0 || !(variant & 4) || p.p_per_split % 64 == 0, "64-position stages need p_per_split % 64 == 0");
   p.slab = (int)slab;
   p.variant = (int)variant;
@@ -276,6 +278,7 @@ void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& par
     TORCH_CHECK(p.ldd % 8 == 0 && p.ldx % 8 == 0, "narrow wgrad: 16-B rows");
     TORCH_CHECK(!dy_affine || (p.Cout == p.Cin && p.K == p.Cin), "narrow Gram: square 1x1");
   }
+  TORCH_CHECK(!halo || (wgrad_halo_legal(p) && chunk == 8 && p.p_per_split > 0), "halo wgrad not legal here");
   TORCH_CHECK(dy.numel() * 2 < 0xFFFFFF00ll && x.numel() * 2 < 0xFFFFFF00ll, "buffer extents must fit 32 bits");
   p.dybytes = (unsigned)(dy.numel() * 2);
   p.xbytes = (unsigned)(x.numel() * 2);
@@ -545,6 +548,16 @@ PYBIND11_MODULE(_C, m) {
     int* f = &q.M;
     for (int i = 0; i < 39 && i < (int)g.size(); ++i) f[i] = (int)g[i];
     return (int64_t)conv_igemm_ut_legal(q, (int)chunk, (int)bk);
+  });
+  m.def("wgrad_halo_legal", [](std::vector<int64_t> g, int64_t variant, int64_t affine) {
+    TORCH_CHECK(g.size() == 23, "wgrad geometry must have 23 entries");
+    WgradParams p{};
+    p.P = g[0]; p.Cout = g[1]; p.K = g[2]; p.Cin = g[3]; p.ldd = g[4]; p.ldx = g[5];
+    p.Ti = g[6]; p.Hi = g[7]; p.Wi = g[8]; p.To = g[9]; p.Ho = g[10]; p.Wo = g[11];
+    p.kt = g[12]; p.kh = g[13]; p.kw = g[14]; p.st = g[15]; p.sh = g[16]; p.sw = g[17];
+    p.pt = g[18]; p.ph = g[19]; p.pw = g[20]; p.splits = g[21]; p.p_per_split = g[22];
+    p.variant = (int)variant; p.affine = (int)affine;
+    return (int64_t)wgrad_halo_legal(p);
   });
   m.def("conv_pw_legal", [](std::vector<int64_t> g, int64_t chunk) {
     ConvParams q{};

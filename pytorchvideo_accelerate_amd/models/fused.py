@@ -183,6 +183,9 @@ class _ConvBN:
             if sp is None:
                 if cfg < 0:
                     sp = wgrad_splits(dy.M, s.cout, K, target_blocks=256 if slab else 1024) + (-1,)
+                elif cfg & 256:   # halo-staged kernel (wgrad_halo.hip): bit 9 = box option
+                    from ..ops.conv import halo_wgrad_plan
+                    sp = halo_wgrad_plan(s, dy.M, (dy.T, dy.H, dy.W), (cfg >> 9) & 1)
                 elif cfg & 128:   # narrow per-wave kernel: bits 2-3 = wave count target, 64 rows per chunk
                     nw = (1024, 2048, 4096)[(cfg >> 2) & 3]
                     pps = ((dy.M + nw - 1) // nw + 63) // 64 * 64
@@ -224,6 +227,16 @@ class _ConvBN:
                         cands.append(c)
                 if C.wgrad_narrow_legal(s.cout, s.cin_pad, K) and s.chunk == 8:
                     cands += [16 | 128 | (tbi << 2) for tbi in range(3)]
+                if not gram:   # halo-staged kernel, two box sizes
+                    from ..ops.conv import halo_wgrad_plan
+                    for o in (0, 1):
+                        plan = halo_wgrad_plan(s, dy.M, (dy.T, dy.H, dy.W), o)
+                        if plan is None:
+                            continue
+                        gh = [dy.M, s.cout, K, s.cin_pad, dy.ld, x.ld, x.T, x.H, x.W, dy.T, dy.H, dy.W,
+                              *s.k, *s.stride, *s.pad, plan[0], plan[1]]
+                        if C.wgrad_halo_legal(gh, plan[2], aff):
+                            cands.append(16 | 256 | (o << 9))
                 for c in cands:
                     launch(c, scratch, cs_scr)
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

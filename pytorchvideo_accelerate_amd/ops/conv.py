@@ -200,6 +200,42 @@ def wgrad_splits(P: int, Cout: int, K: int, target_blocks: int = 1024, min_rows:
     return splits, pps
 
 
+HALO = 32   # wgrad launch-word bit of the halo-staged kernel (csrc/kernels/wgrad_halo.hip)
+
+
+def halo_wgrad_plan(spec: "ConvSpec", P: int, dims: Tuple[int, int, int], option: int = 0,
+                    target_blocks: int = 512) -> Optional[Tuple[int, int, int]]:
+    """(workgroups along the boxes, boxes per workgroup, launch word) of the halo-staged weight gradient for a
+    stride-1 'same'-padded conv whose output grid is ``dims`` = (T, H, W), or None when the shape does not
+    suit it.  ``option`` picks the box: 0 ~128 positions, 1 ~256 (BT x BH rows of the full width)."""
+    T, H, W = dims
+    kt, kh, kw = spec.k
+    if tuple(spec.stride) != (1, 1, 1) or tuple(spec.pad) != ((kt - 1) // 2, (kh - 1) // 2, (kw - 1) // 2):
+        return None
+    if spec.taps == 1 or spec.cout > 128 or spec.cin_pad % 8 or spec.chunk != 8 or W >= 1024 or H >= 1024:
+        return None
+    target = 128 << option
+    BT = 1 if kt == 1 else min(T, 7, 2 << option)
+    BH = max(1, min(H, 15, target // max(1, BT * W)))
+    NT = (spec.cout + 15) // 16
+    if NT not in (1, 2, 4, 8):
+        return None
+    K = spec.taps * spec.cin_pad
+    KT = (K + 15) // 16
+    WK = 8 if KT >= 16 else (2 if KT >= 4 else 1)
+    wpl = {8: 0, 2: 2, 1: 3}[WK]
+    ktw_max = min(8, 24 // NT)   # accumulators <= 96 VGPRs (the box staging needs the rest)
+    groups = -(-KT // (WK * ktw_max))
+    ktb = -(-KT // groups)
+    if ktb > 255:
+        return None
+    nboxes = (P // (T * H * W)) * -(-T // BT) * -(-H // BH)
+    splits = max(1, min(nboxes, -(-target_blocks // groups)))
+    bps = -(-nboxes // splits)
+    splits = -(-nboxes // bps)
+    return splits, bps, HALO | (BH << 8) | (BT << 12) | (wpl << 15) | (ktb << 17)
+
+
 def conv_wgrad(dy: Act, x: Act, spec: ConvSpec, grad: torch.Tensor, workspace: Optional[torch.Tensor] = None,
                in_scale: Optional[torch.Tensor] = None, in_shift: Optional[torch.Tensor] = None,
                in_relu: bool = True, scale: float = 1.0, beta: float = 0.0,
@@ -207,7 +243,8 @@ def conv_wgrad(dy: Act, x: Act, spec: ConvSpec, grad: torch.Tensor, workspace: O
     """grad (fp32, [Cout, Cin, kt, kh, kw]) = beta*grad + scale * dW.
 
     ``variant``: -1 = heuristic tile; else bits 0-1 (+ bit 3 -> tiles 4-7) = tile (16x128, 32x128, 64x64, 128x64,
-    128x128, 256x128, 128x256, 256x256), bit 2 = 64-position LDS stages (two MFMA k-steps per barrier)."""
+    128x128, 256x128, 128x256, 256x256), bit 2 = 64-position LDS stages (two MFMA k-steps per barrier);
+    ``HALO | option`` (option 0/1 in bits 0-1) = the halo-staged kernel with box option ``option``."""
     C = require()
     P = dy.M
     K = spec.taps * spec.cin_pad
@@ -216,6 +253,10 @@ def conv_wgrad(dy: Act, x: Act, spec: ConvSpec, grad: torch.Tensor, workspace: O
         pps = ((P + nw - 1) // nw + 63) // 64 * 64
         splits_pps = ((P + pps - 1) // pps, pps)
         variant = 16
+    if splits_pps is None and variant >= 0 and variant & HALO and variant < 256:   # halo kernel, box option
+        plan = halo_wgrad_plan(spec, P, (dy.T, dy.H, dy.W), variant & 3)
+        assert plan is not None, "halo wgrad does not apply to this conv"
+        splits_pps, variant = plan[:2], plan[2]
     splits, pps = splits_pps or wgrad_splits(P, spec.cout, K, variant=(variant & 11) if variant >= 0 else -1)
     need = spec.cout * K
     if workspace is None or workspace.numel() < need:

@@ -538,3 +538,34 @@ def test_conv_big_tile_bn_epilogue(case):
             torch.testing.assert_close(s[2], (q * (y1.float() - mean1) * rstd1).sum(0), rtol=1e-3, atol=tol)
             ran += 1
     assert ran > 0
+
+
+HALO_CASES = [CASES[2], CASES[6], CASES[8], (16, 16, (1, 3, 3), (1, 1, 1), (0, 1, 1), (2, 3, 9, 13)),
+              (32, 8, (3, 1, 1), (1, 1, 1), (1, 0, 0), (2, 5, 7, 9)), (8, 8, (1, 3, 3), (1, 1, 1), (0, 1, 1), (1, 4, 17, 11)),
+              (128, 128, (1, 3, 3), (1, 1, 1), (0, 1, 1), (1, 2, 10, 12)), (64, 64, (3, 1, 1), (1, 1, 1), (1, 0, 0), (1, 6, 5, 7)),
+              (32, 32, (1, 3, 3), (1, 1, 1), (0, 1, 1), (2, 2, 14, 14))]
+
+
+@pytest.mark.parametrize("case", HALO_CASES)
+@pytest.mark.parametrize("affine", [False, True])
+@pytest.mark.parametrize("option", [0, 1])
+def test_conv_wgrad_halo(case, affine, option):
+    """Halo-staged weight gradient (stride-1 'same' convs): box wrap across rows and frames, partial boxes at
+    the T / H edges, padding taps, Cout < 16, k-tile groups, BN-ReLU recompute of the input."""
+    from pytorchvideo_accelerate_amd.ops.conv import HALO, halo_wgrad_plan
+    x, w, spec = _mk(case, seed=51)
+    C = spec.cin
+    sc = torch.rand(C, device=DEV) + 0.5
+    sh = torch.randn(C, device=DEV) * 0.5
+    xt = torch.relu(x * sc.view(1, C, 1, 1, 1) + sh.view(1, C, 1, 1, 1)) if affine else x
+    xt = xt.to(torch.bfloat16).float()
+    w.requires_grad_(True)
+    ref_y = torch.nn.functional.conv3d(xt, w, None, spec.stride, spec.pad)
+    gy = torch.randn_like(ref_y).to(torch.bfloat16).float()
+    ref_y.backward(gy)
+    dy = Act.from_ncthw(gy)
+    assert halo_wgrad_plan(spec, dy.M, (dy.T, dy.H, dy.W), option) is not None
+    grad = torch.zeros_like(w)
+    conv_wgrad(dy, Act.from_ncthw(x), spec, grad, in_scale=sc if affine else None,
+               in_shift=sh if affine else None, variant=HALO | option)
+    assert rel_err(grad, w.grad) < 1.5e-2
