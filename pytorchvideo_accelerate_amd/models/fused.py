@@ -792,8 +792,15 @@ class FusedNet:
         self._ws: Dict = {}
         self._splits: Dict = {}
         self._bnb: Dict = {}
-        self._scratch: Dict[str, torch.Tensor] = {}
+        self._scratch: Dict[Tuple, torch.Tensor] = {}
         self.grad_beta = 0.0
+        import os
+        self.lane = 0          # 0: main stream, 1: fast-pathway stream (per-lane scratch)
+        self._side = None
+        self._ms_warm = False  # set after the first training step (autotuning runs on one stream)
+        self._ms_bwd = False
+        self._ms_ok = (not deterministic and torch.device(device).type == "cuda"
+                       and os.environ.get("PVA_STREAMS", "1") != "0")
         import os
         # BN folding of the 1x1 conv_c (never materialise its output); units whose conv_c input has at least
         # fold_min_c channels (default: the slow pathway, where the Gram matrices run at MFMA speed)
@@ -869,8 +876,11 @@ class FusedNet:
         p = self.prof or []
         return [(a, e0.elapsed_time(e1)) for (a, e0), (_, e1) in zip(p, p[1:])]
 
-    def _progress(self, hi: int):
-        if self.grad_hook is not None:
+    def _progress(self, hi: int, force: bool = False):
+        """grad[:hi] is final on the current (main) stream.  During two-stream backward the per-block reports
+        are dropped: the stage's pathways finish in any order, so progress is reported once per stage after
+        the streams are joined (``force``)."""
+        if self.grad_hook is not None and (force or not self._ms_bwd):
             self.grad_hook(hi)
 
     # ------------------------------------------------------------------ buffers
@@ -882,14 +892,34 @@ class FusedNet:
         return t
 
     def scratch(self, key: str, numel: int, zero: bool = False) -> torch.Tensor:
-        """Grow-only fp32 scratch shared by sequential (stream-ordered) users.  ``zero``: allocated zeroed
-        (the wgrad accumulator is kept zero by its consumer, wgrad_reduce)."""
-        t = self._scratch.get(key)
+        """Grow-only fp32 scratch shared by sequential (stream-ordered) users of one lane (the main stream
+        and the fast-pathway stream each have their own).  ``zero``: allocated zeroed (the wgrad
+        accumulator is kept zero by its consumer, wgrad_reduce)."""
+        k = (key, self.lane)
+        t = self._scratch.get(k)
         if t is None or t.numel() < numel:
             alloc = torch.zeros if zero else torch.empty
             t = alloc(max(numel, 1 << 20), device=self.device, dtype=torch.float32)
-            self._scratch[key] = t
+            self._scratch[k] = t
         return t[:numel]
+
+    # ------------------------------------------------------------------ two-stream execution
+    def _ms_active(self) -> bool:
+        """The fast pathway runs on its own HIP stream, concurrently with the slow pathway (both are
+        independent between lateral fusions; the narrow fast-path kernels are latency-bound and fill the CUs
+        the slow path's MFMA kernels leave idle).  Off for the first (autotuning) step, in deterministic
+        mode, for single-pathway nets, under the per-op profiler and with ``PVA_STREAMS=0``."""
+        return (self._ms_ok and self._ms_warm and self.npath == 2 and self.prof is None)
+
+    def _side_stream(self):
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=self.device)
+        return self._side
+
+    def _join(self, waiter, signaller):
+        ev = torch.cuda.Event()
+        ev.record(signaller)
+        waiter.wait_event(ev)
 
     def _bn_blocks(self, M, C):
         k = (M, C)
@@ -943,27 +973,43 @@ class FusedNet:
         tag = "t" if train else "e"
         cur = list(xs)
         self._cats = []
+        ms = self._ms_active()
+        main = torch.cuda.current_stream(self.device) if ms else None
+        side = self._side_stream() if ms else None
+        if ms:
+            self._join(side, main)   # inputs were produced on the main stream
         for si, (paths, fuse) in enumerate(self.stages):
-            outs = []
+            outs = [None] * len(paths)
             cat = None
-            for p, mod in enumerate(paths):
+            # fast pathway first (issued to its own stream when two-stream execution is on)
+            for p in range(len(paths) - 1, -1, -1):
+                mod = paths[p]
                 x = cur[p]
                 T, H, W = mod.out_dims(x.T, x.H, x.W)
                 M = x.N * T * H * W
                 co = mod.out_channels()
                 if p == 0 and fuse is not None:
-                    fT, fH, fW = paths[1].out_dims(cur[1].T, cur[1].H, cur[1].W)
                     cat = self.ws(("cat", si, tag), (M, co + fuse.u.C), torch.bfloat16)
                     out = cat[:, :co]
                 else:
                     out = self.ws(("pout", si, p, tag), (M, co), torch.bfloat16)
-                outs.append(mod.fwd(x, out, train, tag))
+                if ms and p == 1:
+                    self.lane = 1
+                    with torch.cuda.stream(side):
+                        outs[p] = mod.fwd(x, out, train, tag)
+                    self.lane = 0
+                else:
+                    outs[p] = mod.fwd(x, out, train, tag)
             if fuse is not None:
+                if ms:
+                    self._join(main, side)   # the fusion reads the fast pathway's output
                 co = outs[0].C
                 fuse.fwd(outs[1], cat[:, co:], train, tag)
                 outs[0] = Act(cat, outs[0].N, outs[0].T, outs[0].H, outs[0].W)
             self._cats.append(cat)
             cur = outs
+        if ms:
+            self._join(main, side)
         return cur
 
     def _pool_features(self, outs: List[Act], tag: str) -> Tuple[torch.Tensor, List]:
@@ -1063,6 +1109,7 @@ class FusedNet:
             self._progress(self._head_hi)
             if train_backbone:
                 self._backward_backbone(outs, gfeat, ks)
+        self._ms_warm = True
         return loss[0], logits
 
     def _backward_backbone(self, outs: List[Act], gfeat: torch.Tensor, ks):
@@ -1077,28 +1124,52 @@ class FusedNet:
             C.avgpool_bwd(gfeat, Ctot, coff, [o.N, o.T, o.H, o.W, o.C], list(k), d)
             douts.append(Act(d, o.N, o.T, o.H, o.W))
             coff += o.C
+        ms = self._ms_active()
+        main = torch.cuda.current_stream(self.device) if ms else None
+        side = self._side_stream() if ms else None
+        self._ms_bwd = ms   # per-block progress reports are deferred to stage ends (grads come from two streams)
         for si in range(len(self.stages) - 1, -1, -1):
             paths, fuse = self.stages[si]
+            if ms:
+                self._join(main, side)   # the fast pathway's dx of the stage above is final
             # grads for this stage's pathway outputs: douts (slow may be the full concat grad)
             if fuse is not None:
                 dcat = douts[0]
                 co = paths[0].out_channels()
                 fuse.bwd(dcat.narrow(co, fuse.u.C), douts[1].t)
-                self._progress(fuse.flat_hi)
+                self._progress(fuse.flat_hi, force=True)
                 douts[0] = dcat.narrow(0, co)
+            if ms:
+                self._join(side, main)   # the fused dfast accumulation is complete
             new = [None] * len(paths)
             # pathways in reverse order: matches the flat (reverse-execution) gradient layout
             for p in range(len(paths) - 1, -1, -1):
                 mod = paths[p]
-                if isinstance(mod, _Stem):
-                    mod.bwd(douts[p])
-                    self._progress(mod.flat_hi)
-                else:
-                    xin = mod.blocks[0].x
-                    dx = self.ws(("dstage_in", si, p), (xin.M, xin.C), torch.bfloat16)
-                    mod.bwd(douts[p], dx, False)
-                    new[p] = Act(dx, xin.N, xin.T, xin.H, xin.W)
+                on_side = ms and p == 1
+                if on_side:
+                    self.lane = 1
+                    ctx = torch.cuda.stream(side)
+                    ctx.__enter__()
+                try:
+                    if isinstance(mod, _Stem):
+                        mod.bwd(douts[p])
+                        if not ms:
+                            self._progress(mod.flat_hi)
+                    else:
+                        xin = mod.blocks[0].x
+                        dx = self.ws(("dstage_in", si, p), (xin.M, xin.C), torch.bfloat16)
+                        mod.bwd(douts[p], dx, False)
+                        new[p] = Act(dx, xin.N, xin.T, xin.H, xin.W)
+                finally:
+                    if on_side:
+                        ctx.__exit__(None, None, None)
+                        self.lane = 0
+            if ms:
+                self._join(main, side)
+                self._progress(max(m.flat_hi if isinstance(m, _Stem) else m.blocks[0].flat_hi for m in paths),
+                               force=True)
             douts = new
+        self._ms_bwd = False
 
     # ------------------------------------------------------------------ misc
     def prepare_inputs(self, xs_ncthw: Sequence[torch.Tensor]) -> List[Act]:

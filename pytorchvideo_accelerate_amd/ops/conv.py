@@ -207,16 +207,35 @@ def halo_wgrad_plan(spec: "ConvSpec", P: int, dims: Tuple[int, int, int], option
                     target_blocks: int = 512) -> Optional[Tuple[int, int, int]]:
     """(workgroups along the boxes, boxes per workgroup, launch word) of the halo-staged weight gradient for a
     stride-1 'same'-padded conv whose output grid is ``dims`` = (T, H, W), or None when the shape does not
-    suit it.  ``option`` picks the box: 0 ~128 positions, 1 ~256 (BT x BH rows of the full width)."""
+    suit it.  ``option`` picks the box size: 0 ~32 KB, 1 ~64 KB staged (BT frames x BH rows of the full width)."""
     T, H, W = dims
     kt, kh, kw = spec.k
     if tuple(spec.stride) != (1, 1, 1) or tuple(spec.pad) != ((kt - 1) // 2, (kh - 1) // 2, (kw - 1) // 2):
         return None
     if spec.taps == 1 or spec.cout > 128 or spec.cin_pad % 8 or spec.chunk != 8 or W >= 1024 or H >= 1024:
         return None
-    target = 128 << option
-    BT = 1 if kt == 1 else min(T, 7, 2 << option)
-    BH = max(1, min(H, 15, target // max(1, BT * W)))
+    # box size by bytes staged per box (dY + halo): ~32 KB (option 0) / ~64 KB (option 1); rows first (up to
+    # the full height), then frames (a kt=1 box of several frames is several 2-D halos)
+    target = (32 << 10) << option
+    coutp = (spec.cout + 15) // 16 * 16
+    per_pos = 2 * (coutp + spec.cin_pad)
+    BT = 1 if kt == 1 else 2
+    BH = max(1, min(H, 15, target // max(1, per_pos * BT * W)))
+    if BH >= H:
+        BT = max(BT, min(T, 7, target // max(1, per_pos * H * W)))
+
+    def fits(bt, bh):   # the kernel's staging limits (wgrad_halo.hip: HX_RA / HX_RB registers, LDS budget)
+        pbp = (bt * bh * W + 31) // 32 * 32
+        hp = (bt + kt - 1) * (bh + kh - 1) * (W + kw - 1)
+        lds = pbp * coutp * 2 + hp * spec.cin_pad * 2 + (2 * pbp + hp) * 4 + spec.cin_pad * 8
+        return pbp * coutp // 8 <= 4 * 512 and hp * spec.cin_pad // 8 <= 6 * 512 and lds <= 150 * 1024
+    while not fits(BT, BH) and (BT > (1 if kt == 1 else 2) or BH > 1):
+        if BT > (1 if kt == 1 else 2):
+            BT -= 1
+        else:
+            BH -= 1
+    if not fits(BT, BH):
+        return None
     NT = (spec.cout + 15) // 16
     if NT not in (1, 2, 4, 8):
         return None

@@ -160,3 +160,24 @@ def test_deterministic_mode_is_bitwise_reproducible():
         losses.append(loss.item())
     assert torch.equal(grads[0], grads[1]) and losses[0] == losses[1]
     assert abs(losses[2] - losses[0]) < 0.05 * abs(losses[0])
+
+
+def test_two_stream_step_matches_single_stream():
+    """The fast pathway on its own HIP stream (after the autotuning step) gives the same loss and gradients
+    as the single-stream schedule on the same inputs (up to fp32-atomic ordering in the weight gradients)."""
+    model = _build(True)
+    eng = FusedNet(model, DEV)
+    acts = eng.prepare_inputs(_inputs(True, seed=3))
+    labels = torch.tensor([2, 5], device=DEV)
+    eng.forward_backward(acts, labels)          # tuning step, single stream
+    assert eng._ms_ok and eng._ms_warm and eng._ms_active()
+    res = {}
+    for ms in (False, True):
+        eng._ms_ok = ms
+        loss, logits = eng.forward_backward(acts, labels, accumulate=False)
+        torch.cuda.synchronize()
+        res[ms] = (float(loss), logits.clone(), eng.flat.grad.clone())
+    (l0, g0_logits, g0), (l1, g1_logits, g1) = res[False], res[True]
+    assert abs(l0 - l1) < 1e-4 * max(1.0, abs(l0))
+    assert _rel(g1_logits, g0_logits) < 1e-4
+    assert _rel(g1, g0) < 1e-3
