@@ -153,17 +153,39 @@ def run(a):
         bounds = sorted(set(eng.flat.span(p)[1] for p in eng.flat.params))
         sync = GradSync(eng.flat.grad, st, a.bucket_mb, boundaries=bounds, first_mb=a.first_bucket_mb,
                         grad_dtype=gdt, timing=st.world_size > 1)
-        eng.grad_hook = sync.progress
+        eng.grad_hook = sync.progress if st.world_size > 1 else None   # (1 GPU: no buckets to launch)
         gen = torch.Generator().manual_seed(1000 + st.rank)
         frames = torch.empty(B, a.src_frames, a.src_h, a.src_w, 3, dtype=torch.uint8, device=dev)
         eng.C.synth_frames(frames, 7 + st.rank)
-        prep = GpuClipBatch(dev, a.frames, a.crop, a.alpha, s2d=eng.input_s2d)
+        # double-buffered on-device preprocessing: micro-batch k+1 is decoded/resized/cropped on its own
+        # stream while micro-batch k trains (a prefetching data loader; every step still pays its batch)
+        preps = [GpuClipBatch(dev, a.frames, a.crop, a.alpha, s2d=eng.input_s2d) for _ in range(2)]
+        pstream = torch.cuda.Stream(dev)
+        pending = {}
         labels_all = torch.randint(0, a.classes, (64, B), generator=gen).to(dev)
 
-        def step(i, tune=False):
+        def prefetch(k):
             params = [sample_params(a.src_frames, a.src_h, a.src_w, a.frames, a.crop, True, generator=gen)
                       for _ in range(B)]
-            xs = prep(frames, params)
+            free = torch.cuda.Event()
+            free.record()   # everything issued so far (the last reader of this buffer) precedes the refill
+            with torch.cuda.stream(pstream):
+                pstream.wait_event(free)
+                xs = preps[k % 2](frames, params)
+                ready = torch.cuda.Event()
+                ready.record(pstream)
+            pending[k] = (xs, ready)
+
+        def batch(k):
+            if k not in pending:
+                prefetch(k)
+            xs, ready = pending.pop(k)
+            torch.cuda.current_stream().wait_event(ready)
+            prefetch(k + 1)
+            return xs
+
+        def step(i, tune=False):
+            xs = batch(-1 if tune else i * a.grad_accum)
             if tune:
                 # untimed autotuning pass: every conv geometry is tuned (ranks agree on the choice) with
                 # no gradient all-reduce in flight and no optimizer step (weights stay rank-identical)
@@ -173,7 +195,7 @@ def run(a):
             opt.zero_grad()
             for j in range(a.grad_accum):
                 if j:
-                    xs = prep(frames, params)
+                    xs = batch(i * a.grad_accum + j)
                 last = j == a.grad_accum - 1
                 sync.begin(last)
                 loss, _ = eng.forward_backward(xs, labels_all[(i * a.grad_accum + j) % 64],
@@ -249,7 +271,8 @@ def run(a):
             "vs_baseline": round(clips / (STOCK_CLIPS_PER_S_1GPU * st.world_size), 3) if headline else None,
             "dtype": "fp32" if a.plumbing else "bf16",
             "data": ("synthetic normal clips, CPU plumbing run" if a.plumbing else
-                     "synthetic uint8 decoded clips (64x256x340), on-device preprocessing; random-init weights"),
+                     "synthetic uint8 decoded clips (64x256x340), on-device preprocessing (next batch prefetched "
+                     "on a side stream); random-init weights"),
             "config": {"model": f"SlowFast-R{a.depth} {a.frames}x2x{a.crop}",
                        "global_batch": B * a.grad_accum * st.world_size,
                        "per_gpu_batch": B, "grad_accum": a.grad_accum, "seq_len": a.frames,

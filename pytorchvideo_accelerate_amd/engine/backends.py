@@ -103,7 +103,7 @@ class FusedBackend:
         self.flat = self.net.flat
         bounds = sorted(set(self.flat.span(p)[1] for p in self.flat.params))
         self.sync = GradSync(self.flat.grad, state, bucket_mb, boundaries=bounds)
-        self.net.grad_hook = self.sync.progress
+        self.net.grad_hook = self.sync.progress if state.world_size > 1 else None
         # fp16 requests get the dynamic loss-scale state machine (compute stays bf16 MFMA)
         self.scaler = FusedGradScaler() if mixed_precision == "fp16" else None
         self._training = True

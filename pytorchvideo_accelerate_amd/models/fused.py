@@ -29,6 +29,7 @@ Semantics follow the pytorchvideo modules in ``models/reference.py`` (reference 
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
@@ -255,6 +256,26 @@ class _ConvBN:
                           + " ".join("%d=%.1fus" % (c, 1e3 * t / 3) for c, t in zip(cands, times))
                           + " -> %d" % cfg, file=sys.stderr, flush=True)
             eng.wtune[tkey] = cfg
+        # off the critical path: a weight gradient that lands in the flat buffer runs on the lane's wgrad
+        # stream, concurrently with the dgrad chain (its inputs are per-unit buffers nothing rewrites before
+        # the end-of-backward join)
+        wst = eng._wgrad_stream() if (dest is None and not gram and not slab and eng._ms_active()) else None
+        if wst is not None:
+            src = torch.cuda.current_stream(eng.device)
+            ev = torch.cuda.Event()
+            ev.record(src)
+            wst.wait_event(ev)
+            lane0 = eng.lane
+            eng.lane = 2 + lane0
+            try:
+                with torch.cuda.stream(wst):
+                    part = eng.scratch("wgrad_acc", s.cout * K, zero=True)
+                    splits = launch(cfg, part, colsum)
+                    C.wgrad_reduce(part, eng.flat.gview(self.conv.weight), splits, s.cout, s.taps, s.cin_pad, s.cin,
+                                   1.0, eng.grad_beta, 0)
+            finally:
+                eng.lane = lane0
+            return splits
         if slab:  # per-split slabs summed in a fixed order: bitwise reproducible weight gradients
             part = eng.scratch("wgrad_slab", geometry(cfg)[0] * s.cout * K)
         else:     # fp32 atomics into one zeroed accumulator (kept zero by wgrad_reduce)
@@ -799,6 +820,8 @@ class FusedNet:
         self._side = None
         self._ms_warm = False  # set after the first training step (autotuning runs on one stream)
         self._ms_bwd = False
+        self._wst = [None, None]          # weight-gradient streams of the two lanes
+        self._wst_used = [False, False]
         self._ms_ok = (not deterministic and torch.device(device).type == "cuda"
                        and os.environ.get("PVA_STREAMS", "1") != "0")
         import os
@@ -881,6 +904,8 @@ class FusedNet:
         are dropped: the stage's pathways finish in any order, so progress is reported once per stage after
         the streams are joined (``force``)."""
         if self.grad_hook is not None and (force or not self._ms_bwd):
+            if force:
+                self._join_wgrads()   # the bucket's weight gradients may still be in flight on the wgrad streams
             self.grad_hook(hi)
 
     # ------------------------------------------------------------------ buffers
@@ -913,8 +938,25 @@ class FusedNet:
 
     def _side_stream(self):
         if self._side is None:
-            self._side = torch.cuda.Stream(device=self.device)
+            # PVA_SIDE_PRIORITY: HIP stream priority of the fast-pathway stream (lower = higher priority)
+            self._side = torch.cuda.Stream(device=self.device,
+                                           priority=int(os.environ.get("PVA_SIDE_PRIORITY", "0")))
         return self._side
+
+    def _wgrad_stream(self):
+        """The weight-gradient stream of the current lane (0: main, 1: fast pathway)."""
+        i = self.lane
+        if self._wst[i] is None:
+            self._wst[i] = torch.cuda.Stream(device=self.device)
+        self._wst_used[i] = True
+        return self._wst[i]
+
+    def _join_wgrads(self):
+        main = torch.cuda.current_stream(self.device)
+        for i, st in enumerate(self._wst):
+            if st is not None and self._wst_used[i]:
+                self._join(main, st)
+                self._wst_used[i] = False
 
     def _join(self, waiter, signaller):
         ev = torch.cuda.Event()
@@ -1169,6 +1211,8 @@ class FusedNet:
                 self._progress(max(m.flat_hi if isinstance(m, _Stem) else m.blocks[0].flat_hi for m in paths),
                                force=True)
             douts = new
+        if ms:
+            self._join_wgrads()
         self._ms_bwd = False
 
     # ------------------------------------------------------------------ misc
