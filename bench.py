@@ -80,7 +80,8 @@ def self_launch(a, argv) -> int:
 
     Called before anything initialises the GPU (``torch.cuda.device_count`` does not), and never via
     exec: the child is a separate process and this one only waits for it."""
-    if not a.plumbing:
+    # PVA_DIST_BACKEND=gloo: a 1-GPU rehearsal of the multi-rank path (ranks share the device)
+    if not a.plumbing and os.environ.get("PVA_DIST_BACKEND") != "gloo":
         ndev = torch.cuda.device_count()
         if ndev < a.gpus:
             print(f"bench.py: --gpus {a.gpus} requested but only {ndev} GPU(s) visible", file=sys.stderr)
