@@ -57,6 +57,14 @@ __device__ __forceinline__ void rs16(float (&v)[L], int lane) {
   if (L == 8) v[0] += __shfl_xor(v[0], 1, 64);
 }
 
+// 16-B output store; NT: non-temporal (streaming) store hint
+template <bool NT>
+__device__ __forceinline__ void st16(uint16_t* dst, const uint4& v) {
+  typedef __attribute__((ext_vector_type(4))) unsigned u32x4_t;
+  if constexpr (NT) __builtin_nontemporal_store(u32x4_t{v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4_t*>(dst));
+  else *reinterpret_cast<uint4*>(dst) = v;
+}
+
 // epilogue operands of one 32-channel chunk (members an epilogue does not use are optimised away)
 template <int TM>
 struct Pre {
@@ -64,7 +72,7 @@ struct Pre {
   unsigned bits[TM];
 };
 
-template <int KS, int TM, int EP, int AFF>
+template <int KS, int TM, int EP, int AFF, bool NTS>
 __global__ __launch_bounds__(PW_THREADS) void conv_pw_kernel(const ConvParams p, int rpb, int gch) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NST = EP == 2 ? 3 : 2;
@@ -227,7 +235,7 @@ __global__ __launch_bounds__(PW_THREADS) void conv_pw_kernel(const ConvParams p,
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = fmaxf(__builtin_fmaf(v[e], cb[e], c2[e]) + r[e], 0.f);
           const uint4 pk = pack8_fast(v);
-          *reinterpret_cast<uint4*>(p.y + (int64_t)m * p.ldy + n) = pk;
+          st16<NTS>(p.y + (int64_t)m * p.ldy + n, pk);
           const uint32_t w4[4] = {pk.x, pk.y, pk.z, pk.w};
           unsigned bits = 0;
 #pragma unroll
@@ -242,7 +250,7 @@ __global__ __launch_bounds__(PW_THREADS) void conv_pw_kernel(const ConvParams p,
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] += cb[e] + o[e];
           const uint4 pk = pack8_fast(v);
-          *reinterpret_cast<uint4*>(p.y + (int64_t)m * p.ldy + n) = pk;
+          st16<NTS>(p.y + (int64_t)m * p.ldy + n, pk);
           if (do_stats) {
             float q[8];
             unpack8(pk, q);
@@ -266,7 +274,7 @@ __global__ __launch_bounds__(PW_THREADS) void conv_pw_kernel(const ConvParams p,
             v[e] = (bits >> e) & 1u ? t : 0.f;
           }
           const uint4 pk = pack8_fast(v);
-          *reinterpret_cast<uint4*>(p.y + (int64_t)m * p.ldy + n) = pk;
+          st16<NTS>(p.y + (int64_t)m * p.ldy + n, pk);
           if (do_stats) {
             float q[8], y1[8];
             unpack8(pk, q);
@@ -308,19 +316,27 @@ __global__ __launch_bounds__(PW_THREADS) void conv_pw_kernel(const ConvParams p,
   }
 }
 
-template <int KS, int TM, int EP>
-void launch_ep(const ConvParams& p, int rpb, int gch, size_t lds, hipStream_t st) {
+template <int KS, int TM, int EP, bool NTS>
+void launch_ep_nt(const ConvParams& p, int rpb, int gch, size_t lds, hipStream_t st) {
   const int ngrp = ((p.Ngemm >> 5) + gch - 1) / gch;
   const dim3 grid(((p.M + rpb - 1) / rpb) * ngrp), block(PW_THREADS);
   if constexpr (EP == 2) {
-    hipLaunchKernelGGL((conv_pw_kernel<KS, TM, 2, 0>), grid, block, lds, st, p, rpb, gch);
+    hipLaunchKernelGGL((conv_pw_kernel<KS, TM, 2, 0, NTS>), grid, block, lds, st, p, rpb, gch);
   } else {
     switch (p.affine) {
-      case 0: hipLaunchKernelGGL((conv_pw_kernel<KS, TM, EP, 0>), grid, block, lds, st, p, rpb, gch); break;
-      case 1: hipLaunchKernelGGL((conv_pw_kernel<KS, TM, EP, 1>), grid, block, lds, st, p, rpb, gch); break;
-      default: hipLaunchKernelGGL((conv_pw_kernel<KS, TM, EP, 2>), grid, block, lds, st, p, rpb, gch); break;
+      case 0: hipLaunchKernelGGL((conv_pw_kernel<KS, TM, EP, 0, NTS>), grid, block, lds, st, p, rpb, gch); break;
+      case 1: hipLaunchKernelGGL((conv_pw_kernel<KS, TM, EP, 1, NTS>), grid, block, lds, st, p, rpb, gch); break;
+      default: hipLaunchKernelGGL((conv_pw_kernel<KS, TM, EP, 2, NTS>), grid, block, lds, st, p, rpb, gch); break;
     }
   }
+}
+
+// non-temporal (streaming) output stores for the BN-folded residual output, whose 16-B rows are never
+// re-read while L2-resident (measured +8 % on the res2 shape, scripts/pw_probe.py); the other epilogues
+// measured 1-3 % slower with them
+template <int KS, int TM, int EP>
+void launch_ep(const ConvParams& p, int rpb, int gch, size_t lds, hipStream_t st) {
+  launch_ep_nt<KS, TM, EP, EP == 1>(p, rpb, gch, lds, st);
 }
 
 // forward epilogues: 64-row tiles (32 at K > 128); the backward-BN epilogue carries 4 operand rows per
