@@ -70,6 +70,14 @@ def main():
             timeit(lambda: C.conv_igemm_epi(dy, wd2, out, 0, dgeo, 8, res, N, mask, None, None, None, None, None,
                                             None, part, None, None, cfg)),
             (dy.numel() + out.numel() + res.numel()) * 2 + mask.numel())
+    # BN-backward apply (dy = A dz*mask + B y + C) at the same shape: reads g, y, mask bits; writes dy
+    y = res
+    coef = torch.randn(3 * N, device=dev)
+    mbits = torch.randint(0, 255, (M, N // 8), dtype=torch.uint8, device=dev)
+    rep("bn_bwd_apply [M,256] mask bits",
+        timeit(lambda: C.bn_bwd_apply(out, N, 3, mbits, N // 8, None, None, y, coef, big, None, None, None, None, 0,
+                                      0, M, N)),
+        3 * out.numel() * 2 + mbits.numel())
     for cfg in (-1,):
         rep("igemm heuristic plain", timeit(lambda: C.conv_igemm(x, wf, out, None, None, None, 0, 0, geo, 8, cfg)),
             (x.numel() + out.numel()) * 2)
