@@ -8,7 +8,7 @@
 // hardware-transpose LDS read ds_read_b64_tr_b16 (cdna_hip_programming.md T10): one 16-lane group
 // reads a 4(p) x 16(col) block and each lane receives one column's 4 p-values.  32-byte column
 // segments are XOR-swizzled with row bits 1 and 3 so the 8 rows a 32-lane half touches land on
-// disjoint bank groups.  The p axis is split over gridDim.z slices whose fp32 tiles are added into one
+// disjoint bank groups.  The p axis is split into slices (XCD-local with their tiles) whose fp32 tiles are added into one
 // accumulator with no-return float atomics (≈1.3 TB/s chip-wide; a serial slab reduce was 17 % of the
 // step); wgrad_reduce then scatters it into PyTorch's [Cout][Cin][kt][kh][kw] layout, accumulating into
 // the fp32 master-gradient buffer, and re-zeroes the accumulator.
@@ -63,9 +63,16 @@ void conv_wgrad_kernel(const WgradParams p) {
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / NWN, wn = wid % NWN;
-  const int n0 = blockIdx.x * BMW;           // cout tile
-  const int k0 = blockIdx.y * BNW;           // k tile
-  const int split = blockIdx.z;
+  // 1-D grid, XCD-aware: the (cout, k) tiles of one position split get consecutive logical ids, which the
+  // bijective remap keeps on one XCD, so the split's dY / im2col rows are fetched from HBM once and served
+  // to the other tiles from that XCD's L2 (the hardware spreads consecutive workgroups over the 8 XCDs)
+  const int ntn = (p.Cout + BMW - 1) / BMW, ntk = (p.K + BNW - 1) / BNW;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = lid / (ntn * ntk);
+  const int tile = lid - split * ntn * ntk;
+  const int kt_idx = tile / ntn;
+  const int n0 = (tile - kt_idx * ntn) * BMW;   // cout tile
+  const int k0 = kt_idx * BNW;                   // k tile
   const int p_begin = split * p.p_per_split;
   const int p_end = min(p.P, p_begin + p.p_per_split);
   const int affine = p.affine;
@@ -88,7 +95,7 @@ void conv_wgrad_kernel(const WgradParams p) {
     dsh[e] = (dy_aff && a_col_ok) ? p.in_shift[a_n + e] : 0.f;
     csum[e] = 0.f;
   }
-  const bool do_csum = dy_aff && p.colsum != nullptr && blockIdx.y == 0;
+  const bool do_csum = dy_aff && p.colsum != nullptr && kt_idx == 0;
   unsigned ra_valid = ~0u;
   int a_vo[A_SLOTS], a_row[A_SLOTS], sa[A_SLOTS];
 #pragma unroll
@@ -371,7 +378,7 @@ void conv_wgrad_kernel(const WgradParams p) {
   // with several, slabs accumulate into one zero-initialised fp32 buffer with no-return
   // global_atomic_add_f32 (each wave-instruction = 4 rows x 64 contiguous bytes).
   // deterministic (slab) mode: every split stores its own slab; the convert kernel sums them in order
-  float* out = p.partial + (p.slab ? (int64_t)blockIdx.z * p.Cout * p.K : 0);
+  float* out = p.partial + (p.slab ? (int64_t)split * p.Cout * p.K : 0);
   const bool atomic = p.splits > 1 && !p.slab;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -571,7 +578,7 @@ void launch_narrow_k(const WgradParams& p, hipStream_t stream) {
 template <int BMW, int BNW, int WMW, int WNW, int CH, int BP>
 void launch_w(const WgradParams& p, hipStream_t stream) {
   constexpr int NT = (BMW / WMW) * (BNW / WNW) * 64;
-  dim3 grid((p.Cout + BMW - 1) / BMW, (p.K + BNW - 1) / BNW, p.splits);
+  const dim3 grid(((p.Cout + BMW - 1) / BMW) * ((p.K + BNW - 1) / BNW) * p.splits);
   const size_t lds = 2 * BP * (BMW + BNW) * 2;
   const bool dense = p.kt == 1 && p.kh == 1 && p.kw == 1 && p.st == 1 && p.sh == 1 && p.sw == 1 &&
                      p.pt == 0 && p.ph == 0 && p.pw == 0;

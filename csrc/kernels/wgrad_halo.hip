@@ -17,7 +17,7 @@
 //     the next box's loads are issued before the current box's MFMAs (one barrier pair per box for the LDS
 //     hand-over).  The producer's BN+ReLU is recomputed on the halo when it is stored (padding stays zero).
 // Launch word (WgradParams::variant): bit 5 = this kernel; bits 8-11 BH, 12-14 BT, 15-16 log2 WP,
-// 17-24 k-tiles per workgroup (gridDim.y = k-tile groups); p_per_split = boxes per workgroup.
+// 17-24 k-tiles per workgroup (k-tile groups x box splits, XCD-local); p_per_split = boxes per workgroup.
 // (WP = 1, 4 or 8; NTW = 1, 2, 4 or 8 n-tiles of 16 = Cout rounded up.)
 #include "common.h"
 #include "conv_params.h"
@@ -94,7 +94,11 @@ __global__ __launch_bounds__(HX_THREADS) void wgrad_halo_kernel(const WgradParam
   // this wave's k-tiles: per-lane (halo row offset of the tap, column byte) of the 4 columns it supplies
   const int KT = (p.K + 15) >> 4;
   const int ktb = (p.variant >> 17) & 255;
-  const int kt0 = blockIdx.y * ktb;
+  // 1-D XCD-aware grid: the k-tile groups of one box range are neighbours on one XCD (its L2 serves them)
+  const int ngroups = (KT + ktb - 1) / ktb;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int bsplit = lid / ngroups;
+  const int kt0 = (lid - bsplit * ngroups) * ktb;
   const int kt_end = min(KT, kt0 + ktb);
   int ktoff[KTW], kcolb[KTW];
   bool kok[KTW];
@@ -204,7 +208,7 @@ __global__ __launch_bounds__(HX_THREADS) void wgrad_halo_kernel(const WgradParam
     }
   };
 
-  const int box0 = blockIdx.x * p.p_per_split;
+  const int box0 = bsplit * p.p_per_split;
   const int box1 = min(G.nboxes, box0 + p.p_per_split);
   const int nchunk = G.PBp >> 5;
   __syncthreads();   // tables
@@ -326,7 +330,7 @@ int wgrad_halo_legal(const WgradParams& p) {
 void wgrad_halo_launch(const WgradParams& p, hipStream_t s) {
   const HostGeo h = host_geo(p);
   const int splits = (h.nboxes + p.p_per_split - 1) / p.p_per_split;
-  const dim3 grid(splits, (h.KT + h.ktb - 1) / h.ktb);
+  const dim3 grid(splits * ((h.KT + h.ktb - 1) / h.ktb));
   switch (h.ntw) {
     case 1: launch_wp<1>(p, h.wpl, h.ktw, grid, h.lds, s); break;
     case 2: launch_wp<2>(p, h.wpl, h.ktw, grid, h.lds, s); break;
