@@ -29,7 +29,8 @@ DIRECT_2K = 64        #   with 2048 rows per workgroup (else 512)
 DMA = 128             # uniform-tap loader staged by LDS-DMA (buffer_load ... lds); launches without input affine
 BIG = 256             # 256x256 tile of 8 waves (N >= 256; the backward-BN epilogue in 64-row slices)
 PW = 512              # streaming pointwise kernel (csrc/kernels/conv_pw.hip): dense 1x1x1 GEMMs, K <= 256,
-PW_ROWS = (1024, 2048, 4096)   # N % 32 == 0, weights in LDS; bits 0-1 select the rows per workgroup
+PW_ROWS = (1024, 2048, 4096)   # N % 32 == 0, weights in LDS; bits 0-1 select the rows per workgroup,
+PW_SOLO = 4                     # bit 2 one workgroup per CU
 TILE_BN = (128, 64, 32, 16)   # variants 0..3
 TILE_BM = (128, 128, 256, 256)
 
@@ -39,7 +40,7 @@ def describe(cfg: int) -> str:
     if cfg < 0 or not cfg & EXPLICIT:
         return "heuristic"
     if cfg & PW:
-        return "pw%d" % PW_ROWS[cfg & 3]
+        return "pw%d%s" % (PW_ROWS[cfg & 3], "s" if cfg & PW_SOLO else "")
     if cfg & DIRECT:
         return "direct%d" % (2048 if cfg & DIRECT_2K else 512)
     if cfg & BIG:
@@ -59,6 +60,13 @@ class ConvTuner:
         self.direct = os.environ.get("PVA_CONV_DIRECT", "1") != "0"
         self.dma = os.environ.get("PVA_CONV_DMA", "1") != "0"
         self.pw = os.environ.get("PVA_CONV_PW", "1") != "0"
+        # debugging aid: PVA_PW_KINDS=f,fres,er,... restricts the pointwise kernel to launches whose key
+        # starts with one of these kinds (models/fused.py: f fres fw2 eb er d)
+        kinds = os.environ.get("PVA_PW_KINDS")
+        self.pw_kinds = None if kinds is None else set(k for k in kinds.split(",") if k)
+        self._pw_now = True
+        self.pw_only: Optional[int] = None   # debugging aid: allow the pointwise kernel on the n-th PW-legal tuning only
+        self._pw_seen = 0
         self.log = os.environ.get("PVA_TUNE_LOG", "0") != "0"
         self.reps = reps
         self.cache: Dict[Tuple, int] = {}
@@ -97,8 +105,10 @@ class ConvTuner:
                         out.append(w | DMA)
         if direct and self.direct and self.C.conv_direct_legal(list(g), chunk):
             out += [EXPLICIT | DIRECT, EXPLICIT | DIRECT | DIRECT_2K]
-        if self.pw and self.C.conv_pw_legal(list(g), chunk):
-            out += [EXPLICIT | PW | v for v in range(len(PW_ROWS))]
+        if self.pw and self._pw_now and self.C.conv_pw_legal(list(g), chunk):
+            self._pw_seen += 1
+            if self.pw_only is None or self.pw_only == self._pw_seen - 1:
+                out += [EXPLICIT | PW | s | v for s in (0, PW_SOLO) for v in range(len(PW_ROWS))]
         return out
 
     def bm(self, cfg: int, N: int) -> int:
@@ -122,7 +132,9 @@ class ConvTuner:
         epilogue the direct kernel lacks (fused residual output, bias)."""
         cfg = self.cache.get(key)
         if cfg is None:
+            self._pw_now = self.pw_kinds is None or (len(key) > 0 and key[0] in self.pw_kinds)
             cfg = self._tune(g, chunk, run, aff, epi, direct) if self.enabled else -1
+            self._pw_now = True
             self.cache[key] = cfg
         run(cfg, False)
         return cfg

@@ -47,29 +47,45 @@ def main():
         print("%-40s %8.1f us %6.2f TB/s" % rows[-1], flush=True)
 
     rep("torch copy [M,256]", timeit(lambda: big.copy_(res)), 2 * res.numel() * 2)
-    for v in range(3):
+    for v in (0, 1, 2, 4, 5, 6):
         cfg = EXPLICIT | PW | v
         r = C.conv_cfg_bm(cfg, N)
         stats = torch.empty((M + r - 1) // r, 2, N, device=dev)
-        rep("pw%d plain" % r, timeit(lambda: C.conv_igemm(x, wf, out, None, None, None, 0, 0, geo, 8, cfg)),
+        rep("pw%d%s plain" % (r, "s" * (v >> 2)), timeit(lambda: C.conv_igemm(x, wf, out, None, None, None, 0, 0, geo, 8, cfg)),
             (x.numel() + out.numel()) * 2)
-        rep("pw%d stats+affine" % r, timeit(lambda: C.conv_igemm(x, wf, out, stats, ksc, ksh, 2, 0, geo, 8, cfg)),
+        rep("pw%d%s stats+affine" % (r, "s" * (v >> 2)), timeit(lambda: C.conv_igemm(x, wf, out, stats, ksc, ksh, 2, 0, geo, 8, cfg)),
             (x.numel() + out.numel()) * 2)
-        rep("pw%d fres" % r, timeit(lambda: C.conv_igemm_fres(x, wf, out, ksc, ksh, 2, geo, 8, cfg, sc, sh, res, N,
+        rep("pw%d%s fres" % (r, "s" * (v >> 2)), timeit(lambda: C.conv_igemm_fres(x, wf, out, ksc, ksh, 2, geo, 8, cfg, sc, sh, res, N,
                                                              None, None, mask)),
             (x.numel() + out.numel() + res.numel()) * 2 + mask.numel())
     # backward-BN epilogue: conv_a dgrad of res2 (dy [M,64] -> dx [M,256]) with residual, mask, partials
     dy = x
     dgeo = list(dgrad_phases(ConvSpec(N, K, (1, 1, 1)), 1, (1, M, 1), (1, M, 1), K, N)[0])
     _, wd2 = pack_weight(torch.randn(K, N, 1, 1, 1, device=dev) * 0.1, ConvSpec(N, K, (1, 1, 1)))
-    for v in range(3):
+    for v in (0, 1, 2, 4, 5, 6):
         cfg = EXPLICIT | PW | v
         r = C.conv_cfg_bm(cfg, N)
         part = torch.empty((M + r - 1) // r, 3, N, device=dev)
-        rep("pw%d dgrad res+mask+part" % r,
+        rep("pw%d%s dgrad res+mask+part" % (r, "s" * (v >> 2)),
             timeit(lambda: C.conv_igemm_epi(dy, wd2, out, 0, dgeo, 8, res, N, mask, None, None, None, None, None,
                                             None, part, None, None, cfg)),
             (dy.numel() + out.numel() + res.numel()) * 2 + mask.numel())
+    # backward-BN epilogue with the producer's BN input (conv_c dgrad of res2: dy [M,256] -> [M,64], ReLU mask
+    # from affine(y_b), partial sums of sum(dz), sum(dz y_b))
+    cgeo = list(dgrad_phases(ConvSpec(K, N, (1, 1, 1)), 1, (1, M, 1), (1, M, 1), N, K)[0])
+    _, wdc = pack_weight(torch.randn(N, K, 1, 1, 1, device=dev) * 0.1, ConvSpec(K, N, (1, 1, 1)))
+    dyc = res
+    yb = torch.randn(M, K, device=dev).to(torch.bfloat16)
+    outk = torch.empty(M, K, device=dev, dtype=torch.bfloat16)
+    mk, rk = torch.zeros(K, device=dev), torch.ones(K, device=dev)
+    for v in (0, 1, 2, 4, 5, 6):
+        cfg = EXPLICIT | PW | v
+        r = C.conv_cfg_bm(cfg, K)
+        part = torch.empty((M + r - 1) // r, 3, K, device=dev)
+        rep("pw%d%s dgrad bn(y0)+part K=256" % (r, "s" * (v >> 2)),
+            timeit(lambda: C.conv_igemm_epi(dyc, wdc, outk, 0, cgeo, 8, None, 0, None, yb, mk, rk, None, None,
+                                            None, part, ksc, ksh, cfg)),
+            (dyc.numel() + outk.numel() + yb.numel()) * 2)
     # BN-backward apply (dy = A dz*mask + B y + C) at the same shape: reads g, y, mask bits; writes dy
     y = res
     coef = torch.randn(3 * N, device=dev)
