@@ -320,45 +320,51 @@ __global__ void bn_bwd_apply_kernel(const uint16_t* __restrict__ g, int ldg, int
 // ------------------------------------------------------------------------------------------
 __global__ void stem_pool_fwd_kernel(const uint16_t* __restrict__ y, const float* __restrict__ scale,
                                      const float* __restrict__ shift, uint16_t* __restrict__ out,
-                                     uint8_t* __restrict__ arg, int NT_, int H, int W, int Ho, int Wo, int C, int ldo) {
-  const int vecs = C >> 3;
-  const int64_t total = (int64_t)NT_ * Ho * Wo * vecs;
-  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < total; i += (int64_t)gridDim.x * NT) {
-    int64_t r = i;
-    const int cv = r % vecs; r /= vecs;
-    const int wo = r % Wo; r /= Wo;
-    const int ho = r % Ho; r /= Ho;
-    const int64_t nt = r;
-    const int c = cv << 3;
-    float best[8];
-    uint8_t bi[8];
+                                     uint8_t* __restrict__ arg, uint16_t* __restrict__ ymax, int NT_, int H, int W,
+                                     int Ho, int Wo, int C, int ldo) {
+  // lane -> (pooled position, 8-channel vector); 32-bit index math (positions < 2^31, checked by the binding);
+  // the 9 window loads are issued before any compare (independent loads in flight)
+  ROW_VEC_SETUP(C);
+  float sc[8], sh[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) { best[e] = -INFINITY; bi[e] = 0; }
-    float sc[8], sh[8];
+  for (int e = 0; e < 8; ++e) { sc[e] = scale[c + e]; sh[e] = shift[c + e]; }
+  const int Q = NT_ * Ho * Wo;
+  for (int q = blockIdx.x * rpi + lr; q < Q; q += gridDim.x * rpi) {
+    const int wo = q % Wo;
+    const int r = q / Wo;
+    const int ho = r % Ho;
+    const int nt = r / Ho;
+    uint4 v[9];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) { sc[e] = scale[c + e]; sh[e] = shift[c + e]; }
-    for (int dh = 0; dh < 3; ++dh) {
-      const int h = ho * 2 - 1 + dh;
-      if ((unsigned)h >= (unsigned)H) continue;
+    for (int dh = 0; dh < 3; ++dh)
+#pragma unroll
       for (int dw = 0; dw < 3; ++dw) {
-        const int w = wo * 2 - 1 + dw;
-        if ((unsigned)w >= (unsigned)W) continue;
-        float f[8];
-        unpack8(*reinterpret_cast<const uint4*>(y + ((nt * H + h) * W + w) * C + c), f);
+        const int h = min(max(ho * 2 - 1 + dh, 0), H - 1), w = min(max(wo * 2 - 1 + dw, 0), W - 1);
+        v[dh * 3 + dw] = *reinterpret_cast<const uint4*>(y + (((int64_t)nt * H + h) * W + w) * C + c);
+      }
+    float best[8], yb[8];
+    uint32_t bi[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float a = fmaxf(f[e] * sc[e] + sh[e], 0.f);
-          if (a > best[e]) { best[e] = a; bi[e] = (uint8_t)(dh * 3 + dw); }
-        }
+    for (int e = 0; e < 8; ++e) { best[e] = -INFINITY; bi[e] = 0; yb[e] = 0.f; }
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const int h = ho * 2 - 1 + k / 3, w = wo * 2 - 1 + k % 3;
+      if ((unsigned)h >= (unsigned)H || (unsigned)w >= (unsigned)W) continue;
+      float f[8];
+      unpack8(v[k], f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float a = fmaxf(f[e] * sc[e] + sh[e], 0.f);
+        if (a > best[e]) { best[e] = a; bi[e] = (uint32_t)k; yb[e] = f[e]; }
       }
     }
-    const int64_t pos = (nt * Ho + ho) * Wo + wo;
-    const int64_t o = pos * C + c;
-    *reinterpret_cast<uint4*>(out + pos * ldo + c) = pack8(best);
+    const int64_t o = (int64_t)q * C + c;
+    *reinterpret_cast<uint4*>(out + (int64_t)q * ldo + c) = pack8(best);
     uint2 pk;
-    pk.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((uint32_t)bi[3] << 24);
-    pk.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | ((uint32_t)bi[7] << 24);
+    pk.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | (bi[3] << 24);
+    pk.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | (bi[7] << 24);
     *reinterpret_cast<uint2*>(arg + o) = pk;
+    if (ymax) *reinterpret_cast<uint4*>(ymax + o) = pack8(yb);   // raw conv output at the argmax (exact)
   }
 }
 
@@ -398,6 +404,154 @@ __global__ void stem_pool_bwd_kernel(const uint16_t* __restrict__ dout, int ldd,
       }
     }
     *reinterpret_cast<uint4*>(dact + ((nt * H + h) * W + w) * C + c) = pack8(acc);
+  }
+}
+
+// Stem backward, max-pool and BatchNorm fused.  dz (grad wrt relu(BN(y))) is non-zero only at window argmaxes,
+// so the BN-backward sums sum(dz*mask), sum(dz*mask*xhat) are taken over the POOLED grid (bn_bwd_reduce on
+// dout and the raw y at each argmax, ``ymax`` of stem_pool_fwd: 4x fewer bytes than the full-resolution dz),
+// and this kernel produces dy = A*dz*mask + B*y + C in one pass: the argmax gather of dz, the ReLU mask from
+// y's own affine and the BN apply — dz is never written.  Thread -> (position lane, 8-channel vector).
+__global__ void stem_pool_bn_apply_kernel(const uint16_t* __restrict__ dout, int ldd, const uint8_t* __restrict__ arg,
+                                          const uint16_t* __restrict__ y, const float* __restrict__ ms,
+                                          const float* __restrict__ mh, const float* __restrict__ coef,
+                                          uint16_t* __restrict__ dy, int NT_, int H, int W, int Ho, int Wo, int C) {
+  // One lane owns the 2x2 input block (2ho+a, 2wo+b) of pooled window (ho, wo) for 8 channels.  Input row
+  // 2ho+a lies in window ho (offset a+1) and, for a = 1, in window ho+1 (offset 0); likewise columns.  So
+  // the four windows (ho..ho+1, wo..wo+1) are loaded once (unconditionally: independent loads in flight)
+  // and serve all four positions.
+  ROW_VEC_SETUP(C);
+  float A[8], B[8], Cc[8], MS[8], MH[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    A[e] = coef[c + e]; B[e] = coef[C + c + e]; Cc[e] = coef[2 * C + c + e];
+    MS[e] = ms[c + e]; MH[e] = mh[c + e];
+  }
+  const int Q = NT_ * Ho * Wo;   // < 2^31 (checked by the launcher)
+  for (int q = blockIdx.x * rpi + lr; q < Q; q += gridDim.x * rpi) {
+    const int wo = q % Wo;
+    const int r = q / Wo;
+    const int ho = r % Ho;
+    const int nt = r / Ho;
+    uint2 ag[2][2];
+    float g[2][2][8];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const bool ok = ho + i < Ho && wo + j < Wo;
+        const int64_t o = ((int64_t)nt * Ho + min(ho + i, Ho - 1)) * Wo + min(wo + j, Wo - 1);
+        ag[i][j] = *reinterpret_cast<const uint2*>(arg + o * C + c);
+        if (!ok) ag[i][j] = make_uint2(0xffffffffu, 0xffffffffu);   // matches no offset
+        unpack8(*reinterpret_cast<const uint4*>(dout + o * ldd + c), g[i][j]);
+      }
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const int h = 2 * ho + a;
+      if (h >= H) continue;
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int w = 2 * wo + b;
+        if (w >= W) continue;
+        const int64_t m = ((int64_t)nt * H + h) * W + w;
+        float yv[8], acc[8];
+        unpack8(*reinterpret_cast<const uint4*>(y + m * C + c), yv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+#pragma unroll
+        for (int i = 0; i <= a; ++i)
+#pragma unroll
+          for (int j = 0; j <= b; ++j) {
+            const uint32_t want = (uint32_t)((i ? 0 : a + 1) * 3 + (j ? 0 : b + 1));
+            const uint2 pk = ag[i][j];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const uint32_t bi = ((e < 4 ? pk.x : pk.y) >> (8 * (e & 3))) & 255u;
+              acc[e] += bi == want ? g[i][j][e] : 0.f;
+            }
+          }
+        float o8[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float dz = (yv[e] * MS[e] + MH[e]) > 0.f ? acc[e] : 0.f;
+          o8[e] = A[e] * dz + B[e] * yv[e] + Cc[e];
+        }
+        *reinterpret_cast<uint4*>(dy + m * C + c) = pack8(o8);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Global average pool (window = the whole T x H x W volume, the SlowFast head at 224/256 crops):
+// position-split partial sums [N][S][C] (16-B loads, 8 channels per lane, deterministic LDS reduction),
+// then a fixed-order sum over the splits.  Backward is a pure 16-B broadcast store.
+// ------------------------------------------------------------------------------------------
+__global__ void avgpool_global_part_kernel(const uint16_t* __restrict__ x, int vol, int C, int S,
+                                           float* __restrict__ part) {
+  const int n = blockIdx.x / S, sp = blockIdx.x % S;
+  const int vecs = C >> 3;
+  const int rpi = NT / vecs;     // vecs <= NT (C <= 2048, checked by the launcher)
+  const int lr = threadIdx.x / vecs;
+  const int c = (threadIdx.x - lr * vecs) << 3;
+  const int per = (vol + S - 1) / S;
+  const int p0 = sp * per, p1 = min(vol, p0 + per);
+  float s[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s[e] = 0.f;
+  if (lr < rpi) {
+    const uint16_t* base = x + (int64_t)n * vol * C + c;
+    int p = p0 + lr;
+    for (; p + 3 * rpi < p1; p += 4 * rpi) {   // 4 independent 16-B loads in flight per lane
+      uint4 q[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) q[k] = *reinterpret_cast<const uint4*>(base + (int64_t)(p + k * rpi) * C);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float f[8];
+        unpack8(q[k], f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s[e] += f[e];
+      }
+    }
+    for (; p < p1; p += rpi) {
+      float f[8];
+      unpack8(*reinterpret_cast<const uint4*>(base + (int64_t)p * C), f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s[e] += f[e];
+    }
+  }
+  __shared__ float red[NT * 8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[threadIdx.x * 8 + e] = s[e];
+  __syncthreads();
+  for (int i = threadIdx.x; i < C; i += NT) {   // channel i = vector i/8, element i%8; rows in fixed order
+    const int v = i >> 3, e = i & 7;
+    float t = 0.f;
+    for (int k = 0; k < rpi; ++k) t += red[(k * vecs + v) * 8 + e];
+    part[((int64_t)n * S + sp) * C + i] = t;
+  }
+}
+
+__global__ void avgpool_global_final_kernel(const float* __restrict__ part, int S, int C, float inv,
+                                            float* __restrict__ out, int ldo, int coff, int N) {
+  const int i = blockIdx.x * NT + threadIdx.x;
+  if (i >= N * C) return;
+  const int n = i / C, c = i % C;
+  float t = 0.f;
+  for (int k = 0; k < S; ++k) t += part[((int64_t)n * S + k) * C + c];
+  out[(int64_t)n * ldo + coff + c] = t * inv;
+}
+
+__global__ void avgpool_global_bwd_kernel(const float* __restrict__ dout, int ldo, int coff, int vol, int C,
+                                          float inv, uint16_t* __restrict__ dx, int64_t M) {
+  ROW_VEC_SETUP(C);
+  for (int64_t m = (int64_t)blockIdx.x * rpi + lr; m < M; m += (int64_t)gridDim.x * rpi) {
+    const int64_t n = m / vol;
+    const float4* src = reinterpret_cast<const float4*>(dout + n * ldo + coff + c);
+    const float4 u = src[0], v = src[1];
+    float f[8] = {u.x * inv, u.y * inv, u.z * inv, u.w * inv, v.x * inv, v.y * inv, v.z * inv, v.w * inv};
+    *reinterpret_cast<uint4*>(dx + m * C + c) = pack8(f);
   }
 }
 
@@ -534,9 +688,16 @@ void bn_bwd_apply_launch(const uint16_t* g, int ldg, int mask_mode, const void* 
 }
 
 void stem_pool_fwd_launch(const uint16_t* y, const float* scale, const float* shift, uint16_t* out, uint8_t* arg,
-                          int NT_, int H, int W, int Ho, int Wo, int C, int ldo, hipStream_t s) {
-  hipLaunchKernelGGL(stem_pool_fwd_kernel, dim3(grid_for((int64_t)NT_ * Ho * Wo * (C / 8))), dim3(NT), 0, s, y, scale,
-                     shift, out, arg, NT_, H, W, Ho, Wo, C, ldo);
+                          uint16_t* ymax, int NT_, int H, int W, int Ho, int Wo, int C, int ldo, hipStream_t s) {
+  hipLaunchKernelGGL(stem_pool_fwd_kernel, dim3(grid_rows((int64_t)NT_ * Ho * Wo, C)), dim3(NT), 0, s, y, scale,
+                     shift, out, arg, ymax, NT_, H, W, Ho, Wo, C, ldo);
+}
+
+void stem_pool_bn_apply_launch(const uint16_t* dout, int ldd, const uint8_t* arg, const uint16_t* y, const float* ms,
+                               const float* mh, const float* coef, uint16_t* dy, int NT_, int H, int W, int Ho, int Wo,
+                               int C, hipStream_t s) {
+  hipLaunchKernelGGL(stem_pool_bn_apply_kernel, dim3(grid_rows((int64_t)NT_ * Ho * Wo, C)), dim3(NT), 0, s, dout, ldd,
+                     arg, y, ms, mh, coef, dy, NT_, H, W, Ho, Wo, C);
 }
 
 void stem_pool_bwd_launch(const uint16_t* dout, int ldd, const uint8_t* arg, uint16_t* dact, int NT_, int H, int W,
@@ -545,9 +706,23 @@ void stem_pool_bwd_launch(const uint16_t* dout, int ldd, const uint8_t* arg, uin
                      arg, dact, NT_, H, W, Ho, Wo, C);
 }
 
+int avgpool_global_splits(int N, int vol) {
+  int S = (1024 + N - 1) / N;            // >= ~1024 blocks over the chip
+  if (S > vol / 8) S = vol / 8 > 0 ? vol / 8 : 1;
+  return S;
+}
+
 void avgpool_fwd_launch(const uint16_t* x, int N, int T, int H, int W, int C, int kt, int kh, int kw, float* out,
-                        int ldo, int coff, hipStream_t s) {
+                        int ldo, int coff, float* scratch, hipStream_t s) {
   const int P = (T - kt + 1) * (H - kh + 1) * (W - kw + 1);
+  if (P == 1 && C % 8 == 0 && C <= 8 * NT && scratch) {   // global pool: split-position partials + final sum
+    const int vol = T * H * W;
+    const int S = avgpool_global_splits(N, vol);
+    hipLaunchKernelGGL(avgpool_global_part_kernel, dim3(N * S), dim3(NT), 0, s, x, vol, C, S, scratch);
+    hipLaunchKernelGGL(avgpool_global_final_kernel, dim3((N * C + NT - 1) / NT), dim3(NT), 0, s, scratch, S, C,
+                       1.f / (float)vol, out, ldo, coff, N);
+    return;
+  }
   const int blocks = N * P * ((C + 63) / 64);
   hipLaunchKernelGGL(avgpool_fwd_kernel, dim3(blocks), dim3(NT), 0, s, x, T, H, W, C, kt, kh, kw, out, ldo, coff, N);
 }
@@ -555,6 +730,12 @@ void avgpool_fwd_launch(const uint16_t* x, int N, int T, int H, int W, int C, in
 void avgpool_bwd_launch(const float* dout, int ldo, int coff, int N, int T, int H, int W, int C, int kt, int kh,
                         int kw, uint16_t* dx, hipStream_t s) {
   const int64_t total = (int64_t)N * T * H * W * C;
+  if (kt == T && kh == H && kw == W && C % 8 == 0 && C <= 8 * NT && ldo % 4 == 0 && coff % 4 == 0) {
+    const int64_t M = (int64_t)N * T * H * W;
+    hipLaunchKernelGGL(avgpool_global_bwd_kernel, dim3(grid_rows(M, C)), dim3(NT), 0, s, dout, ldo, coff, T * H * W, C,
+                       1.f / (float)(T * H * W), dx, M);
+    return;
+  }
   hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(grid_for(total)), dim3(NT), 0, s, dout, ldo, coff, T, H, W, C, kt, kh,
                      kw, dx, N);
 }

@@ -52,11 +52,15 @@ void bn_bwd_apply_launch(const uint16_t* g, int ldg, int mask_mode, const void* 
                          const float* coef1, uint16_t* dy1, uint16_t* dzout, int lddz, int dz_accum, int64_t M, int C,
                          hipStream_t s);
 void stem_pool_fwd_launch(const uint16_t* y, const float* scale, const float* shift, uint16_t* out, uint8_t* arg,
-                          int NT_, int H, int W, int Ho, int Wo, int C, int ldo, hipStream_t s);
+                          uint16_t* ymax, int NT_, int H, int W, int Ho, int Wo, int C, int ldo, hipStream_t s);
+void stem_pool_bn_apply_launch(const uint16_t* dout, int ldd, const uint8_t* arg, const uint16_t* y, const float* ms,
+                               const float* mh, const float* coef, uint16_t* dy, int NT_, int H, int W, int Ho, int Wo,
+                               int C, hipStream_t s);
+int avgpool_global_splits(int N, int vol);
 void stem_pool_bwd_launch(const uint16_t* dout, int ldd, const uint8_t* arg, uint16_t* dact, int NT_, int H, int W,
                           int Ho, int Wo, int C, hipStream_t s);
 void avgpool_fwd_launch(const uint16_t* x, int N, int T, int H, int W, int C, int kt, int kh, int kw, float* out,
-                        int ldo, int coff, hipStream_t s);
+                        int ldo, int coff, float* scratch, hipStream_t s);
 void avgpool_bwd_launch(const float* dout, int ldo, int coff, int N, int T, int H, int W, int C, int kt, int kh,
                         int kw, uint16_t* dx, hipStream_t s);
 void sgd_momentum_launch(float* p, const float* g, float* buf, int64_t n, const float* lr, float momentum, float wd,
@@ -371,11 +375,31 @@ void bn_bwd_apply(const at::Tensor& g, int64_t ldg, int64_t mask_mode, const Opt
                       cur_stream());
 }
 
+// ymax (optional, dense [NT*Ho*Wo, C] bf16): the raw y at each window's argmax, for the pooled-grid BN-backward sums
 void stem_pool_fwd(const at::Tensor& y, const at::Tensor& scale, const at::Tensor& shift, const at::Tensor& out,
                    int64_t ldo, const at::Tensor& arg, int64_t NT_, int64_t H, int64_t W, int64_t Ho, int64_t Wo,
-                   int64_t C) {
-  stem_pool_fwd_launch(bfp(y), f32(scale), f32(shift), bfpm(out), arg.data_ptr<uint8_t>(), (int)NT_, (int)H, (int)W,
-                       (int)Ho, (int)Wo, (int)C, (int)ldo, cur_stream());
+                   int64_t C, const OptT& ymax) {
+  TORCH_CHECK(C % 8 == 0 && ldo % 8 == 0, "stem pool: channels / row stride must be multiples of 8");
+  TORCH_CHECK(arg.numel() >= NT_ * Ho * Wo * C, "stem pool: argmax buffer too small");
+  TORCH_CHECK(!ymax.has_value() || ymax->numel() >= NT_ * Ho * Wo * C, "stem pool: ymax buffer too small");
+  TORCH_CHECK(NT_ * H * W < ((int64_t)1 << 31) && C <= 2048, "stem pool: position count exceeds int32");
+  TORCH_CHECK(Ho == (H - 1) / 2 + 1 && Wo == (W - 1) / 2 + 1, "stem pool: 3x3/s2/p1 output dims");
+  stem_pool_fwd_launch(bfp(y), f32(scale), f32(shift), bfpm(out), arg.data_ptr<uint8_t>(), bfom(ymax), (int)NT_,
+                       (int)H, (int)W, (int)Ho, (int)Wo, (int)C, (int)ldo, cur_stream());
+}
+
+// fused max-pool backward (argmax gather) + ReLU mask + BN-backward apply: dy = A*dz*mask + B*y + C
+void stem_pool_bn_apply(const at::Tensor& dout, int64_t ldd, const at::Tensor& arg, const at::Tensor& y,
+                        const at::Tensor& ms, const at::Tensor& mh, const at::Tensor& coef, const at::Tensor& dy,
+                        int64_t NT_, int64_t H, int64_t W, int64_t Ho, int64_t Wo, int64_t C) {
+  TORCH_CHECK(C % 8 == 0 && ldd % 8 == 0 && C <= 2048, "stem pool bwd: channel layout");
+  TORCH_CHECK(NT_ * H * W < ((int64_t)1 << 31), "stem pool bwd: position count exceeds int32");
+  TORCH_CHECK(y.numel() >= NT_ * H * W * C && dy.numel() >= NT_ * H * W * C, "stem pool bwd: y/dy too small");
+  TORCH_CHECK(arg.numel() >= NT_ * Ho * Wo * C && dout.dim() == 2 && dout.size(0) >= NT_ * Ho * Wo &&
+              dout.size(1) >= C && dout.stride(0) == ldd, "stem pool bwd: pooled buffers / row stride");
+  TORCH_CHECK(Ho == (H - 1) / 2 + 1 && Wo == (W - 1) / 2 + 1, "stem pool bwd: 3x3/s2/p1 output dims");
+  stem_pool_bn_apply_launch(bfp(dout), (int)ldd, arg.data_ptr<uint8_t>(), bfp(y), f32(ms), f32(mh), f32(coef), bfpm(dy),
+                            (int)NT_, (int)H, (int)W, (int)Ho, (int)Wo, (int)C, cur_stream());
 }
 
 void stem_pool_bwd(const at::Tensor& dout, int64_t ldd, const at::Tensor& arg, const at::Tensor& dact, int64_t NT_,
@@ -386,8 +410,12 @@ void stem_pool_bwd(const at::Tensor& dout, int64_t ldd, const at::Tensor& arg, c
 
 void avgpool_fwd(const at::Tensor& x, std::vector<int64_t> dims, std::vector<int64_t> k, const at::Tensor& out,
                  int64_t ldo, int64_t coff) {
-  avgpool_fwd_launch(bfp(x), (int)dims[0], (int)dims[1], (int)dims[2], (int)dims[3], (int)dims[4], (int)k[0],
-                     (int)k[1], (int)k[2], f32(out), (int)ldo, (int)coff, cur_stream());
+  const int N = (int)dims[0], T = (int)dims[1], H = (int)dims[2], W = (int)dims[3], C = (int)dims[4];
+  at::Tensor scratch;
+  if (k[0] == T && k[1] == H && k[2] == W)   // global pool: per-split partial sums (deterministic)
+    scratch = at::empty({(int64_t)N * avgpool_global_splits(N, T * H * W) * C}, out.options());
+  avgpool_fwd_launch(bfp(x), N, T, H, W, C, (int)k[0], (int)k[1], (int)k[2], f32(out), (int)ldo, (int)coff,
+                     scratch.defined() ? scratch.data_ptr<float>() : nullptr, cur_stream());
 }
 
 void avgpool_bwd(const at::Tensor& dout, int64_t ldo, int64_t coff, std::vector<int64_t> dims, std::vector<int64_t> k,
@@ -602,7 +630,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_bwd_reduce", &bn_bwd_reduce);
   m.def("bn_bwd_finalize", &bn_bwd_finalize);
   m.def("bn_bwd_apply", &bn_bwd_apply);
-  m.def("stem_pool_fwd", &stem_pool_fwd);
+  m.def("stem_pool_fwd", &stem_pool_fwd, py::arg("y"), py::arg("scale"), py::arg("shift"), py::arg("out"),
+        py::arg("ldo"), py::arg("arg"), py::arg("NT"), py::arg("H"), py::arg("W"), py::arg("Ho"), py::arg("Wo"),
+        py::arg("C"), py::arg("ymax") = py::none());
+  m.def("stem_pool_bn_apply", &stem_pool_bn_apply);
   m.def("stem_pool_bwd", &stem_pool_bwd);
   m.def("avgpool_fwd", &avgpool_fwd);
   m.def("avgpool_bwd", &avgpool_bwd);

@@ -538,20 +538,37 @@ class _Stem:
         C = self.eng.C
         y = self._conv_s2d(x, train, tag) if self.s2d else self.u.fwd(x, None, train, tag)
         Ho, Wo = (y.H - 1) // 2 + 1, (y.W - 1) // 2 + 1
-        arg = self.eng.ws((self.name, "arg"), (y.N * y.T * Ho * Wo, self.u.C), torch.uint8)
+        P = y.N * y.T * Ho * Wo
+        arg = self.eng.ws((self.name, "arg"), (P, self.u.C), torch.uint8)
+        # training: also the raw y at every window argmax — the BN-backward sums are then taken on the pooled grid
+        ymax = self.eng.ws((self.name, "ymax"), (P, self.u.C), torch.bfloat16) if train else None
         self.eng.mark(self.name + ".pool")
         C.stem_pool_fwd(y.t, self.u.scale, self.u.shift, out, out.stride(0), arg, y.N * y.T, y.H, y.W, Ho, Wo,
-                        self.u.C)
-        self.x, self.y, self.arg = x, y, arg
+                        self.u.C, ymax)
+        self.x, self.y, self.arg, self.ymax = x, y, arg, ymax
         return Act(out, y.N, y.T, Ho, Wo)
 
     def bwd(self, dout: Act):
-        eng, C = self.eng, self.eng.C
+        """Max-pool + ReLU + BN backward without materialising the full-resolution dz: the BN sums come from the
+        pooled grid (dout and the raw y at each argmax), then one kernel gathers dz through the argmax bytes and
+        writes dy = A dz mask + B y + C (csrc/kernels/bn_eltwise.hip stem_pool_bn_apply)."""
+        eng, C, u = self.eng, self.eng.C, self.u
         y = self.y
-        dact = eng.ws((self.name, "dact"), (y.M, self.u.C), torch.bfloat16)
+        assert self.ymax is not None, "stem backward needs a training-mode forward"
+        P = dout.M
+        blocks, rpb = eng._bn_blocks(P, u.C)
+        eng.mark(u.name + ".bnred")
+        part = eng.scratch("bnpart", blocks * 3 * u.C)
+        C.bn_bwd_reduce(dout.t, dout.ld, 2, None, 0, u.scale, u.shift, self.ymax, u.mean, u.rstd, None, None, None,
+                        P, u.C, blocks, rpb, part)
+        fg = eng.flat
+        C.bn_bwd_finalize(part, blocks, u.C, y.M, 0, u.bn.weight, u.mean, u.rstd, fg.gview(u.bn.weight),
+                          fg.gview(u.bn.bias), eng.grad_beta, u.coef)
+        dyt = eng.ws((u.name, "dy"), (y.M, u.C), torch.bfloat16)
         eng.mark(self.name + ".poolbwd")
-        C.stem_pool_bwd(dout.t, dout.ld, self.arg, dact, y.N * y.T, y.H, y.W, dout.H, dout.W, self.u.C)
-        dy, _ = self.u.bn_backward(Act(dact, y.N, y.T, y.H, y.W), y, 2, None, self.u.xf())
+        C.stem_pool_bn_apply(dout.t, dout.ld, self.arg, y.t, u.scale, u.shift, u.coef, dyt, y.N * y.T, y.H, y.W,
+                             dout.H, dout.W, u.C)
+        dy = Act(dyt, y.N, y.T, y.H, y.W)
         if self.s2d:
             x = self.x
             acc = eng.scratch("stem_acc_" + self.name, self.u.C * self.kt * 256, zero=True)
@@ -647,6 +664,8 @@ class _ResBlock:
         self.a.wgrad(dya, x, None)
         if self.one is not None:
             self.one.wgrad(dy1, x, None)
+            if self._strided_one(prev):
+                return self._dgrad_strided_one(dya, dy1, dx, dx_accum)
             self.one.dgrad(dy1, (x.T, x.H, x.W), dx, dx_accum)
             acc = True
         else:
@@ -714,6 +733,8 @@ class _ResBlock:
         if one is not None:
             d1 = Act(dy1, x.N, yb.T, yb.H, yb.W)
             one.wgrad(d1, x, None)
+            if self._strided_one(prev):
+                return self._dgrad_strided_one(dya, d1, dx, dx_accum)
             one.dgrad(d1, (x.T, x.H, x.W), dx, dx_accum)
             acc = True
         else:
@@ -724,6 +745,20 @@ class _ResBlock:
             self.a.dgrad(dya, (x.T, x.H, x.W), dx, acc)
             return None
         return self.a.dgrad(dya, (x.T, x.H, x.W), dx, acc, res=res, epi=prev)
+
+    def _strided_one(self, prev) -> bool:
+        """Spatially strided branch1 and no fused epilogue on conv_a's dgrad (first unit of a stage)."""
+        return (self.one is not None and tuple(self.one.spec.stride) != (1, 1, 1)
+                and tuple(self.a.spec.stride) == (1, 1, 1) and (prev is None or not self._epi_ok(prev)))
+
+    def _dgrad_strided_one(self, dya: Act, dy1: Act, dx: torch.Tensor, dx_accum: bool):
+        """conv_a's dgrad covers every input position, the strided 1x1 branch1 only the stride-phase positions:
+        writing conv_a's first and accumulating branch1's second touches dx once in full plus once at those
+        positions (the other order writes zeros at 3/4 of dx and then reads + rewrites all of it)."""
+        x = self.x
+        self.a.dgrad(dya, (x.T, x.H, x.W), dx, dx_accum)
+        self.one.dgrad(dy1, (x.T, x.H, x.W), dx, True)
+        return None
 
     def _epi_ok(self, prev: "_ResBlock") -> bool:
         s = self.a.spec

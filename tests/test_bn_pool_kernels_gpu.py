@@ -135,7 +135,8 @@ def test_stem_pool_fwd_bwd(C, H, W):
 
 
 @pytest.mark.parametrize("dims,k", [((2, 3, 7, 5, 16), (2, 3, 3)), ((1, 4, 9, 9, 8), (4, 9, 9)),
-                                    ((3, 2, 5, 7, 24), (1, 2, 3))])
+                                    ((3, 2, 5, 7, 24), (1, 2, 3)), ((5, 8, 7, 7, 2048), (8, 7, 7)),
+                                    ((3, 32, 7, 7, 256), (32, 7, 7)), ((2, 3, 5, 5, 40), (3, 5, 5))])
 def test_avgpool_fwd_bwd(dims, k):
     K = _C()
     N, T, H, W, C = dims
@@ -158,3 +159,54 @@ def test_avgpool_fwd_bwd(dims, k):
     ref.backward(dout[:, coff:coff + C].view(N, To, Ho, Wo, C).permute(0, 4, 1, 2, 3))
     want = xr.grad.permute(0, 2, 3, 4, 1).reshape(-1, C)
     assert _rel(dx.cpu(), want) < 5e-3
+
+
+@pytest.mark.parametrize("C,H,W", [(8, 15, 13), (64, 12, 9), (16, 8, 7)])
+def test_stem_pool_bn_backward_fused(C, H, W):
+    """Stem backward on the fused path (pooled-grid BN sums from ``ymax`` + stem_pool_bn_apply) vs float64
+    autograd of maxpool(relu(BN_train(y))) — dgamma, dbeta and dy."""
+    K = _C()
+    NT = 3
+    g = torch.Generator().manual_seed(C * 7 + H)
+    M = NT * H * W
+    y = (torch.randn(M, C, generator=g) * 1.3 + 0.2).to(torch.bfloat16)
+    gamma = torch.rand(C, generator=g) + 0.5
+    beta = torch.randn(C, generator=g) * 0.3
+    yf = y.double()
+    mu, var = yf.mean(0), yf.var(0, unbiased=False)
+    rstd = 1 / (var + 1e-5).sqrt()
+    scale = (gamma.double() * rstd).float()
+    shift = (beta.double() - mu * gamma.double() * rstd).float()
+    Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    P = NT * Ho * Wo
+    ldo = C + 8
+    out = torch.zeros(P, ldo, dtype=torch.bfloat16, device=DEV)
+    arg = torch.empty(P * C, dtype=torch.uint8, device=DEV)
+    ymax = torch.empty(P, C, dtype=torch.bfloat16, device=DEV)
+    yd = y.to(DEV)
+    sc_d, sh_d = scale.to(DEV), shift.to(DEV)
+    K.stem_pool_fwd(yd, sc_d, sh_d, out, ldo, arg, NT, H, W, Ho, Wo, C, ymax)
+    dout = torch.randn(P, ldo, generator=g).to(torch.bfloat16)
+    doutd = dout.to(DEV)
+    mean_d, rstd_d = mu.float().to(DEV), rstd.float().to(DEV)
+    blocks, rpb = K.bn_bwd_blocks(P, C)
+    part = torch.full((blocks, 3, C), float("nan"), device=DEV)
+    K.bn_bwd_reduce(doutd, ldo, 2, None, 0, sc_d, sh_d, ymax, mean_d, rstd_d, None, None, None, P, C, blocks, rpb, part)
+    dgamma, dbeta = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+    coef = torch.empty(3 * C, device=DEV)
+    K.bn_bwd_finalize(part, blocks, C, M, 0, gamma.to(DEV), mean_d, rstd_d, dgamma, dbeta, 0.0, coef)
+    dy = torch.empty(M, C, dtype=torch.bfloat16, device=DEV)
+    K.stem_pool_bn_apply(doutd, ldo, arg, yd, sc_d, sh_d, coef, dy, NT, H, W, Ho, Wo, C)
+    torch.cuda.synchronize()
+    # float64 reference (BN with batch statistics of y, ReLU, 3x3/s2/p1 max pool)
+    yr = yf.clone().requires_grad_(True)
+    gr = gamma.double().requires_grad_(True)
+    br = beta.double().requires_grad_(True)
+    m_r = yr.mean(0)
+    v_r = ((yr - m_r) ** 2).mean(0)
+    a = torch.relu((yr - m_r) / (v_r + 1e-5).sqrt() * gr + br)
+    pooled = F.max_pool2d(a.view(NT, H, W, C).permute(0, 3, 1, 2), 3, 2, 1)
+    pooled.backward(dout[:, :C].double().view(NT, Ho, Wo, C).permute(0, 3, 1, 2))
+    assert _rel(dbeta.cpu(), br.grad) < 1e-4
+    assert _rel(dgamma.cpu(), gr.grad) < 1e-3
+    assert _rel(dy.cpu(), yr.grad) < 2e-2
