@@ -147,7 +147,8 @@ __global__ void bn_bwd_reduce_kernel(const uint16_t* __restrict__ g, int ldg, in
                                      const float* __restrict__ rstd0,
                                      const uint16_t* __restrict__ y1, const float* __restrict__ mean1,
                                      const float* __restrict__ rstd1,
-                                     int64_t M, int C, int rows_per_block, float* __restrict__ part) {
+                                     int64_t M, int C, int rows_per_block, float* __restrict__ part,
+                                     uint16_t* __restrict__ dzout, int lddz) {
   extern __shared__ __attribute__((aligned(16))) float red[];  // [slots][3][C], NT*96 bytes
   const uint16_t* mo = static_cast<const uint16_t*>(mo_);
   const uint8_t* mb = static_cast<const uint8_t*>(mo_);
@@ -184,6 +185,7 @@ __global__ void bn_bwd_reduce_kernel(const uint16_t* __restrict__ g, int ldg, in
 #pragma unroll
         for (int e = 0; e < 8; ++e) dz[e] = (a[e] * MS[e] + MH[e]) > 0.f ? dz[e] : 0.f;
       }
+      if (dzout) *reinterpret_cast<uint4*>(dzout + m * lddz + c) = pack8(dz);   // masked dz, same pass
 #pragma unroll
       for (int e = 0; e < 8; ++e) { sdz[e] += dz[e]; s0[e] += dz[e] * (a[e] - m0[e]) * r0[e]; }
       if (y1) {
@@ -667,9 +669,9 @@ int bn_bwd_reduce_blocks(int64_t M, int C, int* rows_per_block) {
 void bn_bwd_reduce_launch(const uint16_t* g, int ldg, int mask_mode, const void* mo, int ldm, const float* ms,
                           const float* mh, const uint16_t* y0, const float* mean0, const float* rstd0,
                           const uint16_t* y1, const float* mean1, const float* rstd1, int64_t M, int C, int blocks,
-                          int rows_per_block, float* part, hipStream_t s) {
+                          int rows_per_block, float* part, uint16_t* dzout, int lddz, hipStream_t s) {
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(blocks), dim3(NT), NT * 96, s, g, ldg, mask_mode, mo,
-                     ldm, ms, mh, y0, mean0, rstd0, y1, mean1, rstd1, M, C, rows_per_block, part);
+                     ldm, ms, mh, y0, mean0, rstd0, y1, mean1, rstd1, M, C, rows_per_block, part, dzout, lddz);
 }
 
 void bn_bwd_finalize_launch(const float* part, int blocks, int C, int64_t count, int which, const float* gamma,

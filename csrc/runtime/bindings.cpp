@@ -43,7 +43,7 @@ int bn_bwd_reduce_blocks(int64_t M, int C, int* rows_per_block);
 void bn_bwd_reduce_launch(const uint16_t* g, int ldg, int mask_mode, const void* mo, int ldm, const float* ms,
                           const float* mh, const uint16_t* y0, const float* mean0, const float* rstd0,
                           const uint16_t* y1, const float* mean1, const float* rstd1, int64_t M, int C, int blocks,
-                          int rows_per_block, float* part, hipStream_t s);
+                          int rows_per_block, float* part, uint16_t* dzout, int lddz, hipStream_t s);
 void bn_bwd_finalize_launch(const float* part, int blocks, int C, int64_t count, int which, const float* gamma,
                             const float* mean, const float* rstd, float* dgamma, float* dbeta, float beta_acc,
                             float* coef, hipStream_t s);
@@ -347,13 +347,14 @@ std::vector<int64_t> bn_bwd_blocks(int64_t M, int64_t C) {
 void bn_bwd_reduce(const at::Tensor& g, int64_t ldg, int64_t mask_mode, const OptT& mo, int64_t ldm, const OptT& ms,
                    const OptT& mh, const OptT& y0, const OptT& mean0, const OptT& rstd0,
                    const OptT& y1, const OptT& mean1, const OptT& rstd1, int64_t M, int64_t C, int64_t blocks,
-                   int64_t rpb, const at::Tensor& part) {
+                   int64_t rpb, const at::Tensor& part, const OptT& dzout, int64_t lddz) {
   TORCH_CHECK(C % 8 == 0 && C <= 2048, "bn_bwd_reduce channel constraint");
+  TORCH_CHECK(!dzout.has_value() || (lddz % 8 == 0 && dzout->size(0) >= M), "bn_bwd_reduce: dz output layout");
   TORCH_CHECK(!y0.has_value() || (mean0.has_value() && rstd0.has_value()), "y0 needs mean0/rstd0");
   TORCH_CHECK(mask_mode != 2 || y0.has_value(), "mask mode 2 reads y0");
   bn_bwd_reduce_launch(bfp(g), (int)ldg, (int)mask_mode, mask_ptr(mask_mode, mo), (int)ldm, f32o(ms), f32o(mh), bfo(y0), f32o(mean0),
                        f32o(rstd0), bfo(y1), f32o(mean1), f32o(rstd1), M, (int)C, (int)blocks, (int)rpb, f32(part),
-                       cur_stream());
+                       bfom(dzout), (int)lddz, cur_stream());
 }
 
 void bn_bwd_finalize(const at::Tensor& part, int64_t blocks, int64_t C, int64_t count, int64_t which,
@@ -627,7 +628,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_act", &bn_act);
   m.def("res_out", &res_out);
   m.def("bn_bwd_blocks", &bn_bwd_blocks);
-  m.def("bn_bwd_reduce", &bn_bwd_reduce);
+  m.def("bn_bwd_reduce", &bn_bwd_reduce, py::arg("g"), py::arg("ldg"), py::arg("mask_mode"), py::arg("mo"),
+        py::arg("ldm"), py::arg("ms"), py::arg("mh"), py::arg("y0"), py::arg("mean0"), py::arg("rstd0"), py::arg("y1"),
+        py::arg("mean1"), py::arg("rstd1"), py::arg("M"), py::arg("C"), py::arg("blocks"), py::arg("rpb"),
+        py::arg("part"), py::arg("dzout") = py::none(), py::arg("lddz") = 0);
   m.def("bn_bwd_finalize", &bn_bwd_finalize);
   m.def("bn_bwd_apply", &bn_bwd_apply);
   m.def("stem_pool_fwd", &stem_pool_fwd, py::arg("y"), py::arg("scale"), py::arg("shift"), py::arg("out"),

@@ -697,13 +697,15 @@ class _ResBlock:
             blocks, rpb = eng._bn_blocks(M, Cc)
             eng.mark(self.c.name + ".bnred")
             part = eng.scratch("bnpart", blocks * 3 * Cc)
+            # identity shortcut: the same pass writes dz = dout * bits into dx (conv_a's dgrad accumulates on it)
             C.bn_bwd_reduce(dout.t, dout.ld, 3, self.mask, Cc // 8, None, None, None, None, None,
                             None if one is None else y1.t, None if one is None else one.mean,
-                            None if one is None else one.rstd, M, Cc, blocks, rpb, part)
+                            None if one is None else one.rstd, M, Cc, blocks, rpb, part,
+                            dxa.t if one is None else None, dxa.ld if one is None else 0)
             tiles = blocks
             if one is None:
                 assert not dx_accum, "identity unit with an accumulating input gradient"
-                dz = dxa            # dz lands in dx; conv_a's dgrad accumulates on top of it
+                dz = dxa
             else:
                 dz = Act(eng.ws((self.name, "dz"), (M, Cc), torch.bfloat16), x.N, yb.T, yb.H, yb.W)
         if one is not None:
@@ -717,10 +719,6 @@ class _ResBlock:
             else:
                 C.bn_bwd_apply(dout.t, dout.ld, 3, self.mask, Cc // 8, None, None, None, None, None, y1.t, one.coef,
                                dy1, dz.t, dz.ld, 0, M, Cc)
-        elif pre is None:
-            eng.mark(self.c.name + ".dz")
-            C.bn_bwd_apply(dout.t, dout.ld, 3, self.mask, Cc // 8, None, None, None, None, None, None, None, None,
-                           dxa.t, dxa.ld, 0, M, Cc)
         dab = eng.ws((self.name, "dab"), (yb.M, self.b.C), torch.bfloat16)
         pb = self.c.fold_backward(dz, part, tiles, yb, self.b, dab)
         dyb, _ = self.b.bn_backward(Act(dab, yb.N, yb.T, yb.H, yb.W), yb, 0, None, None, pre=pb)

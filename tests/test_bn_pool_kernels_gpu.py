@@ -90,8 +90,10 @@ def test_bn_backward_chain(C, M, mask_mode):
     mo = _bits(maskb.to(DEV)) if mask_mode == 3 else None
     msd, mhd = (ms.to(DEV), mh.to(DEV)) if mask_mode == 2 else (None, None)
     mean_d, rstd_d = mu.float().to(DEV), rstd.float().to(DEV)
+    dzw = torch.full((M, C + 8), 5.0, dtype=torch.bfloat16, device=DEV)   # masked dz written by the same pass
     K.bn_bwd_reduce(doutd, C, mask_mode, mo, C // 8, msd, mhd, yd, mean_d, rstd_d, None, None, None, M, C, blocks,
-                    rpb, part)
+                    rpb, part, dzw, C + 8)
+    assert torch.equal(dzw[:, :C].cpu().double(), dz) and torch.all(dzw[:, C:] == 5.0)
     dgamma, dbeta = torch.full((C,), 2.0, device=DEV), torch.full((C,), 3.0, device=DEV)
     coef = torch.empty(3 * C, device=DEV)
     K.bn_bwd_finalize(part, blocks, C, M, 0, gamma.to(DEV), mean_d, rstd_d, dgamma, dbeta, 0.5, coef)
