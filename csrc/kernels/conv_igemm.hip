@@ -39,7 +39,10 @@ __host__ __device__ constexpr int main_lds_bytes(int BM, int BN, int BK, int EPI
 }
 
 __host__ __device__ constexpr int dma_stages(int BM, int BN, int BK, bool dma) {
-  return (dma && 3 * (BM + BN) * BK * 2 <= 96 * 1024) ? 3 : 2;
+  // the 256x256 tile runs one workgroup per CU anyway: at BK = 32 a 4-buffer ring (128 KB, two tiles in flight
+  // across each barrier) fits beside its epilogue/statistics area
+  return (dma && BM * BN > 128 * 128 && 4 * (BM + BN) * BK * 2 <= 128 * 1024) ? 4
+         : (dma && 3 * (BM + BN) * BK * 2 <= 96 * 1024) ? 3 : 2;
 }
 
 template <int N>
@@ -75,6 +78,35 @@ template <int BK>
 __device__ __forceinline__ int lds_off(int row, int slot) {
   if constexpr (BK == 32) return row * 64 + ((slot ^ (((row >> 2) & 1) << 1)) << 4);
   else return row * 128 + ((slot ^ (row & 6)) << 4);
+}
+
+// MFMAs of one LDS k tile.  The fragments of k-step kk+1 are read while the MFMAs of kk run (register double
+// buffer); the scheduling barrier keeps the compiler from sinking those reads back next to their use, where
+// each read exposes the LDS latency to the MFMA pipe (the compiler otherwise reads 2 fragments 4 MFMAs ahead).
+template <int BK, int TM, int TN>
+__device__ __forceinline__ void mma_ktile(const char* A, const int (&fa)[BK / 32][TM], const int (&fb)[BK / 32][TN],
+                                          f32x4_t (&acc)[TM][TN]) {
+  bf16x8_t af[2][TM], bfr[2][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) af[0][i] = *reinterpret_cast<const bf16x8_t*>(A + fa[0][i]);
+#pragma unroll
+  for (int j = 0; j < TN; ++j) bfr[0][j] = *reinterpret_cast<const bf16x8_t*>(A + fb[0][j]);
+#pragma unroll
+  for (int kk = 0; kk < BK / 32; ++kk) {
+    const int c = kk & 1;
+    if (kk + 1 < BK / 32) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[c ^ 1][i] = *reinterpret_cast<const bf16x8_t*>(A + fa[kk + 1][i]);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[c ^ 1][j] = *reinterpret_cast<const bf16x8_t*>(A + fb[kk + 1][j]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[c][j], af[c][i], acc[i][j], 0, 0, 0);
+  }
 }
 
 template <int BM, int BN, int WM, int WN, int CH, int BK, int EPI, int UT>
@@ -320,7 +352,9 @@ void conv_igemm_kernel(const ConvParams p) {
     nb_w = __builtin_amdgcn_readfirstlane(nb_w);
     if constexpr (glds_ut) {
       issue_dma(0);
-      if (NSTAGE == 3 && nsteps > 1) issue_dma(1);
+#pragma unroll
+      for (int i = 1; i + 1 < NSTAGE; ++i)
+        if (nsteps > i) issue_dma(i);
     } else {
       // register ring one stage ahead of LDS: tile s+1 is written right after the barrier that frees its
       // buffer, and tile s+2 is re-issued immediately, so each load has a full k-step of MFMA to land
@@ -328,14 +362,71 @@ void conv_igemm_kernel(const ConvParams p) {
       store_lds(0);
       if (nsteps > 1) load();
     }
+    if constexpr (glds_ut && NSTAGE == 2 && BK == 64) {
+      // 2 buffers x 2 MFMA k-steps, software-pipelined across the barrier: the barrier sits between the two
+      // k-steps of a tile, where (a) this tile's second-half fragments are already in registers, so every read
+      // of the tile is done and its buffer can take the DMA of tile step+2, and (b) tile step+1 has landed, so
+      // its first-half fragments are read while the second-half MFMAs of this tile run.  No k-step starts on
+      // fragments still in flight; only barrier skew is exposed.
+      bf16x8_t fa0[TM], fb0[TN], fa1[TM], fb1[TN];
+      vm_wait<0>();
+      __syncthreads();   // tile 0 landed
+      if (nsteps > 1) issue_dma(1);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) fa0[i] = *reinterpret_cast<const bf16x8_t*>(smem + fa[0][i]);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) fb0[j] = *reinterpret_cast<const bf16x8_t*>(smem + fb[0][j]);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) fa1[i] = *reinterpret_cast<const bf16x8_t*>(smem + fa[1][i]);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) fb1[j] = *reinterpret_cast<const bf16x8_t*>(smem + fb[1][j]);
+      for (int step = 0; step < nsteps; ++step) {
+        const int cur = step & 1;
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb0[j], fa0[i], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        vm_wait<0>();   // this wave's DMA of tile step+1
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's reads of tile step
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        const bool more = step + 1 < nsteps;
+        if (step + 2 < nsteps) issue_dma(cur);
+        const char* An = smem + (cur ^ 1) * TILE_BYTES;
+        if (more) {
+#pragma unroll
+          for (int i = 0; i < TM; ++i) fa0[i] = *reinterpret_cast<const bf16x8_t*>(An + fa[0][i]);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) fb0[j] = *reinterpret_cast<const bf16x8_t*>(An + fb[0][j]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[j], fa1[i], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (more) {
+#pragma unroll
+          for (int i = 0; i < TM; ++i) fa1[i] = *reinterpret_cast<const bf16x8_t*>(An + fa[1][i]);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) fb1[j] = *reinterpret_cast<const bf16x8_t*>(An + fb[1][j]);
+        }
+      }
+    } else
     for (int step = 0; step < nsteps; ++step) {
       const int cur = step & 1;
       const char* A;
-      if constexpr (glds_ut && NSTAGE == 3) {
-        // 3-buffer ring: tile step+1 stays in flight across this barrier (counted vmcnt, raw s_barrier —
-        // __syncthreads would drain the pending LDS-DMA with vmcnt(0)); buffer (step+2)%3 held tile step-1,
-        // whose readers all passed this barrier
-        if (step + 1 < nsteps) {
+      if constexpr (glds_ut && NSTAGE >= 3) {
+        // NSTAGE-buffer ring: tiles step+1 .. step+NSTAGE-2 stay in flight across this barrier (counted vmcnt,
+        // raw s_barrier — __syncthreads would drain the pending LDS-DMA with vmcnt(0)); buffer
+        // (step+NSTAGE-1)%NSTAGE held tile step-1, whose readers all passed this barrier
+        if (NSTAGE == 4 && step + 2 < nsteps) {
+          vm_wait_dyn<2 * A_SLOTS, 2 * B_SLOTS>(2 * nb_w);   // leave the DMAs of tiles step+1 and step+2
+        } else if (step + 1 < nsteps) {
           vm_wait_dyn<A_SLOTS, B_SLOTS>(nb_w);   // leave this wave's A_SLOTS + nb_w DMAs of tile step+1
         } else {
           vm_wait<0>();
@@ -343,8 +434,8 @@ void conv_igemm_kernel(const ConvParams p) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (step + 2 < nsteps) issue_dma((step + 2) % 3);
-        A = smem + (step % 3) * TILE_BYTES;
+        if (step + NSTAGE - 1 < nsteps) issue_dma((step + NSTAGE - 1) % NSTAGE);
+        A = smem + (step % NSTAGE) * TILE_BYTES;
       } else if constexpr (glds_ut) {
         // 2 buffers (large tiles): tile step landed -> barrier -> DMA of tile step+1 during this step's MFMAs
         vm_wait<0>();
@@ -359,18 +450,22 @@ void conv_igemm_kernel(const ConvParams p) {
         }
         A = smem + cur * TILE_BYTES;
       }
+      if constexpr (glds_ut) {   // no register staging ring: room for the fragment double buffer
+        mma_ktile<BK, TM, TN>(A, fa, fb, acc);
+      } else {
 #pragma unroll
-      for (int kk = 0; kk < BK / 32; ++kk) {
-        bf16x8_t af[TM], bfr[TN];
+        for (int kk = 0; kk < BK / 32; ++kk) {
+          bf16x8_t af[TM], bfr[TN];
 #pragma unroll
-        for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8_t*>(A + fa[kk][i]);
+          for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8_t*>(A + fa[kk][i]);
 #pragma unroll
-        for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const bf16x8_t*>(A + fb[kk][j]);
+          for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const bf16x8_t*>(A + fb[kk][j]);
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
+          for (int i = 0; i < TM; ++i)
 #pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+            for (int j = 0; j < TN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+        }
       }
     }
   } else {
