@@ -859,7 +859,10 @@ class FusedNet:
                        and os.environ.get("PVA_STREAMS", "1") != "0")
         import os
         # BN folding of the 1x1 conv_c (never materialise its output); units whose conv_c input has at least
-        # fold_min_c channels (default: the slow pathway, where the Gram matrices run at MFMA speed)
+        # fold_min_c channels (default: the slow pathway, where the Gram matrices run at MFMA speed).  Folding
+        # the 8/16-channel fast-pathway units too is 1-3 % faster on the bench step (scripts/gpu_r2_foldc.sh) but
+        # their Gram-derived variances (E[y^2] - E[y]^2 over fp32-atomic Gram sums) are not reproducible run to
+        # run at small batches (scripts/diag_ms_fold.py: loss spread ~1 % at S=64, N=2), so it stays opt-in.
         self.bn_fold = os.environ.get("PVA_BN_FOLD", "1") != "0"
         self.fold_min_c = int(os.environ.get("PVA_BN_FOLD_MIN_C", "32"))
         blocks = list(model.blocks)

@@ -2,7 +2,7 @@
 # Round-2 re-entry checkpoint: GPU test suite, headline bench, steady-state kernel trace, per-op profile (B=160).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
-out=gpurun_out/r2e
+out=gpurun_out/${OUTD:-r2e}
 mkdir -p $out
 export TMPDIR=/tmp
 timeout -k 10 700 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > $out/gt.log 2>&1 || { tail -40 $out/gt.log; exit 1; }
