@@ -689,7 +689,7 @@ void conv_igemm_kernel(const ConvParams p) {
             for (int r = 0; r < 4; ++r) v[r] += o[r];
           }
           const uint2 pk = pack4(v);
-          *reinterpret_cast<uint2*>(dst) = pk;
+          if (!p.nostore) *reinterpret_cast<uint2*>(dst) = pk;
           if (do_stats) {
             float q[4];
             unpack4(pk, q);
@@ -1034,11 +1034,12 @@ void conv_igemm_launch(const ConvParams& p, int chunk, hipStream_t stream, int c
   if ((p.eres || p.emask || p.epart || p.fres) && chunk != 8) return;  // host binding rejects this combination
   int v, bk, ut_force;
   bool dma = false;
+  if (p.nostore && cfg >= 0 && (cfg & 16) && (cfg & 512)) cfg = -1;   // the pointwise kernel always stores
   if (cfg >= 0 && (cfg & 16) && (cfg & 512)) {   // streaming pointwise kernel (legality checked by the bindings)
     conv_pw_launch(p, cfg, stream);
     return;
   }
-  if ((p.fres || p.ebias) && cfg >= 0 && (cfg & 32)) cfg = -1;   // the direct kernel has no fres / bias epilogue
+  if ((p.fres || p.ebias || p.nostore) && cfg >= 0 && (cfg & 32)) cfg = -1;   // direct kernel: no fres / bias / nostore
   if (cfg >= 0 && (cfg & 16) && (cfg & 32)) {  // narrow direct-to-register kernel (conv_direct.hip)
     conv_direct_launch(p, cfg, stream);
     return;

@@ -63,6 +63,9 @@ struct ConvParams {
   const float* rsc;
   const float* rsh;
   uint8_t* emask_out;
+  // 1: statistics-only forward (EPI 0 with stats): the per-tile BN partial sums of the bf16-rounded output are
+  // produced, the output itself is never stored (exact BN statistics of a folded conv, models/fused.py)
+  int nostore;
 };
 
 // Weight gradient: dW[n = cout][k = (tap, cin)] = sum_p dY[p][cout] * im2col(X)[p][k]

@@ -165,8 +165,11 @@ static void check_pw(const ConvParams& p, int64_t chunk, int64_t cfg) {
 
 void conv_igemm(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, const OptT& stats,
                 const OptT& scale, const OptT& shift, int64_t affine, int64_t accum, std::vector<int64_t> g,
-                int64_t chunk, int64_t cfg, const OptT& bias) {
+                int64_t chunk, int64_t cfg, const OptT& bias, int64_t nostore) {
   ConvParams p = conv_params(x, w, y, accum, g, chunk);
+  p.nostore = (int)nostore;
+  TORCH_CHECK(!nostore || (stats.has_value() && !accum && !bias.has_value()),
+              "statistics-only forward needs stats and no accumulate / bias");
   p.ebias = f32o(bias);
   TORCH_CHECK(!bias.has_value() || bias->numel() >= p.Ngemm, "bias too small");
   p.stats = f32o(stats);
@@ -566,7 +569,7 @@ PYBIND11_MODULE(_C, m) {
   m.doc() = "gfx950 HIP kernels for pytorchvideo_accelerate_amd";
   m.def("conv_igemm", &conv_igemm, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("stats"), py::arg("scale"),
         py::arg("shift"), py::arg("affine"), py::arg("accum"), py::arg("g"), py::arg("chunk"), py::arg("cfg") = -1,
-        py::arg("bias") = py::none());
+        py::arg("bias") = py::none(), py::arg("nostore") = 0);
   m.def("conv_igemm_fres", &conv_igemm_fres);
   m.def("bnfold_fwd_stats", &bnfold_fwd_stats);
   m.def("bnfold_bwd", &bnfold_bwd);

@@ -304,11 +304,36 @@ class _ConvBN:
         splits = self.wgrad(yb, yb, bxf, spec=self.gspec, dest=Ga, beta=0.0, gram=True, colsum=slab)
         self.T = eng.ws((self.name, "foldT"), (Co, c), torch.float32)
         self.s = eng.ws((self.name, "folds"), (c,), torch.float32)
+        exact = c < eng.fold_exact_below
         eng.mark(self.name + ".foldstats")
+        # T = Wc Ga and the column sums (backward); with ``exact`` the statistics come from the pass below
         C.bnfold_fwd_stats(self.wf, Ga, slab, splits, Co, c, yb.M, self.T, self.s, bn.weight, bn.bias,
-                           bn.running_mean, bn.running_var, bn.num_batches_tracked,
+                           None if exact else bn.running_mean, None if exact else bn.running_var,
+                           None if exact else bn.num_batches_tracked,
                            bn.momentum if bn.momentum is not None else 0.1, bn.eps, self.mean, self.rstd,
                            self.scale, self.shift)
+        if exact:
+            # narrow (fast-pathway) folds: E[y^2] - E[y]^2 from fp32-atomic Gram sums loses the variance of
+            # near-constant channels, so their statistics come from a statistics-only conv pass instead (the
+            # per-tile two-moment slabs of the unfolded path; the output is computed but never stored)
+            eng.mark(self.name + ".foldexact")
+            key = ("fg", yb.N, yb.T, yb.H, yb.W, yb.ld)
+            g = self._geo.get(key)
+            if g is None:
+                g = self._geo[key] = fwd_geometry(s, yb.N, yb.T, yb.H, yb.W, yb.ld, Co)
+            stats = eng.ws((self.name, "stats"), ((yb.M + 127) // 128, 2, Co), torch.float32)
+            dummy = eng.ws(("nostore_y",), (1, 8), torch.bfloat16)
+            tuner = eng.tuner
+            aff = 2 if bxf.relu else 1
+
+            def run(cfg, scratch):
+                C.conv_igemm(yb.t, self.wf, dummy, tuner.scratch_like(stats) if scratch else stats, bxf.scale,
+                             bxf.shift, aff, 0, g, s.chunk, cfg, None, 1)
+            cfg = tuner.launch(("fst", aff) + tuple(g), g, s.chunk, run, aff=aff, direct=False, pw=False)
+            tiles = (yb.M + tuner.bm(cfg, Co) - 1) // tuner.bm(cfg, Co)
+            C.bn_finalize(stats, tiles, Co, yb.M, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                          bn.num_batches_tracked, bn.momentum if bn.momentum is not None else 0.1, bn.eps,
+                          self.mean, self.rstd, self.scale, self.shift)
 
     def fold_output(self, yb: Act, bxf: _Xf, out: torch.Tensor, res: Act, rxf: Optional[_Xf],
                     mask: torch.Tensor, tag: str) -> Act:
@@ -859,12 +884,15 @@ class FusedNet:
                        and os.environ.get("PVA_STREAMS", "1") != "0")
         import os
         # BN folding of the 1x1 conv_c (never materialise its output); units whose conv_c input has at least
-        # fold_min_c channels (default: the slow pathway, where the Gram matrices run at MFMA speed).  Folding
-        # the 8/16-channel fast-pathway units too is 1-3 % faster on the bench step (scripts/gpu_r2_foldc.sh) but
-        # their Gram-derived variances (E[y^2] - E[y]^2 over fp32-atomic Gram sums) are not reproducible run to
-        # run at small batches (scripts/diag_ms_fold.py: loss spread ~1 % at S=64, N=2), so it stays opt-in.
+        # fold_min_c channels (default: the slow pathway, where the Gram matrices run at MFMA speed).  Narrow
+        # (fast-pathway) folds take exact statistics from a statistics-only conv pass (Gram-derived variances
+        # E[y^2] - E[y]^2 over fp32-atomic sums were not reproducible there: scripts/diag_ms_fold.py); with that
+        # pass, folding them too measures even with not folding (1034 vs 1030 clips/s, scripts/gpu_r2_exact.sh),
+        # so it stays opt-in (PVA_BN_FOLD_MIN_C=8).
         self.bn_fold = os.environ.get("PVA_BN_FOLD", "1") != "0"
         self.fold_min_c = int(os.environ.get("PVA_BN_FOLD_MIN_C", "32"))
+        # folds with fewer input channels than this take exact statistics from a statistics-only conv pass
+        self.fold_exact_below = int(os.environ.get("PVA_BN_FOLD_EXACT_BELOW", "32"))
         blocks = list(model.blocks)
         self.slowfast = isinstance(blocks[0], R.MultiPathWayWithFuse)
         self.stages: List[Tuple[List, Optional[_Fuse]]] = []

@@ -77,7 +77,7 @@ class ConvTuner:
 
     # ---------------------------------------------------------------- candidates
     def candidates(self, g: Sequence[int], chunk: int, aff: int = 0, epi: bool = False,
-                   direct: bool = True) -> List[int]:
+                   direct: bool = True, pw: bool = True) -> List[int]:
         N, Cg = g[1], g[3]
         K = g[28] * g[29] * g[30] * Cg
         out = []
@@ -105,7 +105,7 @@ class ConvTuner:
                         out.append(w | DMA)
         if direct and self.direct and self.C.conv_direct_legal(list(g), chunk):
             out += [EXPLICIT | DIRECT, EXPLICIT | DIRECT | DIRECT_2K]
-        if self.pw and self._pw_now and self.C.conv_pw_legal(list(g), chunk):
+        if pw and self.pw and self._pw_now and self.C.conv_pw_legal(list(g), chunk):
             self._pw_seen += 1
             if self.pw_only is None or self.pw_only == self._pw_seen - 1:
                 out += [EXPLICIT | PW | s | v for s in (0, PW_SOLO) for v in range(len(PW_ROWS))]
@@ -126,22 +126,23 @@ class ConvTuner:
 
     # ---------------------------------------------------------------- launch
     def launch(self, key: Tuple, g: Sequence[int], chunk: int, run: Callable[[int, bool], None],
-               aff: int = 0, epi: bool = False, direct: bool = True) -> int:
+               aff: int = 0, epi: bool = False, direct: bool = True, pw: bool = True) -> int:
         """``run(cfg, scratch)`` performs the launch (into scratch outputs when ``scratch``).  Returns the
-        configuration used for the real launch (-1 = kernel heuristic).  ``direct=False``: the launch needs an
-        epilogue the direct kernel lacks (fused residual output, bias)."""
+        configuration used for the real launch (-1 = kernel heuristic).  ``direct=False`` / ``pw=False``: the
+        launch needs an epilogue the direct / pointwise kernel lacks (fused residual output, bias, statistics
+        without the output)."""
         cfg = self.cache.get(key)
         if cfg is None:
             self._pw_now = self.pw_kinds is None or (len(key) > 0 and key[0] in self.pw_kinds)
-            cfg = self._tune(g, chunk, run, aff, epi, direct) if self.enabled else -1
+            cfg = self._tune(g, chunk, run, aff, epi, direct, pw) if self.enabled else -1
             self._pw_now = True
             self.cache[key] = cfg
         run(cfg, False)
         return cfg
 
     def _tune(self, g: Sequence[int], chunk: int, run: Callable[[int, bool], None], aff: int = 0,
-              epi: bool = False, direct: bool = True) -> int:
-        cands = self.candidates(g, chunk, aff, epi, direct)
+              epi: bool = False, direct: bool = True, pw: bool = True) -> int:
+        cands = self.candidates(g, chunk, aff, epi, direct, pw)
         if len(cands) <= 1:
             return cands[0] if cands else -1
         times = []
