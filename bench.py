@@ -62,6 +62,8 @@ def parse(argv=None):
     ap.add_argument("--lr", type=float, default=0.1)
     ap.add_argument("--grad-accum", type=int, default=1,
                     help="micro-batches of --batch clips per optimizer step (gradients all-reduced once, on the last)")
+    ap.add_argument("--graph", type=int, default=int(os.environ.get("PVA_BENCH_GRAPH", "0")),
+                    help="1: replay each micro-step (+ SGD) as a captured HIP graph (single process; engine/graph.py)")
     ap.add_argument("--plumbing", action="store_true", help="CPU/gloo rehearsal on the PyTorch modules")
     ap.add_argument("--dump", default=None, help="(plumbing) write rank-0 first-step gradients + final params here")
     return ap.parse_args(argv)
@@ -120,6 +122,7 @@ def run(a):
     gdt = torch.bfloat16 if a.grad_dtype == "bf16" else None
     B = a.batch
     dump = {}
+    gstep = None   # engine.graph.GraphedStep when --graph 1 (single process)
     if a.plumbing:
         from pytorchvideo_accelerate_amd.engine.backends import TorchBackend
         be = TorchBackend(plumbing_model(a), st, "no", a.bucket_mb)
@@ -185,8 +188,24 @@ def run(a):
             prefetch(k + 1)
             return xs
 
+        if a.graph and st.world_size == 1:
+            from pytorchvideo_accelerate_amd.engine.graph import GraphedStep
+
         def step(i, tune=False):
+            nonlocal gstep
             xs = batch(-1 if tune else i * a.grad_accum)
+            if a.graph and st.world_size == 1 and not tune and i >= 1:
+                # captured after the eager tuning step and the first (state-binding) optimizer step; the two
+                # preprocessing buffers give two graph keys, captured during warmup
+                if gstep is None:
+                    gstep = GraphedStep(eng, opt)
+                for j in range(a.grad_accum):
+                    if j:
+                        xs = batch(i * a.grad_accum + j)
+                    last = j == a.grad_accum - 1
+                    loss, _ = gstep(xs, labels_all[(i * a.grad_accum + j) % 64], loss_scale=1.0 / a.grad_accum,
+                                    accumulate=j > 0, optimizer_step=last)
+                return loss
             if tune:
                 # untimed autotuning pass: every conv geometry is tuned (ranks agree on the choice) with
                 # no gradient all-reduce in flight and no optimizer step (weights stay rank-identical)
@@ -278,7 +297,7 @@ def run(a):
                        "global_batch": B * a.grad_accum * st.world_size,
                        "per_gpu_batch": B, "grad_accum": a.grad_accum, "seq_len": a.frames,
                        "parallelism": f"dp{st.world_size}", "backend": st.backend or "none",
-                       "grad_dtype": a.grad_dtype, "classes": a.classes,
+                       "grad_dtype": a.grad_dtype, "classes": a.classes, "hip_graph": bool(gstep is not None),
                        "final_loss": round(float(loss), 4) if loss is not None else None,
                        "peak_mem_gb": (round(torch.cuda.max_memory_allocated(dev) / 2**30, 1)
                                        if dev.type == "cuda" else None),

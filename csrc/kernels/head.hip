@@ -42,7 +42,9 @@ typedef __attribute__((ext_vector_type(4))) float f4;
 
 // xm[n][c] = scale/P * sum_p keep * feat[n][p][c]   (thresh24 = 0: no dropout)
 __global__ void head_pool_kernel(const float* __restrict__ feat, int N, int P, int C, float* __restrict__ xm,
-                                 uint32_t k0, uint32_t k1, uint32_t thresh24, float keep_scale) {
+                                 uint32_t k0, uint32_t k1, uint32_t thresh24, float keep_scale,
+                                 const uint64_t* __restrict__ seedp) {
+  if (seedp) { const uint64_t sd = *seedp; k0 = (uint32_t)sd; k1 = (uint32_t)(sd >> 32); }
   const int n = blockIdx.y;
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
@@ -249,7 +251,9 @@ __global__ void head_transpose_kernel(const float* __restrict__ in, int R, int C
 // dfeat[n][p][c] = (sum_k dlogits[n][k] W[k][c]) * keep(n,p,c) * keep_scale / P    via WT [C][K]
 __global__ __launch_bounds__(256) void head_dfeat_kernel(const float* __restrict__ dl, const float* __restrict__ WT,
                                                         int N, int K, int C, int P, float* __restrict__ dfeat,
-                                                        uint32_t k0, uint32_t k1, uint32_t thresh24, float keep_scale) {
+                                                        uint32_t k0, uint32_t k1, uint32_t thresh24, float keep_scale,
+                                                        const uint64_t* __restrict__ seedp) {
+  if (seedp) { const uint64_t sd = *seedp; k0 = (uint32_t)sd; k1 = (uint32_t)(sd >> 32); }
   __shared__ __attribute__((aligned(16))) float red[4 * 64 * 4];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int i0 = blockIdx.y * 16, j0 = blockIdx.x * 16;   // i: sample n, j: feature c
@@ -272,6 +276,17 @@ __global__ __launch_bounds__(256) void head_dfeat_kernel(const float* __restrict
   }
 }
 
+// device-resident dropout key (graph-capturable steps: the key advances on the device, one splitmix64 step per
+// training forward, instead of being baked into the kernel arguments)
+__global__ void head_seed_advance_kernel(uint64_t* __restrict__ s) {
+  if (threadIdx.x == 0) {
+    uint64_t z = s[0] + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    s[0] = z ^ (z >> 31);
+  }
+}
+
 __global__ void head_dropout_mask_kernel(int64_t total, uint32_t k0, uint32_t k1, uint32_t thresh24,
                                          uint8_t* __restrict__ out) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x)
@@ -290,11 +305,11 @@ static uint32_t thresh_of(float p) {
 
 // forward of the training/eval head.  feat [N][P][C] fp32; xm scratch [N][C]; logits [N][K].
 void head_forward_launch(const float* feat, int N, int P, int C, const float* W, const float* b, int K, float p_drop,
-                         uint64_t seed, float* xm, float* logits, hipStream_t s) {
+                         uint64_t seed, const uint64_t* seedp, float* xm, float* logits, hipStream_t s) {
   const uint32_t th = thresh_of(p_drop);
   const float ks = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
   hipLaunchKernelGGL(head_pool_kernel, dim3((C + 255) / 256, N), dim3(256), 0, s, feat, N, P, C, xm,
-                     (uint32_t)seed, (uint32_t)(seed >> 32), th, ks);
+                     (uint32_t)seed, (uint32_t)(seed >> 32), th, ks, seedp);
   hipLaunchKernelGGL(head_linear_fwd_kernel, dim3((K + 15) / 16, (N + 15) / 16), dim3(256), 0, s, xm, W, b, logits, N,
                      K, C);
 }
@@ -310,8 +325,8 @@ void head_ce_launch(const float* logits, const int64_t* labels, int N, int K, fl
 // backward: dW/db into the flat gradient (beta 0 overwrite / 1 accumulate), dfeat [N][P][C].
 // scratch: dlT [K][N], xmT [C][N], WT [C][K]
 void head_backward_launch(const float* dlogits, const float* xm, const float* W, int N, int P, int C, int K,
-                          float p_drop, uint64_t seed, float* dW, float* db, float beta, float* dfeat, float* dlT,
-                          float* xmT, float* WT, hipStream_t s) {
+                          float p_drop, uint64_t seed, const uint64_t* seedp, float* dW, float* db, float beta,
+                          float* dfeat, float* dlT, float* xmT, float* WT, hipStream_t s) {
   const uint32_t th = thresh_of(p_drop);
   const float ks = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
   hipLaunchKernelGGL(head_transpose_kernel, dim3((K + 31) / 32, (N + 31) / 32), dim3(256), 0, s, dlogits, N, K, dlT);
@@ -321,7 +336,11 @@ void head_backward_launch(const float* dlogits, const float* xm, const float* W,
                      dW, db, beta);
   if (dfeat)
     hipLaunchKernelGGL(head_dfeat_kernel, dim3((C + 15) / 16, (N + 15) / 16), dim3(256), 0, s, dlogits, WT, N, K, C,
-                       P, dfeat, (uint32_t)seed, (uint32_t)(seed >> 32), th, ks);
+                       P, dfeat, (uint32_t)seed, (uint32_t)(seed >> 32), th, ks, seedp);
+}
+
+void head_seed_advance_launch(uint64_t* seed, hipStream_t s) {
+  hipLaunchKernelGGL(head_seed_advance_kernel, dim3(1), dim3(64), 0, s, seed);
 }
 
 void head_dropout_mask_launch(int64_t total, float p_drop, uint64_t seed, uint8_t* out, hipStream_t s) {

@@ -88,12 +88,13 @@ void bnfold_bwd_launch(const float* part, int tiles, const uint16_t* Wf, const u
                        const float* mean, const float* rstd, float* dgamma, float* dbeta, float* dW, float beta_acc,
                        float* coef, uint16_t* W1t, uint16_t* W2, float* bias, hipStream_t st);
 void head_forward_launch(const float* feat, int N, int P, int C, const float* W, const float* b, int K, float p_drop,
-                         uint64_t seed, float* xm, float* logits, hipStream_t s);
+                         uint64_t seed, const uint64_t* seedp, float* xm, float* logits, hipStream_t s);
+void head_seed_advance_launch(uint64_t* seed, hipStream_t s);
 void head_ce_launch(const float* logits, const int64_t* labels, int N, int K, float gscale, float* dlogits,
                     float* row_loss, int* row_correct, float* loss, int64_t* counts, int acc_counts, hipStream_t s);
 void head_backward_launch(const float* dlogits, const float* xm, const float* W, int N, int P, int C, int K,
-                          float p_drop, uint64_t seed, float* dW, float* db, float beta, float* dfeat, float* dlT,
-                          float* xmT, float* WT, hipStream_t s);
+                          float p_drop, uint64_t seed, const uint64_t* seedp, float* dW, float* db, float beta,
+                          float* dfeat, float* dlT, float* xmT, float* WT, hipStream_t s);
 void head_dropout_mask_launch(int64_t total, float p_drop, uint64_t seed, uint8_t* out, hipStream_t s);
 
 void register_clip_reader(pybind11::module& m);
@@ -486,16 +487,23 @@ void stem_wgrad(const at::Tensor& x, const at::Tensor& dy, const at::Tensor& acc
 
 // ---- classification head (csrc/kernels/head.hip) ----
 // feat [N][P][C] fp32, W [K][C] fp32, b [K] (nullable); xm [N][C], logits [N][K] outputs
+inline const uint64_t* seed_ptr(const OptT& t) {
+  if (!t.has_value()) return nullptr;
+  TORCH_CHECK(t->scalar_type() == at::kLong && t->numel() >= 1 && t->is_cuda(), "device seed must be int64 [1]");
+  return reinterpret_cast<const uint64_t*>(t->data_ptr<int64_t>());
+}
+
+// seed_dev (optional int64 [1] on the device): the dropout key is read there instead of ``seed``
 void head_forward(const at::Tensor& feat, const at::Tensor& W, const OptT& b, double p_drop, int64_t seed,
-                  const at::Tensor& xm, const at::Tensor& logits) {
+                  const at::Tensor& xm, const at::Tensor& logits, const OptT& seed_dev) {
   TORCH_CHECK(feat.dim() == 3 && feat.is_contiguous(), "feat must be [N][P][C] contiguous");
   const int N = feat.size(0), P = feat.size(1), C = feat.size(2), K = W.size(0);
   TORCH_CHECK(W.dim() == 2 && W.size(1) == C && W.is_contiguous(), "W must be [K][C]");
   TORCH_CHECK(xm.numel() >= (int64_t)N * C && logits.numel() >= (int64_t)N * K, "head outputs too small");
   TORCH_CHECK(p_drop >= 0.0 && p_drop < 1.0, "dropout probability must be in [0, 1)");
   if (N == 0) return;
-  head_forward_launch(f32(feat), N, P, C, f32(W), f32o(b), K, (float)p_drop, (uint64_t)seed, f32(xm), f32(logits),
-                      cur_stream());
+  head_forward_launch(f32(feat), N, P, C, f32(W), f32o(b), K, (float)p_drop, (uint64_t)seed, seed_ptr(seed_dev),
+                      f32(xm), f32(logits), cur_stream());
 }
 
 // cross-entropy: loss [1] (mean over rows), dlogits (nullable) = (softmax - onehot) * gscale, counts int64 [2]
@@ -514,14 +522,15 @@ void head_ce(const at::Tensor& logits, const OptT& labels, double gscale, const 
 
 void head_backward(const at::Tensor& dlogits, const at::Tensor& xm, const at::Tensor& W, int64_t P, double p_drop,
                    int64_t seed, const at::Tensor& dW, const OptT& db, double beta, const OptT& dfeat,
-                   const at::Tensor& scratch) {
+                   const at::Tensor& scratch, const OptT& seed_dev) {
   const int N = dlogits.size(0), K = dlogits.size(1), C = W.size(1);
   TORCH_CHECK(xm.numel() >= (int64_t)N * C && dW.numel() == (int64_t)K * C, "head backward shapes");
   TORCH_CHECK(!dfeat.has_value() || dfeat->numel() >= (int64_t)N * P * C, "dfeat too small");
   TORCH_CHECK(scratch.numel() >= (int64_t)K * N + (int64_t)C * N + (int64_t)C * K, "head scratch too small");
   if (N == 0) return;
   float* sc = f32(scratch);
-  head_backward_launch(f32(dlogits), f32(xm), f32(W), N, (int)P, C, K, (float)p_drop, (uint64_t)seed, f32(dW),
+  head_backward_launch(f32(dlogits), f32(xm), f32(W), N, (int)P, C, K, (float)p_drop, (uint64_t)seed,
+                       seed_ptr(seed_dev), f32(dW),
                        f32o(db), (float)beta, f32o(dfeat), sc, sc + (int64_t)K * N, sc + (int64_t)K * N + (int64_t)C * N,
                        cur_stream());
 }
@@ -552,6 +561,11 @@ void bnfold_bwd(const at::Tensor& part, int64_t tiles, const at::Tensor& Wf, con
   bnfold_bwd_launch(f32(part), (int)tiles, bfp(Wf), bfp(Wd), f32(G), f32(T), f32(s), (int)C, (int)c, count,
                     f32(gamma), f32(mean), f32(rstd), f32o(dgamma), f32o(dbeta), f32(dW), (float)beta_acc, f32(coef),
                     bfpm(W1t), bfpm(W2), f32(bias), cur_stream());
+}
+
+void head_seed_advance(const at::Tensor& seed_dev) {
+  TORCH_CHECK(seed_dev.scalar_type() == at::kLong && seed_dev.numel() >= 1 && seed_dev.is_cuda(), "int64 [1] seed");
+  head_seed_advance_launch(reinterpret_cast<uint64_t*>(seed_dev.data_ptr<int64_t>()), cur_stream());
 }
 
 void head_dropout_mask(const at::Tensor& out, double p_drop, int64_t seed) {
@@ -654,9 +668,13 @@ PYBIND11_MODULE(_C, m) {
   m.def("synth_frames", &synth_frames);
   m.def("stem_tiles", [](int64_t Ho, int64_t Wo, int64_t N) { return stem_tiles((int)Ho, (int)Wo, (int)N); });
   m.def("stem_supported", [](int64_t Cout, int64_t kt) { return stem_s2d_supported((int)Cout, (int)kt); });
-  m.def("head_forward", &head_forward);
+  m.def("head_forward", &head_forward, py::arg("feat"), py::arg("W"), py::arg("b"), py::arg("p_drop"), py::arg("seed"),
+        py::arg("xm"), py::arg("logits"), py::arg("seed_dev") = py::none());
+  m.def("head_seed_advance", &head_seed_advance);
   m.def("head_ce", &head_ce);
-  m.def("head_backward", &head_backward);
+  m.def("head_backward", &head_backward, py::arg("dlogits"), py::arg("xm"), py::arg("W"), py::arg("P"),
+        py::arg("p_drop"), py::arg("seed"), py::arg("dW"), py::arg("db"), py::arg("beta"), py::arg("dfeat"),
+        py::arg("scratch"), py::arg("seed_dev") = py::none());
   m.def("head_dropout_mask", &head_dropout_mask);
   m.def("stem_fwd", &stem_fwd);
   m.def("stem_wgrad", &stem_wgrad);

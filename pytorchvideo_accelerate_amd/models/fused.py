@@ -876,6 +876,7 @@ class FusedNet:
         import os
         self.lane = 0          # 0: main stream, 1: fast-pathway stream (per-lane scratch)
         self._side = None
+        self._seed_dev = None   # device-resident dropout key (int64 [1]), see _head_forward
         self._ms_warm = False  # set after the first training step (autotuning runs on one stream)
         self._ms_bwd = False
         self._wst = [None, None]          # weight-gradient streams of the two lanes
@@ -1148,13 +1149,21 @@ class FusedNet:
         h = self.head
         W, b = h.proj.weight, h.proj.bias
         p = float(h.dropout.p) if (train and h.dropout is not None) else 0.0
-        # per-step Philox key from torch's CPU generator (reproducible under set_seed; no device sync)
-        seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if p > 0 else 0
+        # per-step Philox key kept on the device: first drawn from torch's CPU generator (reproducible under
+        # set_seed), then advanced by one splitmix64 step per training forward ON the device, so a step captured
+        # into a HIP graph (engine/graph.py) draws a fresh mask on every replay exactly as the eager step does
+        seed = 0
+        if p > 0:
+            if self._seed_dev is None:
+                self._seed_dev = torch.tensor([int(torch.randint(0, 2 ** 62, (1,)).item())], device=self.device,
+                                              dtype=torch.long)
+            self.C.head_seed_advance(self._seed_dev)
         N = feat.shape[0]
         xm = self.ws(("head_xm", tag), (N, feat.shape[2]), torch.float32)
         logits = torch.empty(N, W.shape[0], device=self.device, dtype=torch.float32)
         self.mark("head.fwd")
-        self.C.head_forward(feat, self.flat.view(W), None if b is None else self.flat.view(b), p, seed, xm, logits)
+        self.C.head_forward(feat, self.flat.view(W), None if b is None else self.flat.view(b), p, seed, xm, logits,
+                            self._seed_dev if p > 0 else None)
         return logits, xm, p, seed
 
     @torch.no_grad()
@@ -1211,7 +1220,8 @@ class FusedNet:
             scratch = self.scratch("head_bwd", K * N + Ct * N + Ct * K)
             self.mark("head.bwd")
             self.C.head_backward(dlogits, xm, self.flat.view(W), feat.shape[1], p, seed, self.flat.gview(W),
-                                 None if b is None else self.flat.gview(b), self.grad_beta, gfeat, scratch)
+                                 None if b is None else self.flat.gview(b), self.grad_beta, gfeat, scratch,
+                                 self._seed_dev if p > 0 else None)
             self._progress(self._head_hi)
             if train_backbone:
                 self._backward_backbone(outs, gfeat, ks)

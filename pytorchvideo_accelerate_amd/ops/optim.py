@@ -84,6 +84,17 @@ class FusedSGD(torch.optim.SGD):
             self.after_step()
         return None
 
+    def graph_kernels(self):
+        """The device work of one plain (non-first, no loss-scale check) step, for capture into a HIP graph:
+        the lr lives in ``lr_t`` (refreshed by ``set_lr_tensor`` before each replay, outside the graph)."""
+        assert self._C is not None and not self._first, "capture after the first (state-binding) step"
+        g = self.param_groups[0]
+        lo, hi = self.span if self.span is not None else (0, self.flat.numel)
+        self._C.sgd_momentum(self.flat.data[lo:hi], self.flat.grad[lo:hi], self.buf[lo:hi], self.lr_t,
+                             g["momentum"], g["weight_decay"], 1.0, 0, None)
+        if self.after_step is not None:
+            self.after_step()
+
     def zero_grad(self, set_to_none: bool = True):
         # No memset: the next backward *overwrites* the flat gradient buffer instead of accumulating
         # (wgrad/BN kernels take beta = 0; FusedNet.forward_backward reads ``flat.zeroed``).
