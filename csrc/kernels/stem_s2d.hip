@@ -49,8 +49,16 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds, uint3
 #endif
 }
 
+// LDS position swizzle of the wgrad kernels' 32-byte-position images: bit 2 of the position flips with bit 3.
+// Their transpose reads fetch positions p..p+3 (lanes 0-15) and p+8..p+11 (lanes 16-31) in one 32-lane bank
+// group; unswizzled, positions 8 apart (256 B) hit the same banks (2-way conflict on every read, brute-force
+// checked); swizzled, the two quads cover all 64 banks.  An involution within aligned 16-position groups.
+__device__ __forceinline__ int pswz(int pos) { return pos ^ ((pos >> 1) & 4); }
+
 // one input frame's s2d patch -> LDS slot by LDS-DMA; positions outside the frame / image read zeros
 // through out-of-range buffer offsets.  No VGPR staging, no ds_write: the copy overlaps the MFMA loop.
+// SWZ: LDS position k holds patch position pswz(k) (the DMA stays lane-linear; the swizzle moves to the source).
+template <bool SWZ = false>
 __device__ __forceinline__ void dma_patch(__amdgpu_buffer_rsrc_t r, const StemParams& p, int ti, int hs0, int ws0,
                                           char* slot) {
   const int tid = threadIdx.x, w = tid >> 6;
@@ -58,10 +66,10 @@ __device__ __forceinline__ void dma_patch(__amdgpu_buffer_rsrc_t r, const StemPa
   for (int s = 0; s < 2; ++s) {
     if (s == 1 && w == 3) break;  // chunks 448.. do not exist (wave-uniform)
     const int idx = tid + s * 256;
-    const int pos = idx >> 1, half = idx & 1;
+    const int pos = SWZ ? pswz(idx >> 1) : (idx >> 1), half = idx & 1;
     const int r_ = pos / PW, c_ = pos - r_ * PW;
     const int hs = hs0 + r_ - 2, ws = ws0 + c_ - 2;
-    const bool ok = idx < PH * PW * 2 && ti >= 0 && ti < p.T && (unsigned)hs < (unsigned)p.Hs &&
+    const bool ok = pos < PH * PW && ti >= 0 && ti < p.T && (unsigned)hs < (unsigned)p.Hs &&
                     (unsigned)ws < (unsigned)p.Ws;
     const uint32_t vo = ok ? (uint32_t)((((ti * p.Hs + hs) * p.Ws + ws) * 16 + half * 8) * 2) : OOB;
     dma16(r, slot + (w * 64 + s * 256) * 16, vo);  // chunks 418..447 land in the slot padding
@@ -414,7 +422,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void s
   const __amdgpu_buffer_rsrc_t yr =
       clip_rsrc(p.dy + (int64_t)n * p.To * p.Ho * p.Wo * 8, (uint32_t)(p.To * p.Ho * p.Wo * 16));
   // dY chunk of this lane: position tid >> 1 of the tile, frame t0 + (tid & 1); LDS offset tid * 16
-  const int dpos = tid >> 1, dfh = tid & 1;
+  const int dpos = pswz(tid >> 1), dfh = tid & 1;   // swizzled dY image (see pswz)
   const int dho = ho0 + dpos / TW, dwo = wo0 + dpos % TW;
   const bool dok = dho < p.Ho && dwo < p.Wo;
   auto dma_dy = [&](int t0, char* buf) {
@@ -431,7 +439,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void s
 #pragma unroll
     for (int s = 0; s < 4; ++s) acc[j][s] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  for (int f = 0; f < J; ++f) dma_patch(xr, p, f - p.pt, ho0, wo0, smem + f * SLOT_BYTES);
+  for (int f = 0; f < J; ++f) dma_patch<true>(xr, p, f - p.pt, ho0, wo0, smem + f * SLOT_BYTES);
   dma_dy(0, dyt);
   __syncthreads();
   const int rq = li >> 2, cb = (li & 3) * 8;
@@ -439,8 +447,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void s
     const char* dcur = dyt + ((t0 >> 1) & 1) * DYB;
     if (t0 + 2 < p.To) {
       const int tn = t0 - p.pt + J;
-      dma_patch(xr, p, tn, ho0, wo0, smem + ((t0 + J) % SLOTS) * SLOT_BYTES);
-      dma_patch(xr, p, tn + 1, ho0, wo0, smem + ((t0 + J + 1) % SLOTS) * SLOT_BYTES);
+      dma_patch<true>(xr, p, tn, ho0, wo0, smem + ((t0 + J) % SLOTS) * SLOT_BYTES);
+      dma_patch<true>(xr, p, tn + 1, ho0, wo0, smem + ((t0 + J + 1) % SLOTS) * SLOT_BYTES);
       dma_dy(t0 + 2, dyt + (((t0 >> 1) + 1) & 1) * DYB);
     }
 #pragma unroll
@@ -449,8 +457,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void s
       const int wq = 8 * (g & 1) + rq;
       bf16x8_t a;
       {
-        const char* base = dcur + (hh * TW + wq) * 32 + cb;
-        s16x4_t lo = trr(base), hi = trr(base + 4 * 32);
+        const int dp = hh * TW + wq;
+        s16x4_t lo = trr(dcur + pswz(dp) * 32 + cb), hi = trr(dcur + pswz(dp + 4) * 32 + cb);
         s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         a = __builtin_bit_cast(bf16x8_t, v);
       }
@@ -459,8 +467,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void s
         const char* slot = smem + ((t0 + j) % SLOTS) * SLOT_BYTES;
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-          const char* base = slot + ((hh + w) * PW + (wq + s)) * POSB + cb;
-          s16x4_t lo = trr(base), hi = trr(base + 4 * POSB);
+          const int ip = (hh + w) * PW + (wq + s);
+          s16x4_t lo = trr(slot + pswz(ip) * POSB + cb), hi = trr(slot + pswz(ip + 4) * POSB + cb);
           s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
           acc[j][s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf16x8_t, v), acc[j][s], 0, 0, 0);
         }
