@@ -68,32 +68,6 @@ __global__ void bn_finalize_kernel(const float* __restrict__ part, int tiles, in
   }
 }
 
-// Tile-partial pre-reduction for the finalize kernels: in [tiles][W] -> out [S][W], block s summing tiles
-// [s*per, (s+1)*per) in a fixed order.  The conv epilogues emit one partial row per 128-256-row tile, i.e. up to
-// ~125k rows for the 16M-position fast-pathway tensors; a one-block-per-channel finalize over that many rows runs
-// on a handful of CUs (latency-bound), so the rows are first folded on S blocks spread over the chip.
-__global__ void tile_partial_kernel(const float* __restrict__ in, int tiles, int W, int per, float* __restrict__ out) {
-  const int s = blockIdx.x;
-  const int t0 = s * per, t1 = min(tiles, t0 + per);
-  __shared__ float red[NT];
-  for (int w0 = 0; w0 < W; w0 += NT) {
-    const int Wc = min(NT, W - w0);
-    const int TL = NT / Wc;   // tile lanes per column
-    const int tl = threadIdx.x / Wc, w = threadIdx.x - tl * Wc;
-    float acc = 0.f;
-    if (tl < TL)
-      for (int t = t0 + tl; t < t1; t += TL) acc += in[(int64_t)t * W + w0 + w];
-    red[threadIdx.x] = tl < TL ? acc : 0.f;
-    __syncthreads();
-    if (threadIdx.x < Wc) {
-      float sum = 0.f;
-      for (int k = 0; k < TL; ++k) sum += red[k * Wc + threadIdx.x];
-      out[(int64_t)s * W + w0 + threadIdx.x] = sum;
-    }
-    __syncthreads();
-  }
-}
-
 // eval-mode affine from running statistics
 __global__ void bn_eval_affine_kernel(int C, const float* gamma, const float* beta, const float* rm, const float* rv,
                                       float eps, float* scale, float* shift) {
@@ -654,21 +628,6 @@ int grid_rows(int64_t M, int C) {
 }
 
 }  // namespace
-
-// rows of the pre-reduced partials (0: no pre-reduction) and the tiles each folds
-int tile_partial_rows(int tiles, int* per) {
-  if (tiles <= 1024) return 0;
-  int S = (tiles + 63) / 64;
-  if (S > 1024) S = 1024;
-  *per = (tiles + S - 1) / S;
-  return (tiles + *per - 1) / *per;
-}
-
-void tile_partial_launch(const float* in, int tiles, int W, float* out, hipStream_t s) {
-  int per = 0;
-  const int S = tile_partial_rows(tiles, &per);
-  hipLaunchKernelGGL(tile_partial_kernel, dim3(S), dim3(NT), 0, s, in, tiles, W, per, out);
-}
 
 void bn_finalize_launch(const float* part, int tiles, int C, int64_t count, const float* gamma, const float* beta,
                         float* rm, float* rv, int64_t* nbt, float momentum, float eps, float* smean, float* srstd,

@@ -44,8 +44,6 @@ void bn_bwd_reduce_launch(const uint16_t* g, int ldg, int mask_mode, const void*
                           const float* mh, const uint16_t* y0, const float* mean0, const float* rstd0,
                           const uint16_t* y1, const float* mean1, const float* rstd1, int64_t M, int C, int blocks,
                           int rows_per_block, float* part, uint16_t* dzout, int lddz, hipStream_t s);
-int tile_partial_rows(int tiles, int* per);
-void tile_partial_launch(const float* in, int tiles, int W, float* out, hipStream_t s);
 void bn_bwd_finalize_launch(const float* part, int blocks, int C, int64_t count, int which, const float* gamma,
                             const float* mean, const float* rstd, float* dgamma, float* dbeta, float beta_acc,
                             float* coef, hipStream_t s);
@@ -307,18 +305,7 @@ void bn_finalize(const at::Tensor& part, int64_t tiles, int64_t C, int64_t count
                  const at::Tensor& beta, const OptT& rm, const OptT& rv, const OptT& nbt, double momentum, double eps,
                  const at::Tensor& smean, const at::Tensor& srstd, const at::Tensor& scale, const at::Tensor& shift) {
   int64_t* nb = nbt.has_value() ? nbt->data_ptr<int64_t>() : nullptr;
-  TORCH_CHECK(part.numel() >= tiles * 2 * C, "bn_finalize: partials too small");
-  const float* pp = f32(part);
-  int per = 0;
-  const int S = tile_partial_rows((int)tiles, &per);
-  at::Tensor red;
-  if (S > 0) {   // many tiles: fold them on S blocks first (tile_partial_kernel)
-    red = at::empty({(int64_t)S * 2 * C}, part.options());
-    tile_partial_launch(pp, (int)tiles, (int)(2 * C), red.data_ptr<float>(), cur_stream());
-    pp = red.data_ptr<float>();
-    tiles = S;
-  }
-  bn_finalize_launch(pp, (int)tiles, (int)C, count, f32(gamma), f32(beta), f32o(rm), f32o(rv), nb,
+  bn_finalize_launch(f32(part), (int)tiles, (int)C, count, f32(gamma), f32(beta), f32o(rm), f32o(rv), nb,
                      (float)momentum, (float)eps, f32(smean), f32(srstd), f32(scale), f32(shift), cur_stream());
 }
 
@@ -377,18 +364,7 @@ void bn_bwd_reduce(const at::Tensor& g, int64_t ldg, int64_t mask_mode, const Op
 void bn_bwd_finalize(const at::Tensor& part, int64_t blocks, int64_t C, int64_t count, int64_t which,
                      const at::Tensor& gamma, const at::Tensor& mean, const at::Tensor& rstd, const OptT& dgamma,
                      const OptT& dbeta, double beta_acc, const at::Tensor& coef) {
-  TORCH_CHECK(part.numel() >= blocks * 3 * C, "bn_bwd_finalize: partials too small");
-  const float* pp = f32(part);
-  int per = 0;
-  const int S = tile_partial_rows((int)blocks, &per);
-  at::Tensor red;
-  if (S > 0) {   // many tiles: fold them on S blocks first (tile_partial_kernel)
-    red = at::empty({(int64_t)S * 3 * C}, part.options());
-    tile_partial_launch(pp, (int)blocks, (int)(3 * C), red.data_ptr<float>(), cur_stream());
-    pp = red.data_ptr<float>();
-    blocks = S;
-  }
-  bn_bwd_finalize_launch(pp, (int)blocks, (int)C, count, (int)which, f32(gamma), f32(mean), f32(rstd),
+  bn_bwd_finalize_launch(f32(part), (int)blocks, (int)C, count, (int)which, f32(gamma), f32(mean), f32(rstd),
                          f32o(dgamma), f32o(dbeta), (float)beta_acc, f32(coef), cur_stream());
 }
 
@@ -582,17 +558,7 @@ void bnfold_bwd(const at::Tensor& part, int64_t tiles, const at::Tensor& Wf, con
   TORCH_CHECK(c % 8 == 0 && Wf.numel() >= C * c && Wd.numel() >= C * c && G.numel() >= C * c && T.numel() >= C * c &&
               dW.numel() == C * c && coef.numel() >= 4 * C && W1t.numel() >= C * c && W2.numel() >= c * c &&
               bias.numel() >= 2 * c && part.numel() >= tiles * 3 * C, "bnfold_bwd shapes");
-  const float* pp = f32(part);
-  int per = 0;
-  const int S = tile_partial_rows((int)tiles, &per);
-  at::Tensor red;
-  if (S > 0) {   // many tiles: fold them on S blocks first (tile_partial_kernel)
-    red = at::empty({(int64_t)S * 3 * C}, part.options());
-    tile_partial_launch(pp, (int)tiles, (int)(3 * C), red.data_ptr<float>(), cur_stream());
-    pp = red.data_ptr<float>();
-    tiles = S;
-  }
-  bnfold_bwd_launch(pp, (int)tiles, bfp(Wf), bfp(Wd), f32(G), f32(T), f32(s), (int)C, (int)c, count,
+  bnfold_bwd_launch(f32(part), (int)tiles, bfp(Wf), bfp(Wd), f32(G), f32(T), f32(s), (int)C, (int)c, count,
                     f32(gamma), f32(mean), f32(rstd), f32o(dgamma), f32o(dbeta), f32(dW), (float)beta_acc, f32(coef),
                     bfpm(W1t), bfpm(W2), f32(bias), cur_stream());
 }

@@ -26,8 +26,7 @@ def _bits(mask):
     return (mask.view(M, C // 8, 8).to(torch.int32) * w).sum(-1).to(torch.uint8)
 
 
-@pytest.mark.parametrize("C,tiles,count", [(8, 5, 1001), (16, 37, 4097), (24, 1, 2), (8, 70001, 140002),
-                                           (64, 3000, 9000)])
+@pytest.mark.parametrize("C,tiles,count", [(8, 5, 1001), (16, 37, 4097), (24, 1, 2)])
 def test_bn_finalize_running_stats(C, tiles, count):
     K = _C()
     g = torch.Generator().manual_seed(C)
@@ -213,24 +212,3 @@ def test_stem_pool_bn_backward_fused(C, H, W):
     assert _rel(dbeta.cpu(), br.grad) < 1e-4
     assert _rel(dgamma.cpu(), gr.grad) < 1e-3
     assert _rel(dy.cpu(), yr.grad) < 2e-2
-
-
-@pytest.mark.parametrize("C,blocks", [(8, 125003), (24, 1500), (40, 7)])
-def test_bn_bwd_finalize_many_tiles(C, blocks):
-    """bn_bwd_finalize over many epilogue tiles (pre-reduced on the chip first when > 1024) vs float64 sums."""
-    K = _C()
-    g = torch.Generator().manual_seed(C + blocks)
-    part = torch.randn(blocks, 3, C, generator=g, dtype=torch.float64)
-    gamma, mean = torch.rand(C, generator=g) + 0.5, torch.randn(C, generator=g)
-    rstd = torch.rand(C, generator=g) + 0.5
-    count = blocks * 128
-    dgamma, dbeta = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
-    coef = torch.empty(3 * C, device=DEV)
-    K.bn_bwd_finalize(part.float().to(DEV), blocks, C, count, 1, gamma.to(DEV), mean.to(DEV), rstd.to(DEV),
-                      dgamma, dbeta, 0.0, coef)
-    torch.cuda.synchronize()
-    db, dg = part[:, 0].sum(0), part[:, 2].sum(0)   # which=1: the second BN's sum(dz*xhat)
-    assert _rel(dbeta.cpu(), db) < 1e-5 and _rel(dgamma.cpu(), dg) < 1e-5
-    gm, r, mu = gamma.double(), rstd.double(), mean.double()
-    want_b = -gm * r * r * dg / count
-    assert _rel(coef[C:2 * C].cpu(), want_b) < 1e-4
