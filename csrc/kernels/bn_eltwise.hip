@@ -255,8 +255,12 @@ __global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int block
   }
 }
 
-// dy_k = A_k*dz + B_k*y_k + C_k  (k = 0, 1) ; optionally dz itself (identity shortcut gradient)
-__global__ void bn_bwd_apply_kernel(const uint16_t* __restrict__ g, int ldg, int mask_mode,
+// dy_k = A_k*dz + B_k*y_k + C_k  (k = 0, 1) ; optionally dz itself (identity shortcut gradient).
+// Specialised at compile time on the mask mode and on which of y0 / y1 / dz take part: the common interior
+// apply (no mask, y0 only) then needs ~1/2 of the registers of the all-modes kernel (116 VGPRs), i.e. twice
+// the waves per SIMD to hide the latency of this streaming pass.
+template <int MM, bool Y0, bool Y1, bool DZ>
+__global__ void bn_bwd_apply_kernel(const uint16_t* __restrict__ g, int ldg,
                                     const void* __restrict__ mo_, int ldm,
                                     const float* __restrict__ ms, const float* __restrict__ mh,
                                     const uint16_t* __restrict__ y0, const float* __restrict__ coef0,
@@ -271,40 +275,41 @@ __global__ void bn_bwd_apply_kernel(const uint16_t* __restrict__ g, int ldg, int
   float A0[8], B0[8], C0[8], A1[8], B1[8], C1[8], MS[8], MH[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    A0[e] = y0 ? coef0[c + e] : 0.f; B0[e] = y0 ? coef0[C + c + e] : 0.f; C0[e] = y0 ? coef0[2 * C + c + e] : 0.f;
-    A1[e] = y1 ? coef1[c + e] : 0.f; B1[e] = y1 ? coef1[C + c + e] : 0.f; C1[e] = y1 ? coef1[2 * C + c + e] : 0.f;
-    MS[e] = mask_mode == 2 ? ms[c + e] : 0.f; MH[e] = mask_mode == 2 ? mh[c + e] : 0.f;
+    if constexpr (Y0) { A0[e] = coef0[c + e]; B0[e] = coef0[C + c + e]; C0[e] = coef0[2 * C + c + e]; }
+    if constexpr (Y1) { A1[e] = coef1[c + e]; B1[e] = coef1[C + c + e]; C1[e] = coef1[2 * C + c + e]; }
+    if constexpr (MM == 2) { MS[e] = ms[c + e]; MH[e] = mh[c + e]; }
   }
   for (int64_t m = (int64_t)blockIdx.x * rpi + lr; m < M; m += (int64_t)gridDim.x * rpi) {
     float dz[8], a[8];
     unpack8(*reinterpret_cast<const uint4*>(g + m * ldg + c), dz);
-    unpack8(y0 ? *reinterpret_cast<const uint4*>(y0 + m * C + c) : uint4{0, 0, 0, 0}, a);
-    if (mask_mode == 1) {
+    if constexpr (Y0) unpack8(*reinterpret_cast<const uint4*>(y0 + m * C + c), a);
+    if constexpr (MM == 1) {
       float o[8];
       unpack8(*reinterpret_cast<const uint4*>(mo + m * ldm + c), o);
 #pragma unroll
       for (int e = 0; e < 8; ++e) dz[e] = o[e] > 0.f ? dz[e] : 0.f;
-    } else if (mask_mode == 3) {
+    } else if constexpr (MM == 3) {
       const unsigned bits = mb[m * ldm + (c >> 3)];
 #pragma unroll
       for (int e = 0; e < 8; ++e) dz[e] = (bits >> e) & 1u ? dz[e] : 0.f;
-    } else if (mask_mode == 2) {
+    } else if constexpr (MM == 2) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) dz[e] = (a[e] * MS[e] + MH[e]) > 0.f ? dz[e] : 0.f;
     }
     float o[8];
-    if (y0) {   // y0 == nullptr: only dz (identity shortcut) / dy1 are produced
+    if constexpr (Y0) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) o[e] = A0[e] * dz[e] + B0[e] * a[e] + C0[e];
       *reinterpret_cast<uint4*>(dy0 + m * C + c) = pack8(o);
     }
-    if (y1) {
-      unpack8(*reinterpret_cast<const uint4*>(y1 + m * C + c), a);
+    if constexpr (Y1) {
+      float b[8];
+      unpack8(*reinterpret_cast<const uint4*>(y1 + m * C + c), b);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = A1[e] * dz[e] + B1[e] * a[e] + C1[e];
+      for (int e = 0; e < 8; ++e) o[e] = A1[e] * dz[e] + B1[e] * b[e] + C1[e];
       *reinterpret_cast<uint4*>(dy1 + m * C + c) = pack8(o);
     }
-    if (dzout) {
+    if constexpr (DZ) {
       uint16_t* d = dzout + m * lddz + c;
       if (dz_accum) {
         float q[8];
@@ -685,8 +690,30 @@ void bn_bwd_apply_launch(const uint16_t* g, int ldg, int mask_mode, const void* 
                          const float* mh, const uint16_t* y0, const float* coef0, uint16_t* dy0, const uint16_t* y1,
                          const float* coef1, uint16_t* dy1, uint16_t* dzout, int lddz, int dz_accum, int64_t M, int C,
                          hipStream_t s) {
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_rows(M, C)), dim3(NT), 0, s, g, ldg, mask_mode, mo, ldm, ms,
-                     mh, y0, coef0, dy0, y1, coef1, dy1, dzout, lddz, dz_accum, M, C);
+  const dim3 grid(grid_rows(M, C)), block(NT);
+#define PVA_APPLY(MMv, Y0v, Y1v, DZv)                                                                       \
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<MMv, Y0v, Y1v, DZv>), grid, block, 0, s, g, ldg, mo, ldm, ms, mh, y0, \
+                     coef0, dy0, y1, coef1, dy1, dzout, lddz, dz_accum, M, C)
+#define PVA_APPLY_MM(Y0v, Y1v, DZv)                       \
+  switch (mask_mode) {                                    \
+    case 1: PVA_APPLY(1, Y0v, Y1v, DZv); break;            \
+    case 2: PVA_APPLY(2, Y0v, Y1v, DZv); break;            \
+    case 3: PVA_APPLY(3, Y0v, Y1v, DZv); break;            \
+    default: PVA_APPLY(0, Y0v, Y1v, DZv); break;           \
+  }
+  const int sel = (y0 ? 4 : 0) | (y1 ? 2 : 0) | (dzout ? 1 : 0);
+  switch (sel) {
+    case 1: PVA_APPLY_MM(false, false, true); break;
+    case 2: PVA_APPLY_MM(false, true, false); break;
+    case 3: PVA_APPLY_MM(false, true, true); break;
+    case 4: PVA_APPLY_MM(true, false, false); break;
+    case 5: PVA_APPLY_MM(true, false, true); break;
+    case 6: PVA_APPLY_MM(true, true, false); break;
+    case 7: PVA_APPLY_MM(true, true, true); break;
+    default: break;   // nothing to produce
+  }
+#undef PVA_APPLY_MM
+#undef PVA_APPLY
 }
 
 void stem_pool_fwd_launch(const uint16_t* y, const float* scale, const float* shift, uint16_t* out, uint8_t* arg,
