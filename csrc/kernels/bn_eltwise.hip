@@ -140,7 +140,8 @@ __global__ void res_out_kernel(const uint16_t* __restrict__ yc, const float* __r
 //   mask_mode 0: dz = g ; 1: dz = g * (mo > 0) ; 2: dz = g * (y0*ms + mh > 0) ;
 //   3: dz = g * bit(mo)  (mo = uint8 ReLU mask bits [M][C/8] written by res_out)
 // ------------------------------------------------------------------------------------------
-__global__ void bn_bwd_reduce_kernel(const uint16_t* __restrict__ g, int ldg, int mask_mode,
+template <int MM, bool Y0, bool Y1, bool DZ>
+__global__ void bn_bwd_reduce_kernel(const uint16_t* __restrict__ g, int ldg,
                                      const void* __restrict__ mo_, int ldm,
                                      const float* __restrict__ ms, const float* __restrict__ mh,
                                      const uint16_t* __restrict__ y0, const float* __restrict__ mean0,
@@ -162,33 +163,39 @@ __global__ void bn_bwd_reduce_kernel(const uint16_t* __restrict__ g, int ldg, in
   if (lr < rpi) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      m0[e] = y0 ? mean0[c + e] : 0.f; r0[e] = y0 ? rstd0[c + e] : 0.f;
-      m1[e] = y1 ? mean1[c + e] : 0.f; r1[e] = y1 ? rstd1[c + e] : 0.f;
-      MS[e] = mask_mode == 2 ? ms[c + e] : 0.f; MH[e] = mask_mode == 2 ? mh[c + e] : 0.f;
+      m0[e] = Y0 ? mean0[c + e] : 0.f; r0[e] = Y0 ? rstd0[c + e] : 0.f;
+      m1[e] = Y1 ? mean1[c + e] : 0.f; r1[e] = Y1 ? rstd1[c + e] : 0.f;
+      MS[e] = MM == 2 ? ms[c + e] : 0.f; MH[e] = MM == 2 ? mh[c + e] : 0.f;
     }
     const int64_t mbeg = (int64_t)blockIdx.x * rows_per_block;
     const int64_t mend = min<int64_t>(M, mbeg + rows_per_block);
     for (int64_t m = mbeg + lr; m < mend; m += rpi) {
       float dz[8], a[8];
       unpack8(*reinterpret_cast<const uint4*>(g + m * ldg + c), dz);
-      unpack8(y0 ? *reinterpret_cast<const uint4*>(y0 + m * C + c) : uint4{0, 0, 0, 0}, a);
-      if (mask_mode == 1) {
+      if constexpr (Y0) unpack8(*reinterpret_cast<const uint4*>(y0 + m * C + c), a);
+      else
+#pragma unroll
+        for (int e = 0; e < 8; ++e) a[e] = 0.f;
+      if constexpr (MM == 1) {
         float o[8];
         unpack8(*reinterpret_cast<const uint4*>(mo + m * ldm + c), o);
 #pragma unroll
         for (int e = 0; e < 8; ++e) dz[e] = o[e] > 0.f ? dz[e] : 0.f;
-      } else if (mask_mode == 3) {
+      } else if constexpr (MM == 3) {
         const unsigned bits = mb[m * ldm + (c >> 3)];
 #pragma unroll
         for (int e = 0; e < 8; ++e) dz[e] = (bits >> e) & 1u ? dz[e] : 0.f;
-      } else if (mask_mode == 2) {
+      } else if constexpr (MM == 2) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) dz[e] = (a[e] * MS[e] + MH[e]) > 0.f ? dz[e] : 0.f;
       }
-      if (dzout) *reinterpret_cast<uint4*>(dzout + m * lddz + c) = pack8(dz);   // masked dz, same pass
+      if constexpr (DZ) *reinterpret_cast<uint4*>(dzout + m * lddz + c) = pack8(dz);   // masked dz, same pass
 #pragma unroll
-      for (int e = 0; e < 8; ++e) { sdz[e] += dz[e]; s0[e] += dz[e] * (a[e] - m0[e]) * r0[e]; }
-      if (y1) {
+      for (int e = 0; e < 8; ++e) {
+        sdz[e] += dz[e];
+        if constexpr (Y0) s0[e] += dz[e] * (a[e] - m0[e]) * r0[e];
+      }
+      if constexpr (Y1) {
         float b[8];
         unpack8(*reinterpret_cast<const uint4*>(y1 + m * C + c), b);
 #pragma unroll
@@ -675,8 +682,29 @@ void bn_bwd_reduce_launch(const uint16_t* g, int ldg, int mask_mode, const void*
                           const float* mh, const uint16_t* y0, const float* mean0, const float* rstd0,
                           const uint16_t* y1, const float* mean1, const float* rstd1, int64_t M, int C, int blocks,
                           int rows_per_block, float* part, uint16_t* dzout, int lddz, hipStream_t s) {
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(blocks), dim3(NT), NT * 96, s, g, ldg, mask_mode, mo,
-                     ldm, ms, mh, y0, mean0, rstd0, y1, mean1, rstd1, M, C, rows_per_block, part, dzout, lddz);
+  // compile-time mask mode / operand set (as bn_bwd_apply: fewer registers, more waves per SIMD)
+#define PVA_RED(MMv, Y0v, Y1v, DZv)                                                                               \
+  hipLaunchKernelGGL((bn_bwd_reduce_kernel<MMv, Y0v, Y1v, DZv>), dim3(blocks), dim3(NT), NT * 96, s, g, ldg, mo, ldm, \
+                     ms, mh, y0, mean0, rstd0, y1, mean1, rstd1, M, C, rows_per_block, part, dzout, lddz)
+#define PVA_RED_MM(Y0v, Y1v, DZv)                       \
+  switch (mask_mode) {                                  \
+    case 1: PVA_RED(1, Y0v, Y1v, DZv); break;            \
+    case 2: PVA_RED(2, Y0v, Y1v, DZv); break;            \
+    case 3: PVA_RED(3, Y0v, Y1v, DZv); break;            \
+    default: PVA_RED(0, Y0v, Y1v, DZv); break;           \
+  }
+  switch ((y0 ? 4 : 0) | (y1 ? 2 : 0) | (dzout ? 1 : 0)) {
+    case 0: PVA_RED_MM(false, false, false); break;
+    case 1: PVA_RED_MM(false, false, true); break;
+    case 2: PVA_RED_MM(false, true, false); break;
+    case 3: PVA_RED_MM(false, true, true); break;
+    case 4: PVA_RED_MM(true, false, false); break;
+    case 5: PVA_RED_MM(true, false, true); break;
+    case 6: PVA_RED_MM(true, true, false); break;
+    default: PVA_RED_MM(true, true, true); break;
+  }
+#undef PVA_RED_MM
+#undef PVA_RED
 }
 
 void bn_bwd_finalize_launch(const float* part, int blocks, int C, int64_t count, int which, const float* gamma,
