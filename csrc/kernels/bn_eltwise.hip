@@ -682,9 +682,14 @@ void bn_bwd_reduce_launch(const uint16_t* g, int ldg, int mask_mode, const void*
                           const float* mh, const uint16_t* y0, const float* mean0, const float* rstd0,
                           const uint16_t* y1, const float* mean1, const float* rstd1, int64_t M, int C, int blocks,
                           int rows_per_block, float* part, uint16_t* dzout, int lddz, hipStream_t s) {
-  // compile-time mask mode / operand set (as bn_bwd_apply: fewer registers, more waves per SIMD)
+  // compile-time mask mode / operand set (as bn_bwd_apply: fewer registers, more waves per SIMD); LDS sized to
+  // the reduction slots actually used ([slots][3][C] fp32: 4 wave slots when C/8 < 64, else one per row group),
+  // not the 24 KB worst case, so small-C launches are not LDS-occupancy-limited
+  const int vecs_ = C / 8;
+  const bool wred_ = vecs_ < 64 && (vecs_ & (vecs_ - 1)) == 0;
+  const size_t red_lds = (size_t)(wred_ ? NT / 64 : NT / vecs_) * 3 * C * sizeof(float);
 #define PVA_RED(MMv, Y0v, Y1v, DZv)                                                                               \
-  hipLaunchKernelGGL((bn_bwd_reduce_kernel<MMv, Y0v, Y1v, DZv>), dim3(blocks), dim3(NT), NT * 96, s, g, ldg, mo, ldm, \
+  hipLaunchKernelGGL((bn_bwd_reduce_kernel<MMv, Y0v, Y1v, DZv>), dim3(blocks), dim3(NT), red_lds, s, g, ldg, mo, ldm, \
                      ms, mh, y0, mean0, rstd0, y1, mean1, rstd1, M, C, rows_per_block, part, dzout, lddz)
 #define PVA_RED_MM(Y0v, Y1v, DZv)                       \
   switch (mask_mode) {                                  \
