@@ -326,9 +326,16 @@ void direct_launch_cfg(const ConvParams& p, int rpb, bool epi, hipStream_t s) {
 }
 
 // loads in flight per lane = RT x KB: 8 row groups for single-k-step convs, else 4 (2 for NB >= 3) x up to 3
+// ``half``: half the row groups in flight (fewer VGPRs -> more waves per SIMD; an autotuner candidate, cfg bit 7)
 template <int NB>
-void direct_launch_nb(const ConvParams& p, int rpb, bool epi, hipStream_t s) {
+void direct_launch_nb(const ConvParams& p, int rpb, bool epi, bool half, hipStream_t s) {
   const int KS = direct_ks(p);
+  if (half) {
+    if (KS == 1) direct_launch_cfg<NB, (NB <= 2 ? 4 : 2), 1>(p, rpb, epi, s);
+    else if (KS == 2) direct_launch_cfg<NB, (NB <= 2 ? 2 : 1), 2>(p, rpb, epi, s);
+    else direct_launch_cfg<NB, (NB <= 2 ? 2 : 1), 3>(p, rpb, epi, s);
+    return;
+  }
   if (KS == 1) direct_launch_cfg<NB, (NB <= 2 ? 8 : 4), 1>(p, rpb, epi, s);
   else if (KS == 2) direct_launch_cfg<NB, (NB <= 2 ? 4 : 2), 2>(p, rpb, epi, s);
   else direct_launch_cfg<NB, (NB <= 2 ? 4 : 2), 3>(p, rpb, epi, s);
@@ -350,10 +357,11 @@ int conv_direct_legal(const ConvParams& p, int chunk) {
 void conv_direct_launch(const ConvParams& p, int cfg, hipStream_t s) {
   const int rpb = conv_direct_rows(cfg);
   const bool epi = p.eres || p.emask || p.epart;
+  const bool half = (cfg & 128) != 0;
   switch ((p.Ngemm + 15) / 16) {
-    case 1: direct_launch_nb<1>(p, rpb, epi, s); break;
-    case 2: direct_launch_nb<2>(p, rpb, epi, s); break;
-    case 3: direct_launch_nb<3>(p, rpb, epi, s); break;
-    default: direct_launch_nb<4>(p, rpb, epi, s); break;
+    case 1: direct_launch_nb<1>(p, rpb, epi, half, s); break;
+    case 2: direct_launch_nb<2>(p, rpb, epi, half, s); break;
+    case 3: direct_launch_nb<3>(p, rpb, epi, half, s); break;
+    default: direct_launch_nb<4>(p, rpb, epi, half, s); break;
   }
 }

@@ -27,6 +27,7 @@ UT = 8
 DIRECT = 32           # narrow direct-to-register kernel (csrc/kernels/conv_direct.hip)
 DIRECT_2K = 64        #   with 2048 rows per workgroup (else 512)
 DMA = 128             # uniform-tap loader staged by LDS-DMA (buffer_load ... lds); launches without input affine
+DIRECT_HALF = 128     #   (with DIRECT) half the row groups in flight per wave: fewer VGPRs, more waves per SIMD
 BIG = 256             # 256x256 tile of 8 waves (N >= 256; the backward-BN epilogue in 64-row slices)
 PW = 512              # streaming pointwise kernel (csrc/kernels/conv_pw.hip): dense 1x1x1 GEMMs, K <= 256,
 PW_ROWS = (1024, 2048, 4096)   # N % 32 == 0, weights in LDS; bits 0-1 select the rows per workgroup,
@@ -42,7 +43,7 @@ def describe(cfg: int) -> str:
     if cfg & PW:
         return "pw%d%s" % (PW_ROWS[cfg & 3], "s" if cfg & PW_SOLO else "")
     if cfg & DIRECT:
-        return "direct%d" % (2048 if cfg & DIRECT_2K else 512)
+        return "direct%d%s" % (2048 if cfg & DIRECT_2K else 512, "/rt2" if cfg & DIRECT_HALF else "")
     if cfg & BIG:
         return "256x256/bk%d%s%s" % (64 if cfg & BK64 else 32, "/ut" if cfg & UT else "", "/dma" if cfg & DMA else "")
     return "%dx%d/bk%d%s%s" % (TILE_BM[cfg & 3], TILE_BN[cfg & 3], 64 if cfg & BK64 else 32, "/ut" if cfg & UT else "",
@@ -104,7 +105,7 @@ class ConvTuner:
                     if aff == 0 and self.dma:
                         out.append(w | DMA)
         if direct and self.direct and self.C.conv_direct_legal(list(g), chunk):
-            out += [EXPLICIT | DIRECT, EXPLICIT | DIRECT | DIRECT_2K]
+            out += [EXPLICIT | DIRECT | r | h for r in (0, DIRECT_2K) for h in (0, DIRECT_HALF)]
         if pw and self.pw and self._pw_now and self.C.conv_pw_legal(list(g), chunk):
             self._pw_seen += 1
             if self.pw_only is None or self.pw_only == self._pw_seen - 1:

@@ -8,7 +8,7 @@ import pytest
 import torch
 
 from pytorchvideo_accelerate_amd.ops.conv import Act, ConvSpec, dgrad_phases, fwd_geometry, pack_weight
-from pytorchvideo_accelerate_amd.ops.tune import DIRECT, DIRECT_2K, EXPLICIT
+from pytorchvideo_accelerate_amd.ops.tune import DIRECT, DIRECT_2K, DIRECT_HALF, EXPLICIT
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -25,7 +25,8 @@ CASES = [
     (32, 64, (1, 1, 1), (1, 2, 2), (0, 0, 0), (2, 8, 14, 14)),      # fast branch1 stride 2
     (64, 64, (1, 3, 3), (1, 1, 1), (0, 1, 1), (2, 4, 7, 7)),        # fast res5 conv_b, K = 576
 ]
-CFGS = [EXPLICIT | DIRECT, EXPLICIT | DIRECT | DIRECT_2K]
+CFGS = [EXPLICIT | DIRECT, EXPLICIT | DIRECT | DIRECT_2K, EXPLICIT | DIRECT | DIRECT_HALF,
+        EXPLICIT | DIRECT | DIRECT_2K | DIRECT_HALF]
 
 
 def C():
@@ -71,7 +72,7 @@ def test_direct_fwd_affine_stats(case, cfg):
     torch.testing.assert_close(stats.sum(0)[1], (yf * yf).sum(0), rtol=1e-3, atol=1e-3)
 
 
-@pytest.mark.parametrize("cfg", CFGS[:1])
+@pytest.mark.parametrize("cfg", CFGS[::2])
 @pytest.mark.parametrize("case", CASES)
 def test_direct_dgrad_phases_accum(case, cfg):
     x, w, spec = _mk(case, 32)
@@ -105,9 +106,10 @@ def _bits(mask):
     return (mask.view(M, Ch // 8, 8).to(torch.int32) * w).sum(-1).to(torch.uint8)
 
 
+@pytest.mark.parametrize("cfg", CFGS[::2])
 @pytest.mark.parametrize("mode", ["dual_accum", "single", "affine_mask"])
 @pytest.mark.parametrize("case", [CASES[1], CASES[4], (64, 32, (3, 1, 1), (1, 1, 1), (1, 0, 0), (2, 8, 14, 14))])
-def test_direct_dgrad_bn_epilogue(case, mode):
+def test_direct_dgrad_bn_epilogue(case, mode, cfg):
     x, w, spec = _mk(case, 33)
     N, Ci, T, H, W = x.shape
     if Ci > 64 or Ci % 8:
@@ -128,7 +130,6 @@ def test_direct_dgrad_bn_epilogue(case, mode):
     dy = Act.from_ncthw(gy)
     geo = dgrad_phases(spec, N, (T, H, W), (dy.T, dy.H, dy.W), dy.ld, Ci)
     assert len(geo) == 1
-    cfg = EXPLICIT | DIRECT
     rows = C().conv_cfg_bm(cfg, Ci)
     part = torch.full(((M + rows - 1) // rows, 3, Ci), float("nan"), device=DEV)
     if mode == "dual_accum":
