@@ -188,12 +188,12 @@ class _ConvBN:
                     from ..ops.conv import halo_wgrad_plan
                     sp = halo_wgrad_plan(s, dy.M, (dy.T, dy.H, dy.W), (cfg >> 9) & 1)
                 elif cfg & 128:   # narrow per-wave kernel: bits 2-3 = wave count target, 64 rows per chunk
-                    nw = (1024, 2048, 4096)[(cfg >> 2) & 3]
+                    nw = (1024, 2048, 4096, 8192)[(cfg >> 2) & 3]
                     pps = ((dy.M + nw - 1) // nw + 63) // 64 * 64
                     sp = ((dy.M + pps - 1) // pps, pps, 16)
                 else:   # bits 0-1 (+ bit 6: tiles 4-7) tile variant, 2-3 split-K target, 5: 64-position stages
                     v = (cfg & 3) | (8 if cfg & 64 else 0)
-                    tb = (512, 1024, 2048)[(cfg >> 2) & 3]
+                    tb = (512, 1024, 2048, 4096)[(cfg >> 2) & 3]
                     sp = wgrad_splits(dy.M, s.cout, K, target_blocks=tb, variant=v) + (v | (4 if cfg & 32 else 0),)
                 eng._splits[key] = sp
             return sp
@@ -221,13 +221,14 @@ class _ConvBN:
                     bmw, bnw = C.wgrad_tile(s.cout, K, vw)
                     if bmw > max(16, s.cout) or bmw * 8 < s.cout or (v >= 4 and bnw > 2 * K):
                         continue
-                    for tbi, bp in ((t, b) for t in range(3) for b in (0, 32)):
+                    for tbi, bp in ((t, b) for t in range(4) for b in (0, 32)):
                         c = 16 | (v & 3) | (64 if v >= 4 else 0) | (tbi << 2) | bp
                         if gram and geometry(c)[0] > 4096:
                             continue
                         cands.append(c)
                 if C.wgrad_narrow_legal(s.cout, s.cin_pad, K) and s.chunk == 8:
-                    cands += [16 | 128 | (tbi << 2) for tbi in range(3)]
+                    cands += [c for c in (16 | 128 | (tbi << 2) for tbi in range(4))
+                              if not (gram and geometry(c)[0] > 4096)]   # colsum slab holds 4096 splits
                 if not gram:   # halo-staged kernel, two box sizes
                     from ..ops.conv import halo_wgrad_plan
                     for o in (0, 1):
