@@ -65,7 +65,12 @@ def parse(argv=None):
     ap.add_argument("--graph", type=int, default=int(os.environ.get("PVA_BENCH_GRAPH", "0")),
                     help="1: replay each micro-step (+ SGD) as a captured HIP graph (single process; engine/graph.py)")
     ap.add_argument("--plumbing", action="store_true", help="CPU/gloo rehearsal on the PyTorch modules")
-    ap.add_argument("--dump", default=None, help="(plumbing) write rank-0 first-step gradients + final params here")
+    ap.add_argument("--dump", default=None,
+                    help="write the first optimizer step's (all-reduced) flat gradient and every rank's final "
+                         "parameters here (cross-rank numerics tests)")
+    ap.add_argument("--data-rank", type=int, default=-1,
+                    help="draw the synthetic data of this rank instead of the own one (single-process oracle runs "
+                         "of a multi-rank job's shards)")
     return ap.parse_args(argv)
 
 
@@ -158,9 +163,10 @@ def run(a):
         sync = GradSync(eng.flat.grad, st, a.bucket_mb, boundaries=bounds, first_mb=a.first_bucket_mb,
                         grad_dtype=gdt, timing=st.world_size > 1)
         eng.grad_hook = sync.progress if st.world_size > 1 else None   # (1 GPU: no buckets to launch)
-        gen = torch.Generator().manual_seed(1000 + st.rank)
+        drank = st.rank if a.data_rank < 0 else a.data_rank
+        gen = torch.Generator().manual_seed(1000 + drank)
         frames = torch.empty(B, a.src_frames, a.src_h, a.src_w, 3, dtype=torch.uint8, device=dev)
-        eng.C.synth_frames(frames, 7 + st.rank)
+        eng.C.synth_frames(frames, 7 + drank)
         # double-buffered on-device preprocessing: micro-batch k+1 is decoded/resized/cropped on its own
         # stream while micro-batch k trains (a prefetching data loader; every step still pays its batch)
         preps = [GpuClipBatch(dev, a.frames, a.crop, a.alpha, s2d=eng.input_s2d) for _ in range(2)]
@@ -221,6 +227,8 @@ def run(a):
                 loss, _ = eng.forward_backward(xs, labels_all[(i * a.grad_accum + j) % 64],
                                                loss_scale=1.0 / a.grad_accum)
                 sync.finish()
+            if i == 0 and a.dump:
+                dump["grad"] = eng.flat.grad.clone()
             opt.step()
             return loss
 

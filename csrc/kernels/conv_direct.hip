@@ -326,7 +326,7 @@ void direct_launch_cfg(const ConvParams& p, int rpb, bool epi, hipStream_t s) {
 }
 
 // loads in flight per lane = RT x KB: 8 row groups for single-k-step convs, else 4 (2 for NB >= 3) x up to 3
-// ``half``: half the row groups in flight (fewer VGPRs -> more waves per SIMD; an autotuner candidate, cfg bit 7)
+// ``half``: half the row groups in flight (fewer VGPRs -> more waves per SIMD; an autotuner candidate, cfg bit 10)
 template <int NB>
 void direct_launch_nb(const ConvParams& p, int rpb, bool epi, bool half, hipStream_t s) {
   const int KS = direct_ks(p);
@@ -357,7 +357,7 @@ int conv_direct_legal(const ConvParams& p, int chunk) {
 void conv_direct_launch(const ConvParams& p, int cfg, hipStream_t s) {
   const int rpb = conv_direct_rows(cfg);
   const bool epi = p.eres || p.emask || p.epart;
-  const bool half = (cfg & 128) != 0;
+  const bool half = (cfg & 1024) != 0;
   switch ((p.Ngemm + 15) / 16) {
     case 1: direct_launch_nb<1>(p, rpb, epi, half, s); break;
     case 2: direct_launch_nb<2>(p, rpb, epi, half, s); break;

@@ -74,15 +74,24 @@ class SyntheticVideoPaths(LabeledVideoPaths):
     """Virtual Kinetics-like corpus for runs without data (``--synthetic``)."""
 
     def __init__(self, num_videos: int, num_classes: int, num_frames: int = 300, height: int = 256,
-                 width: int = 340, fps: float = 30.0, seed: int = 0):
+                 width: int = 340, fps: float = 30.0, seed: int = 0, min_frames: Optional[int] = None):
+        """``min_frames``: video lengths vary deterministically in [min_frames, num_frames] (as real Kinetics
+        videos do, so the number of uniform validation clips differs per video and per rank); default: all
+        ``num_frames`` long."""
         items = [(f"synthetic://{i}", {"label": i % num_classes}) for i in range(num_videos)]
         super().__init__(items, [f"class_{c}" for c in range(num_classes)])
         self.spec = (num_frames, height, width, fps)
         self.seed = seed
+        self.min_frames = num_frames if min_frames is None else max(1, min(int(min_frames), num_frames))
+
+    def frames_of(self, i: int) -> int:
+        T = self.spec[0]
+        span = T - self.min_frames + 1
+        return T if span <= 1 else self.min_frames + (i * 7919 + self.seed * 104729) % span
 
     def open(self, i: int) -> Video:
-        T, H, W, fps = self.spec
-        return SyntheticVideo(f"video_{i}", self.seed * 7919 + i, T, H, W, fps)
+        _, H, W, fps = self.spec
+        return SyntheticVideo(f"video_{i}", self.seed * 7919 + i, self.frames_of(i), H, W, fps)
 
 
 def distributed_video_indices(n: int, rank: int, world: int, seed: int = 0, epoch: int = 0,

@@ -60,15 +60,25 @@ class Accelerator:
         self.trackers = Trackers(log_with, logging_dir, self.state.is_main_process)
         self.logging_dir = logging_dir
         self.bucket_mb = bucket_mb
-        # On a GPU the fused gfx950 kernels always run (bf16 MFMA compute, fp32 master weights and
-        # optimizer; fp16 adds the dynamic loss-scale state machine).  The PyTorch/MIOpen module path is
-        # an explicit debugging / oracle opt-in (kernels="torch"), never a silent fallback; on CPU it is
-        # the only path.
+        # Precision policy (what runs is what was asked for; recorded as ``compute_dtype``):
+        #  * bf16 / fp16 on a GPU -> the fused gfx950 kernels: bf16 MFMA compute, fp32 master weights and optimizer;
+        #    fp16 additionally runs the dynamic loss-scale state machine of the reference recipe (run_slowfast_r50.sh)
+        #    on top of bf16 compute (documented alias: the kernels have no fp16 variant);
+        #  * "no" (the reference default, fp32 math) on a GPU -> the PyTorch fp32 module path, unless the fused
+        #    kernels are requested explicitly with kernels="fused" (then bf16 compute, said so in compute_dtype);
+        #  * CPU -> the PyTorch path.
         if kernels == "auto":
-            kernels = "fused" if self.device.type == "cuda" else "torch"
-            if kernels == "fused" and mixed_precision == "no" and self.state.is_main_process:
-                print("note: --mixed_precision no on the fused MI355X path computes convolutions in bf16 with fp32 "
-                      "master weights/optimizer; pass --kernels torch for fp32 PyTorch execution", flush=True)
+            if self.device.type == "cuda" and mixed_precision in ("bf16", "fp16"):
+                kernels = "fused"
+            else:
+                kernels = "torch"
+                if self.device.type == "cuda" and self.state.is_main_process:
+                    print("note: --mixed_precision no requests fp32 math: running the PyTorch fp32 path; "
+                          "--mixed_precision bf16 (or --kernels fused) selects the fused MI355X kernels", flush=True)
+        if kernels == "fused":
+            self.compute_dtype = "bf16" if mixed_precision != "fp16" else "bf16+fp16-loss-scaling"
+        else:
+            self.compute_dtype = {"bf16": "bf16-autocast", "fp16": "fp16-autocast"}.get(mixed_precision, "fp32")
         self.kernels = kernels
         self._models: List[Any] = []
         self._optimizers: List[Any] = []

@@ -34,13 +34,15 @@ class GraphedStep:
         """One replayed micro-step; returns (loss [device scalar], logits) — graph-owned outputs, overwritten by
         the next replay of the same key."""
         eng = self.eng
-        if self.labels is None or self.labels.shape != labels.shape:
+        if self.labels is None or self.labels.shape != labels.shape or self.labels.dtype != labels.dtype:
+            # graphs captured earlier read the old label buffer: they are invalid once it is replaced
             self.labels = torch.empty_like(labels, device=eng.device)
+            self.graphs.clear()
         self.labels.copy_(labels, non_blocking=True)
         step = optimizer_step and self.opt is not None
         if step:
             self.opt.set_lr_tensor()
-        key = (tuple(x.t.data_ptr() for x in xs), bool(accumulate), step, float(loss_scale))
+        key = (tuple(x.t.data_ptr() for x in xs), self.labels.data_ptr(), bool(accumulate), step, float(loss_scale))
         entry = self.graphs.get(key)
         if entry is None:
             entry = self._capture(xs, loss_scale, accumulate, step)

@@ -107,8 +107,9 @@ def build_model(args, num_labels: int) -> torch.nn.Module:
 def _datasets(args, acc: Accelerator, mode: str):
     clip_duration = (args.sampling_rate * args.num_frames) / args.frames_per_second
     if args.synthetic:
-        train_v = SyntheticVideoPaths(args.synthetic_videos, args.synthetic_classes, seed=1)
-        val_v = SyntheticVideoPaths(max(args.synthetic_videos // 4, 1), args.synthetic_classes, seed=2)
+        mf = getattr(args, "synthetic_min_frames", None)
+        train_v = SyntheticVideoPaths(args.synthetic_videos, args.synthetic_classes, seed=1, min_frames=mf)
+        val_v = SyntheticVideoPaths(max(args.synthetic_videos // 4, 1), args.synthetic_classes, seed=2, min_frames=mf)
     else:
         train_v = LabeledVideoPaths.from_directory(os.path.join(args.data_dir, "train"))
         val_v = LabeledVideoPaths.from_directory(os.path.join(args.data_dir, "val"))
@@ -203,10 +204,12 @@ def training_function(args: Namespace) -> dict:
     if args.with_tracking:
         run = str(args.logging_dir).replace(".", "").replace("/", "").replace("\\", "")
         acc.print(f"Initializing tracker for run {run}")
-        acc.init_trackers(run, vars(args))
+        # the precision / execution path that actually runs is part of the logged config (auditable runs)
+        acc.init_trackers(run, {**vars(args), "compute_dtype": acc.compute_dtype, "backend": backend.name})
 
     gas = args.gradient_accumulation_steps
-    history = {"train_loss_epoch": [], "accuracy": [], "clips_per_sec": [], "perf": []}
+    history = {"train_loss_epoch": [], "accuracy": [], "clips_per_sec": [], "perf": [],
+               "compute_dtype": acc.compute_dtype, "backend": backend.name}
     timer = StepTimer(acc.device)
     backend.timer = timer
     val_metric = Accuracy(acc.device, acc.state)

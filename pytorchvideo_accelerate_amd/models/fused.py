@@ -874,7 +874,6 @@ class FusedNet:
         self._bnb: Dict = {}
         self._scratch: Dict[Tuple, torch.Tensor] = {}
         self.grad_beta = 0.0
-        import os
         self.lane = 0          # 0: main stream, 1: fast-pathway stream (per-lane scratch)
         self._side = None
         self._seed_dev = None   # device-resident dropout key (int64 [1]), see _head_forward
@@ -884,7 +883,6 @@ class FusedNet:
         self._wst_used = [False, False]
         self._ms_ok = (not deterministic and torch.device(device).type == "cuda"
                        and os.environ.get("PVA_STREAMS", "1") != "0")
-        import os
         # BN folding of the 1x1 conv_c (never materialise its output); units whose conv_c input has at least
         # fold_min_c channels (default: the slow pathway, where the Gram matrices run at MFMA speed).  Narrow
         # (fast-pathway) folds take exact statistics from a statistics-only conv pass (Gram-derived variances
@@ -1169,9 +1167,17 @@ class FusedNet:
 
     @torch.no_grad()
     def forward_eval(self, xs: List[Act]) -> torch.Tensor:
-        outs = self._forward_backbone(xs, train=False)
-        feat, _ = self._pool_features(outs, "e")
-        logits, _, _, _ = self._head_forward(feat, False, "e")
+        """Eval forward.  Kernel choices for eval geometries are tuned rank-locally: under data parallelism each
+        rank's validation shard has its own batch count and last-batch size (uniform clips per video differ), so
+        a cross-rank agreement collective here would only run on the ranks that see a new shape and hang the
+        others.  No cross-rank math depends on eval kernel choices (every configuration computes the same sums)."""
+        agree, self.tuner.agree = self.tuner.agree, None
+        try:
+            outs = self._forward_backbone(xs, train=False)
+            feat, _ = self._pool_features(outs, "e")
+            logits, _, _, _ = self._head_forward(feat, False, "e")
+        finally:
+            self.tuner.agree = agree
         return logits
 
     @torch.no_grad()

@@ -27,7 +27,7 @@ UT = 8
 DIRECT = 32           # narrow direct-to-register kernel (csrc/kernels/conv_direct.hip)
 DIRECT_2K = 64        #   with 2048 rows per workgroup (else 512)
 DMA = 128             # uniform-tap loader staged by LDS-DMA (buffer_load ... lds); launches without input affine
-DIRECT_HALF = 128     #   (with DIRECT) half the row groups in flight per wave: fewer VGPRs, more waves per SIMD
+DIRECT_HALF = 1024    #   (with DIRECT) half the row groups in flight per wave: fewer VGPRs, more waves per SIMD
 BIG = 256             # 256x256 tile of 8 waves (N >= 256; the backward-BN epilogue in 64-row slices)
 PW = 512              # streaming pointwise kernel (csrc/kernels/conv_pw.hip): dense 1x1x1 GEMMs, K <= 256,
 PW_ROWS = (1024, 2048, 4096)   # N % 32 == 0, weights in LDS; bits 0-1 select the rows per workgroup,

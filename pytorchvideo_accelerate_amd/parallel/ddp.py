@@ -61,7 +61,9 @@ class GradSync:
         self.buckets: List[Tuple[int, int]] = [(cuts[i], cuts[i + 1]) for i in range(len(cuts) - 1)]
         self.grad_dtype = grad_dtype if grad_dtype not in (None, grad.dtype) else None
         self._lowp: Optional[torch.Tensor] = None
-        self.timing = timing and grad.is_cuda
+        # per-bucket timing needs a non-blocking Work.wait (RCCL: a stream wait); with gloo it would block the host
+        # inside backward and serialise every bucket, so the gloo rehearsal runs untimed
+        self.timing = timing and grad.is_cuda and state.backend == "nccl"
         self._comm_stream = torch.cuda.Stream(grad.device) if self.timing else None
         self._ev: List = []          # per step: (list of (ready, done) per bucket, (exp0, exp1))
         self._next = 0

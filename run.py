@@ -48,6 +48,7 @@ def main(
     synthetic: bool = False,
     synthetic_videos: int = 64,
     synthetic_classes: int = 10,
+    synthetic_min_frames: int = None,
     kernels: str = "auto",
     reference_val: bool = False,
     pretrained_path: str = None,
@@ -60,6 +61,7 @@ def main(
       model              slowfast_r50 | slowfast_r101 | slow_r50 (default from --is_slowfast)
       synthetic          use a synthetic Kinetics-like corpus instead of --data_dir
       synthetic_videos / synthetic_classes   its size
+      synthetic_min_frames  vary synthetic video lengths in [this, 300] frames (default: all 300)
       kernels            auto | fused | torch  (fused = gfx950 HIP kernels, bf16)
       reference_val      evaluate only one clip per video (reference LimitDataset behaviour)
       pretrained_path    local weights for --pretrained (no network)

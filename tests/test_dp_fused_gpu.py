@@ -1,0 +1,94 @@
+"""Multi-rank data parallelism through the FUSED executor on the GPU (reference ``run.py:196-198,257,289-303``).
+
+Two ranks share the one GPU of the test box over gloo (``PVA_DIST_BACKEND=gloo``; RCCL refuses two ranks on one
+device), each started by a child ``torch.distributed.run`` (never exec).  What runs is the production multi-rank
+path: two-stream execution (fast pathway on its own HIP stream), weight gradients on side streams joined per
+stage, per-stage bucket progress driving the overlapped all-reduce (``parallel/ddp.GradSync``), and autotuner
+agreement across ranks.  Checked against single-process fused runs on each rank's shard:
+
+* the all-reduced flat gradient of the first optimizer step equals the mean of the two single-process gradients
+  (per-rank BN batch statistics, DDP averaging);
+* parameters are bitwise identical on both ranks after 4 optimizer steps;
+* ``run.py`` over a corpus whose videos give the two ranks different numbers of uniform validation clips (so
+  different eval batch counts and last-batch shapes) completes a full evaluation — eval-time kernel tuning is
+  rank-local, so no rank waits in a collective the other never joins.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+sys.path.insert(0, REPO)
+
+BENCH = ["--batch", "4", "--steps", "3", "--warmup", "1", "--bucket-mb", "8", "--first-bucket-mb", "1"]
+
+
+def _env(**kw):
+    env = dict(os.environ, OMP_NUM_THREADS="2", PVA_DIST_BACKEND="gloo", **kw)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    return env
+
+
+def _bench(extra, tmp_path, name):
+    dump = str(tmp_path / f"{name}.pt")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py")] + BENCH + extra + ["--dump", dump],
+                       capture_output=True, text=True, timeout=400, cwd=str(tmp_path), env=_env())
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return json.loads(lines[0]), torch.load(dump, weights_only=True)
+
+
+def test_fused_two_rank_gradients_and_params(tmp_path):
+    res2, d2 = _bench(["--gpus", "2"], tmp_path, "dp2")
+    assert res2["n_gpus"] == 2 and res2["config"]["parallelism"] == "dp2" and res2["config"]["backend"] == "gloo"
+    assert d2["world_size"] == 2
+    # every rank ends with the same weights, bit for bit
+    assert torch.equal(d2["params"][0], d2["params"][1])
+    singles = [_bench(["--gpus", "1", "--data-rank", str(r)], tmp_path, f"r{r}")[1]["grad"] for r in range(2)]
+    ref = (singles[0] + singles[1]) / 2
+    got = d2["grad"]
+    assert got.shape == ref.shape and torch.isfinite(got).all()
+    # the two single runs differ by far more than the tolerance (the check has teeth) ...
+    spread = float((singles[0] - singles[1]).norm() / ref.norm())
+    err = float((got - ref).norm() / ref.norm())
+    assert spread > 0.1, spread
+    # ... while the all-reduced gradient matches their mean up to fp32 split-K summation order
+    assert err < 2e-3, (err, spread)
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_run_py_two_ranks_unequal_val_shards(tmp_path):
+    from pytorchvideo_accelerate_amd.data.kinetics import SyntheticVideoPaths, VideoClipDataset
+    # the val corpus run.py builds (seed 2, 7 videos = 28 // 4), sharded over 2 ranks: unequal clip counts
+    kw = dict(num_frames=8, crop_size=64, slowfast_alpha=4, world=2, distributed=True, seed=42, mode="gpu")
+    vv = SyntheticVideoPaths(7, 3, seed=2, min_frames=40)
+    counts = [len(VideoClipDataset(vv, 2 * 8 / 30, False, rank=r, **kw)) for r in range(2)]
+    assert counts[0] != counts[1], counts
+    out = tmp_path / "o"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(REPO, "run.py"),
+           "--synthetic", "--synthetic_videos", "28", "--synthetic_classes", "3", "--synthetic_min_frames", "40",
+           "--is_slowfast", "--num_frames", "8", "--sampling_rate", "2", "--crop_size", "64", "--batch_size", "3",
+           "--num_workers", "0", "--num_epochs", "1", "--limit_val_batches", "-1", "--mixed_precision", "bf16",
+           "--gradient_accumulation_steps", "1", "--lr", "0.01", "--output_dir", str(out), "--quiet"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, cwd=str(tmp_path), env=_env())
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "val accuracy" in r.stdout
+    assert (out / "final" / "model.safetensors").exists()

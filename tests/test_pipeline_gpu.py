@@ -71,17 +71,20 @@ def test_run_py_fused_gpu(tmp_path):
     assert h2["global_step"] == 6
 
 
-@pytest.mark.parametrize("mp", ["fp16", "no"])
-def test_run_py_fused_fp16_and_default_precision(tmp_path, mp):
-    """fp16 = fused kernels + dynamic loss scaling (scaler.pt saved/restored); "no" (the reference default)
-    also runs the fused kernels on the GPU (PyTorch/MIOpen only with an explicit --kernels torch)."""
+@pytest.mark.parametrize("mp,kernels", [("fp16", "auto"), ("no", "fused"), ("no", "auto")])
+def test_run_py_precision_policy(tmp_path, mp, kernels):
+    """fp16 = fused kernels + dynamic loss scaling (scaler.pt saved/restored); "no" (the reference default, fp32
+    math) runs the PyTorch fp32 path unless the fused kernels are asked for explicitly — and the precision that
+    ran is recorded (history / tracker config ``compute_dtype``)."""
     import run
     kw = dict(synthetic=True, synthetic_videos=8, synthetic_classes=4, is_slowfast=True, num_frames=8, crop_size=64,
               batch_size=4, num_workers=0, limit_val_batches=0, mixed_precision=mp, checkpointing_steps="epoch",
               output_dir=str(tmp_path / "o"), gradient_accumulation_steps=2, lr=0.01, quiet=True,
-              logging_dir=str(tmp_path / "l"))
+              logging_dir=str(tmp_path / "l"), kernels=kernels)
     h = run.main(num_epochs=1, **kw)
-    assert h["global_step"] == 2 and h["backend"] == "fused"
+    fused = mp == "fp16" or kernels == "fused"
+    assert h["global_step"] == 2 and h["backend"] == ("fused" if fused else "torch")
+    assert h["compute_dtype"] == {"fp16": "bf16+fp16-loss-scaling", "no": "bf16" if fused else "fp32"}[mp]
     assert (tmp_path / "o" / "epoch_0" / "scaler.pt").exists() == (mp == "fp16")
     if mp == "fp16":
         sd = torch.load(tmp_path / "o" / "epoch_0" / "scaler.pt", weights_only=True)
