@@ -121,6 +121,7 @@ def run(a):
     from pytorchvideo_accelerate_amd.parallel.dist import DistState
     from pytorchvideo_accelerate_amd.parallel.ddp import GradSync
     from pytorchvideo_accelerate_amd.ops.optim import FusedSGD
+    from pytorchvideo_accelerate_amd.utils.profiling import trace_range
 
     st = DistState.from_env(cpu=a.plumbing)
     dev = st.device
@@ -229,7 +230,8 @@ def run(a):
                 sync.finish()
             if i == 0 and a.dump:
                 dump["grad"] = eng.flat.grad.clone()
-            opt.step()
+            with trace_range("sgd"):
+                opt.step()
             return loss
 
     if not a.plumbing:
@@ -250,7 +252,8 @@ def run(a):
             ev0 = torch.cuda.Event(enable_timing=True)
             ev1 = torch.cuda.Event(enable_timing=True)
             ev0.record()
-            loss = step(a.warmup + i)
+            with trace_range(f"step{i}"):
+                loss = step(a.warmup + i)
             ev1.record()
             times.append((ev0, ev1))
         else:

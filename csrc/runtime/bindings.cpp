@@ -6,6 +6,7 @@
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 #include <hip/hip_runtime.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include "../kernels/conv_params.h"
 #include <cstddef>
@@ -581,6 +582,10 @@ void synth_frames(const at::Tensor& out, int64_t seed) {
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "gfx950 HIP kernels for pytorchvideo_accelerate_amd";
+  // ROCTx ranges / marks (host timeline; recorded by rocprofv3 --marker-trace, no-ops without a tool attached)
+  m.def("range_push", [](const std::string& s) { return (int64_t)roctxRangePushA(s.c_str()); });
+  m.def("range_pop", []() { return (int64_t)roctxRangePop(); });
+  m.def("trace_mark", [](const std::string& s) { roctxMarkA(s.c_str()); });
   m.def("conv_igemm", &conv_igemm, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("stats"), py::arg("scale"),
         py::arg("shift"), py::arg("affine"), py::arg("accum"), py::arg("g"), py::arg("chunk"), py::arg("cfg") = -1,
         py::arg("bias") = py::none(), py::arg("nostore") = 0);

@@ -25,6 +25,7 @@ CSRC = os.path.join(REPO, "csrc")
 BUILD = os.path.join(REPO, "build", "obj")
 ARCH = os.environ.get("PVA_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ROCM_LIB = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "lib")
 
 
 def ext_path() -> str:
@@ -81,7 +82,8 @@ def build(jobs: int = 0, force: bool = False, verbose: bool = False) -> str:
         futs += [ex.submit(_compile, s, bind_flags, hdr, force) for s in runtime]
         objs = [f.result() for f in futs]
     out = ext_path()
-    libs = ["-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python"]
+    libs = ["-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
+            f"-L{ROCM_LIB}", f"-Wl,-rpath,{ROCM_LIB}", "-lrocprofiler-sdk-roctx"]   # ROCTx ranges
     stamp = hashlib.sha1(" ".join(objs).encode()).hexdigest()
     stamp_file = out + ".stamp"
     if os.path.exists(out) and not force and os.path.exists(stamp_file) and open(stamp_file).read() == stamp:

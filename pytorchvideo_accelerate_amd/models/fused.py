@@ -39,6 +39,7 @@ import torch.nn.functional as F
 from ..ops._ext import require
 from ..ops.conv import Act, ConvSpec, dgrad_phases, fwd_geometry
 from . import reference as R
+from ..utils.profiling import trace_range
 
 
 class _Xf:
@@ -1085,35 +1086,36 @@ class FusedNet:
         if ms:
             self._join(side, main)   # inputs were produced on the main stream
         for si, (paths, fuse) in enumerate(self.stages):
-            outs = [None] * len(paths)
-            cat = None
-            # fast pathway first (issued to its own stream when two-stream execution is on)
-            for p in range(len(paths) - 1, -1, -1):
-                mod = paths[p]
-                x = cur[p]
-                T, H, W = mod.out_dims(x.T, x.H, x.W)
-                M = x.N * T * H * W
-                co = mod.out_channels()
-                if p == 0 and fuse is not None:
-                    cat = self.ws(("cat", si, tag), (M, co + fuse.u.C), torch.bfloat16)
-                    out = cat[:, :co]
-                else:
-                    out = self.ws(("pout", si, p, tag), (M, co), torch.bfloat16)
-                if ms and p == 1:
-                    self.lane = 1
-                    with torch.cuda.stream(side):
+            with trace_range(f"fwd/b{si}"):
+                outs = [None] * len(paths)
+                cat = None
+                # fast pathway first (issued to its own stream when two-stream execution is on)
+                for p in range(len(paths) - 1, -1, -1):
+                    mod = paths[p]
+                    x = cur[p]
+                    T, H, W = mod.out_dims(x.T, x.H, x.W)
+                    M = x.N * T * H * W
+                    co = mod.out_channels()
+                    if p == 0 and fuse is not None:
+                        cat = self.ws(("cat", si, tag), (M, co + fuse.u.C), torch.bfloat16)
+                        out = cat[:, :co]
+                    else:
+                        out = self.ws(("pout", si, p, tag), (M, co), torch.bfloat16)
+                    if ms and p == 1:
+                        self.lane = 1
+                        with torch.cuda.stream(side):
+                            outs[p] = mod.fwd(x, out, train, tag)
+                        self.lane = 0
+                    else:
                         outs[p] = mod.fwd(x, out, train, tag)
-                    self.lane = 0
-                else:
-                    outs[p] = mod.fwd(x, out, train, tag)
-            if fuse is not None:
-                if ms:
-                    self._join(main, side)   # the fusion reads the fast pathway's output
-                co = outs[0].C
-                fuse.fwd(outs[1], cat[:, co:], train, tag)
-                outs[0] = Act(cat, outs[0].N, outs[0].T, outs[0].H, outs[0].W)
-            self._cats.append(cat)
-            cur = outs
+                if fuse is not None:
+                    if ms:
+                        self._join(main, side)   # the fusion reads the fast pathway's output
+                    co = outs[0].C
+                    fuse.fwd(outs[1], cat[:, co:], train, tag)
+                    outs[0] = Act(cat, outs[0].N, outs[0].T, outs[0].H, outs[0].W)
+                self._cats.append(cat)
+                cur = outs
         if ms:
             self._join(main, side)
         return cur
@@ -1252,46 +1254,47 @@ class FusedNet:
         side = self._side_stream() if ms else None
         self._ms_bwd = ms   # per-block progress reports are deferred to stage ends (grads come from two streams)
         for si in range(len(self.stages) - 1, -1, -1):
-            paths, fuse = self.stages[si]
-            if ms:
-                self._join(main, side)   # the fast pathway's dx of the stage above is final
-            # grads for this stage's pathway outputs: douts (slow may be the full concat grad)
-            if fuse is not None:
-                dcat = douts[0]
-                co = paths[0].out_channels()
-                fuse.bwd(dcat.narrow(co, fuse.u.C), douts[1].t)
-                self._progress(fuse.flat_hi, force=True)
-                douts[0] = dcat.narrow(0, co)
-            if ms:
-                self._join(side, main)   # the fused dfast accumulation is complete
-            new = [None] * len(paths)
-            # pathways in reverse order: matches the flat (reverse-execution) gradient layout
-            for p in range(len(paths) - 1, -1, -1):
-                mod = paths[p]
-                on_side = ms and p == 1
-                if on_side:
-                    self.lane = 1
-                    ctx = torch.cuda.stream(side)
-                    ctx.__enter__()
-                try:
-                    if isinstance(mod, _Stem):
-                        mod.bwd(douts[p])
-                        if not ms:
-                            self._progress(mod.flat_hi)
-                    else:
-                        xin = mod.blocks[0].x
-                        dx = self.ws(("dstage_in", si, p), (xin.M, xin.C), torch.bfloat16)
-                        mod.bwd(douts[p], dx, False)
-                        new[p] = Act(dx, xin.N, xin.T, xin.H, xin.W)
-                finally:
+            with trace_range(f"bwd/b{si}"):
+                paths, fuse = self.stages[si]
+                if ms:
+                    self._join(main, side)   # the fast pathway's dx of the stage above is final
+                # grads for this stage's pathway outputs: douts (slow may be the full concat grad)
+                if fuse is not None:
+                    dcat = douts[0]
+                    co = paths[0].out_channels()
+                    fuse.bwd(dcat.narrow(co, fuse.u.C), douts[1].t)
+                    self._progress(fuse.flat_hi, force=True)
+                    douts[0] = dcat.narrow(0, co)
+                if ms:
+                    self._join(side, main)   # the fused dfast accumulation is complete
+                new = [None] * len(paths)
+                # pathways in reverse order: matches the flat (reverse-execution) gradient layout
+                for p in range(len(paths) - 1, -1, -1):
+                    mod = paths[p]
+                    on_side = ms and p == 1
                     if on_side:
-                        ctx.__exit__(None, None, None)
-                        self.lane = 0
-            if ms:
-                self._join(main, side)
-                self._progress(max(m.flat_hi if isinstance(m, _Stem) else m.blocks[0].flat_hi for m in paths),
-                               force=True)
-            douts = new
+                        self.lane = 1
+                        ctx = torch.cuda.stream(side)
+                        ctx.__enter__()
+                    try:
+                        if isinstance(mod, _Stem):
+                            mod.bwd(douts[p])
+                            if not ms:
+                                self._progress(mod.flat_hi)
+                        else:
+                            xin = mod.blocks[0].x
+                            dx = self.ws(("dstage_in", si, p), (xin.M, xin.C), torch.bfloat16)
+                            mod.bwd(douts[p], dx, False)
+                            new[p] = Act(dx, xin.N, xin.T, xin.H, xin.W)
+                    finally:
+                        if on_side:
+                            ctx.__exit__(None, None, None)
+                            self.lane = 0
+                if ms:
+                    self._join(main, side)
+                    self._progress(max(m.flat_hi if isinstance(m, _Stem) else m.blocks[0].flat_hi for m in paths),
+                                   force=True)
+                douts = new
         if ms:
             self._join_wgrads()
         self._ms_bwd = False

@@ -31,6 +31,7 @@ from typing import Dict, List, Optional, Tuple
 
 import torch
 
+from ..utils.profiling import trace_mark, trace_range
 from .dist import DistState
 
 
@@ -100,12 +101,13 @@ class GradSync:
             comm = low
         else:
             comm = t
-        if self.state.backend == "nccl":
-            w = dist.all_reduce(comm, op=dist.ReduceOp.AVG, async_op=True)
-            post = None
-        else:
-            w = dist.all_reduce(comm, op=dist.ReduceOp.SUM, async_op=True)
-            post = "div"
+        with trace_range(f"allreduce/bucket{b}"):
+            if self.state.backend == "nccl":
+                w = dist.all_reduce(comm, op=dist.ReduceOp.AVG, async_op=True)
+                post = None
+            else:
+                w = dist.all_reduce(comm, op=dist.ReduceOp.SUM, async_op=True)
+                post = "div"
         self._works.append((w, t, comm, post))
         if self.timing:
             # the side stream waits for this collective only: its event marks the bucket's completion
@@ -129,7 +131,8 @@ class GradSync:
             self._launch(self._next)
             self._next += 1
         e0 = self._event() if self.timing else None
-        for w, t, comm, post in self._works:
+        for b, (w, t, comm, post) in enumerate(self._works):
+            trace_mark(f"allreduce/wait{b}")
             w.wait()
             if post == "div":
                 comm.div_(self.state.world_size)

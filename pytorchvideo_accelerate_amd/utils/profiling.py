@@ -9,14 +9,55 @@ phase times, logged by the trainer as ``step_time_ms``, ``step_time_p90_ms``, ``
 
 For kernel-level traces use ``rocprofv3 --kernel-trace --stats`` (scripts/gpu_bench.sh PROFILE=...) or the
 per-op event profiler of the fused executor (``FusedNet.prof`` / scripts/layer_profile.py).
+
+ROCTx ranges (:func:`trace_range`, :func:`trace_mark`) name the host-side phases on the rocprofv3 timeline
+(``rocprofv3 --marker-trace --kernel-trace``): ``fwd/b{i}`` / ``bwd/b{i}`` per stage, ``allreduce/bucket{k}``
+per gradient bucket, ``step`` / ``sgd`` in the trainer and bench.  They call libroctx through the in-tree
+extension and cost ~1 µs each; without a profiler attached they are no-ops.  ``PVA_ROCTX=0`` disables them.
 """
 from __future__ import annotations
 
 import contextlib
+import os
 import time
 from typing import Dict, List, Optional
 
 import torch
+
+_RTX = None   # extension module with range_push/range_pop/trace_mark, False when unavailable
+
+
+def _rtx():
+    global _RTX
+    if _RTX is None:
+        _RTX = False
+        if os.environ.get("PVA_ROCTX", "1") != "0" and torch.cuda.is_available():
+            from ..ops._ext import load
+            mod = load()
+            if mod is not None and hasattr(mod, "range_push"):
+                _RTX = mod
+    return _RTX
+
+
+@contextlib.contextmanager
+def trace_range(name: str):
+    """ROCTx push/pop range around the block (host timeline)."""
+    m = _rtx()
+    if not m:
+        yield
+        return
+    m.range_push(name)
+    try:
+        yield
+    finally:
+        m.range_pop()
+
+
+def trace_mark(name: str):
+    """ROCTx instantaneous marker."""
+    m = _rtx()
+    if m:
+        m.trace_mark(name)
 
 
 class StepTimer:
