@@ -68,6 +68,9 @@ def parse(argv=None):
     ap.add_argument("--dump", default=None,
                     help="write the first optimizer step's (all-reduced) flat gradient and every rank's final "
                          "parameters here (cross-rank numerics tests)")
+    ap.add_argument("--deterministic", action="store_true",
+                    help="bitwise-reproducible fused executor (fixed-order reductions, one stream; cross-rank exactness "
+                         "tests)")
     ap.add_argument("--data-rank", type=int, default=-1,
                     help="draw the synthetic data of this rank instead of the own one (single-process oracle runs "
                          "of a multi-rank job's shards)")
@@ -154,7 +157,7 @@ def run(a):
         assert dev.type == "cuda", "bench.py needs a GPU (or --plumbing)"
         torch.manual_seed(1234)
         model = R.create_slowfast(a.depth, a.classes)
-        eng = FusedNet(model, dev)
+        eng = FusedNet(model, dev, deterministic=a.deterministic)
         if st.world_size > 1:
             eng.tuner.agree = st.agree_times
         st.broadcast_tensors([eng.flat.data] + [b for b in model.buffers()])
@@ -309,6 +312,7 @@ def run(a):
                        "per_gpu_batch": B, "grad_accum": a.grad_accum, "seq_len": a.frames,
                        "parallelism": f"dp{st.world_size}", "backend": st.backend or "none",
                        "grad_dtype": a.grad_dtype, "classes": a.classes, "hip_graph": bool(gstep is not None),
+                       "deterministic": a.deterministic,
                        "final_loss": round(float(loss), 4) if loss is not None else None,
                        "peak_mem_gb": (round(torch.cuda.max_memory_allocated(dev) / 2**30, 1)
                                        if dev.type == "cuda" else None),

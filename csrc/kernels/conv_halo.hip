@@ -1,0 +1,378 @@
+// Halo-staged implicit-GEMM forward and dgrad of stride-1 'same' (1,3,3) convolutions on MFMA (gfx950):
+// the spatial conv_b of every bottleneck whose output rows are the input rows (SlowFast slow res2-res4).
+//
+//   y[p][n] = sum_{tap, c} x'[p + off(tap)][c] * w[n][tap][c]        (x' = BN+ReLU(x) recomputed, or x)
+//
+// The tile kernel of conv_igemm.hip gathers one im2col row per (position, tap): each activation is fetched
+// from L2 and put through the consumer-side BN+ReLU nine times, and at 64-128 channels that L2 traffic
+// (~1.2 KB per output position at K = 576) bounds the GEMM well below the matrix cores (slow res2 conv_b ran
+// at ~420 TF/s).  Here a workgroup owns R full image rows x all W columns of one frame (P = R*W <= 224
+// positions) and an n-tile of 64 or 128 output channels:
+//   * the input HALO [(R+2) x (W+2)][CK channels] is staged into LDS ONCE (global -> registers -> BN+ReLU ->
+//     ds_write; padding positions are zeros, so no bounds test in the MFMA loop), in slices of CK <= 128
+//     channels;
+//   * LDS image is channel-group-major: [CK/8][positions padded to 16][8 bf16], so the 16 positions x 4
+//     channel groups of one ds_read_b128 fragment land on 16 distinct 16-B bank groups (position p of group g
+//     at unit (g*NPOSP + p) mod 16 with NPOSP = 0 mod 16) with no XOR swizzle, and every tap of a fragment is
+//     the same per-lane address plus a wave-uniform offset (dh*(W+2) + dw)*16;
+//   * the weight fragments are read straight from global memory into registers (16 B per lane, L2-resident,
+//     prefetched two k-steps ahead), so the k loop has no barrier at all;
+//   * 4 waves = 2 position halves x 2 channel halves, each wave up to 7 x (NTILE/32) 16x16 accumulators;
+//     v_mfma_f32_16x16x32_bf16 with swapped operands (D = W X^T) so each lane holds 4 consecutive channels of
+//     one position (8-B stores, 16-lane shuffles for the channel sums), exactly like conv_igemm.hip;
+//   * epilogues: EPI 0 = raw output + BN partial sums [tiles][2][N] (sum, sum of squares of the bf16 output);
+//     EPI 1 = the dgrad epilogue of a conv whose input is relu(BN_a(y0)): ReLU mask recomputed from y0,
+//     masked gradient stored, BN_a backward partials [tiles][3][N] (sum v, sum v*xhat0, 0).
+// Launch word (conv_igemm_launch): bit 4 explicit, bit 11 this kernel, bit 0 = 64-channel n-tiles (else 128),
+// bits 12+ = positions per tile P (so conv_cfg_bm = P and the partial-sum tile count is M / P).
+#include "common.h"
+#include "conv_params.h"
+
+namespace {
+
+constexpr int HC_THREADS = 256;
+constexpr int HC_MW = 7;        // 16-position blocks per wave (two position halves of <= 112)
+constexpr int HC_PMAX = 2 * HC_MW * 16;
+constexpr int HC_RING = 3;      // weight-fragment ring depth (k-steps in flight)
+
+// rows per tile: the largest divisor R of H with R*W <= 224 (every tile is whole rows of one frame)
+__host__ __device__ inline int halo_rows(int H, int W) {
+  for (int r = H; r >= 1; --r)
+    if (H % r == 0 && r * W <= HC_PMAX) return r;
+  return 0;
+}
+
+__host__ __device__ inline int halo_ck(int Cg) { return Cg <= 128 ? Cg : 128; }
+
+template <int NTILE, int EPI, int AFF>
+__global__ __launch_bounds__(HC_THREADS, 2) void conv_halo_kernel(const ConvParams p, const int R) {
+  constexpr int NWB = NTILE / 32;   // 16-channel blocks per wave
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid & 1, wn = wid >> 1;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int W = p.Rw, H = p.Rh;
+  const int PW = W + 2;
+  const int P = R * W;
+  const int NPOS = (R + 2) * PW, NPOSP = (NPOS + 15) & ~15;
+  const int CK = halo_ck(p.Cg);
+  const int G8 = CK >> 3;
+  const int box_bytes = G8 * NPOSP * 16;
+  float* red = reinterpret_cast<float*>(smem + box_bytes);    // [2 halves][2 or 3][NTILE]
+  float* aff = red + (EPI ? 6 : 4) * NTILE;                   // [2][Cg] consumer-side affine
+  float* bnp = aff + (AFF ? 2 * p.Cg : 0);                    // EPI 1: [4][NTILE] mean0 rstd0 msc msh
+
+  const int n_tiles = (p.Ngemm + NTILE - 1) / NTILE;
+  const int t = xcd_remap(blockIdx.x, gridDim.x);   // the n-tiles of one m-tile (same halo) share an XCD
+  const int tile_m = t / n_tiles, tile_n = t - (t / n_tiles) * n_tiles;
+  const int tpf = H / R;
+  const int frame = tile_m / tpf, r0 = (tile_m - frame * tpf) * R;
+  const int n0 = tile_n * NTILE;
+  const int fbase = frame * H * W;   // first row of this frame (gathered and output tensors share the grid)
+
+  if constexpr (AFF != 0) {
+    for (int i = tid; i < p.Cg; i += HC_THREADS) { aff[i] = p.in_scale[i]; aff[p.Cg + i] = p.in_shift[i]; }
+  }
+  if constexpr (EPI == 1) {
+    for (int i = tid; i < NTILE; i += HC_THREADS) {
+      const int n = min(n0 + i, p.Ngemm - 1);
+      bnp[i] = p.emean0[n]; bnp[NTILE + i] = p.erstd0[n];
+      bnp[2 * NTILE + i] = p.emsc[n]; bnp[3 * NTILE + i] = p.emsh[n];
+    }
+  }
+
+  // ---- per-lane fragment addresses
+  const int mwr = min(HC_MW, ((P + 15) / 16 + 1) / 2);   // live 16-position blocks per wave
+  int abase[HC_MW];
+#pragma unroll
+  for (int i = 0; i < HC_MW; ++i) {
+    const int pl = min((wm * mwr + i) * 16 + fr, P - 1);
+    const int h = pl / W, w = pl - h * W;
+    abase[i] = (fg * NPOSP + (h + 1) * PW + (w + 1)) * 16;
+  }
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, (int)p.wbytes, 0x00020000);
+  int bvo[NWB];
+#pragma unroll
+  for (int j = 0; j < NWB; ++j) {
+    const int n = min(n0 + wn * (NTILE / 2) + j * 16 + fr, p.Ngemm - 1);
+    bvo[j] = (n * p.Kfull + fg * 8) * 2;
+  }
+  // k-steps: (slice c, tap, 32-channel step kc); taps in (jh, jw) order
+  const int ksl = CK / 32;
+  const int nsteps = (p.Cg / 32) * 9;
+  auto step_w = [&](int s) {   // byte offset of step s in a packed weight row
+    const int c = s / (9 * ksl);
+    const int r = s - c * 9 * ksl;
+    const int tap = r / ksl, kc = r - tap * ksl;
+    const int jh = tap / 3, jw = tap - jh * 3;
+    const int wt = (p.bt0 * p.kh + p.bh0 + jh * p.bhs) * p.kw + p.bw0 + jw * p.bws;
+    return (wt * p.Cg + c * CK + kc * 32) * 2;
+  };
+  auto step_a = [&](int s) {   // uniform byte offset of step s in the halo image
+    const int c = s / (9 * ksl);
+    const int r = s - c * 9 * ksl;
+    const int tap = r / ksl, kc = r - tap * ksl;
+    const int jh = tap / 3, jw = tap - jh * 3;
+    const int dh = p.aoh + p.dir * jh, dw = p.aow + p.dir * jw;
+    return (dh * PW + dw + kc * 4 * NPOSP) * 16;
+  };
+
+  f32x4_t acc[HC_MW][NWB];
+#pragma unroll
+  for (int i = 0; i < HC_MW; ++i)
+#pragma unroll
+    for (int j = 0; j < NWB; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  uint4 bq[HC_RING][NWB];
+  auto bload = [&](int s, uint4 (&dst)[NWB]) {
+    const int so = step_w(min(s, nsteps - 1));
+#pragma unroll
+    for (int j = 0; j < NWB; ++j)
+      dst[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wr, bvo[j], so, 0));
+  };
+  bload(0, bq[0]);
+  bload(1, bq[1]);
+
+  // ---- halo staging: thread -> (channel group cg, 8 consecutive box positions per pass-row)
+  const int cg = (tid >> 3) % G8;
+  const int ppp = HC_THREADS / G8;                  // box positions per pass
+  const int b_first = ((tid >> 3) / G8) * 8 + (tid & 7);
+  auto stage = [&](int c) {
+    float sc[8], sh[8];
+    if constexpr (AFF != 0) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { sc[e] = aff[c * CK + cg * 8 + e]; sh[e] = aff[p.Cg + c * CK + cg * 8 + e]; }
+    }
+    const int coff = c * CK + cg * 8;
+    int hh = b_first / PW, ww = b_first - (b_first / PW) * PW;
+    constexpr int BATCH = 6;
+    for (int b0 = b_first; b0 < NPOS; b0 += BATCH * ppp) {
+      uint4 v[BATCH];
+      bool ok[BATCH];
+      int bb[BATCH];
+#pragma unroll
+      for (int u = 0; u < BATCH; ++u) {
+        const int b = b0 + u * ppp;
+        bb[u] = b;
+        const int h = r0 - 1 + hh, w = ww - 1;
+        ok[u] = b < NPOS && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+        v[u] = uint4{0, 0, 0, 0};
+        if (ok[u]) v[u] = *reinterpret_cast<const uint4*>(p.x + (size_t)(fbase + h * W + w) * p.ldx + coff);
+        ww += ppp;
+        while (ww >= PW) { ww -= PW; ++hh; }
+      }
+#pragma unroll
+      for (int u = 0; u < BATCH; ++u) {
+        if (bb[u] >= NPOS) break;
+        uint4 o = v[u];
+        if constexpr (AFF != 0) {
+          float f[8];
+          unpack8(o, f);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) f[e] = __builtin_fmaf(f[e], sc[e], sh[e]);
+          o = pack8_fast(f);
+          if constexpr (AFF == 2) o = relu_bf16x8(o);
+          if (!ok[u]) o = uint4{0, 0, 0, 0};   // zero padding of the activation itself
+        }
+        *reinterpret_cast<uint4*>(smem + (cg * NPOSP + bb[u]) * 16) = o;
+      }
+    }
+  };
+
+  __syncthreads();   // affine / BN tables
+  const int nslices = p.Cg / CK;
+  int s = 0;
+  for (int c = 0; c < nslices; ++c) {
+    if (c > 0) __syncthreads();   // every wave is done with the previous slice
+    stage(c);
+    __syncthreads();
+    const int send = s + 9 * ksl;
+    // three k-steps per iteration: the weight ring slot of each is compile-time
+    for (; s < send; s += HC_RING) {
+#pragma unroll
+      for (int u = 0; u < HC_RING; ++u) {
+        const int ss = s + u;
+        bload(ss + 2, bq[(u + 2) % HC_RING]);
+        const int ao = step_a(ss);
+        bf16x8_t af[HC_MW];
+#pragma unroll
+        for (int i = 0; i < HC_MW; ++i)
+          if (i < mwr) af[i] = *reinterpret_cast<const bf16x8_t*>(smem + abase[i] + ao);
+#pragma unroll
+        for (int i = 0; i < HC_MW; ++i) {
+          if (i >= mwr) continue;
+#pragma unroll
+          for (int j = 0; j < NWB; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, bq[u][j]), af[i],
+                                                                acc[i][j], 0, 0, 0);
+        }
+      }
+    }
+  }
+
+  // ---- epilogue
+  const int ncol0 = wn * (NTILE / 2);
+  if constexpr (EPI == 0) {
+    const bool do_stats = p.stats != nullptr;
+    float cs[NWB][4], cq[NWB][4];
+#pragma unroll
+    for (int j = 0; j < NWB; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { cs[j][r] = 0.f; cq[j][r] = 0.f; }
+#pragma unroll
+    for (int i = 0; i < HC_MW; ++i) {
+      if (i >= mwr) continue;
+      const int pl = (wm * mwr + i) * 16 + fr;
+      if (pl >= P) continue;
+      const int row = fbase + r0 * W + pl;
+#pragma unroll
+      for (int j = 0; j < NWB; ++j) {
+        const int n = n0 + ncol0 + j * 16 + 4 * fg;
+        if (n >= p.Ngemm) continue;
+        const float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        const uint2 pk = pack4(v);
+        *reinterpret_cast<uint2*>(p.y + (size_t)row * p.ldy + n) = pk;
+        if (do_stats) {
+          float q[4];
+          unpack4(pk, q);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) { cs[j][r] += q[r]; cq[j][r] += q[r] * q[r]; }
+        }
+      }
+    }
+    if (!do_stats) return;
+#pragma unroll
+    for (int j = 0; j < NWB; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float a = sum16(cs[j][r]), b = sum16(cq[j][r]);
+        if (fr == 0) {
+          const int nl = ncol0 + j * 16 + 4 * fg + r;
+          red[(wm * 2) * NTILE + nl] = a;
+          red[(wm * 2 + 1) * NTILE + nl] = b;
+        }
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    for (int i = tid; i < NTILE; i += HC_THREADS) {
+      const int n = n0 + i;
+      if (n < p.Ngemm) {
+        p.stats[(tile_m * 2) * p.Ngemm + n] = red[i] + red[2 * NTILE + i];
+        p.stats[(tile_m * 2 + 1) * p.Ngemm + n] = red[NTILE + i] + red[3 * NTILE + i];
+      }
+    }
+  } else {
+    // dgrad of a conv whose input is relu(BN_a(y0)): v = acc * (y0*msc + msh > 0); sums v, v*y0
+    float sv[NWB][4], s0[NWB][4];
+#pragma unroll
+    for (int j = 0; j < NWB; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { sv[j][r] = 0.f; s0[j][r] = 0.f; }
+#pragma unroll
+    for (int i = 0; i < HC_MW; ++i) {
+      if (i >= mwr) continue;
+      const int pl = (wm * mwr + i) * 16 + fr;
+      if (pl >= P) continue;
+      const int row = fbase + r0 * W + pl;
+#pragma unroll
+      for (int j = 0; j < NWB; ++j) {
+        const int nl = ncol0 + j * 16 + 4 * fg;
+        const int n = n0 + nl;
+        if (n >= p.Ngemm) continue;
+        float a[4];
+        unpack4(*reinterpret_cast<const uint2*>(p.ey0 + (size_t)row * p.Ngemm + n), a);
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          v[r] = (a[r] * bnp[2 * NTILE + nl + r] + bnp[3 * NTILE + nl + r] > 0.f) ? acc[i][j][r] : 0.f;
+        const uint2 pk = pack4(v);
+        *reinterpret_cast<uint2*>(p.y + (size_t)row * p.ldy + n) = pk;
+        float q[4];
+        unpack4(pk, q);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { sv[j][r] += q[r]; s0[j][r] += q[r] * a[r]; }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NWB; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int nl = ncol0 + j * 16 + 4 * fg + r;
+        const float a = sum16(sv[j][r]), b = sum16(s0[j][r]);
+        if (fr == 0) {
+          red[(wm * 3) * NTILE + nl] = a;
+          red[(wm * 3 + 1) * NTILE + nl] = (b - bnp[nl] * a) * bnp[NTILE + nl];   // sum v*xhat0
+        }
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    for (int i = tid; i < NTILE; i += HC_THREADS) {
+      const int n = n0 + i;
+      if (n < p.Ngemm) {
+        p.epart[(tile_m * 3) * p.Ngemm + n] = red[i] + red[3 * NTILE + i];
+        p.epart[(tile_m * 3 + 1) * p.Ngemm + n] = red[NTILE + i] + red[4 * NTILE + i];
+        p.epart[(tile_m * 3 + 2) * p.Ngemm + n] = 0.f;
+      }
+    }
+  }
+}
+
+template <int NTILE, int EPI, int AFF>
+void launch_one(const ConvParams& p, int R, hipStream_t st) {
+  const int W = p.Rw;
+  const int NPOSP = (((R + 2) * (W + 2)) + 15) & ~15;
+  const int CK = halo_ck(p.Cg);
+  const size_t lds = (size_t)(CK / 8) * NPOSP * 16 + (EPI ? 6 : 4) * NTILE * 4 + (AFF ? 2 * p.Cg * 4 : 0) +
+                     (EPI ? 4 * NTILE * 4 : 0);
+  const int m_tiles = p.M / (R * W);
+  const int n_tiles = (p.Ngemm + NTILE - 1) / NTILE;
+  hipLaunchKernelGGL((conv_halo_kernel<NTILE, EPI, AFF>), dim3(m_tiles * n_tiles), dim3(HC_THREADS), lds, st, p, R);
+}
+
+template <int NTILE>
+void launch_ntile(const ConvParams& p, int R, bool epi, hipStream_t st) {
+  if (epi) { launch_one<NTILE, 1, 0>(p, R, st); return; }
+  switch (p.affine) {
+    case 0: launch_one<NTILE, 0, 0>(p, R, st); break;
+    case 1: launch_one<NTILE, 0, 1>(p, R, st); break;
+    default: launch_one<NTILE, 0, 2>(p, R, st); break;
+  }
+}
+
+}  // namespace
+
+// Positions per tile when the halo kernel can run this launch's geometry, else 0.  Geometry only: the epilogue
+// conditions (no accumulate / residual / bias / ReLU bits) are checked by conv_halo_epi_ok.
+int conv_halo_legal(const ConvParams& p, int chunk) {
+  if (chunk != 8 || p.nt != 1 || p.nh != 3 || p.nw != 3) return 0;
+  if (p.Rt != p.Gt || p.Rt != p.Ot || p.Rh != p.Gh || p.Rh != p.Oh || p.Rw != p.Gw || p.Rw != p.Ow) return 0;
+  if (p.ost != 1 || p.osh != 1 || p.osw != 1 || p.ort || p.orh || p.orw) return 0;
+  if (p.ast != 1 || p.ash != 1 || p.asw != 1 || p.aot != 0) return 0;
+  // every tap offset within the one-position halo
+  for (int j = 0; j < 3; ++j) {
+    const int dh = p.aoh + p.dir * j, dw = p.aow + p.dir * j;
+    if (dh < -1 || dh > 1 || dw < -1 || dw > 1) return 0;
+  }
+  if (p.Cg % 32 != 0 || (p.Cg > 128 && p.Cg % 128 != 0) || p.Ngemm % 64 != 0) return 0;
+  if (p.ldx % 8 != 0 || p.ldy % 4 != 0) return 0;
+  const int R = halo_rows(p.Rh, p.Rw);
+  // at least 128 positions per tile: the callers size the BN partial-sum slabs for 128-row tiles
+  if (R == 0 || R * p.Rw < 128 || p.M % (p.Rh * p.Rw) != 0) return 0;
+  return R * p.Rw;
+}
+
+int conv_halo_epi_ok(const ConvParams& p) {
+  if (p.accum || p.fres || p.ebias || p.nostore || p.eres || p.emask || p.ey1) return 0;
+  const bool epi = p.epart != nullptr;
+  if (epi) return (p.ey0 && p.emsc && p.emsh && p.emean0 && p.erstd0 && !p.affine) ? 1 : 0;
+  return 1;
+}
+
+void conv_halo_launch(const ConvParams& p, int cfg, hipStream_t st) {
+  const int R = halo_rows(p.Rh, p.Rw);
+  const bool epi = p.epart != nullptr;
+  if ((cfg & 1) || p.Ngemm % 128 != 0) launch_ntile<64>(p, R, epi, st);
+  else launch_ntile<128>(p, R, epi, st);
+}

@@ -1007,8 +1007,12 @@ void conv_direct_launch(const ConvParams& p, int cfg, hipStream_t s);
 int conv_pw_rows(int cfg);
 int conv_pw_legal(const ConvParams& p, int chunk);
 void conv_pw_launch(const ConvParams& p, int cfg, hipStream_t st);
+// bit 11 = the halo-staged (1,3,3) kernel of conv_halo.hip (bit 0: 64-channel n-tiles; bits 12+: positions per
+// tile, which is its BN partial-sum row tile)
+void conv_halo_launch(const ConvParams& p, int cfg, hipStream_t st);
 
 int conv_cfg_bm(int cfg, int N) {
+  if (cfg >= 0 && (cfg & 16) && (cfg & 2048)) return cfg >> 12;
   if (cfg >= 0 && (cfg & 16) && (cfg & 512)) return conv_pw_rows(cfg);
   if (cfg >= 0 && (cfg & 16) && (cfg & 32)) return conv_direct_rows(cfg);
   if (cfg >= 0 && (cfg & 16) && (cfg & 256)) return 256;   // 256x256 tile
@@ -1035,6 +1039,10 @@ void conv_igemm_launch(const ConvParams& p, int chunk, hipStream_t stream, int c
   int v, bk, ut_force;
   bool dma = false;
   if (p.nostore && cfg >= 0 && (cfg & 16) && (cfg & 512)) cfg = -1;   // the pointwise kernel always stores
+  if (cfg >= 0 && (cfg & 16) && (cfg & 2048)) {  // halo-staged 3x3 kernel (legality checked by the bindings)
+    conv_halo_launch(p, cfg, stream);
+    return;
+  }
   if (cfg >= 0 && (cfg & 16) && (cfg & 512)) {   // streaming pointwise kernel (legality checked by the bindings)
     conv_pw_launch(p, cfg, stream);
     return;

@@ -20,6 +20,8 @@ int conv_cfg_bm(int cfg, int N);
 int conv_igemm_ut_legal(const ConvParams& p, int chunk, int bk);
 int conv_direct_legal(const ConvParams& p, int chunk);
 int conv_pw_legal(const ConvParams& p, int chunk);
+int conv_halo_legal(const ConvParams& p, int chunk);
+int conv_halo_epi_ok(const ConvParams& p);
 void conv_igemm_set_ut(int mode);
 int conv_igemm_m_tiles(int M, int N);
 int conv_igemm_m_tiles_k(int M, int N, int K, int Cg);
@@ -159,6 +161,12 @@ static ConvParams conv_params(const at::Tensor& x, const at::Tensor& w, const at
 // the streaming pointwise kernel (cfg bit 9) must only get geometries it supports: its slab count and row
 // mapping differ from the tile kernels', so a silent fallback would corrupt the caller's partial sums
 static void check_pw(const ConvParams& p, int64_t chunk, int64_t cfg) {
+  if (cfg >= 0 && (cfg & 16) && (cfg & 2048)) {   // halo-staged 3x3 kernel: geometry, epilogue, tile size
+    const int P = conv_halo_legal(p, (int)chunk);
+    TORCH_CHECK(P > 0 && P == (int)(cfg >> 12), "halo conv kernel selected for an unsupported geometry");
+    TORCH_CHECK(conv_halo_epi_ok(p), "halo conv kernel selected for an unsupported epilogue");
+    return;
+  }
   if (cfg < 0 || !(cfg & 16) || !(cfg & 512)) return;
   TORCH_CHECK(conv_pw_legal(p, (int)chunk), "pointwise conv kernel selected for an unsupported geometry");
   TORCH_CHECK(!p.eres || p.ldr % 8 == 0, "pointwise conv kernel: residual row stride must be a multiple of 8");
@@ -622,6 +630,12 @@ PYBIND11_MODULE(_C, m) {
     q.check = (dim_ok(q.Rt, q.ast, q.aot, q.dir, q.nt, q.Gt) && dim_ok(q.Rh, q.ash, q.aoh, q.dir, q.nh, q.Gh) &&
                dim_ok(q.Rw, q.asw, q.aow, q.dir, q.nw, q.Gw)) ? 0 : 1;
     return (int64_t)conv_pw_legal(q, (int)chunk);
+  });
+  m.def("conv_halo_legal", [](std::vector<int64_t> g, int64_t chunk) {
+    ConvParams q{};
+    int* f = &q.M;
+    for (int i = 0; i < 39 && i < (int)g.size(); ++i) f[i] = (int)g[i];
+    return (int64_t)conv_halo_legal(q, (int)chunk);
   });
   m.def("conv_direct_legal", [](std::vector<int64_t> g, int64_t chunk) {
     ConvParams q{};

@@ -175,7 +175,7 @@ class _ConvBN:
         from ..ops.conv import wgrad_splits
         aff = 0 if xf is None else (2 if xf.relu else 1)
         sc_, sh_ = (None, None) if xf is None else (xf.scale, xf.shift)
-        slab = 1 if eng.deterministic else 0
+        slab = 1 if (eng.deterministic or (eng.fold_slabs and dest is not None)) else 0
         dya = 1 if gram else 0
 
         def geometry(cfg):
@@ -455,7 +455,7 @@ class _ConvBN:
             def run(cfg, scratch, g=g):
                 C.conv_igemm(dy.t, wd, tuner.scratch_like(out) if scratch else out, None, None, None, 0,
                              1 if accum else 0, g, 8, cfg)
-            tuner.launch(("d", accum) + tuple(g), g, 8, run)
+            tuner.launch(("d", accum) + tuple(g), g, 8, run, halo=not accum)
         return None
 
     def bn_backward(self, g: Act, y: Act, mask_mode: int, mo: Optional[Act], mxf: Optional[_Xf],
@@ -862,6 +862,13 @@ class FusedNet:
         statistics are always reduced in a fixed order).  Costs a little speed."""
         self.C = require()
         self.deterministic = deterministic
+        # fixed-order (slab) reduction for the weight-gradient launches whose results feed back into the step —
+        # the BN-fold Gram matrices (forward statistics) and G = dz^T act (backward coefficients) — while the
+        # leaf weight gradients keep their fp32 atomics: the loss and the dgrad chain are then reproducible
+        # run to run and only the weight gradients carry atomic-order noise (~1e-6).  Without it that noise
+        # flips ReLU masks and the random-init network's chaotic backward decorrelates two runs' gradients
+        # (cosine ~0.65 at B=4-32: scripts/diag_ms_race.py).  PVA_FOLD_SLABS=1; implied by ``deterministic``.
+        self.fold_slabs = deterministic or os.environ.get("PVA_FOLD_SLABS", "0") == "1"
         self.stem_s2d = stem_s2d and not deterministic
         self.model = model
         self.device = torch.device(device)

@@ -159,7 +159,8 @@ def conv_m_tiles(M: int, N: int, spec: Optional["ConvSpec"] = None) -> int:
 
 def conv_fwd(x: Act, wpack: torch.Tensor, spec: ConvSpec, out: Optional[torch.Tensor] = None,
              stats: Optional[torch.Tensor] = None, in_scale: Optional[torch.Tensor] = None,
-             in_shift: Optional[torch.Tensor] = None, in_relu: bool = True) -> Act:
+             in_shift: Optional[torch.Tensor] = None, in_relu: bool = True, cfg: int = -1) -> Act:
+    """``cfg``: launch configuration word (ops/tune.py; -1 = the kernel's heuristic)."""
     C = require()
     assert x.C == spec.cin_pad, (x.C, spec.cin_pad)
     To, Ho, Wo = spec.out_dims(x.T, x.H, x.W)
@@ -168,12 +169,12 @@ def conv_fwd(x: Act, wpack: torch.Tensor, spec: ConvSpec, out: Optional[torch.Te
         out = torch.empty(M, spec.cout, device=x.t.device, dtype=torch.bfloat16)
     affine = 0 if in_scale is None else (2 if in_relu else 1)
     g = fwd_geometry(spec, x.N, x.T, x.H, x.W, x.ld, out.stride(0))
-    C.conv_igemm(x.t, wpack, out, stats, in_scale, in_shift, affine, 0, g, spec.chunk)
+    C.conv_igemm(x.t, wpack, out, stats, in_scale, in_shift, affine, 0, g, spec.chunk, cfg)
     return Act(out, x.N, To, Ho, Wo)
 
 
 def conv_dgrad(dy: Act, wt_pack: torch.Tensor, spec: ConvSpec, in_dims: Triple, out: Optional[torch.Tensor] = None,
-               accum: bool = False) -> Act:
+               accum: bool = False, cfg: int = -1) -> Act:
     """dX[N,Ti,Hi,Wi,Cin] = conv_transpose(dY, W); ``accum`` adds into ``out``."""
     C = require()
     Ti, Hi, Wi = in_dims
@@ -184,7 +185,7 @@ def conv_dgrad(dy: Act, wt_pack: torch.Tensor, spec: ConvSpec, in_dims: Triple, 
     for g in dgrad_phases(spec, dy.N, in_dims, (dy.T, dy.H, dy.W), dy.ld, out.stride(0)):
         if accum and g[28] == 0:
             continue
-        C.conv_igemm(dy.t, wt_pack, out, None, None, None, 0, 1 if accum else 0, g, 8)
+        C.conv_igemm(dy.t, wt_pack, out, None, None, None, 0, 1 if accum else 0, g, 8, cfg)
     return Act(out, dy.N, Ti, Hi, Wi)
 
 

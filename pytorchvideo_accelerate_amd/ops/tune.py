@@ -32,6 +32,8 @@ BIG = 256             # 256x256 tile of 8 waves (N >= 256; the backward-BN epilo
 PW = 512              # streaming pointwise kernel (csrc/kernels/conv_pw.hip): dense 1x1x1 GEMMs, K <= 256,
 PW_ROWS = (1024, 2048, 4096)   # N % 32 == 0, weights in LDS; bits 0-1 select the rows per workgroup,
 PW_SOLO = 4                     # bit 2 one workgroup per CU
+HALO = 2048           # halo-staged (1,3,3) stride-1 kernel (csrc/kernels/conv_halo.hip): bit 0 = 64-channel
+                      # n-tiles (else 128), bits 12+ = positions per tile
 TILE_BN = (128, 64, 32, 16)   # variants 0..3
 TILE_BM = (128, 128, 256, 256)
 
@@ -40,6 +42,8 @@ def describe(cfg: int) -> str:
     """Human-readable configuration word (``PVA_TUNE_LOG=1`` prints every candidate's time)."""
     if cfg < 0 or not cfg & EXPLICIT:
         return "heuristic"
+    if cfg & HALO:
+        return "halo%d/n%d" % (cfg >> 12, 64 if cfg & 1 else 128)
     if cfg & PW:
         return "pw%d%s" % (PW_ROWS[cfg & 3], "s" if cfg & PW_SOLO else "")
     if cfg & DIRECT:
@@ -61,6 +65,7 @@ class ConvTuner:
         self.direct = os.environ.get("PVA_CONV_DIRECT", "1") != "0"
         self.dma = os.environ.get("PVA_CONV_DMA", "1") != "0"
         self.pw = os.environ.get("PVA_CONV_PW", "1") != "0"
+        self.halo = os.environ.get("PVA_CONV_HALO", "1") != "0"
         # debugging aid: PVA_PW_KINDS=f,fres,er,... restricts the pointwise kernel to launches whose key
         # starts with one of these kinds (models/fused.py: f fres fw2 eb er d)
         kinds = os.environ.get("PVA_PW_KINDS")
@@ -78,7 +83,7 @@ class ConvTuner:
 
     # ---------------------------------------------------------------- candidates
     def candidates(self, g: Sequence[int], chunk: int, aff: int = 0, epi: bool = False,
-                   direct: bool = True, pw: bool = True) -> List[int]:
+                   direct: bool = True, pw: bool = True, halo: bool = True) -> List[int]:
         N, Cg = g[1], g[3]
         K = g[28] * g[29] * g[30] * Cg
         out = []
@@ -106,6 +111,10 @@ class ConvTuner:
                         out.append(w | DMA)
         if direct and self.direct and self.C.conv_direct_legal(list(g), chunk):
             out += [EXPLICIT | DIRECT | r | h for r in (0, DIRECT_2K) for h in (0, DIRECT_HALF)]
+        if halo and self.halo and (aff == 0 or not epi):
+            P = int(self.C.conv_halo_legal(list(g), chunk))
+            if P > 0:
+                out += [EXPLICIT | HALO | (P << 12) | v for v in ((0, 1) if N % 128 == 0 else (1,))]
         if pw and self.pw and self._pw_now and self.C.conv_pw_legal(list(g), chunk):
             self._pw_seen += 1
             if self.pw_only is None or self.pw_only == self._pw_seen - 1:
@@ -127,23 +136,23 @@ class ConvTuner:
 
     # ---------------------------------------------------------------- launch
     def launch(self, key: Tuple, g: Sequence[int], chunk: int, run: Callable[[int, bool], None],
-               aff: int = 0, epi: bool = False, direct: bool = True, pw: bool = True) -> int:
+               aff: int = 0, epi: bool = False, direct: bool = True, pw: bool = True, halo: bool = True) -> int:
         """``run(cfg, scratch)`` performs the launch (into scratch outputs when ``scratch``).  Returns the
         configuration used for the real launch (-1 = kernel heuristic).  ``direct=False`` / ``pw=False``: the
         launch needs an epilogue the direct / pointwise kernel lacks (fused residual output, bias, statistics
-        without the output)."""
+        without the output); ``halo=False``: an accumulating launch (the halo kernel only stores)."""
         cfg = self.cache.get(key)
         if cfg is None:
             self._pw_now = self.pw_kinds is None or (len(key) > 0 and key[0] in self.pw_kinds)
-            cfg = self._tune(g, chunk, run, aff, epi, direct, pw) if self.enabled else -1
+            cfg = self._tune(g, chunk, run, aff, epi, direct, pw, halo) if self.enabled else -1
             self._pw_now = True
             self.cache[key] = cfg
         run(cfg, False)
         return cfg
 
     def _tune(self, g: Sequence[int], chunk: int, run: Callable[[int, bool], None], aff: int = 0,
-              epi: bool = False, direct: bool = True, pw: bool = True) -> int:
-        cands = self.candidates(g, chunk, aff, epi, direct, pw)
+              epi: bool = False, direct: bool = True, pw: bool = True, halo: bool = True) -> int:
+        cands = self.candidates(g, chunk, aff, epi, direct, pw, halo)
         if len(cands) <= 1:
             return cands[0] if cands else -1
         times = []
