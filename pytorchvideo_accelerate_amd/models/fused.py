@@ -895,7 +895,7 @@ class FusedNet:
         # fold_min_c channels (default: the slow pathway, where the Gram matrices run at MFMA speed).  Narrow
         # (fast-pathway) folds take exact statistics from a statistics-only conv pass (Gram-derived variances
         # E[y^2] - E[y]^2 over fp32-atomic sums were not reproducible there: scripts/diag_ms_fold.py); with that
-        # pass, folding them too measures even with not folding (1034 vs 1030 clips/s, scripts/gpu_r2_exact.sh),
+        # pass, folding them too measures even with not folding (1034 vs 1030 clips/s, round-2 runner gpu_r2_exact.sh, git 3ce07ef),
         # so it stays opt-in (PVA_BN_FOLD_MIN_C=8).
         self.bn_fold = os.environ.get("PVA_BN_FOLD", "1") != "0"
         self.fold_min_c = int(os.environ.get("PVA_BN_FOLD_MIN_C", "32"))
