@@ -71,6 +71,14 @@ def parse(argv=None):
     ap.add_argument("--deterministic", action="store_true",
                     help="bitwise-reproducible fused executor (fixed-order reductions, one stream; cross-rank exactness "
                          "tests)")
+    ap.add_argument("--source", choices=("synthetic", "host"), default="synthetic",
+                    help="synthetic: decoded uint8 clips resident on the device (preprocessing only); host: a raw-frame "
+                         ".npy corpus read by the native C++ reader into pinned memory, H2D on a copy stream, then "
+                         "the same on-device preprocessing (the reference's DataLoader + H2D path, run.py:170-183,243)")
+    ap.add_argument("--corpus", default=os.environ.get("PVA_BENCH_CORPUS", "/tmp/pva_bench_corpus"),
+                    help="--source host: corpus directory (generated on first use)")
+    ap.add_argument("--corpus-videos", type=int, default=96)
+    ap.add_argument("--reader-threads", type=int, default=16)
     ap.add_argument("--data-rank", type=int, default=-1,
                     help="draw the synthetic data of this rank instead of the own one (single-process oracle runs "
                          "of a multi-rank job's shards)")
@@ -117,6 +125,57 @@ def plumbing_batch(a, rank: int, i: int):
     fast = torch.randn(a.batch, 3, a.frames, a.crop, a.crop, generator=g)
     idx = torch.linspace(0, a.frames - 1, a.frames // a.alpha).long()
     return [fast.index_select(2, idx).contiguous(), fast], torch.randint(0, a.classes, (a.batch,), generator=g)
+
+
+# ---------------------------------------------------------------------------------------------- host source
+def build_corpus(a, rank: int) -> str:
+    """Raw-frame Kinetics-layout corpus (README 'Data'): ``corpus-videos`` uint8 [src_frames, H, W, 3] .npy videos
+    at 30 fps over 8 classes, random pixels.  Written once (rank 0; the others wait on a marker file)."""
+    import numpy as np
+    root = os.path.join(a.corpus, f"{a.src_frames}x{a.src_h}x{a.src_w}_{a.corpus_videos}")
+    done = os.path.join(root, ".complete")
+    if os.path.exists(done):
+        return root
+    if rank != 0:
+        while not os.path.exists(done):
+            time.sleep(0.5)
+        return root
+    rng = np.random.default_rng(0)
+    for i in range(a.corpus_videos):
+        d = os.path.join(root, "train", f"class_{i % 8}")
+        os.makedirs(d, exist_ok=True)
+        path = os.path.join(d, f"v{i:04d}.npy")
+        mm = np.lib.format.open_memmap(path + ".tmp.npy", mode="w+", dtype=np.uint8,
+                                       shape=(a.src_frames, a.src_h, a.src_w, 3))
+        for t in range(a.src_frames):
+            mm[t] = rng.integers(0, 256, size=(a.src_h, a.src_w, 3), dtype=np.uint8)
+        mm.flush()
+        del mm
+        os.replace(path + ".tmp.npy", path)
+    open(done, "w").close()
+    return root
+
+
+def host_loader(a, st, eng, dev):
+    """Endless device batches: VideoClipDataset (random clip, scale, crop, flip per clip; this rank's shard) ->
+    NativeRawSource (C++ thread pool preads the 32 kept frames of each clip into pinned memory) -> DeviceLoader
+    (H2D of batch i+1 on a copy stream while batch i trains) -> fused on-device preprocessing."""
+    from pytorchvideo_accelerate_amd.data.kinetics import LabeledVideoPaths, VideoClipDataset
+    from pytorchvideo_accelerate_amd.data.loader import DeviceLoader, NativeRawSource
+    from pytorchvideo_accelerate_amd.data.transforms import GpuClipBatch
+    root = build_corpus(a, st.rank)
+    vids = LabeledVideoPaths.from_directory(os.path.join(root, "train"))
+    # repeat the video list so one pass covers every step (each repeat draws fresh random clips / augmentations)
+    need = (a.warmup + a.steps + 3) * a.batch * a.grad_accum * st.world_size
+    reps = -(-need // max(len(vids), 1))
+    paths = LabeledVideoPaths([vids[i] for i in range(len(vids))] * reps, vids.classes)
+    ds = VideoClipDataset(paths, a.src_frames / 30.0, True, a.frames, a.crop, a.alpha, rank=st.rank,
+                          world=st.world_size, distributed=st.world_size > 1, seed=0, mode="gpu")
+    src = NativeRawSource(ds, a.batch, threads=a.reader_threads, drop_last=True, prefetch=3)
+    prep = GpuClipBatch(dev, a.frames, a.crop, a.alpha, s2d=eng.input_s2d)
+    while True:
+        for b in DeviceLoader(src, prep, dev):
+            yield b["video"], b["label"]
 
 
 # ---------------------------------------------------------------------------------------------- main
@@ -169,34 +228,47 @@ def run(a):
         eng.grad_hook = sync.progress if st.world_size > 1 else None   # (1 GPU: no buckets to launch)
         drank = st.rank if a.data_rank < 0 else a.data_rank
         gen = torch.Generator().manual_seed(1000 + drank)
-        frames = torch.empty(B, a.src_frames, a.src_h, a.src_w, 3, dtype=torch.uint8, device=dev)
-        eng.C.synth_frames(frames, 7 + drank)
-        # double-buffered on-device preprocessing: micro-batch k+1 is decoded/resized/cropped on its own
-        # stream while micro-batch k trains (a prefetching data loader; every step still pays its batch)
-        preps = [GpuClipBatch(dev, a.frames, a.crop, a.alpha, s2d=eng.input_s2d) for _ in range(2)]
-        pstream = torch.cuda.Stream(dev)
-        pending = {}
         labels_all = torch.randint(0, a.classes, (64, B), generator=gen).to(dev)
+        host_labels = [None]
+        if a.source == "host":
+            assert not a.graph, "--source host replays no graph (fresh input buffers every step)"
+            hl = host_loader(a, st, eng, dev)
 
-        def prefetch(k):
-            params = [sample_params(a.src_frames, a.src_h, a.src_w, a.frames, a.crop, True, generator=gen)
-                      for _ in range(B)]
-            free = torch.cuda.Event()
-            free.record()   # everything issued so far (the last reader of this buffer) precedes the refill
-            with torch.cuda.stream(pstream):
-                pstream.wait_event(free)
-                xs = preps[k % 2](frames, params)
-                ready = torch.cuda.Event()
-                ready.record(pstream)
-            pending[k] = (xs, ready)
+            def batch(k):
+                xs, lab = next(hl)
+                host_labels[0] = lab
+                return xs
+        else:
+            frames = torch.empty(B, a.src_frames, a.src_h, a.src_w, 3, dtype=torch.uint8, device=dev)
+            eng.C.synth_frames(frames, 7 + drank)
+            # double-buffered on-device preprocessing: micro-batch k+1 is decoded/resized/cropped on its own
+            # stream while micro-batch k trains (a prefetching data loader; every step still pays its batch)
+            preps = [GpuClipBatch(dev, a.frames, a.crop, a.alpha, s2d=eng.input_s2d) for _ in range(2)]
+            pstream = torch.cuda.Stream(dev)
+            pending = {}
 
-        def batch(k):
-            if k not in pending:
-                prefetch(k)
-            xs, ready = pending.pop(k)
-            torch.cuda.current_stream().wait_event(ready)
-            prefetch(k + 1)
-            return xs
+            def prefetch(k):
+                params = [sample_params(a.src_frames, a.src_h, a.src_w, a.frames, a.crop, True, generator=gen)
+                          for _ in range(B)]
+                free = torch.cuda.Event()
+                free.record()   # everything issued so far (the last reader of this buffer) precedes the refill
+                with torch.cuda.stream(pstream):
+                    pstream.wait_event(free)
+                    xs = preps[k % 2](frames, params)
+                    ready = torch.cuda.Event()
+                    ready.record(pstream)
+                pending[k] = (xs, ready)
+
+            def batch(k):
+                if k not in pending:
+                    prefetch(k)
+                xs, ready = pending.pop(k)
+                torch.cuda.current_stream().wait_event(ready)
+                prefetch(k + 1)
+                return xs
+
+        def labels_of(k):
+            return host_labels[0] if a.source == "host" else labels_all[k % 64]
 
         if a.graph and st.world_size == 1:
             from pytorchvideo_accelerate_amd.engine.graph import GraphedStep
@@ -220,7 +292,7 @@ def run(a):
                 # untimed autotuning pass: every conv geometry is tuned (ranks agree on the choice) with
                 # no gradient all-reduce in flight and no optimizer step (weights stay rank-identical)
                 sync.begin(False)
-                eng.forward_backward(xs, labels_all[0], accumulate=False)
+                eng.forward_backward(xs, labels_of(0), accumulate=False)
                 return None
             opt.zero_grad()
             for j in range(a.grad_accum):
@@ -228,8 +300,7 @@ def run(a):
                     xs = batch(i * a.grad_accum + j)
                 last = j == a.grad_accum - 1
                 sync.begin(last)
-                loss, _ = eng.forward_backward(xs, labels_all[(i * a.grad_accum + j) % 64],
-                                               loss_scale=1.0 / a.grad_accum)
+                loss, _ = eng.forward_backward(xs, labels_of(i * a.grad_accum + j), loss_scale=1.0 / a.grad_accum)
                 sync.finish()
             if i == 0 and a.dump:
                 dump["grad"] = eng.flat.grad.clone()
@@ -305,6 +376,9 @@ def run(a):
             "vs_baseline": round(clips / (STOCK_CLIPS_PER_S_1GPU * st.world_size), 3) if headline else None,
             "dtype": "fp32" if a.plumbing else "bf16",
             "data": ("synthetic normal clips, CPU plumbing run" if a.plumbing else
+                     "synthetic uint8 raw-frame .npy corpus (64x256x340 per video) read by the native C++ reader into "
+                     "pinned memory, H2D on a copy stream, on-device preprocessing; random-init weights"
+                     if a.source == "host" else
                      "synthetic uint8 decoded clips (64x256x340), on-device preprocessing (next batch prefetched "
                      "on a side stream); random-init weights"),
             "config": {"model": f"SlowFast-R{a.depth} {a.frames}x2x{a.crop}",
@@ -312,7 +386,7 @@ def run(a):
                        "per_gpu_batch": B, "grad_accum": a.grad_accum, "seq_len": a.frames,
                        "parallelism": f"dp{st.world_size}", "backend": st.backend or "none",
                        "grad_dtype": a.grad_dtype, "classes": a.classes, "hip_graph": bool(gstep is not None),
-                       "deterministic": a.deterministic,
+                       "deterministic": a.deterministic, "source": a.source,
                        "final_loss": round(float(loss), 4) if loss is not None else None,
                        "peak_mem_gb": (round(torch.cuda.max_memory_allocated(dev) / 2**30, 1)
                                        if dev.type == "cuda" else None),

@@ -127,7 +127,9 @@ class GpuClipBatch:
         B = desc.shape[0]
         outs = []
         if self.alpha:
-            sel = self.slow_sel.to(tidx.device)
+            sel = self._out.get(("sel", tidx.device))
+            if sel is None:
+                sel = self._out[("sel", tidx.device)] = self.slow_sel.to(tidx.device)
             stidx = tidx.index_select(1, sel).contiguous()
             Ts = stidx.shape[1]
             slow = self._buf("slow", (B * Ts * self.S * self.S, 4))
@@ -153,6 +155,8 @@ class GpuClipBatch:
     def from_packed(self, frames: torch.Tensor, desc: torch.Tensor, num_frames: int):
         """Loader path: packed, already temporally-subsampled clips (tidx = identity)."""
         B = desc.shape[0]
-        tidx = torch.arange(num_frames, dtype=torch.int32).repeat(B, 1)
-        return self._run(frames, desc.to(self.device, non_blocking=True),
-                         tidx.to(self.device, non_blocking=True))
+        key = ("tidx", B, num_frames)
+        tidx = self._out.get(key)
+        if tidx is None:   # device-resident identity index (no pageable H2D copy per batch)
+            tidx = self._out[key] = torch.arange(num_frames, dtype=torch.int32).repeat(B, 1).to(self.device)
+        return self._run(frames, desc.to(self.device, non_blocking=True), tidx)
