@@ -660,7 +660,13 @@ int wgrad_narrow_legal(int Cout, int Cin, int K) { return (Cout <= 32 && Cin % 8
 int wgrad_halo_legal(const WgradParams& p);
 void wgrad_halo_launch(const WgradParams& p, hipStream_t s);
 
+void wgrad_box_launch(const WgradParams& p, hipStream_t st);
+
 void conv_wgrad_launch(const WgradParams& p, int chunk, hipStream_t stream) {
+  if (p.variant >= 0 && (p.variant & (1 << 26))) {   // box-staged (1,3,3) kernel (wgrad_box.hip): per-split slabs
+    wgrad_box_launch(p, stream);
+    return;
+  }
   if (p.variant >= 0 && (p.variant & 32)) {   // halo-staged kernel (wgrad_halo.hip); legality checked by the binding
     wgrad_halo_launch(p, stream);
     return;

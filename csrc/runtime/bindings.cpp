@@ -30,6 +30,9 @@ void conv_wgrad_launch(const WgradParams& p, int chunk, hipStream_t stream);
 void conv_wgrad_tile(int Cout, int K, int variant, int* bmw, int* bnw);
 int wgrad_narrow_legal(int Cout, int Cin, int K);
 int wgrad_halo_legal(const WgradParams& p);
+int wgrad_box_legal(const WgradParams& p);
+void wgrad_box_reduce_launch(const float* slab, float* tmp, float* grad, int splits, int Cout, int taps, int Cin,
+                             int Cin_real, float scale, float beta, hipStream_t st);
 void wgrad_reduce_launch(float* accbuf, float* grad, int splits, int Cout, int taps, int Cin, int Cin_real,
                          float scale, float beta, int slab, hipStream_t stream);
 void bn_finalize_launch(const float* part, int tiles, int C, int64_t count, const float* gamma, const float* beta,
@@ -279,8 +282,9 @@ void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& par
   p.kt = g[12]; p.kh = g[13]; p.kw = g[14]; p.st = g[15]; p.sh = g[16]; p.sw = g[17];
   p.pt = g[18]; p.ph = g[19]; p.pw = g[20]; p.splits = g[21]; p.p_per_split = g[22];
   TORCH_CHECK(p.Cin % chunk == 0 && p.Cout % 8 == 0, "wgrad channel alignment");
-  const bool halo = variant >= 0 && (variant & 32);   // p_per_split = boxes per workgroup
-  TORCH_CHECK(halo || p.p_per_split % 32 == 0, "p_per_split must be a multiple of 32");
+  const bool box = variant >= 0 && (variant & (1 << 26));   // box-staged (1,3,3) kernel: per-split slabs
+  const bool halo = !box && variant >= 0 && (variant & 32);  // p_per_split = boxes per workgroup
+  TORCH_CHECK(halo || box || p.p_per_split % 32 == 0, "p_per_split must be a multiple of 32");
   TORCH_CHECK(variant < 0 || !(variant & 4) || p.p_per_split % 64 == 0, "64-position stages need p_per_split % 64 == 0");
   p.slab = (int)slab;
   p.variant = (int)variant;
@@ -296,11 +300,26 @@ void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& par
     TORCH_CHECK(!dy_affine || (p.Cout == p.Cin && p.K == p.Cin), "narrow Gram: square 1x1");
   }
   TORCH_CHECK(!halo || (wgrad_halo_legal(p) && chunk == 8 && p.p_per_split > 0), "halo wgrad not legal here");
+  if (box) {
+    TORCH_CHECK(wgrad_box_legal(p) && chunk == 8 && slab, "box wgrad not legal here (needs slab mode)");
+    const int64_t boxes = p.P / (p.Wo * (int64_t)wgrad_box_legal(p));
+    TORCH_CHECK(p.p_per_split > 0 && (int64_t)p.splits * p.p_per_split >= boxes, "box wgrad: split cover");
+  }
   TORCH_CHECK(dy.numel() * 2 < 0xFFFFFF00ll && x.numel() * 2 < 0xFFFFFF00ll, "buffer extents must fit 32 bits");
   p.dybytes = (unsigned)(dy.numel() * 2);
   p.xbytes = (unsigned)(x.numel() * 2);
   TORCH_CHECK(partial.numel() >= (int64_t)p.Cout * p.K * (slab ? p.splits : 1), "wgrad accumulator too small");
   conv_wgrad_launch(p, (int)chunk, cur_stream());
+}
+
+// slab [splits][Cout][taps*Cin] of the box kernel -> grad; tmp: >= 16 * Cout*taps*Cin floats
+void wgrad_box_reduce(const at::Tensor& slab, const at::Tensor& tmp, const at::Tensor& grad, int64_t splits,
+                      int64_t Cout, int64_t taps, int64_t Cin, int64_t Cin_real, double scale, double beta) {
+  const int64_t n = Cout * taps * Cin;
+  TORCH_CHECK(slab.numel() >= splits * n && tmp.numel() >= 16 * n && n % 4 == 0, "box wgrad reduce: buffer sizes");
+  TORCH_CHECK(grad.numel() >= Cout * taps * Cin_real, "box wgrad reduce: grad too small");
+  wgrad_box_reduce_launch(f32(slab), f32(tmp), f32(grad), (int)splits, (int)Cout, (int)taps, (int)Cin, (int)Cin_real,
+                          (float)scale, (float)beta, cur_stream());
 }
 
 void wgrad_reduce(const at::Tensor& partial, const at::Tensor& grad, int64_t splits, int64_t Cout, int64_t taps,
@@ -630,6 +649,16 @@ PYBIND11_MODULE(_C, m) {
     q.check = (dim_ok(q.Rt, q.ast, q.aot, q.dir, q.nt, q.Gt) && dim_ok(q.Rh, q.ash, q.aoh, q.dir, q.nh, q.Gh) &&
                dim_ok(q.Rw, q.asw, q.aow, q.dir, q.nw, q.Gw)) ? 0 : 1;
     return (int64_t)conv_pw_legal(q, (int)chunk);
+  });
+  m.def("wgrad_box_reduce", &wgrad_box_reduce);
+  m.def("wgrad_box_legal", [](std::vector<int64_t> g) {
+    // [P, Cout, K, Cin, ldd, ldx, Ti, Hi, Wi, To, Ho, Wo, kt, kh, kw, st, sh, sw, pt, ph, pw]
+    WgradParams q{};
+    q.P = g[0]; q.Cout = g[1]; q.K = g[2]; q.Cin = g[3]; q.ldd = g[4]; q.ldx = g[5];
+    q.Ti = g[6]; q.Hi = g[7]; q.Wi = g[8]; q.To = g[9]; q.Ho = g[10]; q.Wo = g[11];
+    q.kt = g[12]; q.kh = g[13]; q.kw = g[14]; q.st = g[15]; q.sh = g[16]; q.sw = g[17];
+    q.pt = g[18]; q.ph = g[19]; q.pw = g[20];
+    return (int64_t)wgrad_box_legal(q);
   });
   m.def("conv_halo_legal", [](std::vector<int64_t> g, int64_t chunk) {
     ConvParams q{};

@@ -172,7 +172,7 @@ class _ConvBN:
         s = spec or self.spec
         eng.mark(self.name + (".gram" if gram else ".wgrad"))
         K = s.taps * s.cin_pad
-        from ..ops.conv import wgrad_splits
+        from ..ops.conv import box_wgrad_plan, wgrad_splits
         aff = 0 if xf is None else (2 if xf.relu else 1)
         sc_, sh_ = (None, None) if xf is None else (xf.scale, xf.shift)
         slab = 1 if (eng.deterministic or (eng.fold_slabs and dest is not None)) else 0
@@ -185,6 +185,8 @@ class _ConvBN:
             if sp is None:
                 if cfg < 0:
                     sp = wgrad_splits(dy.M, s.cout, K, target_blocks=256 if slab else 1024) + (-1,)
+                elif cfg & 1024:  # box-staged (1,3,3) kernel (wgrad_box.hip): own slabs, fixed-order reduction
+                    sp = box_wgrad_plan(s, dy.M, (dy.T, dy.H, dy.W), dy.ld, x.ld)
                 elif cfg & 256:   # halo-staged kernel (wgrad_halo.hip): bit 9 = box option
                     from ..ops.conv import halo_wgrad_plan
                     sp = halo_wgrad_plan(s, dy.M, (dy.T, dy.H, dy.W), (cfg >> 9) & 1)
@@ -203,8 +205,17 @@ class _ConvBN:
             splits, pps, v = geometry(cfg)
             g = [dy.M, s.cout, K, s.cin_pad, dy.ld, x.ld, x.T, x.H, x.W, dy.T, dy.H, dy.W,
                  *s.k, *s.stride, *s.pad, splits, pps]
-            C.conv_wgrad(dy.t, x.t, part, sc_, sh_, aff, g, s.chunk, slab, v, dya,
+            C.conv_wgrad(dy.t, x.t, part, sc_, sh_, aff, g, s.chunk, 1 if cfg >= 0 and cfg & 1024 else slab, v, dya,
                          None if cs is None else cs[:splits * s.cout])
+            return splits
+
+        def box_run(cfg, grad, beta_):
+            """box-staged kernel into its per-range slabs, then the two-pass fixed-order reduction into ``grad``"""
+            splits = geometry(cfg)[0]
+            part = eng.scratch("wgrad_box_slab", splits * s.cout * K)
+            launch(cfg, part)
+            C.wgrad_box_reduce(part, eng.scratch("wgrad_box_tmp", 16 * s.cout * K), grad, splits, s.cout, s.taps,
+                               s.cin_pad, s.cin, 1.0, beta_)
             return splits
 
         tkey = ("w", dy.M, dy.ld, x.ld, x.T, x.H, x.W, s.cout, K, s.chunk, aff, gram) + tuple(s.k) + tuple(s.stride)
@@ -230,6 +241,8 @@ class _ConvBN:
                 if C.wgrad_narrow_legal(s.cout, s.cin_pad, K) and s.chunk == 8:
                     cands += [c for c in (16 | 128 | (tbi << 2) for tbi in range(4))
                               if not (gram and geometry(c)[0] > 4096)]   # colsum slab holds 4096 splits
+                if not gram and box_wgrad_plan(s, dy.M, (dy.T, dy.H, dy.W), dy.ld, x.ld) is not None:
+                    cands.append(16 | 1024)
                 if not gram:   # halo-staged kernel, two box sizes
                     from ..ops.conv import halo_wgrad_plan
                     for o in (0, 1):
@@ -240,12 +253,19 @@ class _ConvBN:
                               *s.k, *s.stride, *s.pad, plan[0], plan[1]]
                         if C.wgrad_halo_legal(gh, plan[2], aff):
                             cands.append(16 | 256 | (o << 9))
+                gscr = eng.scratch("wgrad_tune_grad", s.cout * K)
+
+                def trial(c):
+                    if c & 1024:
+                        box_run(c, gscr, 0.0)
+                    else:
+                        launch(c, scratch, cs_scr)
                 for c in cands:
-                    launch(c, scratch, cs_scr)
+                    trial(c)
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     e0.record()
                     for _ in range(3):
-                        launch(c, scratch, cs_scr)
+                        trial(c)
                     e1.record()
                     e1.synchronize()
                     times.append(e0.elapsed_time(e1))
@@ -271,13 +291,19 @@ class _ConvBN:
             eng.lane = 2 + lane0
             try:
                 with torch.cuda.stream(wst):
-                    part = eng.scratch("wgrad_acc", s.cout * K, zero=True)
-                    splits = launch(cfg, part, colsum)
-                    C.wgrad_reduce(part, eng.flat.gview(self.conv.weight), splits, s.cout, s.taps, s.cin_pad, s.cin,
-                                   1.0, eng.grad_beta, 0)
+                    if cfg >= 0 and cfg & 1024:
+                        splits = box_run(cfg, eng.flat.gview(self.conv.weight), eng.grad_beta)
+                    else:
+                        part = eng.scratch("wgrad_acc", s.cout * K, zero=True)
+                        splits = launch(cfg, part, colsum)
+                        C.wgrad_reduce(part, eng.flat.gview(self.conv.weight), splits, s.cout, s.taps, s.cin_pad,
+                                       s.cin, 1.0, eng.grad_beta, 0)
             finally:
                 eng.lane = lane0
             return splits
+        if cfg >= 0 and cfg & 1024:
+            return box_run(cfg, eng.flat.gview(self.conv.weight) if dest is None else dest,
+                           eng.grad_beta if beta is None else beta)
         if slab:  # per-split slabs summed in a fixed order: bitwise reproducible weight gradients
             part = eng.scratch("wgrad_slab", geometry(cfg)[0] * s.cout * K)
         else:     # fp32 atomics into one zeroed accumulator (kept zero by wgrad_reduce)

@@ -256,6 +256,27 @@ def halo_wgrad_plan(spec: "ConvSpec", P: int, dims: Tuple[int, int, int], option
     return splits, bps, HALO | (BH << 8) | (BT << 12) | (wpl << 15) | (ktb << 17)
 
 
+BOX = 1 << 26   # wgrad launch-word bit of the box-staged (1,3,3) kernel (csrc/kernels/wgrad_box.hip)
+
+
+def box_wgrad_plan(spec: "ConvSpec", P: int, dims: Tuple[int, int, int], ldd: int, ldx: int,
+                   target_blocks: int = 512) -> Optional[Tuple[int, int, int]]:
+    """(box ranges, boxes per range, launch word) of the box-staged weight gradient of a stride-1 'same' (1,3,3)
+    conv with 64-multiple channel counts whose output grid is ``dims``, or None.  The grid is (Cout/64)*(Cin/64)
+    channel groups x box ranges, ~``target_blocks`` workgroups (two per CU); each range writes its own slab."""
+    T, H, W = dims
+    g = [P, spec.cout, spec.taps * spec.cin_pad, spec.cin_pad, ldd, ldx, T, H, W, T, H, W, *spec.k, *spec.stride,
+         *spec.pad]
+    R = int(require().wgrad_box_legal(g))
+    if R <= 0 or spec.cin_pad != spec.cin:
+        return None
+    groups = (spec.cout // 64) * (spec.cin // 64)
+    nboxes = P // (R * W)
+    splits = max(1, min(nboxes, -(-target_blocks // groups)))
+    bps = -(-nboxes // splits)
+    return -(-nboxes // bps), bps, BOX
+
+
 def conv_wgrad(dy: Act, x: Act, spec: ConvSpec, grad: torch.Tensor, workspace: Optional[torch.Tensor] = None,
                in_scale: Optional[torch.Tensor] = None, in_shift: Optional[torch.Tensor] = None,
                in_relu: bool = True, scale: float = 1.0, beta: float = 0.0,
@@ -264,7 +285,8 @@ def conv_wgrad(dy: Act, x: Act, spec: ConvSpec, grad: torch.Tensor, workspace: O
 
     ``variant``: -1 = heuristic tile; else bits 0-1 (+ bit 3 -> tiles 4-7) = tile (16x128, 32x128, 64x64, 128x64,
     128x128, 256x128, 128x256, 256x256), bit 2 = 64-position LDS stages (two MFMA k-steps per barrier);
-    ``HALO | option`` (option 0/1 in bits 0-1) = the halo-staged kernel with box option ``option``."""
+    ``HALO | option`` (option 0/1 in bits 0-1) = the halo-staged kernel with box option ``option``; ``BOX`` = the
+    box-staged (1,3,3) kernel (64-multiple channels)."""
     C = require()
     P = dy.M
     K = spec.taps * spec.cin_pad
@@ -273,6 +295,18 @@ def conv_wgrad(dy: Act, x: Act, spec: ConvSpec, grad: torch.Tensor, workspace: O
         pps = ((P + nw - 1) // nw + 63) // 64 * 64
         splits_pps = ((P + pps - 1) // pps, pps)
         variant = 16
+    if variant == BOX:   # box-staged kernel: per-range slabs + fixed-order two-pass reduction
+        C = require()
+        splits, bps, word = box_wgrad_plan(spec, P, (dy.T, dy.H, dy.W), dy.ld, x.ld)
+        K = spec.taps * spec.cin_pad
+        slab = torch.empty(splits * spec.cout * K, device=dy.t.device, dtype=torch.float32)
+        tmp = torch.empty(16 * spec.cout * K, device=dy.t.device, dtype=torch.float32)
+        affine = 0 if in_scale is None else (2 if in_relu else 1)
+        g = [P, spec.cout, K, spec.cin_pad, dy.ld, x.ld, x.T, x.H, x.W, dy.T, dy.H, dy.W,
+             *spec.k, *spec.stride, *spec.pad, splits, bps]
+        C.conv_wgrad(dy.t, x.t, slab, in_scale, in_shift, affine, g, spec.chunk, 1, word)
+        C.wgrad_box_reduce(slab, tmp, grad, splits, spec.cout, spec.taps, spec.cin_pad, spec.cin, scale, beta)
+        return grad
     if splits_pps is None and variant >= 0 and variant & HALO and variant < 256:   # halo kernel, box option
         plan = halo_wgrad_plan(spec, P, (dy.T, dy.H, dy.W), variant & 3)
         assert plan is not None, "halo wgrad does not apply to this conv"

@@ -114,3 +114,32 @@ def test_halo_legality():
     assert Cm.conv_halo_legal(fwd_geometry(ConvSpec(64, 64, (3, 1, 1), (1, 1, 1), (1, 0, 0)), 2, 4, 56, 56, 64, 64), 8) == 0
     assert Cm.conv_halo_legal(fwd_geometry(ConvSpec(512, 512, (1, 3, 3), (1, 1, 1), (0, 1, 1)), 2, 4, 7, 7, 512, 512), 8) == 0
     assert Cm.conv_halo_legal(fwd_geometry(ConvSpec(16, 16, (1, 3, 3), (1, 1, 1), (0, 1, 1)), 2, 4, 56, 56, 16, 16), 8) == 0
+
+
+WGRAD_CASES = [(64, 1, 2, 56, 56), (128, 1, 3, 28, 28), (256, 2, 2, 14, 14), (64, 1, 1, 64, 64)]
+
+
+@pytest.mark.parametrize("case", WGRAD_CASES)
+def test_box_wgrad_vs_torch(case):
+    """Box-staged weight gradient (csrc/kernels/wgrad_box.hip) with the producer's BN+ReLU recomputed on the input
+    halo, against torch.nn.grad.conv3d_weight in fp32; accumulate (beta) and scale through the slab reduction."""
+    from pytorchvideo_accelerate_amd.ops.conv import BOX, box_wgrad_plan, conv_wgrad
+    C, N, T, H, W = case
+    x, w, spec = _mk(C, N, T, H, W, seed=7)
+    sc = torch.rand(C, device=DEV) + 0.5
+    sh = torch.randn(C, device=DEV) * 0.5
+    xt = torch.relu(x * sc.view(1, C, 1, 1, 1) + sh.view(1, C, 1, 1, 1)).to(torch.bfloat16).float()
+    gy = torch.randn(N, C, T, H, W, generator=torch.Generator().manual_seed(8)).to(torch.bfloat16).float().to(DEV)
+    ref = torch.nn.grad.conv3d_weight(xt, w.shape, gy, spec.stride, spec.pad)
+    xa, dy = Act.from_ncthw(x), Act.from_ncthw(gy)
+    assert box_wgrad_plan(spec, dy.M, (T, H, W), dy.ld, xa.ld) is not None
+    grad = torch.full_like(ref, float("nan"))
+    conv_wgrad(dy, xa, spec, grad, in_scale=sc, in_shift=sh, in_relu=True, variant=BOX)
+    assert _rel(grad, ref) < 5e-3
+    prev = grad.clone()
+    conv_wgrad(dy, xa, spec, grad, in_scale=sc, in_shift=sh, in_relu=True, variant=BOX, scale=0.5, beta=1.0)
+    assert _rel(grad, prev + 0.5 * ref) < 5e-3
+    # bitwise reproducible (fixed-order slab reduction, no atomics)
+    g2 = torch.empty_like(ref)
+    conv_wgrad(dy, xa, spec, g2, in_scale=sc, in_shift=sh, in_relu=True, variant=BOX)
+    assert torch.equal(g2, prev)
