@@ -341,6 +341,204 @@ void launch_ntile(const ConvParams& p, int R, bool epi, hipStream_t st) {
   }
 }
 
+
+// ------------------------------------------------------------------------------------------------------------------
+// Narrow variant (fast pathway: 8 / 16 / 32 channels in and out, P = R*W <= 1024 positions per tile).  At these
+// widths the conv is a pure streaming problem (K = 9*C <= 288): the halo [(R+2) x (W+2)][C] is staged once
+// (position-major, 16/32/64 B per position), the weights of every k-step live in registers for the whole kernel,
+// and each wave walks 16-position blocks of the tile: a k-step covers 32/C taps, lane group g (= lane >> 4) reads its
+// own tap's 16 B of channels at (position + tap offset) straight into the MFMA operand (the 9 taps padded to whole
+// k-steps with zero weights), so one LDS read per lane feeds each MFMA and nothing is re-gathered from L2.
+constexpr int HN_PMAX = 1024;
+
+__host__ __device__ inline int halo_rows_narrow(int H, int W) {
+  for (int r = H; r >= 1; --r)
+    if (H % r == 0 && r * W <= HN_PMAX) return r;
+  return 0;
+}
+
+template <int CG, int NN, int EPI, int AFF>
+__global__ __launch_bounds__(HC_THREADS) void conv_halo_narrow_kernel(const ConvParams p, const int R) {
+  constexpr int NB = (NN + 15) / 16;          // 16-channel output blocks
+  constexpr int GPT = CG / 8;                 // 16-B channel groups per tap
+  constexpr int TPS = 4 / GPT;                // taps per 32-wide k-step
+  constexpr int NSTEP = (9 + TPS - 1) / TPS;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int W = p.Rw, H = p.Rh, PW = W + 2;
+  const int P = R * W;
+  const int NPOS = (R + 2) * PW;
+  char* box = smem;                                                        // [NPOS][CG]
+  float* red = reinterpret_cast<float*>(smem + ((NPOS * CG * 2 + 15) & ~15));   // [4 waves][2|3][NN]
+  float* aff = red + (EPI ? 3 : 2) * 4 * NN;                               // [2][CG]
+  float* bnp = aff + 2 * CG;                                               // EPI 1: [4][NN]
+
+  const int tile_m = xcd_remap(blockIdx.x, gridDim.x);
+  const int tpf = H / R;
+  const int frame = tile_m / tpf, r0 = (tile_m - frame * tpf) * R;
+  const int fbase = frame * H * W;
+  if constexpr (AFF != 0) {
+    for (int i = tid; i < CG; i += HC_THREADS) { aff[i] = p.in_scale[i]; aff[CG + i] = p.in_shift[i]; }
+  }
+  if constexpr (EPI == 1) {
+    for (int i = tid; i < NN; i += HC_THREADS) {
+      bnp[i] = p.emean0[i]; bnp[NN + i] = p.erstd0[i]; bnp[2 * NN + i] = p.emsc[i]; bnp[3 * NN + i] = p.emsh[i];
+    }
+  }
+  // this lane's weights of every k-step (A operand: row = output channel, 8 k = 8 channels of its group's tap)
+  bf16x8_t wf[NSTEP][NB];
+  int toff[NSTEP];
+  const int chb = (fg % GPT) * 16;
+#pragma unroll
+  for (int s = 0; s < NSTEP; ++s) {
+    const int tap = s * TPS + fg / GPT;
+    const bool real = tap < 9;
+    const int jh = real ? tap / 3 : 1, jw = real ? tap - (tap / 3) * 3 : 1;
+    toff[s] = real ? ((p.aoh + p.dir * jh) * PW + (p.aow + p.dir * jw)) * (CG * 2) : 0;
+    const int wt = (p.bt0 * p.kh + p.bh0 + jh * p.bhs) * p.kw + p.bw0 + jw * p.bws;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int co = j * 16 + fr;
+      uint4 v = uint4{0, 0, 0, 0};
+      if (real && co < p.Ngemm) v = *reinterpret_cast<const uint4*>(p.w + (size_t)co * p.Kfull + wt * CG + (fg % GPT) * 8);
+      wf[s][j] = __builtin_bit_cast(bf16x8_t, v);
+    }
+  }
+  __syncthreads();
+  // ---- stage the halo: chunk c -> box position c / GPT, channel group c % GPT (fixed per thread)
+  {
+    const int cgp = tid % GPT;
+    float sc[8], sh[8];
+    if constexpr (AFF != 0) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { sc[e] = aff[cgp * 8 + e]; sh[e] = aff[CG + cgp * 8 + e]; }
+    }
+    constexpr int PPP = HC_THREADS / GPT;   // box positions per pass
+    const int b_first = tid / GPT;
+    int hh = b_first / PW, ww = b_first - (b_first / PW) * PW;
+    constexpr int BATCH = 4;
+    for (int b0 = b_first; b0 < NPOS; b0 += BATCH * PPP) {
+      uint4 v[BATCH];
+      bool ok[BATCH];
+#pragma unroll
+      for (int u = 0; u < BATCH; ++u) {
+        const int h = r0 - 1 + hh, w = ww - 1;
+        ok[u] = b0 + u * PPP < NPOS && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+        v[u] = ok[u] ? *reinterpret_cast<const uint4*>(p.x + (size_t)(fbase + h * W + w) * p.ldx + cgp * 8)
+                     : uint4{0, 0, 0, 0};
+        ww += PPP;
+        while (ww >= PW) { ww -= PW; ++hh; }
+      }
+#pragma unroll
+      for (int u = 0; u < BATCH; ++u) {
+        const int bb = b0 + u * PPP;
+        if (bb >= NPOS) break;
+        uint4 o = v[u];
+        if constexpr (AFF != 0) {
+          float f[8];
+          unpack8(o, f);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) f[e] = __builtin_fmaf(f[e], sc[e], sh[e]);
+          o = pack8_fast(f);
+          if constexpr (AFF == 2) o = relu_bf16x8(o);
+          if (!ok[u]) o = uint4{0, 0, 0, 0};
+        }
+        *reinterpret_cast<uint4*>(box + bb * (CG * 2) + cgp * 16) = o;
+      }
+    }
+  }
+  __syncthreads();
+  // ---- 16-position blocks, round-robin over the waves
+  float s1[NB][4], s2[NB][4];
+#pragma unroll
+  for (int j = 0; j < NB; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { s1[j][r] = 0.f; s2[j][r] = 0.f; }
+  const int MB = (P + 15) / 16;
+  for (int mb = wid; mb < MB; mb += 4) {
+    const int pl = mb * 16 + fr;
+    const int pc = min(pl, P - 1);
+    const int h = pc / W, w = pc - h * W;
+    const char* src = box + ((h + 1) * PW + (w + 1)) * (CG * 2) + chb;
+    f32x4_t acc[NB];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) acc[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < NSTEP; ++s) {
+      const bf16x8_t xf = *reinterpret_cast<const bf16x8_t*>(src + toff[s]);
+#pragma unroll
+      for (int j = 0; j < NB; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[s][j], xf, acc[j], 0, 0, 0);
+    }
+    if (pl >= P) continue;
+    const int row = fbase + r0 * W + pl;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int n = j * 16 + 4 * fg;
+      if (n >= NN) continue;
+      float v[4] = {acc[j][0], acc[j][1], acc[j][2], acc[j][3]};
+      float a[4];
+      if constexpr (EPI == 1) {
+        unpack4(*reinterpret_cast<const uint2*>(p.ey0 + (size_t)row * NN + n), a);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = (a[r] * bnp[2 * NN + n + r] + bnp[3 * NN + n + r] > 0.f) ? v[r] : 0.f;
+      }
+      const uint2 pk = pack4(v);
+      *reinterpret_cast<uint2*>(p.y + (size_t)row * p.ldy + n) = pk;
+      float q[4];
+      unpack4(pk, q);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        s1[j][r] += q[r];
+        if constexpr (EPI == 1) s2[j][r] += q[r] * a[r]; else s2[j][r] += q[r] * q[r];
+      }
+    }
+  }
+  // ---- per-tile partial sums (EPI 0: sum, sum of squares; EPI 1: sum v, sum v*xhat0, 0)
+  if (EPI == 0 && p.stats == nullptr) return;
+#pragma unroll
+  for (int j = 0; j < NB; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float a = sum16(s1[j][r]), b = sum16(s2[j][r]);
+      const int n = j * 16 + 4 * fg + r;
+      if (fr == 0 && n < NN) {
+        red[(wid * 2) * NN + n] = a;
+        red[(wid * 2 + 1) * NN + n] = b;
+      }
+    }
+  __syncthreads();
+  for (int n = tid; n < NN; n += HC_THREADS) {
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) { a += red[(w * 2) * NN + n]; b += red[(w * 2 + 1) * NN + n]; }
+    if constexpr (EPI == 0) {
+      p.stats[(tile_m * 2) * NN + n] = a;
+      p.stats[(tile_m * 2 + 1) * NN + n] = b;
+    } else {
+      p.epart[(tile_m * 3) * NN + n] = a;
+      p.epart[(tile_m * 3 + 1) * NN + n] = (b - bnp[n] * a) * bnp[NN + n];
+      p.epart[(tile_m * 3 + 2) * NN + n] = 0.f;
+    }
+  }
+}
+
+template <int CG, int NN>
+void launch_narrow(const ConvParams& p, hipStream_t st) {
+  const int R = halo_rows_narrow(p.Rh, p.Rw);
+  const int NPOS = (R + 2) * (p.Rw + 2);
+  const bool epi = p.epart != nullptr;
+  const size_t lds = ((size_t)NPOS * CG * 2 + 15) / 16 * 16 + (size_t)(epi ? 3 : 2) * 4 * NN * 4 + 2 * CG * 4 +
+                     4 * NN * 4;
+  const dim3 grid(p.M / (R * p.Rw)), block(HC_THREADS);
+  if (epi) { hipLaunchKernelGGL((conv_halo_narrow_kernel<CG, NN, 1, 0>), grid, block, lds, st, p, R); return; }
+  switch (p.affine) {
+    case 0: hipLaunchKernelGGL((conv_halo_narrow_kernel<CG, NN, 0, 0>), grid, block, lds, st, p, R); break;
+    case 1: hipLaunchKernelGGL((conv_halo_narrow_kernel<CG, NN, 0, 1>), grid, block, lds, st, p, R); break;
+    default: hipLaunchKernelGGL((conv_halo_narrow_kernel<CG, NN, 0, 2>), grid, block, lds, st, p, R); break;
+  }
+}
+
 }  // namespace
 
 // Positions per tile when the halo kernel can run this launch's geometry, else 0.  Geometry only: the epilogue
@@ -355,8 +553,13 @@ int conv_halo_legal(const ConvParams& p, int chunk) {
     const int dh = p.aoh + p.dir * j, dw = p.aow + p.dir * j;
     if (dh < -1 || dh > 1 || dw < -1 || dw > 1) return 0;
   }
+  if (p.ldx % 8 != 0 || p.ldy % 4 != 0 || p.M % (p.Rh * p.Rw) != 0) return 0;
+  const bool narrow = (p.Cg == 8 || p.Cg == 16 || p.Cg == 32) && (p.Ngemm == 8 || p.Ngemm == 16 || p.Ngemm == 32);
+  if (narrow) {   // conv_halo_narrow_kernel (fast pathway)
+    const int R = halo_rows_narrow(p.Rh, p.Rw);
+    return (R > 0 && R * p.Rw >= 128) ? R * p.Rw : 0;
+  }
   if (p.Cg % 32 != 0 || (p.Cg > 128 && p.Cg % 128 != 0) || p.Ngemm % 64 != 0) return 0;
-  if (p.ldx % 8 != 0 || p.ldy % 4 != 0) return 0;
   const int R = halo_rows(p.Rh, p.Rw);
   // at least 128 positions per tile: the callers size the BN partial-sum slabs for 128-row tiles
   if (R == 0 || R * p.Rw < 128 || p.M % (p.Rh * p.Rw) != 0) return 0;
@@ -371,6 +574,21 @@ int conv_halo_epi_ok(const ConvParams& p) {
 }
 
 void conv_halo_launch(const ConvParams& p, int cfg, hipStream_t st) {
+  if (p.Cg <= 32 && p.Ngemm <= 32) {
+    const int key = p.Cg * 100 + p.Ngemm;
+    switch (key) {
+      case 808: launch_narrow<8, 8>(p, st); break;
+      case 816: launch_narrow<8, 16>(p, st); break;
+      case 832: launch_narrow<8, 32>(p, st); break;
+      case 1608: launch_narrow<16, 8>(p, st); break;
+      case 1616: launch_narrow<16, 16>(p, st); break;
+      case 1632: launch_narrow<16, 32>(p, st); break;
+      case 3208: launch_narrow<32, 8>(p, st); break;
+      case 3216: launch_narrow<32, 16>(p, st); break;
+      default: launch_narrow<32, 32>(p, st); break;
+    }
+    return;
+  }
   const int R = halo_rows(p.Rh, p.Rw);
   const bool epi = p.epart != nullptr;
   if ((cfg & 1) || p.Ngemm % 128 != 0) launch_ntile<64>(p, R, epi, st);

@@ -1,7 +1,9 @@
-"""Halo-staged (1,3,3) conv kernel (csrc/kernels/conv_halo.hip) against plain PyTorch fp32 references:
+"""Halo-staged (1,3,3) conv kernels (csrc/kernels/conv_halo.hip, wide and narrow) and the box-staged weight
+gradient (csrc/kernels/wgrad_box.hip) against plain PyTorch fp32 references:
 forward with the consumer-side BN+ReLU prologue and the BN partial sums, eval forward, plain dgrad, and the
 dgrad epilogue of a conv whose input is relu(BN_a(y0)) (ReLU mask from y0 + BN_a backward partials) — at the
-slow-pathway conv_b shapes (64/128/256 channels at 56/28/14 px; R101's 64 px) and both n-tile widths."""
+slow-pathway conv_b shapes (64/128/256 channels at 56/28/14 px; R101's 64 px), both n-tile widths, and the fast
+pathway's 8/16/32-channel conv_b (narrow variant)."""
 import pytest
 import torch
 import torch.nn.functional as F
@@ -19,6 +21,9 @@ CASES = [
     (128, 1, 3, 28, 28),    # slow res3 conv_b (196-position tiles, partial MFMA block)
     (256, 2, 2, 14, 14),    # slow res4 conv_b (two 128-channel halo slices)
     (64, 1, 1, 64, 64),     # R101 256-crop res2 (128-position tiles)
+    (8, 2, 3, 56, 56),      # fast res2 conv_b (narrow variant, 784-position tiles)
+    (16, 1, 4, 28, 28),     # fast res3 conv_b (narrow, whole frames)
+    (32, 2, 2, 14, 14),     # fast res4 conv_b (narrow, 196-position tiles)
 ]
 
 
@@ -113,7 +118,8 @@ def test_halo_legality():
     assert Cm.conv_halo_legal(fwd_geometry(ConvSpec(64, 64, (1, 3, 3), (1, 2, 2), (0, 1, 1)), 2, 4, 56, 56, 64, 64), 8) == 0
     assert Cm.conv_halo_legal(fwd_geometry(ConvSpec(64, 64, (3, 1, 1), (1, 1, 1), (1, 0, 0)), 2, 4, 56, 56, 64, 64), 8) == 0
     assert Cm.conv_halo_legal(fwd_geometry(ConvSpec(512, 512, (1, 3, 3), (1, 1, 1), (0, 1, 1)), 2, 4, 7, 7, 512, 512), 8) == 0
-    assert Cm.conv_halo_legal(fwd_geometry(ConvSpec(16, 16, (1, 3, 3), (1, 1, 1), (0, 1, 1)), 2, 4, 56, 56, 16, 16), 8) == 0
+    assert Cm.conv_halo_legal(fwd_geometry(ConvSpec(24, 24, (1, 3, 3), (1, 1, 1), (0, 1, 1)), 2, 4, 56, 56, 24, 24), 8) == 0
+    assert Cm.conv_halo_legal(fwd_geometry(ConvSpec(16, 16, (1, 3, 3), (1, 1, 1), (0, 1, 1)), 2, 4, 56, 56, 16, 16), 8) == 784
 
 
 WGRAD_CASES = [(64, 1, 2, 56, 56), (128, 1, 3, 28, 28), (256, 2, 2, 14, 14), (64, 1, 1, 64, 64)]
