@@ -198,6 +198,183 @@ __global__ __launch_bounds__(WB_THREADS, 2) void wgrad_box_kernel(const WgradPar
     }
 }
 
+
+// ------------------------------------------------------------------------------------------------------------------
+// Narrow variant (fast pathway conv_b: Cin = Cout = C in {8, 16, 32}, boxes of P = R*W <= 1024 positions).  dW is tiny
+// (C x 9C), so the four waves split the box's 32-position k-steps instead of dW, each keeping the whole 9-tap block
+// in registers (9 x ceil(C/16)^2 accumulators) and writing its own slab (slab = 4 * range + wave).  Images are
+// position-major [positions][C] (16-64 B per position); the transposed reads of channels >= C (C = 8: column quads
+// 2-3 of a 16-wide block) point at a zero block, so the padded MFMA rows / columns are exact zeros.
+constexpr int WN_PMAX = 1024;
+
+__host__ __device__ inline int wb_rows_narrow(int H, int W) {
+  for (int r = H; r >= 1; --r)
+    if (H % r == 0 && r * W <= WN_PMAX) return r;
+  return 0;
+}
+
+template <int C, int AFF>
+__global__ __launch_bounds__(WB_THREADS) void wgrad_box_narrow_kernel(const WgradParams p, const int R) {
+  constexpr int NB = (C + 15) / 16;
+  constexpr int GP = C / 8;                 // 16-B groups per position
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int W = p.Wo, H = p.Ho;
+  const int PW = W + 2;
+  const int P = R * W;
+  const int PP = (P + 31) & ~31;
+  const int NPOS = (R + 2) * PW;
+  char* Aimg = smem;                                              // [PP][C] dY
+  char* Bimg = Aimg + PP * C * 2;                                 // [NPOS][C] act(x) halo
+  char* zero = Bimg + ((NPOS * C * 2 + 15) & ~15);                // 16 zero bytes (+16 pad)
+  int* bpos = reinterpret_cast<int*>(zero + 32);                  // [PP]
+  float* aff = reinterpret_cast<float*>(bpos + PP);               // [2][C]
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int split = xcd_remap(blockIdx.x, gridDim.x);
+  const int tpf = H / R;
+  const int nboxes = p.P / P;
+  const int b_begin = split * p.p_per_split, b_end = min(nboxes, b_begin + p.p_per_split);
+  for (int k = tid; k < PP; k += WB_THREADS) {
+    int v = 0;
+    if (k < P) {
+      const int h = k / W, w = k - h * W;
+      v = (h + 1) * PW + (w + 1);
+    }
+    bpos[k] = v;
+  }
+  if (tid < 2) reinterpret_cast<uint4*>(zero)[tid] = uint4{0, 0, 0, 0};
+  if constexpr (AFF != 0) {
+    for (int i = tid; i < C; i += WB_THREADS) { aff[i] = p.in_scale[i]; aff[C + i] = p.in_shift[i]; }
+  }
+  for (int idx = tid; idx < (PP - P) * GP; idx += WB_THREADS)
+    *reinterpret_cast<uint4*>(Aimg + P * C * 2 + idx * 16) = uint4{0, 0, 0, 0};
+
+  const int g = lane >> 4, q = (lane >> 2) & 3, pq = lane & 3;
+  int toff[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const int jh = t / 3, jw = t - jh * 3;
+    toff[t] = ((jh - p.ph) * PW + (jw - p.pw)) * C * 2;
+  }
+  // column quad pq of channel block cb: channels 16cb + 4pq .. +3 (>= C -> the zero block, no position stride)
+  int cofs[NB];
+  bool creal[NB];
+#pragma unroll
+  for (int cb = 0; cb < NB; ++cb) {
+    const int ch = 16 * cb + 4 * pq;
+    creal[cb] = ch < C;
+    cofs[cb] = ch * 2;
+  }
+  f32x4_t acc[9][NB][NB];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+#pragma unroll
+      for (int j = 0; j < NB; ++j) acc[t][i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int scg = tid % GP;
+  float sc[8], sh[8];
+  if constexpr (AFF != 0) {
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { sc[e] = aff[scg * 8 + e]; sh[e] = aff[C + scg * 8 + e]; }
+  }
+  constexpr int PPP = WB_THREADS / GP;
+  const int sb0 = tid / GP;
+  for (int b = b_begin; b < b_end; ++b) {
+    const int frame = b / tpf, r0 = (b - frame * tpf) * R;
+    const int fbase = frame * H * W;
+    __syncthreads();
+    {
+      const uint16_t* src = p.dy + (size_t)(fbase + r0 * W) * p.ldd + scg * 8;
+      constexpr int BATCH = 4;
+      for (int k0 = sb0; k0 < P; k0 += PPP * BATCH) {
+        uint4 v[BATCH];
+#pragma unroll
+        for (int u = 0; u < BATCH; ++u) {
+          const int k = k0 + PPP * u;
+          v[u] = k < P ? *reinterpret_cast<const uint4*>(src + (size_t)k * p.ldd) : uint4{0, 0, 0, 0};
+        }
+#pragma unroll
+        for (int u = 0; u < BATCH; ++u) {
+          const int k = k0 + PPP * u;
+          if (k < P) *reinterpret_cast<uint4*>(Aimg + k * C * 2 + scg * 16) = v[u];
+        }
+      }
+    }
+    {
+      int hh = sb0 / PW, ww = sb0 - (sb0 / PW) * PW;
+      constexpr int BATCH = 4;
+      for (int b0 = sb0; b0 < NPOS; b0 += PPP * BATCH) {
+        uint4 v[BATCH];
+        bool ok[BATCH];
+#pragma unroll
+        for (int u = 0; u < BATCH; ++u) {
+          const int h = r0 - 1 + hh, w = ww - 1;
+          ok[u] = b0 + PPP * u < NPOS && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+          v[u] = ok[u] ? *reinterpret_cast<const uint4*>(p.x + (size_t)(fbase + h * W + w) * p.ldx + scg * 8)
+                       : uint4{0, 0, 0, 0};
+          ww += PPP;
+          while (ww >= PW) { ww -= PW; ++hh; }
+        }
+#pragma unroll
+        for (int u = 0; u < BATCH; ++u) {
+          const int bb = b0 + PPP * u;
+          if (bb >= NPOS) break;
+          uint4 o = v[u];
+          if constexpr (AFF != 0) {
+            float f[8];
+            unpack8(o, f);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) f[e] = __builtin_fmaf(f[e], sc[e], sh[e]);
+            o = pack8_fast(f);
+            if constexpr (AFF == 2) o = relu_bf16x8(o);
+            if (!ok[u]) o = uint4{0, 0, 0, 0};
+          }
+          *reinterpret_cast<uint4*>(Bimg + bb * C * 2 + scg * 16) = o;
+        }
+      }
+    }
+    __syncthreads();
+    for (int kc = wid * 32; kc < PP; kc += 4 * 32) {
+      const int k0 = kc + 8 * g + q;
+      bf16x8_t af[NB];
+#pragma unroll
+      for (int cb = 0; cb < NB; ++cb) {
+        const char* a0 = creal[cb] ? Aimg + k0 * C * 2 + cofs[cb] : zero + (pq & 1) * 8;
+        const char* a1 = creal[cb] ? Aimg + (k0 + 4) * C * 2 + cofs[cb] : zero + (pq & 1) * 8;
+        af[cb] = cat8(tr_read(a0), tr_read(a1));
+      }
+      const int hb0 = bpos[k0] * C * 2, hb1 = bpos[k0 + 4] * C * 2;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+#pragma unroll
+        for (int ci = 0; ci < NB; ++ci) {
+          const char* x0 = creal[ci] ? Bimg + hb0 + toff[t] + cofs[ci] : zero + (pq & 1) * 8;
+          const char* x1 = creal[ci] ? Bimg + hb1 + toff[t] + cofs[ci] : zero + (pq & 1) * 8;
+          const bf16x8_t xf = cat8(tr_read(x0), tr_read(x1));
+#pragma unroll
+          for (int co = 0; co < NB; ++co)
+            acc[t][ci][co] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf, af[co], acc[t][ci][co], 0, 0, 0);
+        }
+      }
+    }
+  }
+  // this wave's dW into slab 4*range + wave: lane holds ci = 16*cib + 4g + r of co = 16*cob + (lane & 15)
+  float* slab = p.partial + (size_t)(split * 4 + wid) * p.Cout * p.K;
+  const int col = lane & 15;
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int ci = 0; ci < NB; ++ci)
+#pragma unroll
+      for (int co = 0; co < NB; ++co) {
+        const int n = 16 * co + col, c = 16 * ci + 4 * g;
+        if (n < C && c < C) *reinterpret_cast<f32x4_t*>(slab + (size_t)n * p.K + t * C + c) = acc[t][ci][co];
+      }
+}
+
 // Fixed-order slab reduction in two passes: pass 1 sums `per` consecutive slabs per split group (coalesced float4
 // over the [Cout][K] block), pass 2 sums the groups and writes grad[co][ci][tap] = beta*grad + scale*v.
 __global__ void wgrad_box_sum_kernel(const float* __restrict__ slab, float* __restrict__ tmp, int splits, int per,
@@ -235,14 +412,39 @@ int wgrad_box_legal(const WgradParams& p) {
   if (p.kt != 1 || p.kh != 3 || p.kw != 3 || p.st != 1 || p.sh != 1 || p.sw != 1) return 0;
   if (p.pt != 0 || p.ph != 1 || p.pw != 1) return 0;
   if (p.Ti != p.To || p.Hi != p.Ho || p.Wi != p.Wo) return 0;
-  if (p.Cin % 64 != 0 || p.Cout % 64 != 0 || p.K != 9 * p.Cin || p.dy_affine) return 0;
-  if (p.ldd % 8 != 0 || p.ldx % 8 != 0) return 0;
+  if (p.K != 9 * p.Cin || p.dy_affine || p.ldd % 8 != 0 || p.ldx % 8 != 0) return 0;
+  if (p.Cin == p.Cout && (p.Cin == 8 || p.Cin == 16 || p.Cin == 32)) {   // narrow variant
+    const int R = wb_rows_narrow(p.Ho, p.Wo);
+    return (R > 0 && p.P % (p.Ho * p.Wo) == 0) ? R : 0;
+  }
+  if (p.Cin % 64 != 0 || p.Cout % 64 != 0) return 0;
   const int R = wb_rows(p.Ho, p.Wo);
   if (R == 0 || p.P % (p.Ho * p.Wo) != 0) return 0;
   return R;
 }
 
+template <int C>
+void launch_box_narrow(const WgradParams& p, hipStream_t st) {
+  const int R = wb_rows_narrow(p.Ho, p.Wo);
+  const int W = p.Wo;
+  const int PP = (R * W + 31) & ~31;
+  const int NPOS = (R + 2) * (W + 2);
+  const size_t lds = (size_t)PP * C * 2 + ((size_t)NPOS * C * 2 + 15) / 16 * 16 + 32 + PP * 4 + 2 * C * 4;
+  const dim3 grid(p.splits), block(WB_THREADS);
+  switch (p.affine) {
+    case 0: hipLaunchKernelGGL((wgrad_box_narrow_kernel<C, 0>), grid, block, lds, st, p, R); break;
+    case 1: hipLaunchKernelGGL((wgrad_box_narrow_kernel<C, 1>), grid, block, lds, st, p, R); break;
+    default: hipLaunchKernelGGL((wgrad_box_narrow_kernel<C, 2>), grid, block, lds, st, p, R); break;
+  }
+}
+
 void wgrad_box_launch(const WgradParams& p, hipStream_t st) {
+  if (p.Cin <= 32) {   // narrow variant: p.splits box ranges, 4 slabs each
+    if (p.Cin == 8) launch_box_narrow<8>(p, st);
+    else if (p.Cin == 16) launch_box_narrow<16>(p, st);
+    else launch_box_narrow<32>(p, st);
+    return;
+  }
   const int R = wb_rows(p.Ho, p.Wo);
   const int W = p.Wo;
   const int PP = (R * W + 31) & ~31;

@@ -308,7 +308,8 @@ void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& par
   TORCH_CHECK(dy.numel() * 2 < 0xFFFFFF00ll && x.numel() * 2 < 0xFFFFFF00ll, "buffer extents must fit 32 bits");
   p.dybytes = (unsigned)(dy.numel() * 2);
   p.xbytes = (unsigned)(x.numel() * 2);
-  TORCH_CHECK(partial.numel() >= (int64_t)p.Cout * p.K * (slab ? p.splits : 1), "wgrad accumulator too small");
+  const int64_t nslab = slab ? (int64_t)p.splits * (box && p.Cin < 64 ? 4 : 1) : 1;   // narrow box: a slab per wave
+  TORCH_CHECK(partial.numel() >= (int64_t)p.Cout * p.K * nslab, "wgrad accumulator too small");
   conv_wgrad_launch(p, (int)chunk, cur_stream());
 }
 

@@ -172,7 +172,7 @@ class _ConvBN:
         s = spec or self.spec
         eng.mark(self.name + (".gram" if gram else ".wgrad"))
         K = s.taps * s.cin_pad
-        from ..ops.conv import box_wgrad_plan, wgrad_splits
+        from ..ops.conv import box_wgrad_plan, box_wgrad_slabs, wgrad_splits
         aff = 0 if xf is None else (2 if xf.relu else 1)
         sc_, sh_ = (None, None) if xf is None else (xf.scale, xf.shift)
         slab = 1 if (eng.deterministic or (eng.fold_slabs and dest is not None)) else 0
@@ -211,12 +211,12 @@ class _ConvBN:
 
         def box_run(cfg, grad, beta_):
             """box-staged kernel into its per-range slabs, then the two-pass fixed-order reduction into ``grad``"""
-            splits = geometry(cfg)[0]
-            part = eng.scratch("wgrad_box_slab", splits * s.cout * K)
+            nslab = box_wgrad_slabs(s, geometry(cfg)[0])
+            part = eng.scratch("wgrad_box_slab", nslab * s.cout * K)
             launch(cfg, part)
-            C.wgrad_box_reduce(part, eng.scratch("wgrad_box_tmp", 16 * s.cout * K), grad, splits, s.cout, s.taps,
+            C.wgrad_box_reduce(part, eng.scratch("wgrad_box_tmp", 16 * s.cout * K), grad, nslab, s.cout, s.taps,
                                s.cin_pad, s.cin, 1.0, beta_)
-            return splits
+            return nslab
 
         tkey = ("w", dy.M, dy.ld, x.ld, x.T, x.H, x.W, s.cout, K, s.chunk, aff, gram) + tuple(s.k) + tuple(s.stride)
         cfg = eng.wtune.get(tkey)

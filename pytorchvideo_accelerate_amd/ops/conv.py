@@ -262,19 +262,26 @@ BOX = 1 << 26   # wgrad launch-word bit of the box-staged (1,3,3) kernel (csrc/k
 def box_wgrad_plan(spec: "ConvSpec", P: int, dims: Tuple[int, int, int], ldd: int, ldx: int,
                    target_blocks: int = 512) -> Optional[Tuple[int, int, int]]:
     """(box ranges, boxes per range, launch word) of the box-staged weight gradient of a stride-1 'same' (1,3,3)
-    conv with 64-multiple channel counts whose output grid is ``dims``, or None.  The grid is (Cout/64)*(Cin/64)
-    channel groups x box ranges, ~``target_blocks`` workgroups (two per CU); each range writes its own slab."""
+    conv with 64-multiple channel counts (or Cin = Cout in {8, 16, 32}) whose output grid is ``dims``, or None.
+    The grid is (Cout/64)*(Cin/64) channel groups x box ranges, ~``target_blocks`` workgroups (two per CU); each
+    range writes its own slab (narrow: four, one per wave — see ``box_wgrad_slabs``)."""
     T, H, W = dims
     g = [P, spec.cout, spec.taps * spec.cin_pad, spec.cin_pad, ldd, ldx, T, H, W, T, H, W, *spec.k, *spec.stride,
          *spec.pad]
     R = int(require().wgrad_box_legal(g))
     if R <= 0 or spec.cin_pad != spec.cin:
         return None
-    groups = (spec.cout // 64) * (spec.cin // 64)
+    # wide: (Cout/64)*(Cin/64) channel groups per box range; narrow (C <= 32): one workgroup per range
+    groups = (spec.cout // 64) * (spec.cin // 64) if spec.cin >= 64 else 1
     nboxes = P // (R * W)
     splits = max(1, min(nboxes, -(-target_blocks // groups)))
     bps = -(-nboxes // splits)
     return -(-nboxes // bps), bps, BOX
+
+
+def box_wgrad_slabs(spec: "ConvSpec", splits: int) -> int:
+    """Slabs the box-staged kernel writes for ``splits`` box ranges (narrow variant: one per wave)."""
+    return splits * (4 if spec.cin < 64 else 1)
 
 
 def conv_wgrad(dy: Act, x: Act, spec: ConvSpec, grad: torch.Tensor, workspace: Optional[torch.Tensor] = None,
@@ -299,13 +306,14 @@ def conv_wgrad(dy: Act, x: Act, spec: ConvSpec, grad: torch.Tensor, workspace: O
         C = require()
         splits, bps, word = box_wgrad_plan(spec, P, (dy.T, dy.H, dy.W), dy.ld, x.ld)
         K = spec.taps * spec.cin_pad
-        slab = torch.empty(splits * spec.cout * K, device=dy.t.device, dtype=torch.float32)
+        nslab = box_wgrad_slabs(spec, splits)
+        slab = torch.empty(nslab * spec.cout * K, device=dy.t.device, dtype=torch.float32)
         tmp = torch.empty(16 * spec.cout * K, device=dy.t.device, dtype=torch.float32)
         affine = 0 if in_scale is None else (2 if in_relu else 1)
         g = [P, spec.cout, K, spec.cin_pad, dy.ld, x.ld, x.T, x.H, x.W, dy.T, dy.H, dy.W,
              *spec.k, *spec.stride, *spec.pad, splits, bps]
         C.conv_wgrad(dy.t, x.t, slab, in_scale, in_shift, affine, g, spec.chunk, 1, word)
-        C.wgrad_box_reduce(slab, tmp, grad, splits, spec.cout, spec.taps, spec.cin_pad, spec.cin, scale, beta)
+        C.wgrad_box_reduce(slab, tmp, grad, nslab, spec.cout, spec.taps, spec.cin_pad, spec.cin, scale, beta)
         return grad
     if splits_pps is None and variant >= 0 and variant & HALO and variant < 256:   # halo kernel, box option
         plan = halo_wgrad_plan(spec, P, (dy.T, dy.H, dy.W), variant & 3)

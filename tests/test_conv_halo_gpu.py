@@ -122,7 +122,8 @@ def test_halo_legality():
     assert Cm.conv_halo_legal(fwd_geometry(ConvSpec(16, 16, (1, 3, 3), (1, 1, 1), (0, 1, 1)), 2, 4, 56, 56, 16, 16), 8) == 784
 
 
-WGRAD_CASES = [(64, 1, 2, 56, 56), (128, 1, 3, 28, 28), (256, 2, 2, 14, 14), (64, 1, 1, 64, 64)]
+WGRAD_CASES = [(64, 1, 2, 56, 56), (128, 1, 3, 28, 28), (256, 2, 2, 14, 14), (64, 1, 1, 64, 64),
+               (8, 2, 3, 56, 56), (16, 1, 4, 28, 28), (32, 2, 2, 14, 14)]
 
 
 @pytest.mark.parametrize("case", WGRAD_CASES)
