@@ -12,6 +12,7 @@
 //   dy = A*dz + B*y + C            (A = g*r, B = -g*r^2*dgamma/M, C = g*r*(mean*r*dgamma - dbeta)/M)
 // and bn_bwd_apply materialises dy (bf16) for the dgrad/wgrad of the producing conv.
 #include "common.h"
+#include <algorithm>
 
 namespace {
 
@@ -66,6 +67,118 @@ __global__ void bn_finalize_kernel(const float* __restrict__ part, int tiles, in
     }
     if (c == 0 && nbt) nbt[0] += 1;
   }
+}
+
+
+// ---- two-level single-launch finalize (fwd and bwd share the reduction) -----------------------------------------
+// The one-block-per-channel kernels above read a [tiles][K][C] slab with a 4-byte stride of K*C floats per thread:
+// at 10^4-10^5 tiles that is ~100 dependent cache-line round trips per thread on C (often 8-64) workgroups.  Here
+// grid = (C/64 channel groups) x S tile ranges: 256 threads = 64 channels x 4 tile lanes read whole 256-B rows
+// (coalesced), each workgroup's double partials go to its own scratch row, and the LAST workgroup of a channel group
+// to finish (agent-scope acq_rel counter, reset to 0 for the next use) sums the S partials in a fixed order and
+// finalizes: bitwise deterministic, one launch, all CUs busy.
+constexpr int FIN_TILES_PER_BLOCK = 64;
+
+__device__ __forceinline__ bool fin_reduce_and_elect(const float* __restrict__ part, int tiles, int C, int K, int k0,
+                                                     int k1, double* __restrict__ scratch, unsigned* __restrict__ ctr,
+                                                     double* red) {
+  const int cl = threadIdx.x & 63, tl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  const int S = gridDim.y, sb = blockIdx.y;
+  const int per = (tiles + S - 1) / S;
+  const int t0 = sb * per, t1 = min(tiles, t0 + per);
+  double a = 0.0, b = 0.0;
+  if (c < C) {
+    for (int t = t0 + tl; t < t1; t += 4) {
+      a += part[((int64_t)t * K + k0) * C + c];
+      b += part[((int64_t)t * K + k1) * C + c];
+    }
+  }
+  red[threadIdx.x] = a;
+  red[NT + threadIdx.x] = b;
+  __syncthreads();
+  if (tl == 0 && c < C) {
+    a = red[cl] + red[64 + cl] + red[128 + cl] + red[192 + cl];
+    b = red[NT + cl] + red[NT + 64 + cl] + red[NT + 128 + cl] + red[NT + 192 + cl];
+    scratch[((int64_t)sb * 2) * C + c] = a;
+    scratch[((int64_t)sb * 2 + 1) * C + c] = b;
+  }
+  __syncthreads();   // every partial store of this workgroup issued and drained before the release below
+  __shared__ int last;
+  if (threadIdx.x == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(ctr + blockIdx.x, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    last = prev == (unsigned)(S - 1);
+    if (last) __hip_atomic_store(ctr + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!last) return false;
+  // the last workgroup: fixed-order sum of the S partials (tile lanes split the ranges, then a fixed 4-way sum)
+  a = 0.0; b = 0.0;
+  if (c < C) {
+    for (int r = tl; r < S; r += 4) {
+      a += __builtin_nontemporal_load(scratch + ((int64_t)r * 2) * C + c);
+      b += __builtin_nontemporal_load(scratch + ((int64_t)r * 2 + 1) * C + c);
+    }
+  }
+  red[threadIdx.x] = a;
+  red[NT + threadIdx.x] = b;
+  __syncthreads();
+  if (tl == 0) {
+    red[threadIdx.x] = red[cl] + red[64 + cl] + red[128 + cl] + red[192 + cl];
+    red[NT + threadIdx.x] = red[NT + cl] + red[NT + 64 + cl] + red[NT + 128 + cl] + red[NT + 192 + cl];
+  }
+  return true;
+}
+
+__global__ void bn_finalize2_kernel(const float* __restrict__ part, int tiles, int C, int64_t count,
+                                    const float* __restrict__ gamma, const float* __restrict__ beta,
+                                    float* __restrict__ run_mean, float* __restrict__ run_var,
+                                    int64_t* __restrict__ nbt, float momentum, float eps,
+                                    float* __restrict__ save_mean, float* __restrict__ save_rstd,
+                                    float* __restrict__ scale, float* __restrict__ shift,
+                                    double* __restrict__ scratch, unsigned* __restrict__ ctr) {
+  __shared__ double red[2 * NT];
+  if (!fin_reduce_and_elect(part, tiles, C, 2, 0, 1, scratch, ctr, red)) return;
+  const int cl = threadIdx.x;
+  const int c = blockIdx.x * 64 + cl;
+  if (cl >= 64 || c >= C) return;
+  const double mean = red[cl] / (double)count;
+  double var = red[NT + cl] / (double)count - mean * mean;
+  if (var < 0) var = 0;
+  const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+  save_mean[c] = (float)mean;
+  save_rstd[c] = rstd;
+  const float g = gamma[c], bb = beta[c];
+  scale[c] = g * rstd;
+  shift[c] = bb - (float)mean * g * rstd;
+  if (run_mean) {
+    const double unb = count > 1 ? var * (double)count / (double)(count - 1) : var;
+    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * (float)mean;
+    run_var[c] = (1.f - momentum) * run_var[c] + momentum * (float)unb;
+  }
+  if (c == 0 && nbt) nbt[0] += 1;
+}
+
+__global__ void bn_bwd_finalize2_kernel(const float* __restrict__ part, int blocks, int C, int64_t count, int which,
+                                        const float* __restrict__ gamma, const float* __restrict__ mean,
+                                        const float* __restrict__ rstd, float* __restrict__ dgamma,
+                                        float* __restrict__ dbeta, float beta_acc, float* __restrict__ coef,
+                                        double* __restrict__ scratch, unsigned* __restrict__ ctr) {
+  __shared__ double red[2 * NT];
+  if (!fin_reduce_and_elect(part, blocks, C, 3, 0, 1 + which, scratch, ctr, red)) return;
+  const int cl = threadIdx.x;
+  const int c = blockIdx.x * 64 + cl;
+  if (cl >= 64 || c >= C) return;
+  const float db = (float)red[cl], dg = (float)red[NT + cl];
+  if (dgamma) {
+    dgamma[c] = (beta_acc == 0.f ? 0.f : beta_acc * dgamma[c]) + dg;
+    dbeta[c] = (beta_acc == 0.f ? 0.f : beta_acc * dbeta[c]) + db;
+  }
+  const float gm = gamma[c], r = rstd[c], mu = mean[c];
+  const float inv = 1.f / (float)count;
+  coef[c] = gm * r;
+  coef[C + c] = -gm * r * r * dg * inv;
+  coef[2 * C + c] = gm * r * (mu * r * dg - db) * inv;
 }
 
 // eval-mode affine from running statistics
@@ -641,9 +754,17 @@ int grid_rows(int64_t M, int C) {
 
 }  // namespace
 
+// tile ranges of the two-level finalize (<= 256: the scratch holds 256 x 2 x C doubles)
+int bn_fin_ranges(int tiles) { return std::min(256, std::max(1, (tiles + FIN_TILES_PER_BLOCK - 1) / FIN_TILES_PER_BLOCK)); }
+
 void bn_finalize_launch(const float* part, int tiles, int C, int64_t count, const float* gamma, const float* beta,
                         float* rm, float* rv, int64_t* nbt, float momentum, float eps, float* smean, float* srstd,
-                        float* scale, float* shift, hipStream_t s) {
+                        float* scale, float* shift, hipStream_t s, double* scratch, unsigned* ctr) {
+  if (scratch && ctr) {
+    hipLaunchKernelGGL(bn_finalize2_kernel, dim3((C + 63) / 64, bn_fin_ranges(tiles)), dim3(NT), 0, s, part, tiles, C,
+                       count, gamma, beta, rm, rv, nbt, momentum, eps, smean, srstd, scale, shift, scratch, ctr);
+    return;
+  }
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(NT), 0, s, part, tiles, C, count, gamma, beta, rm, rv, nbt,
                      momentum, eps, smean, srstd, scale, shift);
 }
@@ -714,7 +835,12 @@ void bn_bwd_reduce_launch(const uint16_t* g, int ldg, int mask_mode, const void*
 
 void bn_bwd_finalize_launch(const float* part, int blocks, int C, int64_t count, int which, const float* gamma,
                             const float* mean, const float* rstd, float* dgamma, float* dbeta, float beta_acc,
-                            float* coef, hipStream_t s) {
+                            float* coef, hipStream_t s, double* scratch, unsigned* ctr) {
+  if (scratch && ctr) {
+    hipLaunchKernelGGL(bn_bwd_finalize2_kernel, dim3((C + 63) / 64, bn_fin_ranges(blocks)), dim3(NT), 0, s, part,
+                       blocks, C, count, which, gamma, mean, rstd, dgamma, dbeta, beta_acc, coef, scratch, ctr);
+    return;
+  }
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(NT), 0, s, part, blocks, C, count, which, gamma, mean, rstd,
                      dgamma, dbeta, beta_acc, coef);
 }

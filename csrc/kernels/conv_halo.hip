@@ -16,7 +16,7 @@
 //     at unit (g*NPOSP + p) mod 16 with NPOSP = 0 mod 16) with no XOR swizzle, and every tap of a fragment is
 //     the same per-lane address plus a wave-uniform offset (dh*(W+2) + dw)*16;
 //   * the weight fragments are read straight from global memory into registers (16 B per lane, L2-resident,
-//     prefetched two k-steps ahead), so the k loop has no barrier at all;
+//     prefetched 2 (128-channel tiles) or 5 (64-channel tiles) k-steps ahead), so the k loop has no barrier at all;
 //   * 4 waves = 2 position halves x 2 channel halves, each wave up to 7 x (NTILE/32) 16x16 accumulators;
 //     v_mfma_f32_16x16x32_bf16 with swapped operands (D = W X^T) so each lane holds 4 consecutive channels of
 //     one position (8-B stores, 16-lane shuffles for the channel sums), exactly like conv_igemm.hip;
@@ -33,7 +33,9 @@ namespace {
 constexpr int HC_THREADS = 256;
 constexpr int HC_MW = 7;        // 16-position blocks per wave (two position halves of <= 112)
 constexpr int HC_PMAX = 2 * HC_MW * 16;
-constexpr int HC_RING = 3;      // weight-fragment ring depth (k-steps in flight)
+// weight-fragment ring depth (k-steps in flight): a 64-channel tile's k-step is only 14 MFMAs per wave, so it keeps
+// five steps of L2 latency in flight; a 128-channel tile's 28-MFMA steps need two
+__host__ __device__ constexpr int hc_ring(int ntile) { return ntile == 64 ? 6 : 3; }
 
 // rows per tile: the largest divisor R of H with R*W <= 224 (every tile is whole rows of one frame)
 __host__ __device__ inline int halo_rows(int H, int W) {
@@ -47,6 +49,7 @@ __host__ __device__ inline int halo_ck(int Cg) { return Cg <= 128 ? Cg : 128; }
 template <int NTILE, int EPI, int AFF>
 __global__ __launch_bounds__(HC_THREADS, 2) void conv_halo_kernel(const ConvParams p, const int R) {
   constexpr int NWB = NTILE / 32;   // 16-channel blocks per wave
+  constexpr int HC_RING = hc_ring(NTILE);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid & 1, wn = wid >> 1;
@@ -130,8 +133,8 @@ __global__ __launch_bounds__(HC_THREADS, 2) void conv_halo_kernel(const ConvPara
     for (int j = 0; j < NWB; ++j)
       dst[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wr, bvo[j], so, 0));
   };
-  bload(0, bq[0]);
-  bload(1, bq[1]);
+#pragma unroll
+  for (int u = 0; u < HC_RING - 1; ++u) bload(u, bq[u]);
 
   // ---- halo staging: thread -> (channel group cg, 8 consecutive box positions per pass-row)
   const int cg = (tid >> 3) % G8;
@@ -187,12 +190,12 @@ __global__ __launch_bounds__(HC_THREADS, 2) void conv_halo_kernel(const ConvPara
     stage(c);
     __syncthreads();
     const int send = s + 9 * ksl;
-    // three k-steps per iteration: the weight ring slot of each is compile-time
+    // HC_RING k-steps per iteration: the weight ring slot of each is compile-time
     for (; s < send; s += HC_RING) {
 #pragma unroll
       for (int u = 0; u < HC_RING; ++u) {
         const int ss = s + u;
-        bload(ss + 2, bq[(u + 2) % HC_RING]);
+        bload(ss + HC_RING - 1, bq[(u + HC_RING - 1) % HC_RING]);
         const int ao = step_a(ss);
         bf16x8_t af[HC_MW];
 #pragma unroll

@@ -37,7 +37,8 @@ void wgrad_reduce_launch(float* accbuf, float* grad, int splits, int Cout, int t
                          float scale, float beta, int slab, hipStream_t stream);
 void bn_finalize_launch(const float* part, int tiles, int C, int64_t count, const float* gamma, const float* beta,
                         float* rm, float* rv, int64_t* nbt, float momentum, float eps, float* smean, float* srstd,
-                        float* scale, float* shift, hipStream_t s);
+                        float* scale, float* shift, hipStream_t s, double* scratch, unsigned* ctr);
+int bn_fin_ranges(int tiles);
 void bn_eval_affine_launch(int C, const float* gamma, const float* beta, const float* rm, const float* rv, float eps,
                            float* scale, float* shift, hipStream_t s);
 void bn_act_launch(const uint16_t* y, int ldy, uint16_t* out, int ldo, const float* scale, const float* shift,
@@ -52,7 +53,7 @@ void bn_bwd_reduce_launch(const uint16_t* g, int ldg, int mask_mode, const void*
                           int rows_per_block, float* part, uint16_t* dzout, int lddz, hipStream_t s);
 void bn_bwd_finalize_launch(const float* part, int blocks, int C, int64_t count, int which, const float* gamma,
                             const float* mean, const float* rstd, float* dgamma, float* dbeta, float beta_acc,
-                            float* coef, hipStream_t s);
+                            float* coef, hipStream_t s, double* scratch, unsigned* ctr);
 void bn_bwd_apply_launch(const uint16_t* g, int ldg, int mask_mode, const void* mo, int ldm, const float* ms,
                          const float* mh, const uint16_t* y0, const float* coef0, uint16_t* dy0, const uint16_t* y1,
                          const float* coef1, uint16_t* dy1, uint16_t* dzout, int lddz, int dz_accum, int64_t M, int C,
@@ -330,12 +331,27 @@ void wgrad_reduce(const at::Tensor& partial, const at::Tensor& grad, int64_t spl
                       (float)scale, (float)beta, (int)slab, cur_stream());
 }
 
+// Two-level finalize workspace (bn_eltwise.hip): one float64 tensor = [256][2][C] partial doubles followed by
+// ceil(C/64) zero-initialised uint32 counters (kept zero by the kernels).  Absent: the single-level kernels.
+inline int64_t fin_doubles(int64_t C) { return 256 * 2 * C + (C + 63) / 64; }
+static void fin_buffers(const OptT& fin, int64_t C, double** scr, unsigned** ctr) {
+  if (!fin.has_value()) return;
+  TORCH_CHECK(fin->scalar_type() == at::kDouble && fin->is_cuda() && fin->numel() >= fin_doubles(C),
+              "finalize workspace: float64 [256*2*C + C/64] on the GPU");
+  *scr = fin->data_ptr<double>();
+  *ctr = reinterpret_cast<unsigned*>(*scr + 256 * 2 * C);
+}
+
 void bn_finalize(const at::Tensor& part, int64_t tiles, int64_t C, int64_t count, const at::Tensor& gamma,
                  const at::Tensor& beta, const OptT& rm, const OptT& rv, const OptT& nbt, double momentum, double eps,
-                 const at::Tensor& smean, const at::Tensor& srstd, const at::Tensor& scale, const at::Tensor& shift) {
+                 const at::Tensor& smean, const at::Tensor& srstd, const at::Tensor& scale, const at::Tensor& shift,
+                 const OptT& fin) {
   int64_t* nb = nbt.has_value() ? nbt->data_ptr<int64_t>() : nullptr;
+  double* scr = nullptr;
+  unsigned* ctr = nullptr;
+  fin_buffers(fin, C, &scr, &ctr);
   bn_finalize_launch(f32(part), (int)tiles, (int)C, count, f32(gamma), f32(beta), f32o(rm), f32o(rv), nb,
-                     (float)momentum, (float)eps, f32(smean), f32(srstd), f32(scale), f32(shift), cur_stream());
+                     (float)momentum, (float)eps, f32(smean), f32(srstd), f32(scale), f32(shift), cur_stream(), scr, ctr);
 }
 
 void bn_eval_affine(const at::Tensor& gamma, const at::Tensor& beta, const at::Tensor& rm, const at::Tensor& rv,
@@ -392,9 +408,12 @@ void bn_bwd_reduce(const at::Tensor& g, int64_t ldg, int64_t mask_mode, const Op
 
 void bn_bwd_finalize(const at::Tensor& part, int64_t blocks, int64_t C, int64_t count, int64_t which,
                      const at::Tensor& gamma, const at::Tensor& mean, const at::Tensor& rstd, const OptT& dgamma,
-                     const OptT& dbeta, double beta_acc, const at::Tensor& coef) {
+                     const OptT& dbeta, double beta_acc, const at::Tensor& coef, const OptT& fin) {
+  double* scr = nullptr;
+  unsigned* ctr = nullptr;
+  fin_buffers(fin, C, &scr, &ctr);
   bn_bwd_finalize_launch(f32(part), (int)blocks, (int)C, count, (int)which, f32(gamma), f32(mean), f32(rstd),
-                         f32o(dgamma), f32o(dbeta), (float)beta_acc, f32(coef), cur_stream());
+                         f32o(dgamma), f32o(dbeta), (float)beta_acc, f32(coef), cur_stream(), scr, ctr);
 }
 
 // y0/coef0/dy0 optional (all or none): without them only dy1 and/or dz (dzout) are produced
@@ -689,7 +708,11 @@ PYBIND11_MODULE(_C, m) {
         py::arg("variant") = -1, py::arg("dy_affine") = 0, py::arg("colsum") = py::none());
   m.def("wgrad_reduce", &wgrad_reduce, py::arg("partial"), py::arg("grad"), py::arg("splits"), py::arg("Cout"),
         py::arg("taps"), py::arg("Cin"), py::arg("Cin_real"), py::arg("scale"), py::arg("beta"), py::arg("slab") = 0);
-  m.def("bn_finalize", &bn_finalize);
+  m.def("bn_finalize", &bn_finalize, py::arg("part"), py::arg("tiles"), py::arg("C"), py::arg("count"),
+        py::arg("gamma"), py::arg("beta"), py::arg("rm"), py::arg("rv"), py::arg("nbt"), py::arg("momentum"),
+        py::arg("eps"), py::arg("smean"), py::arg("srstd"), py::arg("scale"), py::arg("shift"),
+        py::arg("fin") = py::none());
+  m.def("fin_doubles", [](int64_t C) { return fin_doubles(C); });
   m.def("bn_eval_affine", &bn_eval_affine);
   m.def("bn_act", &bn_act);
   m.def("res_out", &res_out);
@@ -698,7 +721,9 @@ PYBIND11_MODULE(_C, m) {
         py::arg("ldm"), py::arg("ms"), py::arg("mh"), py::arg("y0"), py::arg("mean0"), py::arg("rstd0"), py::arg("y1"),
         py::arg("mean1"), py::arg("rstd1"), py::arg("M"), py::arg("C"), py::arg("blocks"), py::arg("rpb"),
         py::arg("part"), py::arg("dzout") = py::none(), py::arg("lddz") = 0);
-  m.def("bn_bwd_finalize", &bn_bwd_finalize);
+  m.def("bn_bwd_finalize", &bn_bwd_finalize, py::arg("part"), py::arg("blocks"), py::arg("C"), py::arg("count"),
+        py::arg("which"), py::arg("gamma"), py::arg("mean"), py::arg("rstd"), py::arg("dgamma"), py::arg("dbeta"),
+        py::arg("beta_acc"), py::arg("coef"), py::arg("fin") = py::none());
   m.def("bn_bwd_apply", &bn_bwd_apply);
   m.def("stem_pool_fwd", &stem_pool_fwd, py::arg("y"), py::arg("scale"), py::arg("shift"), py::arg("out"),
         py::arg("ldo"), py::arg("arg"), py::arg("NT"), py::arg("H"), py::arg("W"), py::arg("Ho"), py::arg("Wo"),

@@ -115,6 +115,8 @@ class _ConvBN:
         self.scale = torch.ones(C, device=dev)
         self.shift = torch.zeros(C, device=dev)
         self.coef = torch.zeros(4 * C, device=dev)   # BN-backward coefficients (+ mean(dz) for BN folding)
+        # two-level finalize workspace (partial doubles + zeroed counters, kept zero by the kernels); one per unit
+        self.fin = torch.zeros(eng.C.fin_doubles(C), device=dev, dtype=torch.float64) if dev.type == "cuda" else None
         self._geo = {}
         self.wf = None  # bf16 forward pack view [Cout, taps*Cin_pad]
         self.wd = None  # bf16 dgrad pack view [Cin, taps*Cout]
@@ -155,7 +157,7 @@ class _ConvBN:
             tiles = (M + tuner.bm(cfg, s.cout) - 1) // tuner.bm(cfg, s.cout)
             C.bn_finalize(stats, tiles, s.cout, M, bn.weight, bn.bias, bn.running_mean, bn.running_var,
                           bn.num_batches_tracked, bn.momentum if bn.momentum is not None else 0.1, bn.eps,
-                          self.mean, self.rstd, self.scale, self.shift)
+                          self.mean, self.rstd, self.scale, self.shift, self.fin)
         else:
             C.bn_eval_affine(bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, self.scale, self.shift)
         return Act(y, x.N, To, Ho, Wo)
@@ -361,7 +363,7 @@ class _ConvBN:
             tiles = (yb.M + tuner.bm(cfg, Co) - 1) // tuner.bm(cfg, Co)
             C.bn_finalize(stats, tiles, Co, yb.M, bn.weight, bn.bias, bn.running_mean, bn.running_var,
                           bn.num_batches_tracked, bn.momentum if bn.momentum is not None else 0.1, bn.eps,
-                          self.mean, self.rstd, self.scale, self.shift)
+                          self.mean, self.rstd, self.scale, self.shift, self.fin)
 
     def fold_output(self, yb: Act, bxf: _Xf, out: torch.Tensor, res: Act, rxf: Optional[_Xf],
                     mask: torch.Tensor, tag: str) -> Act:
@@ -510,10 +512,11 @@ class _ConvBN:
                             None if other is None else other.rstd, M, Cc, blocks, rpb, part)
         fg = eng.flat
         C.bn_bwd_finalize(part, blocks, Cc, M, 0, self.bn.weight, self.mean, self.rstd,
-                          fg.gview(self.bn.weight), fg.gview(self.bn.bias), eng.grad_beta, self.coef)
+                          fg.gview(self.bn.weight), fg.gview(self.bn.bias), eng.grad_beta, self.coef, self.fin)
         if other is not None:
             C.bn_bwd_finalize(part, blocks, Cc, M, 1, other.bn.weight, other.mean, other.rstd,
-                              fg.gview(other.bn.weight), fg.gview(other.bn.bias), eng.grad_beta, other.coef)
+                              fg.gview(other.bn.weight), fg.gview(other.bn.bias), eng.grad_beta, other.coef,
+                              other.fin)
         dy = eng.ws((self.name, "dy"), (M, Cc), torch.bfloat16)
         dy1 = eng.ws((other.name, "dy"), (M, Cc), torch.bfloat16) if other is not None else None
         eng.mark(self.name + ".bnapply")
@@ -582,7 +585,7 @@ class _Stem:
         if train:
             C.bn_finalize(stats, tiles, u.C, M, bn.weight, bn.bias, bn.running_mean, bn.running_var,
                           bn.num_batches_tracked, bn.momentum if bn.momentum is not None else 0.1, bn.eps,
-                          u.mean, u.rstd, u.scale, u.shift)
+                          u.mean, u.rstd, u.scale, u.shift, u.fin)
         else:
             C.bn_eval_affine(bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, u.scale, u.shift)
         return Act(y, x.N, x.T, x.H, x.W)
@@ -616,7 +619,7 @@ class _Stem:
                         P, u.C, blocks, rpb, part)
         fg = eng.flat
         C.bn_bwd_finalize(part, blocks, u.C, y.M, 0, u.bn.weight, u.mean, u.rstd, fg.gview(u.bn.weight),
-                          fg.gview(u.bn.bias), eng.grad_beta, u.coef)
+                          fg.gview(u.bn.bias), eng.grad_beta, u.coef, u.fin)
         dyt = eng.ws((u.name, "dy"), (y.M, u.C), torch.bfloat16)
         eng.mark(self.name + ".poolbwd")
         C.stem_pool_bn_apply(dout.t, dout.ld, self.arg, y.t, u.scale, u.shift, u.coef, dyt, y.N * y.T, y.H, y.W,
@@ -764,7 +767,7 @@ class _ResBlock:
         if one is not None:
             # branch1 BN backward from the same sums: dy1 = A1 dz + B1 y1 + C1 (and dz itself when not yet stored)
             C.bn_bwd_finalize(part, tiles, Cc, M, 1, one.bn.weight, one.mean, one.rstd, fg.gview(one.bn.weight),
-                              fg.gview(one.bn.bias), eng.grad_beta, one.coef)
+                              fg.gview(one.bn.bias), eng.grad_beta, one.coef, one.fin)
             eng.mark(one.name + ".bnapply")
             if pre is not None:
                 C.bn_bwd_apply(dz.t, dz.ld, 0, None, 0, None, None, None, None, None, y1.t, one.coef, dy1, None, 0,

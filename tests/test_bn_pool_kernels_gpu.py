@@ -212,3 +212,42 @@ def test_stem_pool_bn_backward_fused(C, H, W):
     assert _rel(dbeta.cpu(), br.grad) < 1e-4
     assert _rel(dgamma.cpu(), gr.grad) < 1e-3
     assert _rel(dy.cpu(), yr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("C,tiles", [(8, 20480), (64, 17920), (256, 1280), (2048, 490), (24, 3)])
+def test_two_level_finalize_matches_single_level(C, tiles):
+    """The coalesced two-level finalize (fin workspace: partial doubles + self-resetting counters) against the
+    one-block-per-channel kernels, forward and backward, repeated (the counters return to zero) at the tile counts
+    of the B=160 step (halo 784/224-position tiles, 128-row tiles, few tiles)."""
+    K = _C()
+    g = torch.Generator().manual_seed(C + tiles)
+    part2 = (torch.randn(tiles, 2, C, generator=g) + 0.5).abs().to(DEV)
+    part3 = torch.randn(tiles, 3, C, generator=g).to(DEV)
+    count = tiles * 100
+    gamma, beta = (torch.rand(C, generator=g) + 0.5).to(DEV), torch.randn(C, generator=g).to(DEV)
+    fin = torch.zeros(K.fin_doubles(C), dtype=torch.float64, device=DEV)
+    ref = [torch.empty(C, device=DEV) for _ in range(4)]
+    K.bn_finalize(part2, tiles, C, count, gamma, beta, None, None, None, 0.1, 1e-5, *ref)
+    rm_a, rv_a = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    rm_b, rv_b = rm_a.clone(), rv_a.clone()
+    K.bn_finalize(part2, tiles, C, count, gamma, beta, rm_a, rv_a, None, 0.1, 1e-5, *[torch.empty(C, device=DEV) for _ in range(4)])
+    for rep in range(3):
+        out = [torch.full((C,), float("nan"), device=DEV) for _ in range(4)]
+        K.bn_finalize(part2, tiles, C, count, gamma, beta, None, None, None, 0.1, 1e-5, *out, fin)
+        for a, b in zip(out, ref):
+            torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-7)
+    K.bn_finalize(part2, tiles, C, count, gamma, beta, rm_b, rv_b, None, 0.1, 1e-5, *[torch.empty(C, device=DEV) for _ in range(4)], fin)
+    torch.testing.assert_close(rm_b, rm_a, rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(rv_b, rv_a, rtol=1e-6, atol=1e-7)
+    mean, rstd = torch.randn(C, device=DEV), torch.rand(C, device=DEV) + 0.5
+    for which in (0, 1):
+        cr, dgr, dbr = torch.empty(3 * C, device=DEV), torch.ones(C, device=DEV), torch.ones(C, device=DEV)
+        K.bn_bwd_finalize(part3, tiles, C, count, which, gamma, mean, rstd, dgr, dbr, 0.5, cr)
+        for rep in range(2):
+            c2, dg2, db2 = torch.empty(3 * C, device=DEV), torch.ones(C, device=DEV), torch.ones(C, device=DEV)
+            K.bn_bwd_finalize(part3, tiles, C, count, which, gamma, mean, rstd, dg2, db2, 0.5, c2, fin)
+            torch.testing.assert_close(c2, cr, rtol=1e-5, atol=1e-7)
+            torch.testing.assert_close(dg2, dgr, rtol=1e-5, atol=1e-6)
+            torch.testing.assert_close(db2, dbr, rtol=1e-5, atol=1e-6)
+    ctr = fin[256 * 2 * C:].view(torch.int32)[: (C + 63) // 64]
+    assert torch.all(ctr == 0), ctr   # every counter reset by its last workgroup
