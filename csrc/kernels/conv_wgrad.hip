@@ -14,6 +14,7 @@
 // the fp32 master-gradient buffer, and re-zeroes the accumulator.
 #include "common.h"
 #include "conv_params.h"
+#include "wgrad_rt_impl.h"
 #include <type_traits>
 
 namespace {
@@ -662,7 +663,28 @@ void wgrad_halo_launch(const WgradParams& p, hipStream_t s);
 
 void wgrad_box_launch(const WgradParams& p, hipStream_t st);
 
+// row-table kernel (wgrad_rt_impl.h): 16-B chunks on both operands, tiles 2-7, no Gram mode
+int wgrad_rt_legal(int Cout, int Cin, int ldd, int ldx, int chunk, int dy_affine) {
+  return (chunk == 8 && Cin % 8 == 0 && Cout % 8 == 0 && ldd % 8 == 0 && ldx % 8 == 0 && !dy_affine) ? 1 : 0;
+}
+
+void wgrad_rt_run_a0(int v, bool bp64, bool check, const wgrad_rt::RtParams& rp, hipStream_t st);
+void wgrad_rt_run_a1(int v, bool bp64, bool check, const wgrad_rt::RtParams& rp, hipStream_t st);
+
 void conv_wgrad_launch(const WgradParams& p, int chunk, hipStream_t stream) {
+  if (p.variant >= 0 && (p.variant & (1 << 25))) {   // row-table kernel; legality checked by the binding
+    wgrad_rt::RtParams rp;
+    rp.p = p;
+    wgrad_rt::magic_div(p.Wo, &rp.mWo, &rp.sWo1, &rp.sWo2);
+    wgrad_rt::magic_div(p.Ho, &rp.mHo, &rp.sHo1, &rp.sHo2);
+    wgrad_rt::magic_div(p.To, &rp.mTo, &rp.sTo1, &rp.sTo2);
+    const int v = wgrad_tile_index(p.variant);
+    const bool bp64 = p.variant & 4;
+    const bool check = p.pt | p.ph | p.pw;
+    if (p.affine) wgrad_rt_run_a1(v < 2 ? 2 : v, bp64, check, rp, stream);
+    else wgrad_rt_run_a0(v < 2 ? 2 : v, bp64, check, rp, stream);
+    return;
+  }
   if (p.variant >= 0 && (p.variant & (1 << 26))) {   // box-staged (1,3,3) kernel (wgrad_box.hip): per-split slabs
     wgrad_box_launch(p, stream);
     return;

@@ -28,6 +28,7 @@ int conv_igemm_m_tiles_k(int M, int N, int K, int Cg);
 void conv_igemm_set_bk(int bk);
 void conv_wgrad_launch(const WgradParams& p, int chunk, hipStream_t stream);
 void conv_wgrad_tile(int Cout, int K, int variant, int* bmw, int* bnw);
+int wgrad_rt_legal(int Cout, int Cin, int ldd, int ldx, int chunk, int dy_affine);
 int wgrad_narrow_legal(int Cout, int Cin, int K);
 int wgrad_halo_legal(const WgradParams& p);
 int wgrad_box_legal(const WgradParams& p);
@@ -301,6 +302,10 @@ void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& par
     TORCH_CHECK(!dy_affine || (p.Cout == p.Cin && p.K == p.Cin), "narrow Gram: square 1x1");
   }
   TORCH_CHECK(!halo || (wgrad_halo_legal(p) && chunk == 8 && p.p_per_split > 0), "halo wgrad not legal here");
+  if (!box && variant >= 0 && (variant & (1 << 25)))
+    TORCH_CHECK(wgrad_rt_legal(p.Cout, p.Cin, p.ldd, p.ldx, (int)chunk, (int)dy_affine) && p.p_per_split > 0 &&
+                    (int64_t)p.splits * p.p_per_split >= p.P,
+                "row-table wgrad not legal here");
   if (box) {
     TORCH_CHECK(wgrad_box_legal(p) && chunk == 8 && slab, "box wgrad not legal here (needs slab mode)");
     const int64_t boxes = p.P / (p.Wo * (int64_t)wgrad_box_legal(p));
@@ -699,6 +704,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_m_tiles", &conv_m_tiles, py::arg("M"), py::arg("N"), py::arg("K") = 0, py::arg("Cg") = 0);
   m.def("conv_set_bk", [](int64_t bk) { conv_igemm_set_bk((int)bk); });
   m.def("conv_set_ut", [](int64_t mode) { conv_igemm_set_ut((int)mode); });
+  m.def("wgrad_rt_legal", [](int64_t Cout, int64_t Cin, int64_t ldd, int64_t ldx, int64_t chunk) {
+    return wgrad_rt_legal((int)Cout, (int)Cin, (int)ldd, (int)ldx, (int)chunk, 0) != 0;
+  });
   m.def("wgrad_tile", &wgrad_tile, py::arg("Cout"), py::arg("K"), py::arg("variant") = -1);
   m.def("wgrad_narrow_legal", [](int64_t Cout, int64_t Cin, int64_t K) {
     return (bool)wgrad_narrow_legal((int)Cout, (int)Cin, (int)K);

@@ -174,7 +174,7 @@ class _ConvBN:
         s = spec or self.spec
         eng.mark(self.name + (".gram" if gram else ".wgrad"))
         K = s.taps * s.cin_pad
-        from ..ops.conv import box_wgrad_plan, box_wgrad_slabs, wgrad_splits
+        from ..ops.conv import RT, box_wgrad_plan, box_wgrad_slabs, wgrad_splits
         aff = 0 if xf is None else (2 if xf.relu else 1)
         sc_, sh_ = (None, None) if xf is None else (xf.scale, xf.shift)
         slab = 1 if (eng.deterministic or (eng.fold_slabs and dest is not None)) else 0
@@ -189,6 +189,11 @@ class _ConvBN:
                     sp = wgrad_splits(dy.M, s.cout, K, target_blocks=256 if slab else 1024) + (-1,)
                 elif cfg & 1024:  # box-staged (1,3,3) kernel (wgrad_box.hip): own slabs, fixed-order reduction
                     sp = box_wgrad_plan(s, dy.M, (dy.T, dy.H, dy.W), dy.ld, x.ld)
+                elif cfg & 2048:  # row-table kernel (wgrad_rt_impl.h): tile / split-K / stage bits as below
+                    v = (cfg & 3) | (8 if cfg & 64 else 0)
+                    tb = (512, 1024, 2048, 4096)[(cfg >> 2) & 3]
+                    sp = wgrad_splits(dy.M, s.cout, K, target_blocks=tb, variant=v) + (
+                        v | (4 if cfg & 32 else 0) | RT,)
                 elif cfg & 256:   # halo-staged kernel (wgrad_halo.hip): bit 9 = box option
                     from ..ops.conv import halo_wgrad_plan
                     sp = halo_wgrad_plan(s, dy.M, (dy.T, dy.H, dy.W), (cfg >> 9) & 1)
@@ -240,6 +245,16 @@ class _ConvBN:
                         if gram and geometry(c)[0] > 4096:
                             continue
                         cands.append(c)
+                dense = s.taps == 1 and tuple(s.stride) == (1, 1, 1)
+                if not gram and not dense and C.wgrad_rt_legal(s.cout, s.cin_pad, dy.ld, x.ld, s.chunk):
+                    # row-table kernel for gathered shapes: tiles 2-7, both stage depths, 512-2048 blocks
+                    for v in range(2, 8):
+                        vw = (v & 3) | (8 if v >= 4 else 0)
+                        bmw, bnw = C.wgrad_tile(s.cout, K, vw)
+                        if bmw > max(64, 2 * s.cout) or (v >= 4 and bnw > 2 * K):
+                            continue
+                        for tbi, bp in ((t, b) for t in range(3) for b in (0, 32)):
+                            cands.append(16 | 2048 | (v & 3) | (64 if v >= 4 else 0) | (tbi << 2) | bp)
                 if C.wgrad_narrow_legal(s.cout, s.cin_pad, K) and s.chunk == 8:
                     cands += [c for c in (16 | 128 | (tbi << 2) for tbi in range(4))
                               if not (gram and geometry(c)[0] > 4096)]   # colsum slab holds 4096 splits

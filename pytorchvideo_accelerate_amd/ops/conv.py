@@ -256,6 +256,7 @@ def halo_wgrad_plan(spec: "ConvSpec", P: int, dims: Tuple[int, int, int], option
     return splits, bps, HALO | (BH << 8) | (BT << 12) | (wpl << 15) | (ktb << 17)
 
 
+RT = 1 << 25    # wgrad launch-word bit of the row-table kernel for gathered shapes (csrc/kernels/wgrad_rt_impl.h)
 BOX = 1 << 26   # wgrad launch-word bit of the box-staged (1,3,3) kernel (csrc/kernels/wgrad_box.hip)
 
 

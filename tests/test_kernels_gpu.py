@@ -290,6 +290,40 @@ def test_conv_wgrad_narrow(case, affine):
     assert rel_err(grad, w.grad) < 1.5e-2
 
 
+RT_CASES = [CASES[1], CASES[2], CASES[3], CASES[4], CASES[5], CASES[6], CASES[8],
+            (64, 128, (3, 1, 1), (1, 1, 1), (1, 0, 0), (3, 5, 7, 9)),      # odd dims: positions past P
+            (32, 64, (1, 3, 3), (1, 1, 1), (0, 1, 1), (2, 3, 5, 11))]
+
+
+@pytest.mark.parametrize("tile", [2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("bp64", [False, True])
+@pytest.mark.parametrize("affine", [False, True])
+@pytest.mark.parametrize("case", RT_CASES)
+def test_conv_wgrad_rowtable(case, tile, bp64, affine):
+    """Row-table weight-gradient kernel (wgrad_rt_impl.h): every tile x stage depth, padding / strides / odd
+    sizes, BN(+ReLU) recompute of X on load, and split-K with several (uneven) position splits."""
+    from pytorchvideo_accelerate_amd.ops.conv import RT, wgrad_splits
+    x, w, spec = _mk(case, seed=31)
+    C = spec.cin
+    sc = torch.rand(C, device=DEV) + 0.5
+    sh = torch.randn(C, device=DEV) * 0.5
+    xt = torch.relu(x * sc.view(1, C, 1, 1, 1) + sh.view(1, C, 1, 1, 1)) if affine else x
+    xt = xt.to(torch.bfloat16).float()
+    w.requires_grad_(True)
+    ref_y = torch.nn.functional.conv3d(xt, w, None, spec.stride, spec.pad)
+    gy = torch.randn_like(ref_y).to(torch.bfloat16).float()
+    ref_y.backward(gy)
+    dy = Act.from_ncthw(gy)
+    v = (tile & 3) | (8 if tile >= 4 else 0)
+    K = spec.taps * spec.cin_pad
+    for tb in (64, 1024):   # one split, then many
+        sp = wgrad_splits(dy.M, spec.cout, K, target_blocks=tb, min_rows=64, variant=v)
+        grad = torch.zeros_like(w)
+        conv_wgrad(dy, Act.from_ncthw(x), spec, grad, in_scale=sc if affine else None,
+                   in_shift=sh if affine else None, splits_pps=sp, variant=RT | v | (4 if bp64 else 0))
+        assert rel_err(grad, w.grad) < 1.5e-2, (tb, sp)
+
+
 def test_conv_wgrad_affine():
     case = CASES[2]
     x, w, spec = _mk(case, seed=4)
