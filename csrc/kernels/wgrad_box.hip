@@ -68,7 +68,9 @@ __global__ __launch_bounds__(WB_THREADS, 2) void wgrad_box_kernel(const WgradPar
   const int b_begin = split * p.p_per_split, b_end = min(nboxes, b_begin + p.p_per_split);
 
   for (int k = tid; k < PP; k += WB_THREADS) {
-    int v = 0;
+    // MFMA pad positions (k >= P, dY rows of zeros) point at the first interior halo position, so that every tap
+    // offset of theirs stays inside the halo image: reading outside it (uninitialised LDS) could give 0 * NaN
+    int v = PW + 1;
     if (k < P) {
       const int h = k / W, w = k - h * W;
       v = (h + 1) * PW + (w + 1);
@@ -235,7 +237,9 @@ __global__ __launch_bounds__(WB_THREADS) void wgrad_box_narrow_kernel(const Wgra
   const int nboxes = p.P / P;
   const int b_begin = split * p.p_per_split, b_end = min(nboxes, b_begin + p.p_per_split);
   for (int k = tid; k < PP; k += WB_THREADS) {
-    int v = 0;
+    // MFMA pad positions (k >= P, dY rows of zeros) point at the first interior halo position, so that every tap
+    // offset of theirs stays inside the halo image: reading outside it (uninitialised LDS) could give 0 * NaN
+    int v = PW + 1;
     if (k < P) {
       const int h = k / W, w = k - h * W;
       v = (h + 1) * PW + (w + 1);

@@ -51,6 +51,32 @@ def main():
     print(f"\n# top {a.top} kernel instantiations (ms/step, launches/step)")
     for k, (t, n) in sorted(per.items(), key=lambda kv: -kv[1][0])[:a.top]:
         print(f"{t / a.steps:9.3f}  {n // a.steps:4d}  {k[:120]}")
+    timeline(sel, a.steps)
+
+
+def timeline(sel, steps):
+    """Union of the kernel intervals: GPU-idle time (no kernel running) and time at each concurrency level."""
+    ev = []
+    for r in sel:
+        ev.append((int(r["Start_Timestamp"]), 1))
+        ev.append((int(r["End_Timestamp"]), -1))
+    ev.sort()
+    level, last = 0, ev[0][0]
+    at = collections.defaultdict(int)
+    gaps = []
+    for t, d in ev:
+        if t > last:
+            at[level] += t - last
+            if level == 0:
+                gaps.append(t - last)
+        level += d
+        last = t
+    tot = sum(at.values())
+    print(f"\n# timeline (ms/step): span {tot / 1e6 / steps:.2f}, idle (no kernel) {at[0] / 1e6 / steps:.2f} "
+          f"in {len(gaps) // steps} gaps/step (gaps > 20 us: {sum(g for g in gaps if g > 20000) / 1e6 / steps:.2f} ms)")
+    for lv in sorted(at):
+        if lv:
+            print(f"  {lv} kernel(s) running: {at[lv] / 1e6 / steps:8.2f} ms/step")
 
 
 if __name__ == "__main__":
