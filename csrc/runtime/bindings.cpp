@@ -6,7 +6,6 @@
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 #include <hip/hip_runtime.h>
-#include <hip/hip_ext.h>
 #include <rocprofiler-sdk-roctx/roctx.h>
 
 #include "../kernels/conv_params.h"
@@ -639,16 +638,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("range_push", [](const std::string& s) { return (int64_t)roctxRangePushA(s.c_str()); });
   m.def("range_pop", []() { return (int64_t)roctxRangePop(); });
   m.def("trace_mark", [](const std::string& s) { roctxMarkA(s.c_str()); });
-  // HIP stream restricted to a CU subset (hipExtStreamCreateWithCUMask): bit i of the mask words enables CU i.
-  // Returned as a raw handle for torch.cuda.ExternalStream; lives for the process (streams are few and long-lived).
-  m.def("cu_mask_stream", [](std::vector<int64_t> words) {
-    std::vector<uint32_t> w(words.begin(), words.end());
-    hipStream_t s = nullptr;
-    TORCH_CHECK(hipExtStreamCreateWithCUMask(&s, (uint32_t)w.size(), w.data()) == hipSuccess,
-                "hipExtStreamCreateWithCUMask failed");
-    return (int64_t)(uintptr_t)s;
-  });
-  m.def("conv_igemm",&conv_igemm, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("stats"), py::arg("scale"),
+  m.def("conv_igemm", &conv_igemm, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("stats"), py::arg("scale"),
         py::arg("shift"), py::arg("affine"), py::arg("accum"), py::arg("g"), py::arg("chunk"), py::arg("cfg") = -1,
         py::arg("bias") = py::none(), py::arg("nostore") = 0);
   m.def("conv_igemm_fres", &conv_igemm_fres);

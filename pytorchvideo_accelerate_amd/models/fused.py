@@ -546,16 +546,6 @@ class _ConvBN:
         return a, b
 
 
-def cu_mask_words(device, n: int, complement: bool = False) -> List[int]:
-    """32-bit CU-mask words selecting ``n`` CUs (a multiple of 64 on 256 CUs), the same number on every XCD whether
-    the logical CU ids interleave over the 8 XCDs (XCD = i % 8) or are contiguous per XCD (XCD = i // 32): CU
-    i = 8a + b is taken when a % 4 < n / 64."""
-    total = torch.cuda.get_device_properties(device).multi_processor_count
-    q = max(1, min(3, n * 4 // total))
-    bits = [((i >> 3) % 4 < q) != complement for i in range(total)]
-    return [sum(1 << j for j in range(32) if w * 32 + j < total and bits[w * 32 + j]) for w in range((total + 31) // 32)]
-
-
 def to_s2d(x_ncthw: torch.Tensor) -> Act:
     """NCTHW float clip -> space-to-depth stem input: 2x2 pixel blocks x RGB0 = 16 bf16 channels."""
     N, C, T, H, W = x_ncthw.shape
@@ -1064,27 +1054,10 @@ class FusedNet:
 
     def _side_stream(self):
         if self._side is None:
-            n = int(os.environ.get("PVA_SIDE_CUS", "0"))
-            if n > 0:
-                # experiment: the fast pathway confined to n CUs (balanced over the XCDs), see cu_mask_words
-                self._side = torch.cuda.ExternalStream(self.C.cu_mask_stream(cu_mask_words(self.device, n)),
-                                                       device=self.device)
-            else:
-                # PVA_SIDE_PRIORITY: HIP stream priority of the fast-pathway stream (lower = higher priority)
-                self._side = torch.cuda.Stream(device=self.device,
-                                               priority=int(os.environ.get("PVA_SIDE_PRIORITY", "0")))
+            # PVA_SIDE_PRIORITY: HIP stream priority of the fast-pathway stream (lower = higher priority)
+            self._side = torch.cuda.Stream(device=self.device,
+                                           priority=int(os.environ.get("PVA_SIDE_PRIORITY", "0")))
         return self._side
-
-    def _slow_stream(self):
-        """With PVA_SIDE_CUS and PVA_MAIN_CU_COMPLEMENT=1: the slow pathway's stream while both pathways run,
-        confined to the CUs the fast pathway's stream does not use (None otherwise: the main stream)."""
-        n = int(os.environ.get("PVA_SIDE_CUS", "0"))
-        if n <= 0 or os.environ.get("PVA_MAIN_CU_COMPLEMENT", "0") != "1":
-            return None
-        if getattr(self, "_slow", None) is None:
-            self._slow = torch.cuda.ExternalStream(self.C.cu_mask_stream(cu_mask_words(self.device, n, True)),
-                                                   device=self.device)
-        return self._slow
 
     def _wgrad_stream(self):
         """The weight-gradient stream of the current lane (0: main, 1: fast pathway)."""
@@ -1161,7 +1134,6 @@ class FusedNet:
         ms = self._ms_active()
         main = torch.cuda.current_stream(self.device) if ms else None
         side = self._side_stream() if ms else None
-        slow = self._slow_stream() if ms else None
         if ms:
             self._join(side, main)   # inputs were produced on the main stream
         for si, (paths, fuse) in enumerate(self.stages):
@@ -1185,11 +1157,6 @@ class FusedNet:
                         with torch.cuda.stream(side):
                             outs[p] = mod.fwd(x, out, train, tag)
                         self.lane = 0
-                    elif slow is not None:
-                        self._join(slow, main)
-                        with torch.cuda.stream(slow):
-                            outs[p] = mod.fwd(x, out, train, tag)
-                        self._join(main, slow)
                     else:
                         outs[p] = mod.fwd(x, out, train, tag)
                 if fuse is not None:
@@ -1336,7 +1303,6 @@ class FusedNet:
         ms = self._ms_active()
         main = torch.cuda.current_stream(self.device) if ms else None
         side = self._side_stream() if ms else None
-        slow = self._slow_stream() if ms else None
         self._ms_bwd = ms   # per-block progress reports are deferred to stage ends (grads come from two streams)
         for si in range(len(self.stages) - 1, -1, -1):
             with trace_range(f"bwd/b{si}"):
@@ -1357,14 +1323,9 @@ class FusedNet:
                 for p in range(len(paths) - 1, -1, -1):
                     mod = paths[p]
                     on_side = ms and p == 1
-                    on_slow = slow is not None and p == 0
                     if on_side:
                         self.lane = 1
                         ctx = torch.cuda.stream(side)
-                        ctx.__enter__()
-                    elif on_slow:
-                        self._join(slow, main)
-                        ctx = torch.cuda.stream(slow)
                         ctx.__enter__()
                     try:
                         if isinstance(mod, _Stem):
@@ -1380,9 +1341,6 @@ class FusedNet:
                         if on_side:
                             ctx.__exit__(None, None, None)
                             self.lane = 0
-                        elif on_slow:
-                            ctx.__exit__(None, None, None)
-                            self._join(main, slow)
                 if ms:
                     self._join(main, side)
                     self._progress(max(m.flat_hi if isinstance(m, _Stem) else m.blocks[0].flat_hi for m in paths),

@@ -16,3 +16,9 @@ run side64 PVA_SIDE_CUS=64
 run side64c PVA_SIDE_CUS=64 PVA_MAIN_CU_COMPLEMENT=1
 run side128c PVA_SIDE_CUS=128 PVA_MAIN_CU_COMPLEMENT=1
 run prio PVA_SIDE_PRIORITY=-1
+# PMC pass 1 (SQ + GRBM) over one steady-state step at the headline batch
+if [ -n "$PMC" ]; then
+  o=gpurun_out/r3pmc; mkdir -p $o
+  timeout -k 10 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d $o/p1 -o p -- python3 bench.py --steps 2 --warmup 1 > $o/p1.log 2>&1 || { tail -5 $o/p1.log; exit 1; }
+  echo pmc1 done
+fi
