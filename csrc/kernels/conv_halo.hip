@@ -346,6 +346,278 @@ void launch_ntile(const ConvParams& p, int R, bool epi, hipStream_t st) {
 
 
 // ------------------------------------------------------------------------------------------------------------------
+// Persistent 64 -> 64 channel variant (slow res2 conv_b, 56x56: the kernel above runs it at ~17 % MFMA busy, waits
+// 0.37, profiles/r3_pmc/halo_bench_pmc.txt).  What changes:
+//   * the whole weight tensor (64 x 9 x 64 bf16 = 72 KB) is staged into LDS ONCE per workgroup, in k-step-major,
+//     channel-group-major order [18 k-steps][4 groups][64 n][8] (a fragment's 16 lanes of one group hit 16 distinct
+//     16-B bank slots), instead of re-fetching weight fragments from L2 every k-step;
+//   * one workgroup of 8 waves per CU walks a contiguous range of tiles (R x W positions of one frame, P <= 224):
+//     the next tile's halo is loaded into registers (6 x 16 B per lane, one 128-B position row per 8 lanes) while
+//     the current tile computes, and written to LDS (BN+ReLU applied) behind one barrier;
+//   * compile-time channel counts: no runtime divisions in the k loop (18 fully unrolled k-steps, per-tap halo
+//     offsets in SGPRs), 8 waves = 2 channel halves (2 x 16-channel blocks) x 4 position groups (3-4 blocks of 16).
+// Epilogues as conv_halo_kernel (EPI 0: raw output + BN partial sums per tile; EPI 1: dgrad with the BN_a ReLU mask
+// from y0 and the BN_a backward partials).  LDS: 72 KB weights + 8 x NPOSP x 16 B halo (<= 44 KB) + reductions.
+constexpr int HP_THREADS = 512;
+constexpr int HP_NPOSP_MAX = 352;   // (R + 2) x (W + 2) halo positions, padded to 16
+constexpr int HP_STG = (HP_NPOSP_MAX * 8 + HP_THREADS - 1) / HP_THREADS;   // 16-B halo chunks per thread
+
+__host__ __device__ inline int hp_nposp(int R, int W) { return (((R + 2) * (W + 2)) + 15) & ~15; }
+
+// DIR = +1 (forward, tap offsets -1..1) or -1 (dgrad, flipped taps); WW x RR = image width x rows per tile: every
+// halo offset is a compile-time constant folded into the ds_read immediates (runtime offsets were hoisted out of the
+// tile loop by the compiler into ~70 address VGPRs and spilled)
+template <int EPI, int AFF, int DIR, int WW, int RR>
+__global__ __launch_bounds__(HP_THREADS, 1) void conv_halo64p_kernel(const ConvParams p, const int ntiles) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int C = 64;
+  constexpr int W = WW, R = RR;
+  constexpr int PW = W + 2;
+  constexpr int P = R * W;
+  constexpr int NPOS = (R + 2) * PW, NPOSP = (NPOS + 15) & ~15;
+  static_assert(NPOSP <= HP_NPOSP_MAX && P <= 224, "halo tile too large");
+  char* WI = smem;                                   // [18][4][64][16 B] weights
+  char* HI = smem + 18 * 4 * 64 * 16;                // [8][NPOSP][16 B] halo
+  const int H = p.Rh;
+  float* red = reinterpret_cast<float*>(HI + 8 * NPOSP * 16);   // [4 wm][3][64]
+  float* bnp = red + 4 * 3 * C;                                 // EPI 1: [4][64] mean0 rstd0 msc msh; then aff
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wn = wid & 1, wm = wid >> 1;
+  const int fr = lane & 15, fg = lane >> 4;
+  // contiguous tile range of this workgroup (neighbouring tiles share halo rows through this XCD's L2)
+  const int t_begin = (int)((long long)blockIdx.x * ntiles / gridDim.x);
+  const int t_end = (int)((long long)(blockIdx.x + 1) * ntiles / gridDim.x);
+  const int tpf = H / R;
+
+  // ---- per-tap uniform offsets (the geometry of conv_halo_kernel's step_w / step_a with one 64-channel slice)
+  int wtap[9];
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) {
+    const int jh = tap / 3, jw = tap - jh * 3;
+    wtap[tap] = (p.bt0 * p.kh + p.bh0 + jh * p.bhs) * p.kw + p.bw0 + jw * p.bws;
+  }
+  // ---- weights -> LDS: chunk q = (s, g, n): k-step s = 2 tap + half, channel group g, output channel n
+  for (int q = tid; q < 18 * 4 * 64; q += HP_THREADS) {
+    const int s = q >> 8, g = (q >> 6) & 3, n = q & 63;
+    const int tap = s >> 1, half = s & 1;
+    int wt = 0;
+#pragma unroll
+    for (int u = 0; u < 9; ++u) wt = (u == tap) ? wtap[u] : wt;
+    *reinterpret_cast<uint4*>(WI + q * 16) =
+        *reinterpret_cast<const uint4*>(p.w + (size_t)n * p.Kfull + wt * C + half * 32 + g * 8);
+  }
+  if constexpr (EPI == 1) {
+    for (int i = tid; i < C; i += HP_THREADS) {
+      bnp[i] = p.emean0[i]; bnp[C + i] = p.erstd0[i]; bnp[2 * C + i] = p.emsc[i]; bnp[3 * C + i] = p.emsh[i];
+    }
+  }
+
+  // ---- staging roles: lane -> channel group cg = lane >> 3, position u*64 + wid*8 + (lane & 7) of pass u
+  const int cg = lane >> 3;
+  float* aff = bnp + 4 * C;   // [2][64] consumer-side affine (read per tile from LDS: fewer live VGPRs)
+  if constexpr (AFF != 0) {
+    for (int i = tid; i < C; i += HP_THREADS) { aff[i] = p.in_scale[i]; aff[C + i] = p.in_shift[i]; }
+  }
+  // per pass: halo row hh (bits 16-23), column-in-image flag (bit 24), row offset (h-1)*W + (w-1) + 2^15 (bits 0-15)
+  int hcode[HP_STG];
+#pragma unroll
+  for (int u = 0; u < HP_STG; ++u) {
+    const int pos = u * 64 + wid * 8 + (lane & 7);
+    const int h = pos / PW, w = pos - h * PW;
+    const bool ok = pos < NPOS && w >= 1 && w <= W;
+    hcode[u] = ok ? ((h << 16) | (1 << 24) | ((h - 1) * W + (w - 1) + 32768)) : 0;
+  }
+  auto load_halo = [&](int t, uint4 (&stg)[HP_STG]) {
+    const int frame = t / tpf, r0 = (t - frame * tpf) * R;
+    const uint16_t* base = p.x + ((size_t)frame * H * W + (size_t)r0 * W) * p.ldx + cg * 8;
+#pragma unroll
+    for (int u = 0; u < HP_STG; ++u) {
+      const int h = r0 - 1 + ((hcode[u] >> 16) & 255);
+      stg[u] = uint4{0, 0, 0, 0};
+      if ((hcode[u] >> 24) && (unsigned)h < (unsigned)H)
+        stg[u] = *reinterpret_cast<const uint4*>(base + (ptrdiff_t)((hcode[u] & 65535) - 32768) * p.ldx);
+    }
+  };
+  auto store_halo = [&](int t, const uint4 (&stg)[HP_STG]) {
+    const int frame = t / tpf, r0 = (t - frame * tpf) * R;
+    float sc[8], sh[8];
+    if constexpr (AFF != 0) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { sc[e] = aff[cg * 8 + e]; sh[e] = aff[C + cg * 8 + e]; }
+    }
+#pragma unroll
+    for (int u = 0; u < HP_STG; ++u) {
+      const int pos = u * 64 + wid * 8 + (lane & 7);
+      if (pos >= NPOS) continue;
+      uint4 o = stg[u];
+      if constexpr (AFF != 0) {
+        float f[8];
+        unpack8(o, f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] = __builtin_fmaf(f[e], sc[e], sh[e]);
+        o = pack8_fast(f);
+        if constexpr (AFF == 2) o = relu_bf16x8(o);
+        const int h = r0 - 1 + ((hcode[u] >> 16) & 255);
+        if (!((hcode[u] >> 24) && (unsigned)h < (unsigned)H)) o = uint4{0, 0, 0, 0};   // padding stays zero
+      }
+      *reinterpret_cast<uint4*>(HI + (cg * NPOSP + pos) * 16) = o;
+    }
+  };
+
+  // ---- this wave's position blocks: NBLK = ceil(P/16) split 4 ways as evenly as possible
+  const int NBLK = (P + 15) >> 4;
+  const int q4 = NBLK >> 2, r4 = NBLK & 3;
+  const int b0 = wm < r4 ? wm * (q4 + 1) : r4 * (q4 + 1) + (wm - r4) * q4;
+  const int nb = q4 + (wm < r4 ? 1 : 0);   // live blocks (<= 4 for P <= 224)
+  int abase[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int pl = min((b0 + i) * 16 + fr, P - 1);
+    const int h = pl / W, w = pl - h * W;
+    abase[i] = (fg * NPOSP + (h + 1) * PW + (w + 1)) * 16;
+  }
+  const int wbase = fg * 1024 + (32 * wn + fr) * 16;   // + s * 4096 + j * 256
+
+  // one tile: halo (in `cur`) -> LDS, prefetch tile t + 1 into `nxt` (the loop is unrolled by two so each register
+  // set is a compile-time array; prefetching two tiles ahead measured no faster), MFMAs, epilogue
+  auto tile = [&](int t, uint4 (&cur)[HP_STG], uint4 (&nxt)[HP_STG]) {
+    __syncthreads();   // previous tile's MFMA reads of HI are done (and, first time, the weight / table writes)
+    store_halo(t, cur);
+    __syncthreads();
+    const int frame = t / tpf, r0 = (t - frame * tpf) * R;
+    const size_t row0 = (size_t)frame * H * W + (size_t)r0 * W;
+    // EPI 1: this tile's y0 rows are requested BEFORE the prefetch, so the epilogue's wait does not cover it
+    uint2 y0v[4][2];
+    if constexpr (EPI == 1) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int pl = min((b0 + i) * 16 + fr, P - 1);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          y0v[i][j] = *reinterpret_cast<const uint2*>(p.ey0 + (row0 + pl) * C + 32 * wn + 16 * j + 4 * fg);
+      }
+    }
+    if (t + 1 < t_end) load_halo(t + 1, nxt);
+
+    // every wave runs 4 position blocks (a 3-block wave's 4th block re-reads clamped positions and is not stored):
+    // branch-free k loop, fragments of step s+1 read while the 8 MFMAs of step s run
+    f32x4_t acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    bf16x8_t wa[2][2], xb[2][4];
+    auto frag = [&](int s, int c) {
+      const int jh = (s >> 1) / 3, jw = (s >> 1) % 3;   // (s is a compile-time constant of the unrolled loop)
+      const int ao = ((-DIR + DIR * jh) * PW + (-DIR + DIR * jw)) * 16 + (s & 1) * 4 * NPOSP * 16;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) wa[c][j] = *reinterpret_cast<const bf16x8_t*>(WI + s * 4096 + j * 256 + wbase);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) xb[c][i] = *reinterpret_cast<const bf16x8_t*>(HI + abase[i] + ao);
+    };
+    frag(0, 0);
+#pragma unroll
+    for (int s = 0; s < 18; ++s) {
+      const int c = s & 1;
+      if (s + 1 < 18) {
+        frag(s + 1, c ^ 1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[c][j], xb[c][i], acc[i][j], 0, 0, 0);
+    }
+
+    // ---- epilogue: lane holds channels 32 wn + 16 j + 4 fg + r of position (b0 + i) * 16 + fr
+    float s1[2][4], s2[2][4];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { s1[j][r] = 0.f; s2[j][r] = 0.f; }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int pl = (b0 + i) * 16 + fr;
+      if (i >= nb || pl >= P) continue;
+      const size_t row = row0 + pl;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int n = 32 * wn + 16 * j + 4 * fg;
+        float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        float a[4];
+        if constexpr (EPI == 1) {
+          unpack4(y0v[i][j], a);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = (a[r] * bnp[2 * C + n + r] + bnp[3 * C + n + r] > 0.f) ? v[r] : 0.f;
+        }
+        const uint2 pk = pack4(v);
+        *reinterpret_cast<uint2*>(p.y + row * p.ldy + n) = pk;
+        float q[4];
+        unpack4(pk, q);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          s1[j][r] += q[r];
+          if constexpr (EPI == 1) s2[j][r] += q[r] * a[r];
+          else s2[j][r] += q[r] * q[r];
+        }
+      }
+    }
+    if (EPI == 0 && p.stats == nullptr) return;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float a = sum16(s1[j][r]), b = sum16(s2[j][r]);
+        if (fr == 0) {
+          const int n = 32 * wn + 16 * j + 4 * fg + r;
+          red[(wm * 3) * C + n] = a;
+          red[(wm * 3 + 1) * C + n] = b;
+        }
+      }
+    __syncthreads();
+    if (tid < C) {
+      const int n = tid;
+      float a = 0.f, b = 0.f;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) { a += red[(m * 3) * C + n]; b += red[(m * 3 + 1) * C + n]; }
+      if constexpr (EPI == 0) {
+        p.stats[((size_t)t * 2) * C + n] = a;
+        p.stats[((size_t)t * 2 + 1) * C + n] = b;
+      } else {
+        p.epart[((size_t)t * 3) * C + n] = a;
+        p.epart[((size_t)t * 3 + 1) * C + n] = (b - bnp[n] * a) * bnp[C + n];
+        p.epart[((size_t)t * 3 + 2) * C + n] = 0.f;
+      }
+    }
+  };
+
+  uint4 stgA[HP_STG], stgB[HP_STG];
+  if (t_begin < t_end) load_halo(t_begin, stgA);
+  for (int t = t_begin; t < t_end; t += 2) {
+    tile(t, stgA, stgB);
+    if (t + 1 < t_end) tile(t + 1, stgB, stgA);
+  }
+}
+
+template <int EPI, int AFF, int DIR, int WW, int RR>
+void launch_halo64p_t(const ConvParams& p, int cfg, hipStream_t st) {
+  const int ntiles = p.M / (RR * WW);
+  const size_t lds = 18 * 4 * 64 * 16 + (size_t)8 * hp_nposp(RR, WW) * 16 + (4 * 3 + 4 + 2) * 64 * 4;
+  const int cap = (cfg & 4) ? 1024 : 256;   // one workgroup per CU (LDS-bound); 4x that for load balance
+  const int grid = ntiles < cap ? ntiles : cap;
+  hipLaunchKernelGGL((conv_halo64p_kernel<EPI, AFF, DIR, WW, RR>), dim3(grid), dim3(HP_THREADS), lds, st, p, ntiles);
+}
+
+template <int EPI, int AFF, int DIR>
+void launch_halo64p(const ConvParams& p, int cfg, hipStream_t st) {
+  if (p.Rw == 56) launch_halo64p_t<EPI, AFF, DIR, 56, 4>(p, cfg, st);
+  else launch_halo64p_t<EPI, AFF, DIR, 64, 2>(p, cfg, st);
+}
+
+
+// ------------------------------------------------------------------------------------------------------------------
 // Narrow variant (fast pathway: 8 / 16 / 32 channels in and out, P = R*W <= 1024 positions per tile).  At these
 // widths the conv is a pure streaming problem (K = 9*C <= 288): the halo [(R+2) x (W+2)][C] is staged once
 // (position-major, 16/32/64 B per position), the weights of every k-step live in registers for the whole kernel,
@@ -569,6 +841,15 @@ int conv_halo_legal(const ConvParams& p, int chunk) {
   return R * p.Rw;
 }
 
+// 1 when the persistent 64-channel variant (launch-word bit 1) can run this geometry (conv_halo_legal > 0 too)
+int conv_halo64p_legal(const ConvParams& p, int chunk) {
+  if (p.Cg != 64 || p.Ngemm != 64 || p.Kfull < 9 * 64 || conv_halo_legal(p, chunk) <= 0) return 0;
+  if (!((p.dir == 1 && p.aoh == -1 && p.aow == -1) || (p.dir == -1 && p.aoh == 1 && p.aow == 1))) return 0;
+  const int R = halo_rows(p.Rh, p.Rw);   // instantiated image widths: 56 (224 crop) and 64 (R101's 256 crop)
+  if (p.epart && p.dir != -1) return 0;
+  return ((p.Rw == 56 && R == 4) || (p.Rw == 64 && R == 2)) ? 1 : 0;
+}
+
 int conv_halo_epi_ok(const ConvParams& p) {
   if (p.accum || p.fres || p.ebias || p.nostore || p.eres || p.emask || p.ey1) return 0;
   const bool epi = p.epart != nullptr;
@@ -594,6 +875,14 @@ void conv_halo_launch(const ConvParams& p, int cfg, hipStream_t st) {
   }
   const int R = halo_rows(p.Rh, p.Rw);
   const bool epi = p.epart != nullptr;
+  if (cfg & 2) {   // persistent 64-channel variant (legality checked by the bindings: conv_halo64p_legal)
+    if (epi) launch_halo64p<1, 0, -1>(p, cfg, st);
+    else if (p.dir < 0) launch_halo64p<0, 0, -1>(p, cfg, st);
+    else if (p.affine == 0) launch_halo64p<0, 0, 1>(p, cfg, st);
+    else if (p.affine == 1) launch_halo64p<0, 1, 1>(p, cfg, st);
+    else launch_halo64p<0, 2, 1>(p, cfg, st);
+    return;
+  }
   if ((cfg & 1) || p.Ngemm % 128 != 0) launch_ntile<64>(p, R, epi, st);
   else launch_ntile<128>(p, R, epi, st);
 }

@@ -22,6 +22,7 @@ int conv_direct_legal(const ConvParams& p, int chunk);
 int conv_pw_legal(const ConvParams& p, int chunk);
 int conv_halo_legal(const ConvParams& p, int chunk);
 int conv_halo_epi_ok(const ConvParams& p);
+int conv_halo64p_legal(const ConvParams& p, int chunk);
 void conv_igemm_set_ut(int mode);
 int conv_igemm_m_tiles(int M, int N);
 int conv_igemm_m_tiles_k(int M, int N, int K, int Cg);
@@ -170,6 +171,8 @@ static void check_pw(const ConvParams& p, int64_t chunk, int64_t cfg) {
     const int P = conv_halo_legal(p, (int)chunk);
     TORCH_CHECK(P > 0 && P == (int)(cfg >> 12), "halo conv kernel selected for an unsupported geometry");
     TORCH_CHECK(conv_halo_epi_ok(p), "halo conv kernel selected for an unsupported epilogue");
+    TORCH_CHECK(!(cfg & 2) || conv_halo64p_legal(p, (int)chunk),
+                "persistent 64-channel halo conv kernel selected for an unsupported geometry");
     return;
   }
   if (cfg < 0 || !(cfg & 16) || !(cfg & 512)) return;
@@ -684,6 +687,12 @@ PYBIND11_MODULE(_C, m) {
     q.kt = g[12]; q.kh = g[13]; q.kw = g[14]; q.st = g[15]; q.sh = g[16]; q.sw = g[17];
     q.pt = g[18]; q.ph = g[19]; q.pw = g[20];
     return (int64_t)wgrad_box_legal(q);
+  });
+  m.def("conv_halo64p_legal", [](std::vector<int64_t> g, int64_t chunk) {
+    ConvParams q{};
+    int* f = &q.M;
+    for (int i = 0; i < 39 && i < (int)g.size(); ++i) f[i] = (int)g[i];
+    return (int64_t)conv_halo64p_legal(q, (int)chunk);
   });
   m.def("conv_halo_legal", [](std::vector<int64_t> g, int64_t chunk) {
     ConvParams q{};

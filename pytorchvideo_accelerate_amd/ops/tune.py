@@ -33,7 +33,9 @@ PW = 512              # streaming pointwise kernel (csrc/kernels/conv_pw.hip): d
 PW_ROWS = (1024, 2048, 4096)   # N % 32 == 0, weights in LDS; bits 0-1 select the rows per workgroup,
 PW_SOLO = 4                     # bit 2 one workgroup per CU
 HALO = 2048           # halo-staged (1,3,3) stride-1 kernel (csrc/kernels/conv_halo.hip): bit 0 = 64-channel
-                      # n-tiles (else 128), bits 12+ = positions per tile
+                      # n-tiles (else 128), bits 12+ = positions per tile; bit 1 = persistent 64-channel variant
+HALO_P = 2            #   (weights resident in LDS; bit 2: 4 workgroups per CU-slot instead of 1)
+HALO_P4 = 4
 TILE_BN = (128, 64, 32, 16)   # variants 0..3
 TILE_BM = (128, 128, 256, 256)
 
@@ -43,6 +45,8 @@ def describe(cfg: int) -> str:
     if cfg < 0 or not cfg & EXPLICIT:
         return "heuristic"
     if cfg & HALO:
+        if cfg & HALO_P:
+            return "halo%d/p%d" % (cfg >> 12, 1024 if cfg & HALO_P4 else 256)
         return "halo%d/n%d" % (cfg >> 12, 64 if cfg & 1 else 128)
     if cfg & PW:
         return "pw%d%s" % (PW_ROWS[cfg & 3], "s" if cfg & PW_SOLO else "")
@@ -115,6 +119,8 @@ class ConvTuner:
             P = int(self.C.conv_halo_legal(list(g), chunk))
             if P > 0:
                 out += [EXPLICIT | HALO | (P << 12) | v for v in ((0, 1) if N % 128 == 0 else (1,))]
+                if self.C.conv_halo64p_legal(list(g), chunk):
+                    out += [EXPLICIT | HALO | (P << 12) | 1 | HALO_P | g4 for g4 in (0, HALO_P4)]
         if pw and self.pw and self._pw_now and self.C.conv_pw_legal(list(g), chunk):
             self._pw_seen += 1
             if self.pw_only is None or self.pw_only == self._pw_seen - 1:

@@ -21,6 +21,7 @@ CASES = [
     (128, 1, 3, 28, 28),    # slow res3 conv_b (196-position tiles, partial MFMA block)
     (256, 2, 2, 14, 14),    # slow res4 conv_b (two 128-channel halo slices)
     (64, 1, 1, 64, 64),     # R101 256-crop res2 (128-position tiles)
+    (64, 4, 8, 56, 56),     # 448 tiles: several tiles per workgroup of the persistent 64-channel variant
     (8, 2, 3, 56, 56),      # fast res2 conv_b (narrow variant, 784-position tiles)
     (16, 1, 4, 28, 28),     # fast res3 conv_b (narrow, whole frames)
     (32, 2, 2, 14, 14),     # fast res4 conv_b (narrow, 196-position tiles)
@@ -42,7 +43,10 @@ def _cfgs(g, C):
     P = require().conv_halo_legal(list(g), 8)
     assert P > 0, "halo kernel must accept this geometry"
     base = EXPLICIT | HALO | (P << 12)
-    return P, ([base, base | 1] if C % 128 == 0 else [base | 1])
+    cfgs = [base, base | 1] if C % 128 == 0 else [base | 1]
+    if require().conv_halo64p_legal(list(g), 8):   # persistent 64-channel variant, 256 / 1024 workgroups
+        cfgs += [base | 1 | 2, base | 1 | 2 | 4]
+    return P, cfgs
 
 
 @pytest.mark.parametrize("case", CASES)
@@ -120,6 +124,8 @@ def test_halo_legality():
     assert Cm.conv_halo_legal(fwd_geometry(ConvSpec(512, 512, (1, 3, 3), (1, 1, 1), (0, 1, 1)), 2, 4, 7, 7, 512, 512), 8) == 0
     assert Cm.conv_halo_legal(fwd_geometry(ConvSpec(24, 24, (1, 3, 3), (1, 1, 1), (0, 1, 1)), 2, 4, 56, 56, 24, 24), 8) == 0
     assert Cm.conv_halo_legal(fwd_geometry(ConvSpec(16, 16, (1, 3, 3), (1, 1, 1), (0, 1, 1)), 2, 4, 56, 56, 16, 16), 8) == 784
+    assert Cm.conv_halo64p_legal(ok, 8) == 1
+    assert Cm.conv_halo64p_legal(fwd_geometry(ConvSpec(128, 128, (1, 3, 3), (1, 1, 1), (0, 1, 1)), 2, 4, 28, 28, 128, 128), 8) == 0
 
 
 WGRAD_CASES = [(64, 1, 2, 56, 56), (128, 1, 3, 28, 28), (256, 2, 2, 14, 14), (64, 1, 1, 64, 64),
