@@ -214,8 +214,6 @@ def run(a):
         from pytorchvideo_accelerate_amd.models.fused import FusedNet
         from pytorchvideo_accelerate_amd.data.transforms import GpuClipBatch, sample_params
         assert dev.type == "cuda", "bench.py needs a GPU (or --plumbing)"
-        if os.environ.get("PVA_MAIN_PRIORITY"):   # stream-priority experiment: the slow pathway / step stream
-            torch.cuda.set_stream(torch.cuda.Stream(dev, priority=int(os.environ["PVA_MAIN_PRIORITY"])))
         torch.manual_seed(1234)
         model = R.create_slowfast(a.depth, a.classes)
         eng = FusedNet(model, dev, deterministic=a.deterministic)

@@ -1063,7 +1063,7 @@ class FusedNet:
         """The weight-gradient stream of the current lane (0: main, 1: fast pathway)."""
         i = self.lane
         if self._wst[i] is None:
-            self._wst[i] = torch.cuda.Stream(device=self.device, priority=int(os.environ.get("PVA_WGRAD_PRIORITY", "0")))
+            self._wst[i] = torch.cuda.Stream(device=self.device)
         self._wst_used[i] = True
         return self._wst[i]
 
