@@ -87,12 +87,28 @@ __device__ __forceinline__ bool fin_reduce_and_elect(const float* __restrict__ p
   const int S = gridDim.y, sb = blockIdx.y;
   const int per = (tiles + S - 1) / S;
   const int t0 = sb * per, t1 = min(tiles, t0 + per);
+  // four rows per tile lane in flight (independent accumulators, combined in a fixed order): the reduction is
+  // latency-bound, one dependent load pair per iteration left most of each workgroup's time waiting
   double a = 0.0, b = 0.0;
   if (c < C) {
-    for (int t = t0 + tl; t < t1; t += 4) {
-      a += part[((int64_t)t * K + k0) * C + c];
-      b += part[((int64_t)t * K + k1) * C + c];
+    double a4[4] = {0.0, 0.0, 0.0, 0.0}, b4[4] = {0.0, 0.0, 0.0, 0.0};
+    int t = t0 + tl;
+    for (; t + 12 < t1; t += 16) {
+      float fa[4], fb[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        fa[u] = part[((int64_t)(t + 4 * u) * K + k0) * C + c];
+        fb[u] = part[((int64_t)(t + 4 * u) * K + k1) * C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) { a4[u] += fa[u]; b4[u] += fb[u]; }
     }
+    for (int u = 0; t < t1; t += 4, ++u) {
+      a4[u & 3] += part[((int64_t)t * K + k0) * C + c];
+      b4[u & 3] += part[((int64_t)t * K + k1) * C + c];
+    }
+    a = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+    b = (b4[0] + b4[1]) + (b4[2] + b4[3]);
   }
   red[threadIdx.x] = a;
   red[NT + threadIdx.x] = b;
@@ -115,10 +131,24 @@ __device__ __forceinline__ bool fin_reduce_and_elect(const float* __restrict__ p
   // the last workgroup: fixed-order sum of the S partials (tile lanes split the ranges, then a fixed 4-way sum)
   a = 0.0; b = 0.0;
   if (c < C) {
-    for (int r = tl; r < S; r += 4) {
-      a += __builtin_nontemporal_load(scratch + ((int64_t)r * 2) * C + c);
-      b += __builtin_nontemporal_load(scratch + ((int64_t)r * 2 + 1) * C + c);
+    double a4[4] = {0.0, 0.0, 0.0, 0.0}, b4[4] = {0.0, 0.0, 0.0, 0.0};
+    int r = tl;
+    for (; r + 12 < S; r += 16) {
+      double fa[4], fb[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        fa[u] = __builtin_nontemporal_load(scratch + ((int64_t)(r + 4 * u) * 2) * C + c);
+        fb[u] = __builtin_nontemporal_load(scratch + ((int64_t)(r + 4 * u) * 2 + 1) * C + c);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) { a4[u] += fa[u]; b4[u] += fb[u]; }
     }
+    for (int u = 0; r < S; r += 4, ++u) {
+      a4[u & 3] += __builtin_nontemporal_load(scratch + ((int64_t)r * 2) * C + c);
+      b4[u & 3] += __builtin_nontemporal_load(scratch + ((int64_t)r * 2 + 1) * C + c);
+    }
+    a = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+    b = (b4[0] + b4[1]) + (b4[2] + b4[3]);
   }
   red[threadIdx.x] = a;
   red[NT + threadIdx.x] = b;

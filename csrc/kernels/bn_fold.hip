@@ -70,8 +70,19 @@ __global__ __launch_bounds__(256) void bnfold_colsum_kernel(const float* __restr
   const int jl = threadIdx.x & 15, kl = threadIdx.x >> 4;
   const int j = blockIdx.x * 16 + jl;
   float t = 0.f;
-  if (j < c)
-    for (int k = kl; k < splits; k += 16) t += sslab[(int64_t)k * c + j];
+  if (j < c) {   // four slab rows in flight per thread, fixed-order combine
+    float t4[4] = {0.f, 0.f, 0.f, 0.f};
+    int k = kl;
+    for (; k + 48 < splits; k += 64) {
+      float f[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) f[u] = sslab[(int64_t)(k + 16 * u) * c + j];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) t4[u] += f[u];
+    }
+    for (int u = 0; k < splits; k += 16, ++u) t4[u & 3] += sslab[(int64_t)k * c + j];
+    t = (t4[0] + t4[1]) + (t4[2] + t4[3]);
+  }
   part[kl][jl] = t;
   __syncthreads();
   if (kl == 0 && j < c) {
@@ -151,7 +162,19 @@ __global__ __launch_bounds__(256) void bnfold_bwd_coef_kernel(
   const int n = blockIdx.x;
   __shared__ double ra[256], rb[256];
   double sdz = 0.0, sy = 0.0;
-  for (int t = threadIdx.x; t < tiles; t += 256) sdz += part[(int64_t)t * 3 * C + n];
+  {   // four strided partial rows in flight per thread (latency-bound), combined in a fixed order
+    double d4[4] = {0.0, 0.0, 0.0, 0.0};
+    int t = threadIdx.x;
+    for (; t + 768 < tiles; t += 1024) {
+      float f[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) f[u] = part[(int64_t)(t + 256 * u) * 3 * C + n];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) d4[u] += f[u];
+    }
+    for (int u = 0; t < tiles; t += 256, ++u) d4[u & 3] += part[(int64_t)t * 3 * C + n];
+    sdz = (d4[0] + d4[1]) + (d4[2] + d4[3]);
+  }
   for (int j = threadIdx.x; j < c; j += 256) sy += (double)bf2f(Wf[(int64_t)n * c + j]) * G[(int64_t)n * c + j];
   ra[threadIdx.x] = sdz; rb[threadIdx.x] = sy;
   __syncthreads();

@@ -388,9 +388,18 @@ __global__ void wgrad_box_sum_kernel(const float* __restrict__ slab, float* __re
   const int g = blockIdx.y;
   const int s0 = g * per, s1 = min(splits, s0 + per);
   const f32x4_t* src = reinterpret_cast<const f32x4_t*>(slab);
-  f32x4_t v = {0.f, 0.f, 0.f, 0.f};
-  for (int s = s0; s < s1; ++s) v += src[(int64_t)s * n4 + i];
-  reinterpret_cast<f32x4_t*>(tmp)[(int64_t)g * n4 + i] = v;
+  // four slabs in flight per thread (independent accumulators, combined in a fixed order)
+  f32x4_t v4[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  int s = s0;
+  for (; s + 3 < s1; s += 4) {
+    f32x4_t f[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) f[u] = src[(int64_t)(s + u) * n4 + i];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v4[u] += f[u];
+  }
+  for (int u = 0; s < s1; ++s, ++u) v4[u] += src[(int64_t)s * n4 + i];
+  reinterpret_cast<f32x4_t*>(tmp)[(int64_t)g * n4 + i] = (v4[0] + v4[1]) + (v4[2] + v4[3]);
 }
 
 __global__ void wgrad_box_final_kernel(const float* __restrict__ tmp, int ngroups, int64_t n, float* __restrict__ grad,
