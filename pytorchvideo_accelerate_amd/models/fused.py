@@ -433,6 +433,55 @@ class _ConvBN:
         tuner.launch(("fw2",) + tuple(g2), g2, 8, run, aff=2, direct=False)
         return self.dgrad(dz, (yb.T, yb.H, yb.W), dab, True, bn=(b, yb), wd=self.W1t, bias=self.fbias[:c])
 
+    # ---- backward BatchNorm folding of a stride-1 1x1 branch1 (same algebra as conv_c's, with a = x, no affine) ----
+    def fold_branch1_forward(self, x: Act):
+        """Gram matrix of the branch input x (wgrad kernel, Gram mode) -> T1 = W1 Gx and s1 = colsum(x), kept for the
+        backward.  The branch's own BN statistics still come from its conv epilogue (y1 is materialised for the unit
+        output); the fold's statistics outputs go to scratch (no running-stat update)."""
+        eng, C, s = self.eng, self.eng.C, self.spec
+        c, Co = s.cin, s.cout
+        if not hasattr(self, "gspec"):
+            self.gspec = ConvSpec(c, c, (1, 1, 1), (1, 1, 1), (0, 0, 0))
+        Gx = eng.scratch("fold1_gram", c * c)
+        slab = eng.scratch("fold_colsum", 4096 * c)
+        if not hasattr(self, "ident"):   # the Gram mode of the wgrad kernel applies an input affine: identity here
+            self.ident = _Xf(torch.ones(c, device=eng.device), torch.zeros(c, device=eng.device), relu=False)
+        splits = self.wgrad(x, x, self.ident, spec=self.gspec, dest=Gx, beta=0.0, gram=True, colsum=slab)
+        self.T = eng.ws((self.name, "foldT"), (Co, c), torch.float32)
+        self.s = eng.ws((self.name, "folds"), (c,), torch.float32)
+        dummy = eng.ws((self.name, "fold1_stats"), (4, Co), torch.float32)
+        bn = self.bn
+        eng.mark(self.name + ".foldstats")
+        C.bnfold_fwd_stats(self.wf, Gx, slab, splits, Co, c, x.M, self.T, self.s, bn.weight, bn.bias, None, None,
+                           None, 0.0, bn.eps, dummy[0], dummy[1], dummy[2], dummy[3])
+
+    def fold_branch1_backward(self, dz: Act, part, tiles: int, x: Act, dx: torch.Tensor, dx_accum: bool):
+        """Branch-1 backward from dz without dy1 or y1: G1 = dz^T x (wgrad kernel), then bnfold_bwd (BN_1 dgamma / dbeta,
+        dW1, W1t = diag(A1) W1, W2 = W1^T diag(B1) W1, the split mean-correction biases); dx = x W2 + biasB (1x1
+        c->c conv, written or accumulated per ``dx_accum``), then dx += dz W1t + biasA (dgrad)."""
+        eng, C, s = self.eng, self.eng.C, self.spec
+        c, Co = s.cin, s.cout
+        G = eng.scratch("fold_G", Co * c)
+        self.wgrad(dz, x, None, dest=G, beta=0.0)
+        if getattr(self, "W1t", None) is None:
+            self.W1t = torch.empty(c, Co, device=eng.device, dtype=torch.bfloat16)
+            self.W2 = torch.empty(c, c, device=eng.device, dtype=torch.bfloat16)
+            self.fbias = torch.empty(2 * c, device=eng.device, dtype=torch.float32)   # [biasA | biasB]
+        fg = eng.flat
+        eng.mark(self.name + ".foldbwd")
+        C.bnfold_bwd(part, tiles, self.wf, self.wd, G, self.T, self.s, Co, c, dz.M, self.bn.weight, self.mean,
+                     self.rstd, fg.gview(self.bn.weight), fg.gview(self.bn.bias), fg.gview(self.conv.weight),
+                     eng.grad_beta, self.coef, self.W1t, self.W2, self.fbias)
+        eng.mark(self.name + ".foldw2")
+        g2 = fwd_geometry(self.gspec, x.N, x.T, x.H, x.W, x.ld, dx.stride(0))
+        tuner = eng.tuner
+
+        def run(cfg, scratch):
+            C.conv_igemm(x.t, self.W2, tuner.scratch_like(dx) if scratch else dx, None, None, None, 0,
+                         1 if dx_accum else 0, g2, 8, cfg, self.fbias[c:])
+        tuner.launch(("fw2x", dx_accum) + tuple(g2), g2, 8, run, direct=False, halo=False)
+        self.dgrad(dz, (x.T, x.H, x.W), dx, True, wd=self.W1t, bias=self.fbias[:c])
+
     def dgrad(self, dy: Act, in_dims, out: torch.Tensor, accum: bool, res: Optional[Act] = None,
               epi: Optional["_ResBlock"] = None, bn: Optional[Tuple["_ConvBN", Act]] = None,
               wd: Optional[torch.Tensor] = None, bias: Optional[torch.Tensor] = None):
@@ -471,7 +520,7 @@ class _ConvBN:
             part, c, one = None, None, None
             if epi is not None:
                 part = self.eng.scratch("bnepi", ((g[0] + 127) // 128) * 3 * g[1])
-                c, one = epi.c, epi.one
+                c, one = epi.c, (None if epi.fold1 else epi.one)   # folded branch1: its sums come from G1
 
             yc = None if (epi is None or epi.yc is None) else epi.yc   # folded conv_c: no raw output
 
@@ -497,8 +546,10 @@ class _ConvBN:
 
             def run(cfg, scratch, g=g):
                 C.conv_igemm(dy.t, wd, tuner.scratch_like(out) if scratch else out, None, None, None, 0,
-                             1 if accum else 0, g, 8, cfg)
-            tuner.launch(("d", accum) + tuple(g), g, 8, run, halo=not accum)
+                             1 if accum else 0, g, 8, cfg, bias)
+            # (the direct kernel has no bias epilogue)
+            tuner.launch(("d", accum, bias is not None) + tuple(g), g, 8, run, halo=not accum and bias is None,
+                         direct=bias is None)
         return None
 
     def bn_backward(self, g: Act, y: Act, mask_mode: int, mo: Optional[Act], mxf: Optional[_Xf],
@@ -663,6 +714,13 @@ class _ResBlock:
         # BN folding of the 1x1 conv_c: its raw output (the widest tensor of the unit) is never written
         self.fold = (eng.bn_fold and tuple(sc.k) == (1, 1, 1) and tuple(sc.stride) == (1, 1, 1) and sc.cin % 8 == 0
                      and sc.cout % 8 == 0 and sc.cin >= eng.fold_min_c)
+        # BN folding of a stride-1 1x1 branch1 in the BACKWARD (slow res2 unit 0): its BN backward and weight/input
+        # gradients come from G1 = dz^T x and the Gram matrix of x (_ConvBN.fold_branch1_*), so neither the
+        # branch-1 BN-backward apply pass (dy1) nor the dual y1 read in the next unit's dgrad epilogue happens
+        s1 = self.one.spec if self.one is not None else None
+        self.fold1 = (self.fold and s1 is not None and eng.bn_fold1 and tuple(s1.k) == (1, 1, 1)
+                      and tuple(s1.stride) == (1, 1, 1) and s1.cin % 8 == 0 and s1.cin == s1.cin_pad
+                      and s1.cin <= 2048)
 
     def out_channels(self):
         return self.c.C
@@ -678,6 +736,8 @@ class _ResBlock:
             # conv_c statistics from the Gram matrix of act_b(yb), then ONE launch writes the unit output
             # relu(BN_c(conv_c) + shortcut) and its ReLU bits (no yc, no res_out pass)
             y1 = self.one.fwd(x, None, train, tag) if self.one is not None else None
+            if self.fold1 and train:
+                self.one.fold_branch1_forward(x)
             self.c.fold_forward(yb, self.b.xf(), train)
             mask = self.eng.ws((self.name, "mask", tag), (yb.M, self.c.C // 8), torch.uint8)
             res, rxf = (x, None) if y1 is None else (y1, self.one.xf(relu=False))
@@ -756,7 +816,8 @@ class _ResBlock:
         M, Cc = yb.M, self.c.C
         fg = eng.flat
         res = None
-        dy1 = eng.ws((one.name, "dy"), (M, Cc), torch.bfloat16) if one is not None else None
+        fold1 = self.fold1
+        dy1 = eng.ws((one.name, "dy"), (M, Cc), torch.bfloat16) if (one is not None and not fold1) else None
         if pre is not None:
             # dout is already the masked dz; its partial sums came from the next unit's dgrad epilogue
             part, tiles = pre
@@ -769,17 +830,27 @@ class _ResBlock:
             eng.mark(self.c.name + ".bnred")
             part = eng.scratch("bnpart", blocks * 3 * Cc)
             # identity shortcut: the same pass writes dz = dout * bits into dx (conv_a's dgrad accumulates on it)
+            dual = one is not None and not fold1
+            dzb = None
+            if one is not None and fold1:   # the folded branch1 needs dz itself: the same pass writes it
+                dzb = Act(eng.ws((self.name, "dz"), (M, Cc), torch.bfloat16), x.N, yb.T, yb.H, yb.W)
             C.bn_bwd_reduce(dout.t, dout.ld, 3, self.mask, Cc // 8, None, None, None, None, None,
-                            None if one is None else y1.t, None if one is None else one.mean,
-                            None if one is None else one.rstd, M, Cc, blocks, rpb, part,
-                            dxa.t if one is None else None, dxa.ld if one is None else 0)
+                            y1.t if dual else None, one.mean if dual else None,
+                            one.rstd if dual else None, M, Cc, blocks, rpb, part,
+                            dxa.t if one is None else (dzb.t if dzb is not None else None),
+                            dxa.ld if one is None else (dzb.ld if dzb is not None else 0))
             tiles = blocks
             if one is None:
                 assert not dx_accum, "identity unit with an accumulating input gradient"
                 dz = dxa
+            elif dzb is not None:
+                dz = dzb
             else:
                 dz = Act(eng.ws((self.name, "dz"), (M, Cc), torch.bfloat16), x.N, yb.T, yb.H, yb.W)
-        if one is not None:
+        if one is not None and fold1:
+            # branch1 first: it consumes the dz partials (`part`) before the conv_c dgrad epilogue reuses that scratch
+            one.fold_branch1_backward(dz, part, tiles, x, dx, dx_accum)
+        elif one is not None:
             # branch1 BN backward from the same sums: dy1 = A1 dz + B1 y1 + C1 (and dz itself when not yet stored)
             C.bn_bwd_finalize(part, tiles, Cc, M, 1, one.bn.weight, one.mean, one.rstd, fg.gview(one.bn.weight),
                               fg.gview(one.bn.bias), eng.grad_beta, one.coef, one.fin)
@@ -799,7 +870,9 @@ class _ResBlock:
         dya, _ = self.a.bn_backward(Act(daa, ya.N, ya.T, ya.H, ya.W), ya, 0 if pa else 2, None,
                                     None if pa else self.a.xf(), pre=pa)
         self.a.wgrad(dya, x, None)
-        if one is not None:
+        if one is not None and fold1:
+            acc = True   # dx already holds the folded branch1's input gradient
+        elif one is not None:
             d1 = Act(dy1, x.N, yb.T, yb.H, yb.W)
             one.wgrad(d1, x, None)
             if self._strided_one(prev):
@@ -943,6 +1016,7 @@ class FusedNet:
         # so it stays opt-in (PVA_BN_FOLD_MIN_C=8).
         self.bn_fold = os.environ.get("PVA_BN_FOLD", "1") != "0"
         self.fold_min_c = int(os.environ.get("PVA_BN_FOLD_MIN_C", "32"))
+        self.bn_fold1 = self.bn_fold and os.environ.get("PVA_BN_FOLD1", "1") != '0'
         # folds with fewer input channels than this take exact statistics from a statistics-only conv pass
         self.fold_exact_below = int(os.environ.get("PVA_BN_FOLD_EXACT_BELOW", "32"))
         blocks = list(model.blocks)

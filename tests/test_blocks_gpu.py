@@ -135,3 +135,23 @@ def test_fusion_pathways(fold, monkeypatch):
     torch.cuda.synchronize()
     assert abs(loss.item() - loss_ref.item()) < 1e-2 * max(1.0, abs(loss_ref.item()))
     _check_grads(net, oracle, xs, labels, floor)
+
+
+@pytest.mark.parametrize("fold1", ["0", "1"])
+def test_res_stage_branch1_fold(fold1, monkeypatch):
+    """Unit 0's stride-1 1x1 branch1 with its BatchNorm folded in the backward (G1 = dz^T x, Gram of x; no dy1 pass,
+    no y1 read in unit 1's dgrad epilogue) vs the unfolded branch1, both against the fp32 oracle."""
+    monkeypatch.setenv("PVA_BN_FOLD_MIN_C", "8")
+    monkeypatch.setenv("PVA_BN_FOLD1", fold1)
+    torch.manual_seed(1)
+    N, C, T, H = 4, 40, 4, 16
+    stage = R.ResStage(3, C, 16, 64, 1, 1)
+    R.init_net_weights(stage)
+    net = R.Net([stage, R.create_res_basic_head(64, 10, pool="default", pool_kernel_size=(T, H, H),
+                                                 dropout_rate=0.0)])
+    x = _x(N, C, T, H, H, seed=3)
+    labels = torch.arange(N, device=DEV) % 10
+    eng_probe = FusedNet(copy.deepcopy(net), DEV)
+    blk0 = eng_probe.stages[0][0][0].blocks[0]
+    assert blk0.fold1 == (fold1 == "1")
+    _run(net, [x], labels, [_act(x)])
