@@ -238,7 +238,9 @@ class _ConvBN:
                 for v in range(8):
                     vw = (v & 3) | (8 if v >= 4 else 0)
                     bmw, bnw = C.wgrad_tile(s.cout, K, vw)
-                    if bmw > max(16, s.cout) or bmw * 8 < s.cout or (v >= 4 and bnw > 2 * K):
+                    # a tile up to twice Cout tall is a candidate (awkward Cout such as 80: one 128-row tile per split
+                    # re-reads dy once, where 64-row tiles re-read it per tile)
+                    if bmw > max(16, 2 * s.cout) or bmw * 8 < s.cout or (v >= 4 and bnw > 2 * K):
                         continue
                     for tbi, bp in ((t, b) for t in range(4) for b in (0, 32)):
                         c = 16 | (v & 3) | (64 if v >= 4 else 0) | (tbi << 2) | bp
