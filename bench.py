@@ -362,7 +362,8 @@ def run(a):
     if st.is_main_process:
         headline = (a.depth, a.frames, a.crop, a.alpha) == (50, 32, 224, 4) and not a.plumbing
         print(json.dumps({
-            "metric": METRIC,
+            "metric": METRIC if headline else
+                      f"clips/sec (whole node) SlowFast-R{a.depth} {a.frames}x2x{a.crop}; step-time p50",
             "value": round(clips, 2),
             "unit": "clips/s",
             "n_gpus": st.world_size,

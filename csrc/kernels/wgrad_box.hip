@@ -473,10 +473,13 @@ void wgrad_box_launch(const WgradParams& p, hipStream_t st) {
 }
 
 // slab [splits][Cout][taps*Cin] -> grad (PyTorch layout [Cout][Cin_real][taps]); tmp holds >= 16 * Cout*taps*Cin
+// first-pass groups of the fixed-order slab reduction (the tmp buffer holds this many copies of dW)
+int wgrad_box_reduce_groups(int splits) { return splits >= 64 ? 16 : (splits >= 16 ? 4 : 1); }
+
 void wgrad_box_reduce_launch(const float* slab, float* tmp, float* grad, int splits, int Cout, int taps, int Cin,
                              int Cin_real, float scale, float beta, hipStream_t st) {
   const int64_t n = (int64_t)Cout * taps * Cin;
-  const int ngroups = splits >= 64 ? 16 : (splits >= 16 ? 4 : 1);
+  const int ngroups = wgrad_box_reduce_groups(splits);
   const int per = (splits + ngroups - 1) / ngroups;
   const int64_t n4 = n / 4;
   hipLaunchKernelGGL(wgrad_box_sum_kernel, dim3((unsigned)((n4 + 255) / 256), ngroups), dim3(256), 0, st, slab, tmp,

@@ -35,6 +35,7 @@ int wgrad_halo_legal(const WgradParams& p);
 int wgrad_box_legal(const WgradParams& p);
 void wgrad_box_reduce_launch(const float* slab, float* tmp, float* grad, int splits, int Cout, int taps, int Cin,
                              int Cin_real, float scale, float beta, hipStream_t st);
+int wgrad_box_reduce_groups(int splits);
 void wgrad_reduce_launch(float* accbuf, float* grad, int splits, int Cout, int taps, int Cin, int Cin_real,
                          float scale, float beta, int slab, hipStream_t stream);
 void bn_finalize_launch(const float* part, int tiles, int C, int64_t count, const float* gamma, const float* beta,
@@ -322,11 +323,12 @@ void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& par
   conv_wgrad_launch(p, (int)chunk, cur_stream());
 }
 
-// slab [splits][Cout][taps*Cin] of the box kernel -> grad; tmp: >= 16 * Cout*taps*Cin floats
+// slab [splits][Cout][taps*Cin] of the box kernel -> grad; tmp: >= box_reduce_groups(splits) * Cout*taps*Cin floats
 void wgrad_box_reduce(const at::Tensor& slab, const at::Tensor& tmp, const at::Tensor& grad, int64_t splits,
                       int64_t Cout, int64_t taps, int64_t Cin, int64_t Cin_real, double scale, double beta) {
   const int64_t n = Cout * taps * Cin;
-  TORCH_CHECK(slab.numel() >= splits * n && tmp.numel() >= 16 * n && n % 4 == 0, "box wgrad reduce: buffer sizes");
+  TORCH_CHECK(slab.numel() >= splits * n && tmp.numel() >= wgrad_box_reduce_groups((int)splits) * n && n % 4 == 0,
+              "box wgrad reduce: buffer sizes");
   TORCH_CHECK(grad.numel() >= Cout * taps * Cin_real, "box wgrad reduce: grad too small");
   wgrad_box_reduce_launch(f32(slab), f32(tmp), f32(grad), (int)splits, (int)Cout, (int)taps, (int)Cin, (int)Cin_real,
                           (float)scale, (float)beta, cur_stream());
@@ -679,6 +681,7 @@ PYBIND11_MODULE(_C, m) {
     return (int64_t)conv_pw_legal(q, (int)chunk);
   });
   m.def("wgrad_box_reduce", &wgrad_box_reduce);
+  m.def("box_reduce_groups", [](int64_t splits) { return (int64_t)wgrad_box_reduce_groups((int)splits); });
   m.def("wgrad_box_legal", [](std::vector<int64_t> g) {
     // [P, Cout, K, Cin, ldd, ldx, Ti, Hi, Wi, To, Ho, Wo, kt, kh, kw, st, sh, sw, pt, ph, pw]
     WgradParams q{};

@@ -13,14 +13,25 @@ Layout of ``<dir>`` (same file names and formats as accelerate 1.x, so ``acceler
                                   "torch_cuda_manual_seed"} — written by every rank
     scaler.pt                    GradScaler state (fp16 only)
 
+    .pva_complete                completion marker (JSON), written last
+
+Saves are atomic: the main process writes the shared files into ``<dir>.tmp``, fsyncs them and renames the
+directory into place (``os.replace``); after a barrier every rank writes its RNG file (temp file + rename), and
+after a second barrier the main process writes the completion marker.  ``latest_checkpoint`` (auto-resume after an
+elastic restart) only considers directories with that marker, so a crash in the middle of a save resumes from the
+previous complete checkpoint instead of failing on a half-written one (``PVA_FAULT_IN_SAVE=N`` injects such a crash
+into the save of global step N: ``tests/test_checkpoint.py``).
+
 Only the main process writes shared files; everything it reads back goes through ``weights_only=True``
 loaders (safetensors / allow-listed torch.load).
 """
 from __future__ import annotations
 
+import json
 import os
+import shutil
 from collections import OrderedDict
-from typing import Any, Dict, List, Optional, Sequence
+from typing import Any, Callable, Dict, List, Optional, Sequence
 
 import torch
 
@@ -31,6 +42,37 @@ MODEL_BIN = "pytorch_model.bin"
 OPTIMIZER_FILE = "optimizer.bin"
 SCHEDULER_FILE = "scheduler.bin"
 SCALER_FILE = "scaler.pt"
+COMPLETE_FILE = ".pva_complete"
+
+
+class InjectedSaveFault(RuntimeError):
+    """Raised by ``PVA_FAULT_IN_SAVE`` (crash in the middle of a checkpoint save; test hook)."""
+
+
+def _fsync_path(path: str):
+    fd = os.open(path, os.O_RDONLY)
+    try:
+        os.fsync(fd)
+    finally:
+        os.close(fd)
+
+
+def _atomic_torch_save(obj, path: str):
+    tmp = path + ".tmp"
+    torch.save(obj, tmp)
+    _fsync_path(tmp)
+    os.replace(tmp, path)
+
+
+def _maybe_fault_in_save(step: int, output_dir: str):
+    at = os.environ.get("PVA_FAULT_IN_SAVE")
+    if not at or step != int(at):
+        return
+    marker = os.path.join(os.path.dirname(output_dir) or ".", f".save_fault_injected_{os.environ.get('RANK', '0')}")
+    if os.path.exists(marker):
+        return
+    open(marker, "w").close()
+    raise InjectedSaveFault(f"injected fault while saving {output_dir}")
 
 
 def _clean_for_safetensors(sd: Dict[str, torch.Tensor]) -> "OrderedDict[str, torch.Tensor]":
@@ -41,23 +83,55 @@ def _clean_for_safetensors(sd: Dict[str, torch.Tensor]) -> "OrderedDict[str, tor
 
 
 def save_state(output_dir: str, model: torch.nn.Module, optimizers: Sequence = (), schedulers: Sequence = (),
-               custom: Sequence = (), step: int = 0, rank: int = 0, is_main: bool = True, scaler=None) -> str:
-    os.makedirs(output_dir, exist_ok=True)
+               custom: Sequence = (), step: int = 0, rank: int = 0, is_main: bool = True, scaler=None,
+               barrier: Optional[Callable[[], None]] = None, world_size: int = 1) -> str:
+    """Atomic save (module docstring).  ``barrier``: the process-group barrier (every rank calls this)."""
+    barrier = barrier or (lambda: None)
+    output_dir = os.path.normpath(output_dir)
     if is_main:
         from safetensors.torch import save_file
-        save_file(_clean_for_safetensors(model.state_dict()), os.path.join(output_dir, MODEL_FILE),
-                  metadata={"format": "pt"})
+        tmp = output_dir + ".tmp"
+        shutil.rmtree(tmp, ignore_errors=True)
+        os.makedirs(tmp)
+        files = []
+
+        def put(name, obj):
+            torch.save(obj, os.path.join(tmp, name))
+            files.append(name)
+        save_file(_clean_for_safetensors(model.state_dict()), os.path.join(tmp, MODEL_FILE), metadata={"format": "pt"})
+        files.append(MODEL_FILE)
+        _maybe_fault_in_save(step, output_dir)
         for i, opt in enumerate(optimizers):
-            name = OPTIMIZER_FILE if i == 0 else f"optimizer_{i}.bin"
-            torch.save(opt.state_dict(), os.path.join(output_dir, name))
+            put(OPTIMIZER_FILE if i == 0 else f"optimizer_{i}.bin", opt.state_dict())
         for i, sch in enumerate(schedulers):
-            name = SCHEDULER_FILE if i == 0 else f"scheduler_{i}.bin"
-            torch.save(sch.state_dict(), os.path.join(output_dir, name))
+            put(SCHEDULER_FILE if i == 0 else f"scheduler_{i}.bin", sch.state_dict())
         for i, obj in enumerate(custom):
-            torch.save(obj.state_dict(), os.path.join(output_dir, f"custom_checkpoint_{i}.pkl"))
+            put(f"custom_checkpoint_{i}.pkl", obj.state_dict())
         if scaler is not None:
-            torch.save(scaler.state_dict(), os.path.join(output_dir, SCALER_FILE))
-    torch.save(rng_state(step), os.path.join(output_dir, f"random_states_{rank}.pkl"))
+            put(SCALER_FILE, scaler.state_dict())
+        for f in files:
+            _fsync_path(os.path.join(tmp, f))
+        _fsync_path(tmp)
+        old = None
+        if os.path.isdir(output_dir):   # re-save into an existing directory: swap, then drop the old one
+            old = output_dir + ".old"
+            shutil.rmtree(old, ignore_errors=True)
+            os.replace(output_dir, old)
+        os.replace(tmp, output_dir)
+        _fsync_path(os.path.dirname(output_dir) or ".")
+        if old is not None:
+            shutil.rmtree(old, ignore_errors=True)
+    barrier()
+    _atomic_torch_save(rng_state(step), os.path.join(output_dir, f"random_states_{rank}.pkl"))
+    barrier()
+    if is_main:
+        mk = os.path.join(output_dir, COMPLETE_FILE)
+        with open(mk + ".tmp", "w") as f:
+            json.dump({"step": int(step), "world_size": int(world_size)}, f)
+            f.flush()
+            os.fsync(f.fileno())
+        os.replace(mk + ".tmp", mk)
+        _fsync_path(output_dir)
     return output_dir
 
 
@@ -104,9 +178,16 @@ def load_state(input_dir: str, model: torch.nn.Module, optimizers: Sequence = ()
     return out
 
 
+def is_complete(path: str) -> bool:
+    """Whether ``path`` holds a checkpoint whose save finished (completion marker present)."""
+    return os.path.isfile(os.path.join(path, COMPLETE_FILE))
+
+
 def latest_checkpoint(root: str) -> Optional[str]:
-    """Most recently written ``epoch_*`` / ``step_*`` directory under ``root`` (the reference's dead
-    "latest checkpoint" branch, ``run.py:208-212``, made real)."""
+    """Most recently written COMPLETE ``epoch_*`` / ``step_*`` directory under ``root`` (the reference's dead
+    "latest checkpoint" branch, ``run.py:208-212``, made real).  Directories without the completion marker (a save
+    that crashed, or a directory another tool wrote: pass those to ``--resume_from_checkpoint`` explicitly) are
+    skipped."""
     if not os.path.isdir(root):
         return None
     cands = []
@@ -115,7 +196,7 @@ def latest_checkpoint(root: str) -> Optional[str]:
         num = d[6:] if d.startswith("epoch_") else d[5:] if d.startswith("step_") else None
         if num is None or not num.isdigit() or not os.path.isdir(full):
             continue
-        if not os.path.exists(os.path.join(full, MODEL_FILE)) and not os.path.exists(os.path.join(full, MODEL_BIN)):
+        if not is_complete(full):
             continue
         cands.append((os.path.getmtime(full), int(num), full))
     return max(cands)[2] if cands else None

@@ -161,7 +161,8 @@ class Accelerator:
         be = self._models[0]
         scaler = getattr(be, "scaler", None)
         _save_state(output_dir, be.model, self._optimizers, self._schedulers, self._custom, step=self.step,
-                    rank=self.process_index, is_main=self.is_main_process, scaler=scaler)
+                    rank=self.process_index, is_main=self.is_main_process, scaler=scaler,
+                    barrier=self.wait_for_everyone, world_size=self.num_processes)
         self.wait_for_everyone()
         return output_dir
 

@@ -96,9 +96,16 @@ class FusedBackend:
         from ..ops.optim import FusedGradScaler
         self.state = state
         self.device = state.device
-        self.net = FusedNet(model, self.device)
-        if state.world_size > 1:   # identical autotuner choices on every rank
+        dp = state.world_size > 1
+        self.net = FusedNet(model, self.device, load_tuning=not dp)
+        if dp:   # identical autotuner choices on every rank
             self.net.tuner.agree = state.agree_times
+            ts = self.net.tune_store
+            # rank 0's persistent table, broadcast once (then only geometries missing from it are tuned and agreed)
+            doc = state.broadcast_object(ts.read() if (ts is not None and state.rank == 0) else None)
+            if ts is not None:
+                ts.restore(doc)
+                ts.writer = state.rank == 0
         self.model = model
         self.flat = self.net.flat
         bounds = sorted(set(self.flat.span(p)[1] for p in self.flat.params))

@@ -6,6 +6,11 @@
 * Reads the accelerate YAML config (``--config_file``, else ``$ACCELERATE_CONFIG_FILE``, else
   ``$HF_HOME/accelerate/default_config.yaml`` / ``~/.cache/huggingface/accelerate/default_config.yaml``) with
   ``yaml.safe_load``; command-line flags override it (accelerate precedence).
+* With no config file, an unset ``--num_processes`` becomes the number of visible GPUs, and more than one GPU turns
+  on multi-GPU training (accelerate's defaults, ``[acc] commands/launch.py:1302-1340``), so the reference's bare
+  ``accelerate launch run.py ...`` (``run_slowfast_r50.sh:1``) starts one rank per GPU.  The count comes from
+  ``HIP_VISIBLE_DEVICES`` / ``CUDA_VISIBLE_DEVICES`` / ``ROCR_VISIBLE_DEVICES`` when set, else from a throwaway child
+  process, so the launcher itself never initialises the GPU.
 * One process on one machine: the script runs as a child process (accelerate's ``simple_launcher``).
   Otherwise ``python -m torch.distributed.run`` (elastic agent) starts ``num_processes // num_machines``
   ranks per node — one process per GPU, RCCL over xGMI — with ``--max_restarts``/``--monitor_interval``.
@@ -22,7 +27,7 @@ import subprocess
 import sys
 from typing import Dict, List, Optional, Tuple
 
-DEFAULTS = {"distributed_type": "NO", "num_processes": 1, "num_machines": 1, "machine_rank": 0,
+DEFAULTS = {"distributed_type": "NO", "num_processes": None, "num_machines": 1, "machine_rank": 0,
             "main_process_ip": "127.0.0.1", "main_process_port": 29500, "mixed_precision": "no", "use_cpu": False,
             "gpu_ids": "all", "max_restarts": 0, "monitor_interval": 5.0, "rdzv_backend": "static"}
 
@@ -34,11 +39,36 @@ def default_config_path() -> str:
     return os.path.join(hf, "accelerate", "default_config.yaml")
 
 
+def _visible_from_env() -> Optional[int]:
+    for k in ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES"):
+        v = os.environ.get(k)
+        if v is not None:
+            return len([d for d in v.split(",") if d.strip() not in ("", "-1")])
+    return None
+
+
+def _device_count() -> int:
+    """Visible GPUs without initialising a GPU in this process (env masks, else ``torch.cuda.device_count()`` in a
+    throwaway child; 0 when that fails)."""
+    n = _visible_from_env()
+    if n is not None:
+        return n
+    try:
+        r = subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],
+                           capture_output=True, text=True, timeout=300)
+        return int(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else 0
+    except (OSError, ValueError, IndexError, subprocess.TimeoutExpired):
+        return 0
+
+
 def load_config(path: Optional[str]) -> Dict:
-    """accelerate config file (YAML or JSON) -> dict of the keys this launcher understands."""
+    """accelerate config file (YAML or JSON) -> dict of the keys this launcher understands (``from_file``: whether
+    a config file was found)."""
     cfg = dict(DEFAULTS)
+    cfg["from_file"] = False
     p = path or default_config_path()
     if p and os.path.exists(p):
+        cfg["from_file"] = True
         import yaml
         with open(p) as f:
             raw = yaml.safe_load(f) or {}
@@ -81,6 +111,18 @@ def resolve(a: argparse.Namespace) -> Dict:
             cfg[k] = v
     if a.cpu is not None:
         cfg["use_cpu"] = a.cpu
+    if cfg["num_processes"] is None:
+        if cfg["from_file"] or cfg["use_cpu"]:
+            cfg["num_processes"] = 1
+        else:
+            # accelerate without a config: one rank per visible GPU (warned, as accelerate does)
+            n = _device_count()
+            cfg["num_processes"] = max(n, 1)
+            print(f"[launch] `--num_processes` was set to a value of `{cfg['num_processes']}`", file=sys.stderr)
+            if n > 1 and not a.multi_gpu:
+                print("[launch] More than one GPU was found, enabling multi-GPU training. If this was unintended "
+                      "please pass in `--num_processes=1`.", file=sys.stderr)
+                a.multi_gpu = True
     if a.multi_gpu:
         cfg["distributed_type"] = "MULTI_GPU"
     if cfg["use_cpu"] and int(cfg["num_processes"]) > 1:

@@ -221,8 +221,8 @@ class _ConvBN:
             nslab = box_wgrad_slabs(s, geometry(cfg)[0])
             part = eng.scratch("wgrad_box_slab", nslab * s.cout * K)
             launch(cfg, part)
-            C.wgrad_box_reduce(part, eng.scratch("wgrad_box_tmp", 16 * s.cout * K), grad, nslab, s.cout, s.taps,
-                               s.cin_pad, s.cin, 1.0, beta_)
+            tmp = eng.scratch("wgrad_box_tmp", C.box_reduce_groups(nslab) * s.cout * K)
+            C.wgrad_box_reduce(part, tmp, grad, nslab, s.cout, s.taps, s.cin_pad, s.cin, 1.0, beta_)
             return nslab
 
         tkey = ("w", dy.M, dy.ld, x.ld, x.T, x.H, x.W, s.cout, K, s.chunk, aff, gram) + tuple(s.k) + tuple(s.stride)
@@ -273,6 +273,7 @@ class _ConvBN:
                         if C.wgrad_halo_legal(gh, plan[2], aff):
                             cands.append(16 | 256 | (o << 9))
                 gscr = eng.scratch("wgrad_tune_grad", s.cout * K)
+                eng.tuner.tuned += 1
 
                 def trial(c):
                     if c & 1024:
@@ -976,9 +977,11 @@ class _Fuse:
 class FusedNet:
     """Executor bound to a reference ``Net`` (SlowFast or Slow ResNet3D) whose parameters it shares."""
 
-    def __init__(self, model: R.Net, device: torch.device, stem_s2d: bool = True, deterministic: bool = False):
+    def __init__(self, model: R.Net, device: torch.device, stem_s2d: bool = True, deterministic: bool = False,
+                 load_tuning: bool = True):
         """``deterministic``: bitwise-reproducible gradients (slab wgrad reduction, generic stems; BN
-        statistics are always reduced in a fixed order).  Costs a little speed."""
+        statistics are always reduced in a fixed order).  Costs a little speed.  ``load_tuning``: restore the
+        persistent autotuner table now (data parallelism restores rank 0's copy instead: ``FusedBackend``)."""
         self.C = require()
         self.deterministic = deterministic
         # fixed-order (slab) reduction for the weight-gradient launches whose results feed back into the step —
@@ -986,8 +989,9 @@ class FusedNet:
         # leaf weight gradients keep their fp32 atomics: the loss and the dgrad chain are then reproducible
         # run to run and only the weight gradients carry atomic-order noise (~1e-6).  Without it that noise
         # flips ReLU masks and the random-init network's chaotic backward decorrelates two runs' gradients
-        # (cosine ~0.65 at B=4-32: scripts/diag_ms_race.py).  PVA_FOLD_SLABS=1; implied by ``deterministic``.
-        self.fold_slabs = deterministic or os.environ.get("PVA_FOLD_SLABS", "0") == "1"
+        # (cosine ~0.65 at B=4-32: scripts/diag_ms_race.py).  On by default (only the few Gram / G launches pay the
+        # slab reduction); PVA_FOLD_SLABS=0 turns it off; implied by ``deterministic``.
+        self.fold_slabs = deterministic or os.environ.get("PVA_FOLD_SLABS", "1") == "1"
         self.stem_s2d = stem_s2d and not deterministic
         self.model = model
         self.device = torch.device(device)
@@ -996,6 +1000,16 @@ class FusedNet:
         from ..ops.tune import ConvTuner
         self.tuner = ConvTuner(require(), enabled=not deterministic and torch.device(device).type == "cuda")
         self.wtune: Dict = {}
+        # eval-only geometries are tuned rank-locally (forward_eval): their choices live in a table of their own so a
+        # training launch never finds an un-agreed choice
+        self._eval_tune: Dict = {}
+        from ..ops.tune import TuneStore
+        self.tune_store = None
+        if self.tuner.enabled:
+            self.tune_store = TuneStore({"conv": self.tuner.cache, "eval": self._eval_tune, "wgrad": self.wtune},
+                                        TuneStore.build_ident(self.device, "bf16"))
+            if load_tuning:
+                self.tune_store.load()
         self._ws: Dict = {}
         self._splits: Dict = {}
         self._bnb: Dict = {}
@@ -1301,12 +1315,16 @@ class FusedNet:
         a cross-rank agreement collective here would only run on the ranks that see a new shape and hang the
         others.  No cross-rank math depends on eval kernel choices (every configuration computes the same sums)."""
         agree, self.tuner.agree = self.tuner.agree, None
+        train_cache, self.tuner.cache = self.tuner.cache, self._eval_tune
         try:
             outs = self._forward_backbone(xs, train=False)
             feat, _ = self._pool_features(outs, "e")
             logits, _, _, _ = self._head_forward(feat, False, "e")
         finally:
             self.tuner.agree = agree
+            self.tuner.cache = train_cache
+        if self.tune_store is not None:
+            self.tune_store.save()
         return logits
 
     @torch.no_grad()
@@ -1362,6 +1380,8 @@ class FusedNet:
             if train_backbone:
                 self._backward_backbone(outs, gfeat, ks)
         self._ms_warm = True
+        if self.tune_store is not None:
+            self.tune_store.save()
         return loss[0], logits
 
     def _backward_backbone(self, outs: List[Act], gfeat: torch.Tensor, ks):

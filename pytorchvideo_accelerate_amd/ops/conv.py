@@ -305,11 +305,13 @@ def conv_wgrad(dy: Act, x: Act, spec: ConvSpec, grad: torch.Tensor, workspace: O
         variant = 16
     if variant == BOX:   # box-staged kernel: per-range slabs + fixed-order two-pass reduction
         C = require()
-        splits, bps, word = box_wgrad_plan(spec, P, (dy.T, dy.H, dy.W), dy.ld, x.ld)
+        plan = box_wgrad_plan(spec, P, (dy.T, dy.H, dy.W), dy.ld, x.ld)
+        assert plan is not None, "box wgrad does not apply to this conv"
+        splits, bps, word = plan
         K = spec.taps * spec.cin_pad
         nslab = box_wgrad_slabs(spec, splits)
         slab = torch.empty(nslab * spec.cout * K, device=dy.t.device, dtype=torch.float32)
-        tmp = torch.empty(16 * spec.cout * K, device=dy.t.device, dtype=torch.float32)
+        tmp = torch.empty(C.box_reduce_groups(nslab) * spec.cout * K, device=dy.t.device, dtype=torch.float32)
         affine = 0 if in_scale is None else (2 if in_relu else 1)
         g = [P, spec.cout, K, spec.cin_pad, dy.ld, x.ld, x.T, x.H, x.W, dy.T, dy.H, dy.W,
              *spec.k, *spec.stride, *spec.pad, splits, bps]

@@ -12,9 +12,17 @@ accumulating dgrads), caches the fastest and launches it for real.  Every config
 the same order, so the result does not depend on the choice.
 
 Disabled by ``PVA_AUTOTUNE=0`` and in deterministic mode (the built-in heuristic is used instead).
+
+Tuned choices persist across processes (:class:`TuneStore`): a JSON table under ``~/.cache/pva/`` (or
+``$PVA_TUNE_CACHE``; ``PVA_TUNE_CACHE=0`` disables it) whose file name hashes the extension's build stamp, the
+device name, the HIP version, the compute dtype and the kernel-selection knobs — a rebuilt ``.so`` or another GPU
+gets a fresh table.  Under data parallelism rank 0 reads it and broadcasts it (one collective), and only rank 0
+writes it back.
 """
 from __future__ import annotations
 
+import hashlib
+import json
 import os
 import sys
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
@@ -79,6 +87,7 @@ class ConvTuner:
         self._pw_seen = 0
         self.log = os.environ.get("PVA_TUNE_LOG", "0") != "0"
         self.reps = reps
+        self.tuned = 0          # geometries timed by this process (conv + weight-gradient tunings)
         self.cache: Dict[Tuple, int] = {}
         self._scratch: Dict[Tuple, torch.Tensor] = {}
         # multi-rank consensus: ``agree(times) -> times`` (e.g. ``DistState.agree_times``, the per-candidate
@@ -161,6 +170,7 @@ class ConvTuner:
         cands = self.candidates(g, chunk, aff, epi, direct, pw, halo)
         if len(cands) <= 1:
             return cands[0] if cands else -1
+        self.tuned += 1
         times = []
         for cfg in cands:
             run(cfg, True)  # warm-up (instruction cache, first-touch)
@@ -180,3 +190,88 @@ class ConvTuner:
                   + " ".join("%s=%.1fus" % (describe(c), 1e3 * t) for c, t in times)
                   + " -> " + describe(best), file=sys.stderr, flush=True)
         return best
+
+
+def _tuplify(v):
+    return tuple(_tuplify(x) for x in v) if isinstance(v, list) else v
+
+
+class TuneStore:
+    """Persistent autotuner table (module docstring).  ``tables``: name -> dict (the live caches, updated in place
+    by :meth:`load` / :meth:`restore`); :meth:`save` writes them when they grew since the last save."""
+
+    KNOBS = ("PVA_CONV_", "PVA_PW_", "PVA_WGRAD_", "PVA_AUTOTUNE")
+
+    def __init__(self, tables: Dict[str, Dict], ident: Dict[str, str], root: Optional[str] = None):
+        self.tables = tables
+        env = os.environ.get("PVA_TUNE_CACHE", "")
+        self.enabled = env != "0"
+        root = root or env or os.path.join(os.path.expanduser("~"), ".cache", "pva")
+        ident = dict(ident)
+        ident.update({k: v for k, v in os.environ.items() if k.startswith(self.KNOBS)})
+        self.ident = ident
+        h = hashlib.sha1(json.dumps(ident, sort_keys=True).encode()).hexdigest()[:16]
+        self.path = os.path.join(root, f"tune-{h}.json")
+        self.writer = True
+        self._saved = -1
+
+    @staticmethod
+    def build_ident(device, dtype: str) -> Dict[str, str]:
+        from .. import _build
+        import torch as _t
+        stamp = ""
+        try:
+            with open(_build.ext_path() + ".stamp") as f:
+                stamp = f.read().strip()
+        except OSError:
+            pass
+        name = _t.cuda.get_device_name(device) if _t.device(device).type == "cuda" else "cpu"
+        return {"so": stamp, "device": name, "hip": str(_t.version.hip), "dtype": dtype}
+
+    def _count(self) -> int:
+        return sum(len(t) for t in self.tables.values())
+
+    def read(self) -> Optional[Dict]:
+        """The stored table (JSON-ready dict) or None (absent / unreadable / other identity)."""
+        if not self.enabled or not os.path.exists(self.path):
+            return None
+        try:
+            with open(self.path) as f:
+                doc = json.load(f)
+        except (OSError, ValueError):
+            return None
+        return doc if doc.get("ident") == self.ident else None
+
+    def restore(self, doc: Optional[Dict]) -> int:
+        """Merge a stored table into the live caches; returns the number of entries restored."""
+        n = 0
+        if doc:
+            for name, rows in doc.get("tables", {}).items():
+                t = self.tables.get(name)
+                if t is None:
+                    continue
+                for k, v in rows:
+                    t.setdefault(_tuplify(k), v)
+                    n += 1
+        self._saved = self._count()
+        return n
+
+    def load(self) -> int:
+        return self.restore(self.read())
+
+    def save(self, force: bool = False) -> bool:
+        n = self._count()
+        if not self.enabled or not self.writer or (n == self._saved and not force):
+            return False
+        doc = {"ident": self.ident, "tables": {k: [[list(kk) if isinstance(kk, tuple) else kk, v]
+                                                   for kk, v in t.items()] for k, t in self.tables.items()}}
+        try:
+            os.makedirs(os.path.dirname(self.path), exist_ok=True)
+            tmp = "%s.%d.tmp" % (self.path, os.getpid())
+            with open(tmp, "w") as f:
+                json.dump(doc, f)
+            os.replace(tmp, self.path)
+        except OSError:
+            return False
+        self._saved = n
+        return True

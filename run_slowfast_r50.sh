@@ -1,8 +1,10 @@
 #!/bin/bash
 # SlowFast-R50 fine-tuning recipe of the reference (run_slowfast_r50.sh), on the MI355X-native engine.
-# --mixed_precision fp16 as in the reference: dynamic loss scaling (GradScaler semantics, scaler.pt) on the
-# fused path; the convolutions compute in bf16 MFMA with fp32 master weights (ops/optim.FusedGradScaler).
-accelerate launch run.py \
+# The launcher (pytorchvideo_accelerate_amd/launch.py, accelerate-launch compatible) starts one rank per visible
+# GPU when no accelerate config file exists, like the reference's bare `accelerate launch`.
+# --mixed_precision fp16 as in the reference: the convolutions run fp16 MFMA kernels with fp32 master weights and
+# dynamic loss scaling (GradScaler semantics, scaler.pt; ops/optim.FusedGradScaler).
+python -m pytorchvideo_accelerate_amd.launch run.py \
     --output_dir outputs \
     --batch_size 8 \
     --num_workers 8 \

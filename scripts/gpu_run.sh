@@ -1,0 +1,68 @@
+#!/bin/bash
+# One parameterised GPU-box runner (replaces the per-experiment gpu_r*_*.sh scripts, which live in git history).
+#   scripts/gpu_run.sh TASK [TASK ...]      every task writes under gpurun_out/$OUT (default: run)
+# tasks (run in the order given; the first failure ends the call — no GPU step after a failed one):
+#   smoke    __graft_entry__.smoke()
+#   tests    pytest -m gpu over $TESTS (default: tests), per-test timeout
+#   bench    bench.py $BENCH_ARGS (tuner log in bench.err)          host   bench.py --source host $BENCH_ARGS
+#   fp16     bench.py --precision fp16 $BENCH_ARGS
+#   ab       bench.py under each setting of $AB (";"-separated env assignments, e.g. AB="PVA_X=0;PVA_X=1")
+#   layers   serialised per-op profile at B=$BATCH (default 160) + roofline table
+#   trace    rocprofv3 kernel trace of 3 steps -> steady-state kernel table
+#   pmc      rocprofv3 PMC passes (one run each) over a bench step at B=$BATCH -> per-kernel summary
+#   runpy    the reference CLI (run.py) at the headline shape on a synthetic corpus
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+out=gpurun_out/${OUT:-run}
+mkdir -p "$out"
+B=${BATCH:-160}
+
+fail() { tail -${2:-30} "$1"; exit 1; }
+
+t_smoke() { timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1 || fail $out/smoke.log; tail -1 $out/smoke.log; }
+t_tests() { timeout -k 10 1500 python -u -m pytest ${TESTS:-tests} -m gpu -x -v --timeout 300 --timeout-method thread > $out/tests.log 2>&1 || fail $out/tests.log 60; tail -2 $out/tests.log; }
+t_bench() { PVA_TUNE_LOG=1 timeout -k 10 400 python bench.py $BENCH_ARGS > $out/bench.json 2> $out/bench.err || fail $out/bench.err; cat $out/bench.json; }
+t_host() { timeout -k 10 400 python bench.py --source host $BENCH_ARGS > $out/bench_host.json 2> $out/bench_host.err || fail $out/bench_host.err; cat $out/bench_host.json; }
+t_fp16() { timeout -k 10 400 python bench.py --precision fp16 $BENCH_ARGS > $out/bench_fp16.json 2> $out/bench_fp16.err || fail $out/bench_fp16.err; cat $out/bench_fp16.json; }
+t_ab() {
+  local i=0
+  IFS=';' read -ra arms <<< "$AB"
+  for arm in "${arms[@]}"; do
+    i=$((i+1))
+    env $arm timeout -k 10 400 python bench.py $BENCH_ARGS > $out/ab$i.json 2> $out/ab$i.err || fail $out/ab$i.err
+    echo "$arm: $(cat $out/ab$i.json)"
+  done
+}
+t_layers() {
+  timeout -k 10 400 python -u scripts/layer_profile.py --batch $B --steps 2 > $out/layers_b$B.txt 2> $out/layers.err || fail $out/layers.err
+  head -1 $out/layers_b$B.txt
+  python scripts/layer_roofline.py $out/layers_b$B.txt --batch $B > $out/layers_roofline_b$B.txt && grep -A 12 "# totals" $out/layers_roofline_b$B.txt
+}
+t_trace() {
+  timeout -k 10 500 rocprofv3 --kernel-trace --output-format csv -d $out/prof -o step -- python3 bench.py --steps 3 --warmup 3 $BENCH_ARGS > $out/prof.log 2>&1 || fail $out/prof.log
+  local f
+  f=$(ls $out/prof/*/step_kernel_trace.csv $out/prof/step_kernel_trace.csv 2>/dev/null | head -1)
+  python scripts/steady_state_kernels.py "$f" --steps 2 > $out/kernels_steady_state.txt && head -3 $out/kernels_steady_state.txt
+  rm -f "$f"
+}
+t_pmc() {
+  local P1="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE"
+  local i=0
+  for P in "$P1" "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
+    i=$((i+1))
+    timeout -k 10 420 rocprofv3 --pmc $P --kernel-trace --output-format csv -d $out/pmc/p$i -o p -- python3 bench.py --steps 2 --warmup 1 --batch $B > $out/pmc_p$i.log 2>&1 || fail $out/pmc_p$i.log 5
+  done
+  python3 scripts/pmc_step_summary.py $out/pmc > $out/pmc_summary_b$B.txt && head -30 $out/pmc_summary_b$B.txt
+}
+t_runpy() {
+  timeout -k 10 600 python -u run.py --synthetic --is_slowfast --num_frames 32 --sampling_rate 2 --crop_size 224 \
+    --batch_size $B --gradient_accumulation_steps 1 --mixed_precision ${PRECISION:-bf16} --num_epochs 2 \
+    --limit_train_batches 8 --limit_val_batches 0 --num_workers 8 --synthetic_videos 1280 --output_dir /tmp/pva_run \
+    > $out/run_py.log 2>&1 || fail $out/run_py.log
+  grep -i "clips/s\|epoch" $out/run_py.log | tail -4
+}
+
+for task in "$@"; do
+  echo "== $task"
+  "t_$task"
+done

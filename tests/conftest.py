@@ -4,6 +4,8 @@ import sys
 import pytest
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+# tests tune kernels per process (isolation); tests of the persistent autotuner table point it at a temp dir
+os.environ.setdefault("PVA_TUNE_CACHE", "0")
 
 
 def pytest_configure(config):

@@ -42,7 +42,7 @@ def test_ours_loads_in_accelerate(tmp_path):
     d = str(tmp_path / "epoch_0")
     save_state(d, m, [opt], [sch], [sch], step=7)
     assert sorted(os.listdir(d)) == sorted(["model.safetensors", "optimizer.bin", "scheduler.bin",
-                                            "custom_checkpoint_0.pkl", "random_states_0.pkl"])
+                                            "custom_checkpoint_0.pkl", "random_states_0.pkl", ".pva_complete"])
     acc = accelerate.Accelerator(cpu=True)
     m2 = _small_model(seed=3)
     o2 = torch.optim.SGD(m2.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
@@ -104,6 +104,35 @@ def test_module_prefix_stripped_and_latest(tmp_path):
     e = tmp_path / "epoch_1"
     e.mkdir()
     save_file({k: v.contiguous() for k, v in m.state_dict().items()}, str(e / "model.safetensors"))
+    # foreign / unfinished directories (no completion marker) are never auto-resumed from
+    assert latest_checkpoint(str(tmp_path)) is None
+    (d / ".pva_complete").write_text("{}")
+    (e / ".pva_complete").write_text("{}")
     os.utime(str(d), (1, 1))
     assert latest_checkpoint(str(tmp_path)) == str(e)
     assert latest_checkpoint(str(tmp_path / "nope")) is None
+
+
+def test_crash_mid_save_resumes_from_previous_complete(tmp_path, monkeypatch):
+    """A save that dies half-way leaves no directory that auto-resume would pick (atomic rename + marker)."""
+    from pytorchvideo_accelerate_amd.ckpt.state import InjectedSaveFault, is_complete
+    m, opt, sch = _ours()
+    save_state(str(tmp_path / "step_2"), m, [opt], [sch], [sch], step=2)
+    monkeypatch.setenv("PVA_FAULT_IN_SAVE", "4")
+    with pytest.raises(InjectedSaveFault):
+        save_state(str(tmp_path / "step_4"), m, [opt], [sch], [sch], step=4)
+    assert not (tmp_path / "step_4").exists() and (tmp_path / "step_4.tmp" / "model.safetensors").exists()
+    assert latest_checkpoint(str(tmp_path)) == str(tmp_path / "step_2") and is_complete(str(tmp_path / "step_2"))
+    # the restarted run passes the hook (marker file) and the retried save completes, replacing the leftover
+    save_state(str(tmp_path / "step_4"), m, [opt], [sch], [sch], step=4)
+    assert is_complete(str(tmp_path / "step_4")) and not (tmp_path / "step_4.tmp").exists()
+    assert latest_checkpoint(str(tmp_path)) == str(tmp_path / "step_4")
+    # re-saving into an existing complete directory (the final save) swaps it atomically
+    m2, _, _ = _ours(seed=5)
+    save_state(str(tmp_path / "step_4"), m2, [opt], [sch], [sch], step=4)
+    from pytorchvideo_accelerate_amd.ckpt.state import load_model_state
+    m3 = _small_model(seed=7)
+    load_model_state(m3, str(tmp_path / "step_4"))
+    for a, b in zip(m2.state_dict().values(), m3.state_dict().values()):
+        torch.testing.assert_close(a, b)
+    assert not (tmp_path / "step_4.old").exists()

@@ -7,8 +7,9 @@ on each rank's shard (``bench.py --data-rank r``):
 * deterministic executor (fixed-order reductions, one stream, per-unit bucket progress): the all-reduced flat
   gradient of the first optimizer step equals the mean of the two single-process gradients to fp32 rounding;
 * production schedule (fast pathway on its own HIP stream, weight gradients on side streams joined per stage,
-  stage-granular bucket progress, heuristic kernels) with fixed-order BN-fold reductions (``PVA_FOLD_SLABS=1``):
-  the same equality within the fp32-atomic noise of the leaf weight gradients.  (Without the fold slabs two runs
+  stage-granular bucket progress, heuristic kernels, and the shipped default with the autotuner on) with the
+  default fixed-order BN-fold reductions: the same equality within the fp32-atomic noise of the leaf weight
+  gradients.  (Without the fold slabs, ``PVA_FOLD_SLABS=0``, two runs
   of the same rank already differ at cosine ~0.65: atomic-order noise in the fold statistics flips ReLU masks
   and the random-init network's backward is chaotic — ``scripts/diag_ms_race.py``, ``scripts/diag_chaos.py``.)
 * default production path (autotuner agreed across ranks): parameters bitwise identical on both ranks;
@@ -73,9 +74,18 @@ def test_fused_two_rank_deterministic_exact(tmp_path):
 
 
 def test_fused_two_rank_streams_and_buckets(tmp_path):
-    err, spread = _dp_vs_singles(tmp_path, [], "ms", PVA_AUTOTUNE="0", PVA_FOLD_SLABS="1")
+    err, spread = _dp_vs_singles(tmp_path, [], "ms", PVA_AUTOTUNE="0")
     assert spread > 0.1, spread
     assert err < 2e-3, (err, spread)   # leaf weight gradients: fp32 split-K atomics in any order
+
+
+def test_fused_two_rank_shipped_default_config(tmp_path):
+    """The shipped defaults exactly as bench.py / run.py run them (autotuner on and agreed across ranks, fold slabs
+    on, two streams): the all-reduced gradient equals the mean of the single-rank gradients within the fp32-atomic
+    noise of the leaf weight gradients (the production DP path checked on gradients, not only params)."""
+    err, spread = _dp_vs_singles(tmp_path, [], "dflt")
+    assert spread > 0.1, spread
+    assert err < 2e-3, (err, spread)
 
 
 def test_fused_two_rank_autotuned_params_identical(tmp_path):

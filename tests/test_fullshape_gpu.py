@@ -85,36 +85,41 @@ def test_slowfast_r101_32x2x256_step_vs_fp32_oracle():
     _check(*_step_vs_oracle(model, xs, labels))
 
 
-def test_fixed_batch_loss_decreases_at_bench_shape():
-    """40 fused SGD steps on one fixed batch of 32x2x224 clips (bench preprocessing, B=16): the loss must fall
-    well below its start (memorisation), i.e. forward, backward and the optimizer agree at full geometry.
-    (bench.py's final_loss > ln(400) comes from fresh random labels every step at lr 0.1: nothing to learn.)
-    The loss falls from ~6.2 to ~2.8 within four steps and then oscillates around 3.0-3.3 (momentum 0.9 on one
-    fixed batch); where it sits in that band varies run to run (fp32-atomic weight-gradient order, and the
-    network's sensitivity to tiny perturbations: scripts/diag_chaos.py).  The check is the drop, over the last
-    ten steps: a broken forward/backward/optimizer does not reach 0.6x the initial loss."""
-    from pytorchvideo_accelerate_amd.data.transforms import GpuClipBatch, sample_params
+def test_fixed_batch_memorisation_tracks_fp32_oracle():
+    """40 SGD steps on ONE fixed batch of 32x2x224 clips (B=16, lr 0.02, momentum 0.9, no dropout), fused executor
+    and the fp32 PyTorch oracle side by side from the same weights: both memorise the batch (the loss falls well
+    below its start) and the fused plateau (mean of the last ten losses) lies within a stated band of the oracle's,
+    while the first steps track it closely.  (the plateau is judged against the oracle's own
+    trajectory, not a free threshold.)"""
     torch.manual_seed(0)
-    model = R.create_slowfast(50, 400)
+    model = R.create_slowfast(50, 400, dropout_rate=0.0)
+    oracle = copy.deepcopy(model).to(DEV).train()
+    opt_ref = torch.optim.SGD(oracle.parameters(), lr=0.02, momentum=0.9, weight_decay=1e-4)
     eng = FusedNet(model, DEV)
     opt = FusedSGD(eng.flat, lr=0.02, momentum=0.9, weight_decay=1e-4, after_step=eng.pack)
     B = 16
-    frames = torch.empty(B, 64, 256, 340, 3, dtype=torch.uint8, device=DEV)
-    eng.C.synth_frames(frames, 5)
-    prep = GpuClipBatch(DEV, 32, 224, 4, s2d=eng.input_s2d)
-    g = torch.Generator().manual_seed(0)
-    params = [sample_params(64, 256, 340, 32, 224, True, generator=g) for _ in range(B)]
-    labels = torch.randint(0, 400, (B,), generator=g).to(DEV)
-    losses = []
+    xs = _clip(B, 32, 224, 4, seed=21)
+    labels = torch.randint(0, 400, (B,), generator=torch.Generator().manual_seed(22)).to(DEV)
+    xd = [x.to(DEV) for x in xs]
+    acts = eng.prepare_inputs(xs)
+    ref, fused = [], []
     for _ in range(40):
-        xs = prep(frames, params)
+        opt_ref.zero_grad(set_to_none=True)
+        loss_ref = F.cross_entropy(oracle(xd), labels)
+        loss_ref.backward()
+        opt_ref.step()
+        ref.append(float(loss_ref))
         opt.zero_grad()
-        loss, _ = eng.forward_backward(xs, labels)
+        loss, _ = eng.forward_backward(acts, labels)
         opt.step()
-        losses.append(float(loss))
-    assert all(torch.isfinite(torch.tensor(losses)))
-    print("losses", " ".join("%.3f" % v for v in losses))
-    assert min(losses[-10:]) < 0.6 * losses[0], losses
+        fused.append(float(loss))
+    print("fp32 ", " ".join("%.3f" % v for v in ref))
+    print("fused", " ".join("%.3f" % v for v in fused))
+    assert all(torch.isfinite(torch.tensor(fused)))
+    assert all(abs(a - b) < 0.05 * b for a, b in zip(fused[:3], ref[:3])), (fused[:3], ref[:3])
+    assert min(ref[-10:]) < 0.5 * ref[0] and min(fused[-10:]) < 0.5 * fused[0], (ref, fused)
+    pf, pr = sum(fused[-10:]) / 10, sum(ref[-10:]) / 10
+    assert abs(pf - pr) < 0.35 * pr + 0.15, (pf, pr)
 
 
 def test_small_batch_lr01_trajectory_tracks_fp32_oracle():

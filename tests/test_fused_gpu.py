@@ -5,6 +5,7 @@ parameter gradient (relative L2), BN running statistics, and that a few fused-SG
 loss on a fixed batch.
 """
 import copy
+import os
 
 import pytest
 import torch
@@ -181,3 +182,28 @@ def test_two_stream_step_matches_single_stream():
     assert abs(l0 - l1) < 1e-4 * max(1.0, abs(l0))
     assert _rel(g1_logits, g0_logits) < 1e-4
     assert _rel(g1, g0) < 1e-3
+
+
+def test_persistent_tune_cache_reused_and_invalidated(tmp_path, monkeypatch):
+    """A second executor on the same build/device/dtype restores every autotuner choice from the table the first
+    one wrote and times nothing; a different build stamp (rebuilt .so) gets a fresh table and tunes again."""
+    from pytorchvideo_accelerate_amd.ops import tune
+    monkeypatch.setenv("PVA_TUNE_CACHE", str(tmp_path))
+    xs = _inputs(True)
+    labels = torch.tensor([1, 7], device=DEV)
+    e1 = FusedNet(_build(True), DEV)
+    l1, _ = e1.forward_backward(e1.prepare_inputs(xs), labels)
+    e1.forward_eval(e1.prepare_inputs(xs))
+    assert e1.tuner.tuned > 0 and os.path.exists(e1.tune_store.path)
+    e2 = FusedNet(_build(True), DEV)
+    assert len(e2.tuner.cache) == len(e1.tuner.cache) and len(e2.wtune) == len(e1.wtune)
+    l2, _ = e2.forward_backward(e2.prepare_inputs(xs), labels)
+    e2.forward_eval(e2.prepare_inputs(xs))
+    assert e2.tuner.tuned == 0
+    assert torch.isfinite(l2) and abs(l1.item() - l2.item()) < 0.05 * abs(l1.item())
+    real = tune.TuneStore.build_ident
+    monkeypatch.setattr(tune.TuneStore, "build_ident", staticmethod(lambda d, t: dict(real(d, t), so="stale")))
+    e3 = FusedNet(_build(True), DEV)
+    assert len(e3.tuner.cache) == 0
+    e3.forward_backward(e3.prepare_inputs(xs), labels)
+    assert e3.tuner.tuned > 0
