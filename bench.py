@@ -59,6 +59,9 @@ def parse(argv=None):
     ap.add_argument("--first-bucket-mb", type=float, default=4.0)
     ap.add_argument("--grad-dtype", choices=("fp32", "bf16"), default="fp32",
                     help="all-reduce payload dtype (bf16 = DDP bf16_compress_hook analogue)")
+    ap.add_argument("--precision", choices=("bf16", "fp16"), default="bf16",
+                    help="16-bit compute type of the fused kernels; fp16 adds dynamic loss scaling (the reference "
+                         "recipe's --mixed_precision fp16, run_slowfast_r50.sh:9)")
     ap.add_argument("--lr", type=float, default=0.1)
     ap.add_argument("--grad-accum", type=int, default=1,
                     help="micro-batches of --batch clips per optimizer step (gradients all-reduced once, on the last)")
@@ -172,7 +175,7 @@ def host_loader(a, st, eng, dev):
     ds = VideoClipDataset(paths, a.src_frames / 30.0, True, a.frames, a.crop, a.alpha, rank=st.rank,
                           world=st.world_size, distributed=st.world_size > 1, seed=0, mode="gpu")
     src = NativeRawSource(ds, a.batch, threads=a.reader_threads, drop_last=True, prefetch=3)
-    prep = GpuClipBatch(dev, a.frames, a.crop, a.alpha, s2d=eng.input_s2d)
+    prep = GpuClipBatch(dev, a.frames, a.crop, a.alpha, s2d=eng.input_s2d, dtype=eng.cdt)
     while True:
         for b in DeviceLoader(src, prep, dev):
             yield b["video"], b["label"]
@@ -191,6 +194,8 @@ def run(a):
     B = a.batch
     dump = {}
     gstep = None   # engine.graph.GraphedStep when --graph 1 (single process)
+    scaler = None
+    skipped = [0]  # fp16: optimizer steps skipped by the loss scaler (overflow)
     if a.plumbing:
         from pytorchvideo_accelerate_amd.engine.backends import TorchBackend
         be = TorchBackend(plumbing_model(a), st, "no", a.bucket_mb)
@@ -216,7 +221,11 @@ def run(a):
         assert dev.type == "cuda", "bench.py needs a GPU (or --plumbing)"
         torch.manual_seed(1234)
         model = R.create_slowfast(a.depth, a.classes)
-        eng = FusedNet(model, dev, deterministic=a.deterministic)
+        from pytorchvideo_accelerate_amd.ops.optim import FusedGradScaler
+        assert not (a.graph and a.precision == "fp16"), "--graph replays no loss-scale check"
+        eng = FusedNet(model, dev, deterministic=a.deterministic,
+                       compute_dtype=torch.float16 if a.precision == "fp16" else torch.bfloat16)
+        scaler = FusedGradScaler() if a.precision == "fp16" else None
         if st.world_size > 1:
             eng.tuner.agree = st.agree_times
         st.broadcast_tensors([eng.flat.data] + [b for b in model.buffers()])
@@ -243,7 +252,7 @@ def run(a):
             eng.C.synth_frames(frames, 7 + drank)
             # double-buffered on-device preprocessing: micro-batch k+1 is decoded/resized/cropped on its own
             # stream while micro-batch k trains (a prefetching data loader; every step still pays its batch)
-            preps = [GpuClipBatch(dev, a.frames, a.crop, a.alpha, s2d=eng.input_s2d) for _ in range(2)]
+            preps = [GpuClipBatch(dev, a.frames, a.crop, a.alpha, s2d=eng.input_s2d, dtype=eng.cdt) for _ in range(2)]
             pstream = torch.cuda.Stream(dev)
             pending = {}
 
@@ -295,17 +304,23 @@ def run(a):
                 eng.forward_backward(xs, labels_of(0), accumulate=False)
                 return None
             opt.zero_grad()
+            ls = scaler.get_scale() if scaler is not None else 1.0
             for j in range(a.grad_accum):
                 if j:
                     xs = batch(i * a.grad_accum + j)
                 last = j == a.grad_accum - 1
                 sync.begin(last)
-                loss, _ = eng.forward_backward(xs, labels_of(i * a.grad_accum + j), loss_scale=1.0 / a.grad_accum)
+                loss, _ = eng.forward_backward(xs, labels_of(i * a.grad_accum + j), loss_scale=ls / a.grad_accum)
                 sync.finish()
             if i == 0 and a.dump:
                 dump["grad"] = eng.flat.grad.clone()
             with trace_range("sgd"):
-                opt.step()
+                if scaler is not None:   # unscale + non-finite check inside the fused SGD; skipped steps back off
+                    scaler.step(opt)
+                    scaler.update()
+                    skipped[0] += int(opt.step_was_skipped)
+                else:
+                    opt.step()
             return loss
 
     if not a.plumbing:
@@ -361,6 +376,7 @@ def run(a):
                         "world_size": st.world_size}, a.dump)
     if st.is_main_process:
         headline = (a.depth, a.frames, a.crop, a.alpha) == (50, 32, 224, 4) and not a.plumbing
+        fp16 = {"loss_scale": scaler.get_scale(), "skipped_steps": skipped[0]} if scaler is not None else {}
         print(json.dumps({
             "metric": METRIC if headline else
                       f"clips/sec (whole node) SlowFast-R{a.depth} {a.frames}x2x{a.crop}; step-time p50",
@@ -374,8 +390,9 @@ def run(a):
             "higher_is_better": True,
             "scaling": "weak",
             # the stock baseline is measured on the headline config only
-            "vs_baseline": round(clips / (STOCK_CLIPS_PER_S_1GPU * st.world_size), 3) if headline else None,
-            "dtype": "fp32" if a.plumbing else "bf16",
+            "vs_baseline": (round(clips / (STOCK_CLIPS_PER_S_1GPU * st.world_size), 3)
+                            if headline and a.precision == "bf16" else None),
+            "dtype": "fp32" if a.plumbing else a.precision,
             "data": ("synthetic normal clips, CPU plumbing run" if a.plumbing else
                      "synthetic uint8 raw-frame .npy corpus (64x256x340 per video) read by the native C++ reader into "
                      "pinned memory, H2D on a copy stream, on-device preprocessing; random-init weights"
@@ -391,7 +408,7 @@ def run(a):
                        "final_loss": round(float(loss), 4) if loss is not None else None,
                        "peak_mem_gb": (round(torch.cuda.max_memory_allocated(dev) / 2**30, 1)
                                        if dev.type == "cuda" else None),
-                       **comm},
+                       **fp16, **comm},
         }), flush=True)
     st.destroy()
 

@@ -14,6 +14,8 @@
 #include "common.h"
 #include <algorithm>
 
+PVA_NS_BEGIN
+
 namespace {
 
 constexpr int NT = 256;
@@ -733,7 +735,7 @@ __global__ void avgpool_fwd_kernel(const uint16_t* __restrict__ x, int T, int H,
   if (c < C) {
     for (int i = w; i < vol; i += 4) {
       const int a = i / (kh * kw), r = i % (kh * kw), bb = r / kw, d = r % kw;
-      s += bf2f(x[((((int64_t)n * T + to + a) * H + ho + bb) * W + wo + d) * C + c]);
+      s += e2f(x[((((int64_t)n * T + to + a) * H + ho + bb) * W + wo + d) * C + c]);
     }
   }
   __shared__ float red[4][64];
@@ -762,7 +764,7 @@ __global__ void avgpool_bwd_kernel(const float* __restrict__ dout, int ldo, int 
       for (int ho = max(0, h - kh + 1); ho <= min(Ho - 1, h); ++ho)
         for (int wo = max(0, w - kw + 1); wo <= min(Wo - 1, w); ++wo)
           s += dout[(((int64_t)n * To + to) * Ho + ho) * Wo * ldo + (int64_t)wo * ldo + coff + c];
-    dx[i] = f2bf(s * inv);
+    dx[i] = f2e(s * inv);
   }
 }
 
@@ -957,3 +959,5 @@ void avgpool_bwd_launch(const float* dout, int ldo, int coff, int N, int T, int 
   hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(grid_for(total)), dim3(NT), 0, s, dout, ldo, coff, T, H, W, C, kt, kh,
                      kw, dx, N);
 }
+
+PVA_NS_END  // namespace PVA_NS

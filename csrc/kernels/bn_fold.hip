@@ -16,15 +16,16 @@
 // All reductions are fixed-order (deterministic); the fp32-MFMA tiles use v_mfma_f32_16x16x4_f32.
 #include "common.h"
 
+PVA_NS_BEGIN
+
 namespace {
 
 typedef __attribute__((ext_vector_type(4))) float f4;
 
-// 4 consecutive row elements as fp32 from a bf16 or fp32 row (k multiple of 4, 8-B / 16-B aligned rows)
+// 4 consecutive row elements as fp32 from a 16-bit or fp32 row (k multiple of 4, 8-B / 16-B aligned rows)
 __device__ __forceinline__ f4 ld4(const uint16_t* row, int k) {
   const uint2 v = *reinterpret_cast<const uint2*>(row + k);
-  return f4{__uint_as_float(v.x << 16), __uint_as_float(v.x & 0xffff0000u), __uint_as_float(v.y << 16),
-            __uint_as_float(v.y & 0xffff0000u)};
+  return f4{lo2f(v.x), hi2f(v.x), lo2f(v.y), hi2f(v.y)};
 }
 __device__ __forceinline__ f4 ld4(const float* row, int k) { return *reinterpret_cast<const f4*>(row + k); }
 
@@ -124,7 +125,7 @@ __global__ __launch_bounds__(256) void bnfold_finalize_kernel(
   if (n >= C) return;   // wave-uniform; no barriers below
   double mu = 0.0, q = 0.0;
   for (int j = lane; j < c; j += 64) {
-    const double w = (double)bf2f(Wf[(int64_t)n * c + j]);
+    const double w = (double)e2f(Wf[(int64_t)n * c + j]);
     mu += w * (double)s[j];
     q += w * (double)T[(int64_t)n * c + j];
   }
@@ -175,7 +176,7 @@ __global__ __launch_bounds__(256) void bnfold_bwd_coef_kernel(
     for (int u = 0; t < tiles; t += 256, ++u) d4[u & 3] += part[(int64_t)t * 3 * C + n];
     sdz = (d4[0] + d4[1]) + (d4[2] + d4[3]);
   }
-  for (int j = threadIdx.x; j < c; j += 256) sy += (double)bf2f(Wf[(int64_t)n * c + j]) * G[(int64_t)n * c + j];
+  for (int j = threadIdx.x; j < c; j += 256) sy += (double)e2f(Wf[(int64_t)n * c + j]) * G[(int64_t)n * c + j];
   ra[threadIdx.x] = sdz; rb[threadIdx.x] = sy;
   __syncthreads();
   for (int o = 128; o > 0; o >>= 1) {
@@ -215,7 +216,7 @@ __global__ __launch_bounds__(256) void bnfold_bwd_grad_kernel(
       const float A = coef[n], B = coef[C + n], D = coef[2 * C + n];
       const float v = A * G[o] + B * (T[o] - mean[n] * s[j]) + D * s[j];
       grad[o] = (beta == 0.f ? 0.f : beta * grad[o]) + v;
-      w1 = f2bf(A * bf2f(Wf[o]));
+      w1 = f2e(A * e2f(Wf[o]));
     }
     tile[y][tx] = w1;
   }
@@ -239,7 +240,7 @@ __global__ __launch_bounds__(256) void bnfold_w2_kernel(const uint16_t* __restri
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int i = i0 + 4 * (lane >> 4) + r;
-      if (i < c && j < c) W2[(int64_t)i * c + j] = f2bf(t[r]);
+      if (i < c && j < c) W2[(int64_t)i * c + j] = f2e(t[r]);
     }
   }
 }
@@ -257,8 +258,8 @@ __global__ __launch_bounds__(256) void bnfold_bias_kernel(const uint16_t* __rest
   __shared__ double r0[256], r1[256];
   double a = 0.0, b = 0.0;
   const double inv = 1.0 / (double)count;
-  for (int n = threadIdx.x; n < C; n += 256) a -= (double)coef[3 * C + n] * bf2f(W1t[(int64_t)j * C + n]);
-  for (int i = threadIdx.x; i < c; i += 256) b -= (double)s[i] * inv * bf2f(W2b[(int64_t)j * c + i]);
+  for (int n = threadIdx.x; n < C; n += 256) a -= (double)coef[3 * C + n] * e2f(W1t[(int64_t)j * C + n]);
+  for (int i = threadIdx.x; i < c; i += 256) b -= (double)s[i] * inv * e2f(W2b[(int64_t)j * c + i]);
   r0[threadIdx.x] = a;
   r1[threadIdx.x] = b;
   __syncthreads();
@@ -292,3 +293,5 @@ void bnfold_bwd_launch(const float* part, int tiles, const uint16_t* Wf, const u
   hipLaunchKernelGGL(bnfold_w2_kernel, dim3((c + 15) / 16, (c + 15) / 16), dim3(256), 0, st, Wd, coef, C, c, W2);
   hipLaunchKernelGGL(bnfold_bias_kernel, dim3(c), dim3(256), 0, st, W1t, W2, coef, s, C, c, count, bias);
 }
+
+PVA_NS_END  // namespace PVA_NS

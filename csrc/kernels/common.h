@@ -1,46 +1,74 @@
 // Shared device helpers for the gfx950 (CDNA4) kernels of pytorchvideo_accelerate_amd.
-// Everything here is written for 64-lane wavefronts and the MFMA 16x16x32 bf16 operand maps
+// Everything here is written for 64-lane wavefronts and the MFMA 16x16x32 bf16/f16 operand maps
 // (cdna_hip_programming.md §3: lane l holds A[l&15][8(l>>4)+j], B[8(l>>4)+j][l&15];
 //  D: col = l&15, row = 4(l>>4)+r).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-typedef uint16_t bf16_t;  // storage type of a bf16 element
-typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+// Compute element type of the translation unit.  Every kernel source is compiled twice (pytorchvideo_accelerate_amd/
+// _build.py): PVA_F16=0 -> bf16 operands in namespace pva_bf16, PVA_F16=1 -> fp16 operands in namespace pva_f16
+// (same kernels, same fp32 accumulation; v_mfma_f32_16x16x32_f16 runs at the bf16 instruction's rate).  The
+// bindings pick the namespace by the dtype of the 16-bit tensors (csrc/kernels/launchers.h).
+#ifndef PVA_F16
+#define PVA_F16 0
+#endif
+#if PVA_F16
+#define PVA_NS pva_f16
+typedef _Float16 e16s_t;                                   // arithmetic type of one element
+#define PVA_MFMA16 __builtin_amdgcn_mfma_f32_16x16x32_f16
+#else
+#define PVA_NS pva_bf16
+typedef __bf16 e16s_t;
+#define PVA_MFMA16 __builtin_amdgcn_mfma_f32_16x16x32_bf16
+#endif
+#define PVA_NS_BEGIN namespace PVA_NS {
+#define PVA_NS_END }
+
+typedef uint16_t e16_t;  // storage type of a 16-bit element (bf16 or fp16 per build)
+typedef __attribute__((ext_vector_type(8))) e16s_t ev8_t;  // MFMA 16x16x32 A/B operand
 typedef __attribute__((ext_vector_type(4))) float f32x4_t;
 typedef __attribute__((ext_vector_type(4))) short s16x4_t;
 typedef __attribute__((ext_vector_type(8))) short s16x8_t;
+typedef __attribute__((ext_vector_type(2))) float f32x2_t;
+typedef __attribute__((ext_vector_type(2))) e16s_t ev2_t;
+typedef __attribute__((ext_vector_type(2))) short s16x2_t;
 
 #define PVA_WAVE 64
 #define PVA_NXCD 8
 
-__device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+// element -> f32 (exact) for a lone element and for the low / high element of a packed pair
+#if PVA_F16
+__device__ __forceinline__ float e2f(e16_t v) { return (float)__builtin_bit_cast(_Float16, v); }
+__device__ __forceinline__ float lo2f(uint32_t w) { return e2f((e16_t)(w & 0xffffu)); }
+__device__ __forceinline__ float hi2f(uint32_t w) { return e2f((e16_t)(w >> 16)); }
+#else
+__device__ __forceinline__ float e2f(e16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+__device__ __forceinline__ float lo2f(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float hi2f(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+#endif
 
-// Round-to-nearest-even with NaN preserved (hipcc lowers the __bf16 cast to v_cvt_pk_bf16_f32).
-__device__ __forceinline__ bf16_t f2bf(float f) {
-  __bf16 b = (__bf16)f;
-  return __builtin_bit_cast(bf16_t, b);
+// Round-to-nearest-even with NaN preserved (hipcc lowers the bf16 cast to v_cvt_pk_bf16_f32; fp16 overflows to inf,
+// which the fp16 loss scaler detects in the weight gradients).
+__device__ __forceinline__ e16_t f2e(float f) {
+  e16s_t b = (e16s_t)f;
+  return __builtin_bit_cast(e16_t, b);
 }
 
-typedef __attribute__((ext_vector_type(2))) float f32x2_t;
-typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
-typedef __attribute__((ext_vector_type(2))) short s16x2_t;
-
-// 2 x f32 -> packed bf16 pair in ONE v_cvt_pk_bf16_f32 (RNE, NaN-preserving).  Two scalar __bf16 casts
-// OR-ed together cost 2 cvt + 4 mask/shift/or VALU ops per pair (measured in the ISA): the packing sits
-// in every epilogue and elementwise kernel, so it matters.
-__device__ __forceinline__ uint32_t cvt_pk_bf16(float a, float b) {
-  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){a, b}, bf16x2_t));
+// 2 x f32 -> packed pair in ONE conversion instruction (v_cvt_pk_bf16_f32; RNE, NaN-preserving).  Two scalar
+// casts OR-ed together cost 2 cvt + 4 mask/shift/or VALU ops per pair (measured in the ISA): the packing sits in
+// every epilogue and elementwise kernel, so it matters.
+__device__ __forceinline__ uint32_t cvt_pk_e16(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){a, b}, ev2_t));
 }
 
-__device__ __forceinline__ uint32_t pack2(float a, float b) { return cvt_pk_bf16(a, b); }
+__device__ __forceinline__ uint32_t pack2(float a, float b) { return cvt_pk_e16(a, b); }
 
 __device__ __forceinline__ void unpack8(const uint4& v, float* f) {
-  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
-  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
-  f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xffff0000u);
-  f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xffff0000u);
+  f[0] = lo2f(v.x); f[1] = hi2f(v.x);
+  f[2] = lo2f(v.y); f[3] = hi2f(v.y);
+  f[4] = lo2f(v.z); f[5] = hi2f(v.z);
+  f[6] = lo2f(v.w); f[7] = hi2f(v.w);
 }
 
 __device__ __forceinline__ uint4 pack8(const float* f) {
@@ -49,22 +77,22 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
 
 
 __device__ __forceinline__ uint4 pack8_fast(const float* f) {
-  return make_uint4(cvt_pk_bf16(f[0], f[1]), cvt_pk_bf16(f[2], f[3]), cvt_pk_bf16(f[4], f[5]), cvt_pk_bf16(f[6], f[7]));
+  return make_uint4(cvt_pk_e16(f[0], f[1]), cvt_pk_e16(f[2], f[3]), cvt_pk_e16(f[4], f[5]), cvt_pk_e16(f[6], f[7]));
 }
 
-// ReLU on packed bf16: bf16 is sign-magnitude, so max as signed int16 against 0 zeroes every negative
-// (and -0) lane and keeps positives: one v_pk_max_i16 per pair.
-__device__ __forceinline__ uint32_t relu_bf16x2(uint32_t w) {
+// ReLU on packed 16-bit floats: bf16 and fp16 are sign-magnitude, so max as signed int16 against 0 zeroes every
+// negative (and -0) lane and keeps positives: one v_pk_max_i16 per pair.
+__device__ __forceinline__ uint32_t relu_e16x2(uint32_t w) {
   return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(s16x2_t, w), (s16x2_t){0, 0}));
 }
 
-__device__ __forceinline__ uint4 relu_bf16x8(const uint4& v) {
-  return make_uint4(relu_bf16x2(v.x), relu_bf16x2(v.y), relu_bf16x2(v.z), relu_bf16x2(v.w));
+__device__ __forceinline__ uint4 relu_e16x8(const uint4& v) {
+  return make_uint4(relu_e16x2(v.x), relu_e16x2(v.y), relu_e16x2(v.z), relu_e16x2(v.w));
 }
 
 __device__ __forceinline__ void unpack4(const uint2& v, float* f) {
-  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
-  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
+  f[0] = lo2f(v.x); f[1] = hi2f(v.x);
+  f[2] = lo2f(v.y); f[3] = hi2f(v.y);
 }
 
 __device__ __forceinline__ uint2 pack4(const float* f) {

@@ -24,6 +24,8 @@
 #include "common.h"
 #include "conv_params.h"
 
+PVA_NS_BEGIN
+
 namespace {
 
 constexpr int DNT = 256;          // threads per workgroup (4 waves)
@@ -169,10 +171,10 @@ __global__ __launch_bounds__(DNT) void conv_direct_kernel(const ConvParams p, in
       for (int kb = 0; kb < KB; ++kb) {
         const int s = s0 + kb;
         if (s >= KS) break;   // wave-uniform
-        bf16x8_t bw[NB];
+        ev8_t bw[NB];
 #pragma unroll
         for (int nb = 0; nb < NB; ++nb)
-          bw[nb] = *reinterpret_cast<const bf16x8_t*>(wfrag + nb * 16 * pitch * 2 + s * 64);
+          bw[nb] = *reinterpret_cast<const ev8_t*>(wfrag + nb * 16 * pitch * 2 + s * 64);
         if (p.affine) {
           const float* sp = aff + cin0[kb];
           const f32x4_t c0 = *reinterpret_cast<const f32x4_t*>(sp);
@@ -188,16 +190,16 @@ __global__ __launch_bounds__(DNT) void conv_direct_kernel(const ConvParams p, in
 #pragma unroll
             for (int k = 0; k < 8; ++k) f[k] = __builtin_fmaf(f[k], sc8[k], sh8[k]);
             uint4 v = pack8_fast(f);
-            if (p.affine == 2) v = relu_bf16x8(v);
+            if (p.affine == 2) v = relu_e16x8(v);
             a[kb][g] = (okm >> (kb * RT + g)) & 1u ? v : uint4{0, 0, 0, 0};
           }
         }
 #pragma unroll
         for (int g = 0; g < RT; ++g) {
-          const bf16x8_t av = __builtin_bit_cast(bf16x8_t, a[kb][g]);
+          const ev8_t av = __builtin_bit_cast(ev8_t, a[kb][g]);
 #pragma unroll
           for (int nb = 0; nb < NB; ++nb)
-            acc[g][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[nb], av, acc[g][nb], 0, 0, 0);
+            acc[g][nb] = PVA_MFMA16(bw[nb], av, acc[g][nb], 0, 0, 0);
         }
       }
     }
@@ -365,3 +367,5 @@ void conv_direct_launch(const ConvParams& p, int cfg, hipStream_t s) {
     default: direct_launch_nb<4>(p, rpb, epi, half, s); break;
   }
 }
+
+PVA_NS_END  // namespace PVA_NS

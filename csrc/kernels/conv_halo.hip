@@ -28,6 +28,8 @@
 #include "common.h"
 #include "conv_params.h"
 
+PVA_NS_BEGIN
+
 namespace {
 
 constexpr int HC_THREADS = 256;
@@ -174,7 +176,7 @@ __global__ __launch_bounds__(HC_THREADS, 2) void conv_halo_kernel(const ConvPara
 #pragma unroll
           for (int e = 0; e < 8; ++e) f[e] = __builtin_fmaf(f[e], sc[e], sh[e]);
           o = pack8_fast(f);
-          if constexpr (AFF == 2) o = relu_bf16x8(o);
+          if constexpr (AFF == 2) o = relu_e16x8(o);
           if (!ok[u]) o = uint4{0, 0, 0, 0};   // zero padding of the activation itself
         }
         *reinterpret_cast<uint4*>(smem + (cg * NPOSP + bb[u]) * 16) = o;
@@ -197,16 +199,16 @@ __global__ __launch_bounds__(HC_THREADS, 2) void conv_halo_kernel(const ConvPara
         const int ss = s + u;
         bload(ss + HC_RING - 1, bq[(u + HC_RING - 1) % HC_RING]);
         const int ao = step_a(ss);
-        bf16x8_t af[HC_MW];
+        ev8_t af[HC_MW];
 #pragma unroll
         for (int i = 0; i < HC_MW; ++i)
-          if (i < mwr) af[i] = *reinterpret_cast<const bf16x8_t*>(smem + abase[i] + ao);
+          if (i < mwr) af[i] = *reinterpret_cast<const ev8_t*>(smem + abase[i] + ao);
 #pragma unroll
         for (int i = 0; i < HC_MW; ++i) {
           if (i >= mwr) continue;
 #pragma unroll
           for (int j = 0; j < NWB; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, bq[u][j]), af[i],
+            acc[i][j] = PVA_MFMA16(__builtin_bit_cast(ev8_t, bq[u][j]), af[i],
                                                                 acc[i][j], 0, 0, 0);
         }
       }
@@ -457,7 +459,7 @@ __global__ __launch_bounds__(HP_THREADS, 1) void conv_halo64p_kernel(const ConvP
 #pragma unroll
         for (int e = 0; e < 8; ++e) f[e] = __builtin_fmaf(f[e], sc[e], sh[e]);
         o = pack8_fast(f);
-        if constexpr (AFF == 2) o = relu_bf16x8(o);
+        if constexpr (AFF == 2) o = relu_e16x8(o);
         const int h = r0 - 1 + ((hcode[u] >> 16) & 255);
         if (!((hcode[u] >> 24) && (unsigned)h < (unsigned)H)) o = uint4{0, 0, 0, 0};   // padding stays zero
       }
@@ -507,14 +509,14 @@ __global__ __launch_bounds__(HP_THREADS, 1) void conv_halo64p_kernel(const ConvP
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    bf16x8_t wa[2][2], xb[2][4];
+    ev8_t wa[2][2], xb[2][4];
     auto frag = [&](int s, int c) {
       const int jh = (s >> 1) / 3, jw = (s >> 1) % 3;   // (s is a compile-time constant of the unrolled loop)
       const int ao = ((-DIR + DIR * jh) * PW + (-DIR + DIR * jw)) * 16 + (s & 1) * 4 * NPOSP * 16;
 #pragma unroll
-      for (int j = 0; j < 2; ++j) wa[c][j] = *reinterpret_cast<const bf16x8_t*>(WI + s * 4096 + j * 256 + wbase);
+      for (int j = 0; j < 2; ++j) wa[c][j] = *reinterpret_cast<const ev8_t*>(WI + s * 4096 + j * 256 + wbase);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) xb[c][i] = *reinterpret_cast<const bf16x8_t*>(HI + abase[i] + ao);
+      for (int i = 0; i < 4; ++i) xb[c][i] = *reinterpret_cast<const ev8_t*>(HI + abase[i] + ao);
     };
     frag(0, 0);
 #pragma unroll
@@ -528,7 +530,7 @@ __global__ __launch_bounds__(HP_THREADS, 1) void conv_halo64p_kernel(const ConvP
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[c][j], xb[c][i], acc[i][j], 0, 0, 0);
+          acc[i][j] = PVA_MFMA16(wa[c][j], xb[c][i], acc[i][j], 0, 0, 0);
     }
 
     // ---- epilogue: lane holds channels 32 wn + 16 j + 4 fg + r of position (b0 + i) * 16 + fr
@@ -662,7 +664,7 @@ __global__ __launch_bounds__(HC_THREADS) void conv_halo_narrow_kernel(const Conv
     }
   }
   // this lane's weights of every k-step (A operand: row = output channel, 8 k = 8 channels of its group's tap)
-  bf16x8_t wf[NSTEP][NB];
+  ev8_t wf[NSTEP][NB];
   int toff[NSTEP];
   const int chb = (fg % GPT) * 16;
 #pragma unroll
@@ -677,7 +679,7 @@ __global__ __launch_bounds__(HC_THREADS) void conv_halo_narrow_kernel(const Conv
       const int co = j * 16 + fr;
       uint4 v = uint4{0, 0, 0, 0};
       if (real && co < p.Ngemm) v = *reinterpret_cast<const uint4*>(p.w + (size_t)co * p.Kfull + wt * CG + (fg % GPT) * 8);
-      wf[s][j] = __builtin_bit_cast(bf16x8_t, v);
+      wf[s][j] = __builtin_bit_cast(ev8_t, v);
     }
   }
   __syncthreads();
@@ -716,7 +718,7 @@ __global__ __launch_bounds__(HC_THREADS) void conv_halo_narrow_kernel(const Conv
 #pragma unroll
           for (int e = 0; e < 8; ++e) f[e] = __builtin_fmaf(f[e], sc[e], sh[e]);
           o = pack8_fast(f);
-          if constexpr (AFF == 2) o = relu_bf16x8(o);
+          if constexpr (AFF == 2) o = relu_e16x8(o);
           if (!ok[u]) o = uint4{0, 0, 0, 0};
         }
         *reinterpret_cast<uint4*>(box + bb * (CG * 2) + cgp * 16) = o;
@@ -741,9 +743,9 @@ __global__ __launch_bounds__(HC_THREADS) void conv_halo_narrow_kernel(const Conv
     for (int j = 0; j < NB; ++j) acc[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < NSTEP; ++s) {
-      const bf16x8_t xf = *reinterpret_cast<const bf16x8_t*>(src + toff[s]);
+      const ev8_t xf = *reinterpret_cast<const ev8_t*>(src + toff[s]);
 #pragma unroll
-      for (int j = 0; j < NB; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[s][j], xf, acc[j], 0, 0, 0);
+      for (int j = 0; j < NB; ++j) acc[j] = PVA_MFMA16(wf[s][j], xf, acc[j], 0, 0, 0);
     }
     if (pl >= P) continue;
     const int row = fbase + r0 * W + pl;
@@ -886,3 +888,5 @@ void conv_halo_launch(const ConvParams& p, int cfg, hipStream_t st) {
   if ((cfg & 1) || p.Ngemm % 128 != 0) launch_ntile<64>(p, R, epi, st);
   else launch_ntile<128>(p, R, epi, st);
 }
+
+PVA_NS_END  // namespace PVA_NS

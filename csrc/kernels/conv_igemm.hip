@@ -22,6 +22,8 @@
 #include "conv_params.h"
 #include <type_traits>
 
+PVA_NS_BEGIN
+
 namespace {
 
 // LDS tile rows are BK bf16 (64 or 128 bytes) of 16-byte slots, XOR-swizzled so that the 16-lane
@@ -86,26 +88,26 @@ __device__ __forceinline__ int lds_off(int row, int slot) {
 template <int BK, int TM, int TN>
 __device__ __forceinline__ void mma_ktile(const char* A, const int (&fa)[BK / 32][TM], const int (&fb)[BK / 32][TN],
                                           f32x4_t (&acc)[TM][TN]) {
-  bf16x8_t af[2][TM], bfr[2][TN];
+  ev8_t af[2][TM], bfr[2][TN];
 #pragma unroll
-  for (int i = 0; i < TM; ++i) af[0][i] = *reinterpret_cast<const bf16x8_t*>(A + fa[0][i]);
+  for (int i = 0; i < TM; ++i) af[0][i] = *reinterpret_cast<const ev8_t*>(A + fa[0][i]);
 #pragma unroll
-  for (int j = 0; j < TN; ++j) bfr[0][j] = *reinterpret_cast<const bf16x8_t*>(A + fb[0][j]);
+  for (int j = 0; j < TN; ++j) bfr[0][j] = *reinterpret_cast<const ev8_t*>(A + fb[0][j]);
 #pragma unroll
   for (int kk = 0; kk < BK / 32; ++kk) {
     const int c = kk & 1;
     if (kk + 1 < BK / 32) {
 #pragma unroll
-      for (int i = 0; i < TM; ++i) af[c ^ 1][i] = *reinterpret_cast<const bf16x8_t*>(A + fa[kk + 1][i]);
+      for (int i = 0; i < TM; ++i) af[c ^ 1][i] = *reinterpret_cast<const ev8_t*>(A + fa[kk + 1][i]);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) bfr[c ^ 1][j] = *reinterpret_cast<const bf16x8_t*>(A + fb[kk + 1][j]);
+      for (int j = 0; j < TN; ++j) bfr[c ^ 1][j] = *reinterpret_cast<const ev8_t*>(A + fb[kk + 1][j]);
       __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[c][j], af[c][i], acc[i][j], 0, 0, 0);
+        acc[i][j] = PVA_MFMA16(bfr[c][j], af[c][i], acc[i][j], 0, 0, 0);
   }
 }
 
@@ -299,7 +301,7 @@ void conv_igemm_kernel(const ConvParams p) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) f[e] = __builtin_fmaf(f[e], sc8[e], sh8[e]);
           v = pack8_fast(f);
-          if constexpr (uaff == 2) v = relu_bf16x8(v);
+          if constexpr (uaff == 2) v = relu_e16x8(v);
           if constexpr (check) if (!((ra_valid >> s) & 1u)) v = uint4{0, 0, 0, 0};  // zero padding of the activation
         }
         *reinterpret_cast<uint4*>(A + sa[s]) = v;
@@ -368,18 +370,18 @@ void conv_igemm_kernel(const ConvParams p) {
       // of the tile is done and its buffer can take the DMA of tile step+2, and (b) tile step+1 has landed, so
       // its first-half fragments are read while the second-half MFMAs of this tile run.  No k-step starts on
       // fragments still in flight; only barrier skew is exposed.
-      bf16x8_t fa0[TM], fb0[TN], fa1[TM], fb1[TN];
+      ev8_t fa0[TM], fb0[TN], fa1[TM], fb1[TN];
       vm_wait<0>();
       __syncthreads();   // tile 0 landed
       if (nsteps > 1) issue_dma(1);
 #pragma unroll
-      for (int i = 0; i < TM; ++i) fa0[i] = *reinterpret_cast<const bf16x8_t*>(smem + fa[0][i]);
+      for (int i = 0; i < TM; ++i) fa0[i] = *reinterpret_cast<const ev8_t*>(smem + fa[0][i]);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) fb0[j] = *reinterpret_cast<const bf16x8_t*>(smem + fb[0][j]);
+      for (int j = 0; j < TN; ++j) fb0[j] = *reinterpret_cast<const ev8_t*>(smem + fb[0][j]);
 #pragma unroll
-      for (int i = 0; i < TM; ++i) fa1[i] = *reinterpret_cast<const bf16x8_t*>(smem + fa[1][i]);
+      for (int i = 0; i < TM; ++i) fa1[i] = *reinterpret_cast<const ev8_t*>(smem + fa[1][i]);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) fb1[j] = *reinterpret_cast<const bf16x8_t*>(smem + fb[1][j]);
+      for (int j = 0; j < TN; ++j) fb1[j] = *reinterpret_cast<const ev8_t*>(smem + fb[1][j]);
       for (int step = 0; step < nsteps; ++step) {
         const int cur = step & 1;
         __builtin_amdgcn_sched_barrier(0);
@@ -387,7 +389,7 @@ void conv_igemm_kernel(const ConvParams p) {
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb0[j], fa0[i], acc[i][j], 0, 0, 0);
+            acc[i][j] = PVA_MFMA16(fb0[j], fa0[i], acc[i][j], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
         vm_wait<0>();   // this wave's DMA of tile step+1
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's reads of tile step
@@ -398,22 +400,22 @@ void conv_igemm_kernel(const ConvParams p) {
         const char* An = smem + (cur ^ 1) * TILE_BYTES;
         if (more) {
 #pragma unroll
-          for (int i = 0; i < TM; ++i) fa0[i] = *reinterpret_cast<const bf16x8_t*>(An + fa[0][i]);
+          for (int i = 0; i < TM; ++i) fa0[i] = *reinterpret_cast<const ev8_t*>(An + fa[0][i]);
 #pragma unroll
-          for (int j = 0; j < TN; ++j) fb0[j] = *reinterpret_cast<const bf16x8_t*>(An + fb[0][j]);
+          for (int j = 0; j < TN; ++j) fb0[j] = *reinterpret_cast<const ev8_t*>(An + fb[0][j]);
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[j], fa1[i], acc[i][j], 0, 0, 0);
+            acc[i][j] = PVA_MFMA16(fb1[j], fa1[i], acc[i][j], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
         if (more) {
 #pragma unroll
-          for (int i = 0; i < TM; ++i) fa1[i] = *reinterpret_cast<const bf16x8_t*>(An + fa[1][i]);
+          for (int i = 0; i < TM; ++i) fa1[i] = *reinterpret_cast<const ev8_t*>(An + fa[1][i]);
 #pragma unroll
-          for (int j = 0; j < TN; ++j) fb1[j] = *reinterpret_cast<const bf16x8_t*>(An + fb[1][j]);
+          for (int j = 0; j < TN; ++j) fb1[j] = *reinterpret_cast<const ev8_t*>(An + fb[1][j]);
         }
       }
     } else
@@ -455,16 +457,16 @@ void conv_igemm_kernel(const ConvParams p) {
       } else {
 #pragma unroll
         for (int kk = 0; kk < BK / 32; ++kk) {
-          bf16x8_t af[TM], bfr[TN];
+          ev8_t af[TM], bfr[TN];
 #pragma unroll
-          for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8_t*>(A + fa[kk][i]);
+          for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const ev8_t*>(A + fa[kk][i]);
 #pragma unroll
-          for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const bf16x8_t*>(A + fb[kk][j]);
+          for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const ev8_t*>(A + fb[kk][j]);
 #pragma unroll
           for (int i = 0; i < TM; ++i)
 #pragma unroll
             for (int j = 0; j < TN; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+              acc[i][j] = PVA_MFMA16(bfr[j], af[i], acc[i][j], 0, 0, 0);
         }
       }
     }
@@ -603,16 +605,16 @@ void conv_igemm_kernel(const ConvParams p) {
       const char* A = smem + cur * TILE_BYTES;
   #pragma unroll
       for (int kk = 0; kk < BK / 32; ++kk) {
-        bf16x8_t af[TM], bfr[TN];
+        ev8_t af[TM], bfr[TN];
   #pragma unroll
-        for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8_t*>(A + fa[kk][i]);
+        for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const ev8_t*>(A + fa[kk][i]);
   #pragma unroll
-        for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const bf16x8_t*>(A + fb[kk][j]);
+        for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const ev8_t*>(A + fb[kk][j]);
   #pragma unroll
         for (int i = 0; i < TM; ++i)
   #pragma unroll
           for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+            acc[i][j] = PVA_MFMA16(bfr[j], af[i], acc[i][j], 0, 0, 0);
       }
     }
   }
@@ -1069,3 +1071,5 @@ void conv_igemm_launch(const ConvParams& p, int chunk, hipStream_t stream, int c
     if (bk == 64) launch_variant<4, 64>(v, p, ut_force, stream); else launch_variant<4, 32>(v, p, ut_force, stream);
   }
 }
+
+PVA_NS_END  // namespace PVA_NS

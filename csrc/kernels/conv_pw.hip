@@ -7,6 +7,8 @@
 #include <cstdio>
 #include <stdexcept>
 
+PVA_NS_BEGIN
+
 bool conv_pw_run_ks1(const ConvParams& p, int ep, int ops, int rpb, int gch, size_t lds, hipStream_t st);
 bool conv_pw_run_ks2(const ConvParams& p, int ep, int ops, int rpb, int gch, size_t lds, hipStream_t st);
 bool conv_pw_run_ks4(const ConvParams& p, int ep, int ops, int rpb, int gch, size_t lds, hipStream_t st);
@@ -88,3 +90,5 @@ void conv_pw_launch(const ConvParams& p, int cfg, hipStream_t st) {
     throw std::runtime_error(msg);
   }
 }
+
+PVA_NS_END  // namespace PVA_NS

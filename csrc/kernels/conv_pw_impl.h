@@ -33,6 +33,8 @@
 #include "conv_params.h"
 #include <algorithm>
 
+PVA_NS_BEGIN
+
 namespace {
 
 constexpr int PW_WAVES = 8;
@@ -253,7 +255,7 @@ __global__ __launch_bounds__(PW_THREADS) void conv_pw_kernel(const ConvParams p,
     if (++ip == nit) { ip = 0; ++tp; }
   };
   if (ntw > 0) load_a(mfirst);
-  bf16x8_t a[TM][KS];
+  ev8_t a[TM][KS];
 #pragma unroll 1
   for (int t = 0; t < ntw; ++t) {
     const int m0 = mfirst + t * tstride;
@@ -279,7 +281,7 @@ __global__ __launch_bounds__(PW_THREADS) void conv_pw_kernel(const ConvParams p,
             }
             v = pack8_fast(f);
           }
-          a[i][s] = __builtin_bit_cast(bf16x8_t, v);
+          a[i][s] = __builtin_bit_cast(ev8_t, v);
         }
       if (t + 1 < ntw) load_a(m0 + tstride);
     }
@@ -303,12 +305,12 @@ __global__ __launch_bounds__(PW_THREADS) void conv_pw_kernel(const ConvParams p,
         const char* wc = smem + (c * 2 * KS) * 1024 + lane * 16;
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
-          const bf16x8_t w0 = *reinterpret_cast<const bf16x8_t*>(wc + s * 1024);
-          const bf16x8_t w1 = *reinterpret_cast<const bf16x8_t*>(wc + (KS + s) * 1024);
+          const ev8_t w0 = *reinterpret_cast<const ev8_t*>(wc + s * 1024);
+          const ev8_t w1 = *reinterpret_cast<const ev8_t*>(wc + (KS + s) * 1024);
 #pragma unroll
           for (int i = 0; i < TM; ++i) {
-            acc[i][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0, a[i][s], acc[i][0], 0, 0, 0);
-            acc[i][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1, a[i][s], acc[i][1], 0, 0, 0);
+            acc[i][0] = PVA_MFMA16(w0, a[i][s], acc[i][0], 0, 0, 0);
+            acc[i][1] = PVA_MFMA16(w1, a[i][s], acc[i][1], 0, 0, 0);
           }
         }
         // ---- epilogue (operands in P[0][cc])
@@ -524,3 +526,4 @@ bool launch_ks(const ConvParams& p, int ep, int ops, int rpb, int gch, size_t ld
 
 }  // namespace
 
+PVA_NS_END  // namespace PVA_NS

@@ -17,6 +17,8 @@
 #include "wgrad_rt_impl.h"
 #include <type_traits>
 
+PVA_NS_BEGIN
+
 namespace {
 
 // BP (template): positions per LDS stage = 32 (one MFMA k-step) or 64 (two k-steps per barrier pair)
@@ -275,7 +277,7 @@ void conv_wgrad_kernel(const WgradParams p) {
         for (int e = 0; e < CH; ++e) f[e] = __builtin_fmaf(f[e], asc[e], ash[e]);
         if constexpr (CH == 8) {
           v = pack8_fast(f);
-          if (affine == 2) v = relu_bf16x8(v);
+          if (affine == 2) v = relu_e16x8(v);
           if ((!DENSE || dy_aff) && !((rb_valid >> s) & 1u)) v = uint4{0, 0, 0, 0};   // padding stays zero
         } else {
           if (affine == 2)
@@ -331,26 +333,26 @@ void conv_wgrad_kernel(const WgradParams p) {
     const char* A = smem + cur * TILE;
 #pragma unroll
     for (int kk = 0; kk < BP / 32; ++kk) {   // rows 32*kk.. of the stage: same swizzle (row bits 0-3)
-      bf16x8_t af[TM], bfr[TN];
+      ev8_t af[TM], bfr[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         s16x4_t lo = tr_read(A + kk * 32 * BMW * 2 + ta[i][0]);
         s16x4_t hi = tr_read(A + kk * 32 * BMW * 2 + ta[i][1]);
         s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        af[i] = __builtin_bit_cast(bf16x8_t, v);
+        af[i] = __builtin_bit_cast(ev8_t, v);
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         s16x4_t lo = tr_read(A + kk * 32 * BNW * 2 + tb[j][0]);
         s16x4_t hi = tr_read(A + kk * 32 * BNW * 2 + tb[j][1]);
         s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        bfr[j] = __builtin_bit_cast(bf16x8_t, v);
+        bfr[j] = __builtin_bit_cast(ev8_t, v);
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = PVA_MFMA16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
   }
 
@@ -511,21 +513,21 @@ __global__ __launch_bounds__(256) void wgrad_narrow_kernel(const WgradParams p) 
 #pragma unroll
     for (int hlf = 0; hlf < 2; ++hlf) {
       const int rb0 = hlf * 32;
-      bf16x8_t af[MT];
+      ev8_t af[MT];
 #pragma unroll
       for (int i = 0; i < MT; ++i) {
         const s16x4_t lo = tr_read(A + img_off<MP>(rb0 + tr_row, i * 32 + tr_colb));
         const s16x4_t hi = tr_read(A + img_off<MP>(rb0 + tr_row + 4, i * 32 + tr_colb));
-        af[i] = __builtin_bit_cast(bf16x8_t, (s16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
+        af[i] = __builtin_bit_cast(ev8_t, (s16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
       }
 #pragma unroll
       for (int j = 0; j < NTN; ++j) {
         const s16x4_t blo = tr_read(B + img_off<KP>(rb0 + tr_row, j * 32 + tr_colb));
         const s16x4_t bhi = tr_read(B + img_off<KP>(rb0 + tr_row + 4, j * 32 + tr_colb));
-        const bf16x8_t bf = __builtin_bit_cast(bf16x8_t,
+        const ev8_t bf = __builtin_bit_cast(ev8_t,
                                                (s16x8_t){blo[0], blo[1], blo[2], blo[3], bhi[0], bhi[1], bhi[2], bhi[3]});
 #pragma unroll
-        for (int i = 0; i < MT; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf, acc[i][j], 0, 0, 0);
+        for (int i = 0; i < MT; ++i) acc[i][j] = PVA_MFMA16(af[i], bf, acc[i][j], 0, 0, 0);
       }
     }
   }
@@ -715,3 +717,5 @@ void wgrad_reduce_launch(float* accbuf, float* grad, int splits, int Cout, int t
   hipLaunchKernelGGL(wgrad_convert_kernel, dim3(blocks), dim3(256), 0, stream, accbuf, grad, total, taps, Cin,
                      Cin_real, scale, beta, slab ? 0 : 1, slab ? splits : 1, (int64_t)Cout * taps * Cin);
 }
+
+PVA_NS_END  // namespace PVA_NS

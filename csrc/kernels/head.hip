@@ -14,6 +14,8 @@
 // backward regenerates them instead of storing them (not bitwise torch's stream: documented deviation).
 #include "common.h"
 
+PVA_NS_BEGIN
+
 namespace {
 
 // ---------------------------------------------------------------------------------- Philox4x32-10
@@ -349,3 +351,5 @@ void head_dropout_mask_launch(int64_t total, float p_drop, uint64_t seed, uint8_
   hipLaunchKernelGGL(head_dropout_mask_kernel, dim3((int)blocks), dim3(256), 0, s, total, (uint32_t)seed,
                      (uint32_t)(seed >> 32), thresh_of(p_drop), out);
 }
+
+PVA_NS_END  // namespace PVA_NS

@@ -12,6 +12,8 @@
 //   (normalisation commutes with the bilinear resize since the weights sum to 1).
 #include "common.h"
 
+PVA_NS_BEGIN
+
 namespace {
 
 // GradScaler pre-pass: flag = 1 if any g*gscale is inf/nan (torch _amp_foreach_non_finite_check_and_unscale_)
@@ -90,7 +92,7 @@ __global__ void pack_weights_kernel(const float* __restrict__ master, uint16_t* 
       const int n = nb + ty + 8 * k, c = cb + tx;
       uint16_t v = 0;
       if (n < d.cout && c < d.cin) {
-        v = f2bf(src[(n * d.cin + c) * d.taps + tap]);
+        v = f2e(src[(n * d.cin + c) * d.taps + tap]);
         fo[(n * d.taps + tap) * d.cin_pad + c] = v;
       }
       tile[ty + 8 * k][tx] = v;
@@ -207,3 +209,5 @@ void synth_frames_launch(uint8_t* out, int64_t n, uint32_t seed, hipStream_t s) 
   if (blocks > 16384) blocks = 16384;
   hipLaunchKernelGGL(synth_frames_kernel, dim3((int)blocks), dim3(256), 0, s, out, n, seed);
 }
+
+PVA_NS_END  // namespace PVA_NS

@@ -19,6 +19,8 @@
 #include "common.h"
 #include <cstdlib>
 
+PVA_NS_BEGIN
+
 namespace {
 
 constexpr int TH = 8, TW = 16;              // output tile (positions = 128 = 4 waves x 2 rows)
@@ -102,12 +104,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void s
   const __amdgpu_buffer_rsrc_t xr =
       clip_rsrc(p.x + (int64_t)n * p.T * p.Hs * p.Ws * 16, (uint32_t)(p.T * p.Hs * p.Ws * 32));
   // weight fragments (A operand: lane holds W[co = 16*c + li][k = 32*ks + 8*g .. +8])
-  bf16x8_t wa[COT][KSTEPS];
+  ev8_t wa[COT][KSTEPS];
 #pragma unroll
   for (int c = 0; c < COT; ++c)
 #pragma unroll
     for (int ks = 0; ks < KSTEPS; ++ks)
-      wa[c][ks] = *reinterpret_cast<const bf16x8_t*>(p.w + (int64_t)(16 * c + li) * (TAPS * 16) + ks * 32 + 8 * g);
+      wa[c][ks] = *reinterpret_cast<const ev8_t*>(p.w + (int64_t)(16 * c + li) * (TAPS * 16) + ks * 32 + 8 * g);
 
   // prologue: frames -pt .. -pt+KT-1 into slots 0..KT-1 (frame ti lives in slot (ti + pt) % SLOTS)
   for (int f = 0; f < KT; ++f) dma_patch(xr, p, f - p.pt, ho0, wo0, smem + f * SLOT_BYTES);
@@ -137,11 +139,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void s
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const int hh = 2 * w + q;
-        const bf16x8_t xb = *reinterpret_cast<const bf16x8_t*>(
+        const ev8_t xb = *reinterpret_cast<const ev8_t*>(
             slot + ((hh + bh) * PW + (ww + bw)) * POSB + half * 16);
 #pragma unroll
         for (int c = 0; c < COT; ++c)
-          acc[q][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[c][ks], xb, acc[q][c], 0, 0, 0);
+          acc[q][c] = PVA_MFMA16(wa[c][ks], xb, acc[q][c], 0, 0, 0);
       }
     }
     __syncthreads();  // next frame landed; window frame 0's slot is free.  Stores after the barrier.
@@ -253,13 +255,13 @@ __global__ __launch_bounds__(256) void stem_wgrad_kernel(const StemParams p) {
       // positions of this k-step: rows 2*kstep, 2*kstep+1; group g -> row 2*kstep + (g >> 1), w 8*(g&1)..+7
       const int hh = 2 * kstep + (g >> 1);
       const int wq = 8 * (g & 1) + rq;          // position column of the lane's tr-read row (first block)
-      bf16x8_t a[COT];
+      ev8_t a[COT];
 #pragma unroll
       for (int c = 0; c < COT; ++c) {
         const char* base = dcur + (hh * TW + wq) * COP * 2 + c * 32 + cb;
         s16x4_t lo = trr(base), hi = trr(base + 4 * COP * 2);
         s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        a[c] = __builtin_bit_cast(bf16x8_t, v);
+        a[c] = __builtin_bit_cast(ev8_t, v);
       }
 #pragma unroll
       for (int t = 0; t < TPW; ++t) {
@@ -269,10 +271,10 @@ __global__ __launch_bounds__(256) void stem_wgrad_kernel(const StemParams p) {
         const char* base = slot + ((hh + bh) * PW + (wq + bw)) * POSB + cb;
         s16x4_t lo = trr(base), hi = trr(base + 4 * POSB);
         s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        const bf16x8_t xb = __builtin_bit_cast(bf16x8_t, v);
+        const ev8_t xb = __builtin_bit_cast(ev8_t, v);
 #pragma unroll
         for (int c = 0; c < COT; ++c)
-          acc[c][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[c], xb, acc[c][t], 0, 0, 0);
+          acc[c][t] = PVA_MFMA16(a[c], xb, acc[c][t], 0, 0, 0);
       }
     }
     __syncthreads();  // next frame + dY tile landed; the window's first slot and this dY buffer are free
@@ -299,9 +301,9 @@ __global__ __launch_bounds__(256) void stem_wgrad_kernel(const StemParams p) {
 // serves both frames — KT+1 input frames per output pair instead of 2*KT (40 % fewer MFMAs at KT = 5).
 // The wgrad kernel mirrors it with the dY tiles of the two frames stacked as 16 "channels".
 // ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ bf16x8_t ld_frag(const uint16_t* p, bool ok) {
+__device__ __forceinline__ ev8_t ld_frag(const uint16_t* p, bool ok) {
   const uint4 u = ok ? *reinterpret_cast<const uint4*>(p) : make_uint4(0, 0, 0, 0);
-  return __builtin_bit_cast(bf16x8_t, u);
+  return __builtin_bit_cast(ev8_t, u);
 }
 
 template <int KT>
@@ -325,7 +327,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void s
 
   for (int f = 0; f < J; ++f) dma_patch(xr, p, f - p.pt, ho0, wo0, smem + f * SLOT_BYTES);
 
-  bf16x8_t wa[J][KS];
+  ev8_t wa[J][KS];
 #pragma unroll
   for (int j = 0; j < J; ++j) {
     const int dt = li < 8 ? j : j - 1;
@@ -355,9 +357,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void s
         const int bh = tap >> 2, bw = tap & 3;
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
-          const bf16x8_t xb = *reinterpret_cast<const bf16x8_t*>(
+          const ev8_t xb = *reinterpret_cast<const ev8_t*>(
               slot + ((2 * w + q + bh) * PW + (li + bw)) * POSB + half * 16);
-          acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[j][ks], xb, acc[q], 0, 0, 0);
+          acc[q] = PVA_MFMA16(wa[j][ks], xb, acc[q], 0, 0, 0);
         }
       }
     }
@@ -455,12 +457,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void s
     for (int kstep = 0; kstep < TH * TW / 32; ++kstep) {
       const int hh = 2 * kstep + (g >> 1);
       const int wq = 8 * (g & 1) + rq;
-      bf16x8_t a;
+      ev8_t a;
       {
         const int dp = hh * TW + wq;
         s16x4_t lo = trr(dcur + pswz(dp) * 32 + cb), hi = trr(dcur + pswz(dp + 4) * 32 + cb);
         s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        a = __builtin_bit_cast(bf16x8_t, v);
+        a = __builtin_bit_cast(ev8_t, v);
       }
 #pragma unroll
       for (int j = 0; j < J; ++j) {
@@ -470,7 +472,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void s
           const int ip = (hh + w) * PW + (wq + s);
           s16x4_t lo = trr(slot + pswz(ip) * POSB + cb), hi = trr(slot + pswz(ip + 4) * POSB + cb);
           s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-          acc[j][s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf16x8_t, v), acc[j][s], 0, 0, 0);
+          acc[j][s] = PVA_MFMA16(a, __builtin_bit_cast(ev8_t, v), acc[j][s], 0, 0, 0);
         }
       }
     }
@@ -524,7 +526,7 @@ __global__ void stem_pack_kernel(const float* __restrict__ w, uint16_t* __restri
     float v = 0.f;
     if (co < Cout && c < 3 && kh >= 0 && kh < 7 && kw >= 0 && kw < 7)
       v = w[(((co * 3 + c) * kt + dt) * 7 + kh) * 7 + kw];
-    out[i] = f2bf(v);
+    out[i] = f2e(v);
   }
 }
 
@@ -600,3 +602,5 @@ void stem_pack_launch(const float* w, uint16_t* out, int Cout, int kt, hipStream
   const int total = Cpad * kt * 256;
   hipLaunchKernelGGL(stem_pack_kernel, dim3((total + 255) / 256), dim3(256), 0, s, w, out, Cout, Cpad, kt);
 }
+
+PVA_NS_END  // namespace PVA_NS

@@ -22,6 +22,8 @@
 #include "common.h"
 #include "conv_params.h"
 
+PVA_NS_BEGIN
+
 namespace {
 
 constexpr int WB_THREADS = 256;
@@ -37,9 +39,9 @@ __device__ __forceinline__ s16x4_t tr_read(const char* base) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(base));
 }
 
-__device__ __forceinline__ bf16x8_t cat8(s16x4_t a, s16x4_t b) {
+__device__ __forceinline__ ev8_t cat8(s16x4_t a, s16x4_t b) {
   const s16x8_t v = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
-  return __builtin_bit_cast(bf16x8_t, v);
+  return __builtin_bit_cast(ev8_t, v);
 }
 
 template <int AFF>
@@ -161,7 +163,7 @@ __global__ __launch_bounds__(WB_THREADS, 2) void wgrad_box_kernel(const WgradPar
 #pragma unroll
             for (int e = 0; e < 8; ++e) f[e] = __builtin_fmaf(f[e], sc[e], sh[e]);
             o = pack8_fast(f);
-            if constexpr (AFF == 2) o = relu_bf16x8(o);
+            if constexpr (AFF == 2) o = relu_e16x8(o);
             if (!ok[u]) o = uint4{0, 0, 0, 0};
           }
           *reinterpret_cast<uint4*>(Bimg + scg * BPL + bb * 16) = o;
@@ -172,7 +174,7 @@ __global__ __launch_bounds__(WB_THREADS, 2) void wgrad_box_kernel(const WgradPar
     // ---- 32-position k-steps
     for (int kc = 0; kc < PP; kc += 32) {
       const int k0 = kc + 8 * g + q;
-      bf16x8_t af[4];
+      ev8_t af[4];
 #pragma unroll
       for (int c = 0; c < 4; ++c)
         af[c] = cat8(tr_read(Aimg + offA + 2 * c * APL + k0 * 16), tr_read(Aimg + offA + 2 * c * APL + (k0 + 4) * 16));
@@ -180,9 +182,9 @@ __global__ __launch_bounds__(WB_THREADS, 2) void wgrad_box_kernel(const WgradPar
       const char* B1 = Bimg + offB + bpos[k0 + 4] * 16;
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
-        const bf16x8_t xf = cat8(tr_read(B0 + toff[t]), tr_read(B1 + toff[t]));
+        const ev8_t xf = cat8(tr_read(B0 + toff[t]), tr_read(B1 + toff[t]));
 #pragma unroll
-        for (int c = 0; c < 4; ++c) acc[c][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf, af[c], acc[c][t], 0, 0, 0);
+        for (int c = 0; c < 4; ++c) acc[c][t] = PVA_MFMA16(xf, af[c], acc[c][t], 0, 0, 0);
       }
     }
   }
@@ -333,7 +335,7 @@ __global__ __launch_bounds__(WB_THREADS) void wgrad_box_narrow_kernel(const Wgra
 #pragma unroll
             for (int e = 0; e < 8; ++e) f[e] = __builtin_fmaf(f[e], sc[e], sh[e]);
             o = pack8_fast(f);
-            if constexpr (AFF == 2) o = relu_bf16x8(o);
+            if constexpr (AFF == 2) o = relu_e16x8(o);
             if (!ok[u]) o = uint4{0, 0, 0, 0};
           }
           *reinterpret_cast<uint4*>(Bimg + bb * C * 2 + scg * 16) = o;
@@ -343,7 +345,7 @@ __global__ __launch_bounds__(WB_THREADS) void wgrad_box_narrow_kernel(const Wgra
     __syncthreads();
     for (int kc = wid * 32; kc < PP; kc += 4 * 32) {
       const int k0 = kc + 8 * g + q;
-      bf16x8_t af[NB];
+      ev8_t af[NB];
 #pragma unroll
       for (int cb = 0; cb < NB; ++cb) {
         const char* a0 = creal[cb] ? Aimg + k0 * C * 2 + cofs[cb] : zero + (pq & 1) * 8;
@@ -357,10 +359,10 @@ __global__ __launch_bounds__(WB_THREADS) void wgrad_box_narrow_kernel(const Wgra
         for (int ci = 0; ci < NB; ++ci) {
           const char* x0 = creal[ci] ? Bimg + hb0 + toff[t] + cofs[ci] : zero + (pq & 1) * 8;
           const char* x1 = creal[ci] ? Bimg + hb1 + toff[t] + cofs[ci] : zero + (pq & 1) * 8;
-          const bf16x8_t xf = cat8(tr_read(x0), tr_read(x1));
+          const ev8_t xf = cat8(tr_read(x0), tr_read(x1));
 #pragma unroll
           for (int co = 0; co < NB; ++co)
-            acc[t][ci][co] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf, af[co], acc[t][ci][co], 0, 0, 0);
+            acc[t][ci][co] = PVA_MFMA16(xf, af[co], acc[t][ci][co], 0, 0, 0);
         }
       }
     }
@@ -487,3 +489,5 @@ void wgrad_box_reduce_launch(const float* slab, float* tmp, float* grad, int spl
   hipLaunchKernelGGL(wgrad_box_final_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, tmp, ngroups, n,
                      grad, taps, Cin, Cin_real, scale, beta);
 }
+
+PVA_NS_END  // namespace PVA_NS

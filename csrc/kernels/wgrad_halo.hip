@@ -22,6 +22,8 @@
 #include "common.h"
 #include "conv_params.h"
 
+PVA_NS_BEGIN
+
 namespace {
 
 constexpr int HX_THREADS = 512;
@@ -220,13 +222,13 @@ __global__ __launch_bounds__(HX_THREADS) void wgrad_halo_kernel(const WgradParam
     if (box + 1 < box1) load(box + 1);   // in flight under this box's MFMAs
     for (int ch = wp; ch < nchunk; ch += WP) {
       const int plo = ch * 32 + 8 * g + (li >> 2), phi = plo + 4;
-      bf16x8_t af[NTW];
+      ev8_t af[NTW];
 #pragma unroll
       for (int i = 0; i < NTW; ++i) {
         const int cb = (i * 16 + 4 * (li & 3)) * 2;
         const s16x4_t lo = tr_read(A + himg(plo, cb, rowA));
         const s16x4_t hi = tr_read(A + himg(phi, cb, rowA));
-        af[i] = __builtin_bit_cast(bf16x8_t, (s16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
+        af[i] = __builtin_bit_cast(ev8_t, (s16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
       }
       const int hlo = htab[plo], hhi = htab[phi];
 #pragma unroll
@@ -234,10 +236,10 @@ __global__ __launch_bounds__(HX_THREADS) void wgrad_halo_kernel(const WgradParam
         if (!kok[j]) continue;   // wave-uniform
         const s16x4_t blo = tr_read(B + himg(hlo + ktoff[j], kcolb[j], rowB));
         const s16x4_t bhi = tr_read(B + himg(hhi + ktoff[j], kcolb[j], rowB));
-        const bf16x8_t bf =
-            __builtin_bit_cast(bf16x8_t, (s16x8_t){blo[0], blo[1], blo[2], blo[3], bhi[0], bhi[1], bhi[2], bhi[3]});
+        const ev8_t bf =
+            __builtin_bit_cast(ev8_t, (s16x8_t){blo[0], blo[1], blo[2], blo[3], bhi[0], bhi[1], bhi[2], bhi[3]});
 #pragma unroll
-        for (int i = 0; i < NTW; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf, acc[i][j], 0, 0, 0);
+        for (int i = 0; i < NTW; ++i) acc[i][j] = PVA_MFMA16(af[i], bf, acc[i][j], 0, 0, 0);
       }
     }
   }
@@ -338,3 +340,5 @@ void wgrad_halo_launch(const WgradParams& p, hipStream_t s) {
     default: launch_wp<8>(p, h.wpl, h.ktw, grid, h.lds, s); break;
   }
 }
+
+PVA_NS_END  // namespace PVA_NS

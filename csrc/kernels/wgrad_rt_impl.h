@@ -22,6 +22,8 @@
 #include "common.h"
 #include "conv_params.h"
 
+PVA_NS_BEGIN
+
 namespace wgrad_rt {
 
 // q / d for 0 <= q < 2^31 with a host-computed magic (Granlund-Montgomery, see magic_div below): 5 VALU, exact.
@@ -211,7 +213,7 @@ void wgrad_rt_kernel(const RtParams rp) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) f[e] = __builtin_fmaf(f[e], asc[e], ash[e]);
         v = pack8_fast(f);
-        if (relu) v = relu_bf16x8(v);
+        if (relu) v = relu_e16x8(v);
         if (!((rb_ok >> s) & 1u)) v = uint4{0, 0, 0, 0};   // padding / past-the-split rows stay zero
       }
       *reinterpret_cast<uint4*>(B + sb[s]) = v;
@@ -265,26 +267,26 @@ void wgrad_rt_kernel(const RtParams rp) {
     const char* A = smem + cur * TILE;
 #pragma unroll
     for (int kk = 0; kk < BP / 32; ++kk) {
-      bf16x8_t af[TM], bfr[TN];
+      ev8_t af[TM], bfr[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         s16x4_t lo = tr_read(A + kk * 32 * BMW * 2 + ta[i][0]);
         s16x4_t hi = tr_read(A + kk * 32 * BMW * 2 + ta[i][1]);
         s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        af[i] = __builtin_bit_cast(bf16x8_t, v);
+        af[i] = __builtin_bit_cast(ev8_t, v);
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         s16x4_t lo = tr_read(A + kk * 32 * BNW * 2 + tb[j][0]);
         s16x4_t hi = tr_read(A + kk * 32 * BNW * 2 + tb[j][1]);
         s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        bfr[j] = __builtin_bit_cast(bf16x8_t, v);
+        bfr[j] = __builtin_bit_cast(ev8_t, v);
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = PVA_MFMA16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
   }
 
@@ -339,3 +341,5 @@ void launch_aff(int v, bool bp64, bool check, const RtParams& rp, hipStream_t st
 }
 
 }  // namespace wgrad_rt
+
+PVA_NS_END  // namespace PVA_NS

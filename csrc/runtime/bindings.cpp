@@ -14,99 +14,13 @@
 static_assert(offsetof(ConvParams, bws) - offsetof(ConvParams, M) == 38 * sizeof(int),
               "ConvParams integer block must be contiguous (filled from a 39-int geometry vector)");
 
-// ---- kernel launchers (defined in csrc/kernels/*.hip) ----
-void conv_igemm_launch(const ConvParams& p, int chunk, hipStream_t stream, int cfg);
-int conv_cfg_bm(int cfg, int N);
-int conv_igemm_ut_legal(const ConvParams& p, int chunk, int bk);
-int conv_direct_legal(const ConvParams& p, int chunk);
-int conv_pw_legal(const ConvParams& p, int chunk);
-int conv_halo_legal(const ConvParams& p, int chunk);
-int conv_halo_epi_ok(const ConvParams& p);
-int conv_halo64p_legal(const ConvParams& p, int chunk);
-void conv_igemm_set_ut(int mode);
-int conv_igemm_m_tiles(int M, int N);
-int conv_igemm_m_tiles_k(int M, int N, int K, int Cg);
-void conv_igemm_set_bk(int bk);
-void conv_wgrad_launch(const WgradParams& p, int chunk, hipStream_t stream);
-void conv_wgrad_tile(int Cout, int K, int variant, int* bmw, int* bnw);
-int wgrad_rt_legal(int Cout, int Cin, int ldd, int ldx, int chunk, int dy_affine);
-int wgrad_narrow_legal(int Cout, int Cin, int K);
-int wgrad_halo_legal(const WgradParams& p);
-int wgrad_box_legal(const WgradParams& p);
-void wgrad_box_reduce_launch(const float* slab, float* tmp, float* grad, int splits, int Cout, int taps, int Cin,
-                             int Cin_real, float scale, float beta, hipStream_t st);
-int wgrad_box_reduce_groups(int splits);
-void wgrad_reduce_launch(float* accbuf, float* grad, int splits, int Cout, int taps, int Cin, int Cin_real,
-                         float scale, float beta, int slab, hipStream_t stream);
-void bn_finalize_launch(const float* part, int tiles, int C, int64_t count, const float* gamma, const float* beta,
-                        float* rm, float* rv, int64_t* nbt, float momentum, float eps, float* smean, float* srstd,
-                        float* scale, float* shift, hipStream_t s, double* scratch, unsigned* ctr);
-int bn_fin_ranges(int tiles);
-void bn_eval_affine_launch(int C, const float* gamma, const float* beta, const float* rm, const float* rv, float eps,
-                           float* scale, float* shift, hipStream_t s);
-void bn_act_launch(const uint16_t* y, int ldy, uint16_t* out, int ldo, const float* scale, const float* shift,
-                   int relu, int64_t M, int C, hipStream_t s);
-void res_out_launch(const uint16_t* yc, const float* sc, const float* hc, const uint16_t* y1, const float* s1,
-                    const float* h1, const uint16_t* x, int ldx, uint16_t* out, int ldo, uint8_t* mask, int64_t M,
-                    int C, hipStream_t s);
-int bn_bwd_reduce_blocks(int64_t M, int C, int* rows_per_block);
-void bn_bwd_reduce_launch(const uint16_t* g, int ldg, int mask_mode, const void* mo, int ldm, const float* ms,
-                          const float* mh, const uint16_t* y0, const float* mean0, const float* rstd0,
-                          const uint16_t* y1, const float* mean1, const float* rstd1, int64_t M, int C, int blocks,
-                          int rows_per_block, float* part, uint16_t* dzout, int lddz, hipStream_t s);
-void bn_bwd_finalize_launch(const float* part, int blocks, int C, int64_t count, int which, const float* gamma,
-                            const float* mean, const float* rstd, float* dgamma, float* dbeta, float beta_acc,
-                            float* coef, hipStream_t s, double* scratch, unsigned* ctr);
-void bn_bwd_apply_launch(const uint16_t* g, int ldg, int mask_mode, const void* mo, int ldm, const float* ms,
-                         const float* mh, const uint16_t* y0, const float* coef0, uint16_t* dy0, const uint16_t* y1,
-                         const float* coef1, uint16_t* dy1, uint16_t* dzout, int lddz, int dz_accum, int64_t M, int C,
-                         hipStream_t s);
-void stem_pool_fwd_launch(const uint16_t* y, const float* scale, const float* shift, uint16_t* out, uint8_t* arg,
-                          uint16_t* ymax, int NT_, int H, int W, int Ho, int Wo, int C, int ldo, hipStream_t s);
-void stem_pool_bn_apply_launch(const uint16_t* dout, int ldd, const uint8_t* arg, const uint16_t* y, const float* ms,
-                               const float* mh, const float* coef, uint16_t* dy, int NT_, int H, int W, int Ho, int Wo,
-                               int C, hipStream_t s);
-int avgpool_global_splits(int N, int vol);
-void stem_pool_bwd_launch(const uint16_t* dout, int ldd, const uint8_t* arg, uint16_t* dact, int NT_, int H, int W,
-                          int Ho, int Wo, int C, hipStream_t s);
-void avgpool_fwd_launch(const uint16_t* x, int N, int T, int H, int W, int C, int kt, int kh, int kw, float* out,
-                        int ldo, int coff, float* scratch, hipStream_t s);
-void avgpool_bwd_launch(const float* dout, int ldo, int coff, int N, int T, int H, int W, int C, int kt, int kh,
-                        int kw, uint16_t* dx, hipStream_t s);
-void sgd_momentum_launch(float* p, const float* g, float* buf, int64_t n, const float* lr, float momentum, float wd,
-                         float gscale, int first, int* found_inf, const int* skip_flag, hipStream_t s);
-void nonfinite_check_launch(const float* g, int64_t n, float gscale, int* flag, hipStream_t s);
-void pack_weights_launch(const float* master, uint16_t* fwd, uint16_t* dgr, const void* descs, int ntensors,
-                         hipStream_t s);
-int pack_desc_size();
-void video_preprocess_launch(const uint8_t* frames, const int* desc, const int* tidx, int B, int T, int S,
-                             const float* mean, const float* std_, uint16_t* out, int s2d, hipStream_t s);
-int stem_tiles(int Ho, int Wo, int N);
-void stem_s2d_launch(int mode, const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, const uint16_t* dy,
-                     float* dw, int N, int T, int Hs, int Ws, int Cout, int kt, hipStream_t s);
-bool stem_s2d_supported(int Cout, int kt);
-void stem_wgrad_convert_launch(float* acc, float* grad, int Cout, int kt, float beta, hipStream_t s);
-void stem_pack_launch(const float* w, uint16_t* out, int Cout, int kt, hipStream_t s);
-void synth_frames_launch(uint8_t* out, int64_t n, uint32_t seed, hipStream_t s);
-
-void bnfold_fwd_stats_launch(const uint16_t* Wf, const float* Ga, const float* sslab, int splits, int C, int c,
-                             int64_t count, float* T, float* s_out, const float* gamma, const float* beta, float* rm,
-                             float* rv, int64_t* nbt, float momentum, float eps, float* smean, float* srstd,
-                             float* scale, float* shift, hipStream_t st);
-void bnfold_bwd_launch(const float* part, int tiles, const uint16_t* Wf, const uint16_t* Wd, const float* G,
-                       const float* T, const float* s, int C, int c, int64_t count, const float* gamma,
-                       const float* mean, const float* rstd, float* dgamma, float* dbeta, float* dW, float beta_acc,
-                       float* coef, uint16_t* W1t, uint16_t* W2, float* bias, hipStream_t st);
-void head_forward_launch(const float* feat, int N, int P, int C, const float* W, const float* b, int K, float p_drop,
-                         uint64_t seed, const uint64_t* seedp, float* xm, float* logits, hipStream_t s);
-void head_seed_advance_launch(uint64_t* seed, hipStream_t s);
-void head_ce_launch(const float* logits, const int64_t* labels, int N, int K, float gscale, float* dlogits,
-                    float* row_loss, int* row_correct, float* loss, int64_t* counts, int acc_counts, hipStream_t s);
-void head_backward_launch(const float* dlogits, const float* xm, const float* W, int N, int P, int C, int K,
-                          float p_drop, uint64_t seed, const uint64_t* seedp, float* dW, float* db, float beta,
-                          float* dfeat, float* dlT, float* xmT, float* WT, hipStream_t s);
-void head_dropout_mask_launch(int64_t total, float p_drop, uint64_t seed, uint8_t* out, hipStream_t s);
-
+// ---- kernel launchers (csrc/kernels/launchers.h), one set per 16-bit compute type ----
+namespace pva_bf16 {
+#include "../kernels/launchers.h"
+}
+namespace pva_f16 {
+#include "../kernels/launchers.h"
+}
 void register_clip_reader(pybind11::module& m);
 
 namespace {
@@ -115,16 +29,27 @@ using OptT = c10::optional<at::Tensor>;
 
 inline hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
 
+// 16-bit compute type of the current call: set from the call's primary 16-bit tensor (kind16); every other 16-bit
+// tensor of the call must match it.  bf16 tensors run the pva_bf16 kernels, fp16 tensors the pva_f16 kernels.
+thread_local at::ScalarType tl_kind = at::kBFloat16;
+inline bool kind16(const at::Tensor& t) {
+  const auto k = t.scalar_type();
+  TORCH_CHECK(k == at::kBFloat16 || k == at::kHalf, "expected a bf16 or fp16 tensor");
+  tl_kind = k;
+  return k == at::kHalf;
+}
+#define KSEL(h, fn) ((h) ? pva_f16::fn : pva_bf16::fn)
+
 inline void check_dev(const at::Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
   TORCH_CHECK(t.is_contiguous() || t.dim() <= 2, name, " must be contiguous");
 }
 inline const uint16_t* bfp(const at::Tensor& t) {
-  TORCH_CHECK(t.scalar_type() == at::kBFloat16, "expected bf16 tensor");
+  TORCH_CHECK(t.scalar_type() == tl_kind, "expected a ", c10::toString(tl_kind), " tensor (one compute dtype per call)");
   return reinterpret_cast<const uint16_t*>(t.data_ptr());
 }
 inline uint16_t* bfpm(const at::Tensor& t) {
-  TORCH_CHECK(t.scalar_type() == at::kBFloat16, "expected bf16 tensor");
+  TORCH_CHECK(t.scalar_type() == tl_kind, "expected a ", c10::toString(tl_kind), " tensor (one compute dtype per call)");
   return reinterpret_cast<uint16_t*>(t.data_ptr());
 }
 inline const uint16_t* bfo(const OptT& t) { return t.has_value() ? bfp(*t) : nullptr; }
@@ -169,15 +94,15 @@ static ConvParams conv_params(const at::Tensor& x, const at::Tensor& w, const at
 // mapping differ from the tile kernels', so a silent fallback would corrupt the caller's partial sums
 static void check_pw(const ConvParams& p, int64_t chunk, int64_t cfg) {
   if (cfg >= 0 && (cfg & 16) && (cfg & 2048)) {   // halo-staged 3x3 kernel: geometry, epilogue, tile size
-    const int P = conv_halo_legal(p, (int)chunk);
+    const int P = pva_bf16::conv_halo_legal(p, (int)chunk);
     TORCH_CHECK(P > 0 && P == (int)(cfg >> 12), "halo conv kernel selected for an unsupported geometry");
-    TORCH_CHECK(conv_halo_epi_ok(p), "halo conv kernel selected for an unsupported epilogue");
-    TORCH_CHECK(!(cfg & 2) || conv_halo64p_legal(p, (int)chunk),
+    TORCH_CHECK(pva_bf16::conv_halo_epi_ok(p), "halo conv kernel selected for an unsupported epilogue");
+    TORCH_CHECK(!(cfg & 2) || pva_bf16::conv_halo64p_legal(p, (int)chunk),
                 "persistent 64-channel halo conv kernel selected for an unsupported geometry");
     return;
   }
   if (cfg < 0 || !(cfg & 16) || !(cfg & 512)) return;
-  TORCH_CHECK(conv_pw_legal(p, (int)chunk), "pointwise conv kernel selected for an unsupported geometry");
+  TORCH_CHECK(pva_bf16::conv_pw_legal(p, (int)chunk), "pointwise conv kernel selected for an unsupported geometry");
   TORCH_CHECK(!p.eres || p.ldr % 8 == 0, "pointwise conv kernel: residual row stride must be a multiple of 8");
   TORCH_CHECK(!p.emask || p.Ngemm % 8 == 0, "pointwise conv kernel: mask layout");
 }
@@ -185,6 +110,7 @@ static void check_pw(const ConvParams& p, int64_t chunk, int64_t cfg) {
 void conv_igemm(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, const OptT& stats,
                 const OptT& scale, const OptT& shift, int64_t affine, int64_t accum, std::vector<int64_t> g,
                 int64_t chunk, int64_t cfg, const OptT& bias, int64_t nostore) {
+  const bool h = kind16(x);
   ConvParams p = conv_params(x, w, y, accum, g, chunk);
   p.nostore = (int)nostore;
   TORCH_CHECK(!nostore || (stats.has_value() && !accum && !bias.has_value()),
@@ -197,7 +123,7 @@ void conv_igemm(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, c
   TORCH_CHECK(!affine || (scale.has_value() && shift.has_value()), "affine needs scale/shift");
   check_pw(p, chunk, cfg);
   if (p.M == 0) return;
-  conv_igemm_launch(p, (int)chunk, cur_stream(), (int)cfg);
+  KSEL(h, conv_igemm_launch)(p, (int)chunk, cur_stream(), (int)cfg);
 }
 
 // forward conv whose epilogue applies its own BatchNorm from known statistics and writes the residual-unit
@@ -207,6 +133,7 @@ void conv_igemm_fres(const at::Tensor& x, const at::Tensor& w, const at::Tensor&
                      const OptT& shift, int64_t affine, std::vector<int64_t> g, int64_t chunk, int64_t cfg,
                      const at::Tensor& osc, const at::Tensor& osh, const at::Tensor& res, int64_t ldr,
                      const OptT& rsc, const OptT& rsh, const at::Tensor& mask) {
+  const bool h = kind16(x);
   ConvParams p = conv_params(x, w, y, 0, g, chunk);
   TORCH_CHECK(chunk == 8, "fres epilogue needs 16-B chunks");
   p.in_scale = f32o(scale); p.in_shift = f32o(shift);
@@ -225,7 +152,7 @@ void conv_igemm_fres(const at::Tensor& x, const at::Tensor& w, const at::Tensor&
   TORCH_CHECK(p.ost == 1 && p.osh == 1 && p.osw == 1, "fres epilogue: dense output rows");
   check_pw(p, chunk, cfg);
   if (p.M == 0) return;
-  conv_igemm_launch(p, (int)chunk, cur_stream(), (int)cfg);
+  KSEL(h, conv_igemm_launch)(p, (int)chunk, cur_stream(), (int)cfg);
 }
 
 // dgrad with the backward-BN epilogue (see ConvParams): residual add, ReLU-bit mask, and partial sums
@@ -235,6 +162,7 @@ void conv_igemm_epi(const at::Tensor& x, const at::Tensor& w, const at::Tensor& 
                     const OptT& y0, const OptT& mean0, const OptT& rstd0, const OptT& y1, const OptT& mean1,
                     const OptT& rstd1, const OptT& part, const OptT& msc, const OptT& msh, int64_t cfg,
                     const OptT& bias) {
+  const bool h = kind16(x);
   ConvParams p = conv_params(x, w, y, accum, g, chunk);
   p.ebias = f32o(bias);
   TORCH_CHECK(!bias.has_value() || bias->numel() >= p.Ngemm, "bias too small");
@@ -255,23 +183,23 @@ void conv_igemm_epi(const at::Tensor& x, const at::Tensor& w, const at::Tensor& 
     p.epart = f32(*part);
     TORCH_CHECK(msc.has_value() == msh.has_value(), "mask affine needs scale and shift");
     p.emsc = f32o(msc); p.emsh = f32o(msh);
-    const int bm = conv_cfg_bm((int)cfg, p.Ngemm);
+    const int bm = KSEL(h, conv_cfg_bm)((int)cfg, p.Ngemm);
     TORCH_CHECK(part->numel() >= (int64_t)((p.M + bm - 1) / bm) * 3 * p.Ngemm, "partials too small");
   }
   check_pw(p, chunk, cfg);
   if (p.M == 0) return;
-  conv_igemm_launch(p, (int)chunk, cur_stream(), (int)cfg);
+  KSEL(h, conv_igemm_launch)(p, (int)chunk, cur_stream(), (int)cfg);
 }
 
 // row tiles of the BN partial-sum buffer a conv launch writes; pass K (= taps * Cg) and Cg for forward
 // launches so the small-channel streaming kernel's 128-row tiles are accounted for
 int64_t conv_m_tiles(int64_t M, int64_t N, int64_t K, int64_t Cg) {
-  return K > 0 ? conv_igemm_m_tiles_k((int)M, (int)N, (int)K, (int)Cg) : conv_igemm_m_tiles((int)M, (int)N);
+  return K > 0 ? pva_bf16::conv_igemm_m_tiles_k((int)M, (int)N, (int)K, (int)Cg) : pva_bf16::conv_igemm_m_tiles((int)M, (int)N);
 }
 
 std::vector<int64_t> wgrad_tile(int64_t Cout, int64_t K, int64_t variant) {
   int a, b;
-  conv_wgrad_tile((int)Cout, (int)K, (int)variant, &a, &b);
+  pva_bf16::conv_wgrad_tile((int)Cout, (int)K, (int)variant, &a, &b);
   return {a, b};
 }
 
@@ -279,6 +207,7 @@ std::vector<int64_t> wgrad_tile(int64_t Cout, int64_t K, int64_t variant) {
 void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& partial, const OptT& scale,
                 const OptT& shift, int64_t affine, std::vector<int64_t> g, int64_t chunk, int64_t slab,
                 int64_t variant, int64_t dy_affine, const OptT& colsum) {
+  const bool h = kind16(dy);
   TORCH_CHECK(g.size() == 23, "wgrad geometry must have 23 entries");
   WgradParams p{};
   p.dy = bfp(dy); p.x = bfp(x); p.partial = f32(partial);
@@ -300,19 +229,19 @@ void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& par
               "Gram mode: 1x1 conv input with an affine, dy = x");
   TORCH_CHECK(!colsum.has_value() || colsum->numel() >= (int64_t)p.splits * p.Cout, "colsum slab too small");
   if (variant >= 0 && (variant & 16)) {
-    TORCH_CHECK(wgrad_narrow_legal(p.Cout, p.Cin, p.K) && chunk == 8 && !slab, "narrow wgrad not legal here");
+    TORCH_CHECK(KSEL(h, wgrad_narrow_legal)(p.Cout, p.Cin, p.K) && chunk == 8 && !slab, "narrow wgrad not legal here");
     TORCH_CHECK(p.p_per_split % 64 == 0 && (int64_t)p.splits * p.p_per_split >= p.P, "narrow wgrad: split cover");
     TORCH_CHECK(p.ldd % 8 == 0 && p.ldx % 8 == 0, "narrow wgrad: 16-B rows");
     TORCH_CHECK(!dy_affine || (p.Cout == p.Cin && p.K == p.Cin), "narrow Gram: square 1x1");
   }
-  TORCH_CHECK(!halo || (wgrad_halo_legal(p) && chunk == 8 && p.p_per_split > 0), "halo wgrad not legal here");
+  TORCH_CHECK(!halo || (KSEL(h, wgrad_halo_legal)(p) && chunk == 8 && p.p_per_split > 0), "halo wgrad not legal here");
   if (!box && variant >= 0 && (variant & (1 << 25)))
-    TORCH_CHECK(wgrad_rt_legal(p.Cout, p.Cin, p.ldd, p.ldx, (int)chunk, (int)dy_affine) && p.p_per_split > 0 &&
+    TORCH_CHECK(KSEL(h, wgrad_rt_legal)(p.Cout, p.Cin, p.ldd, p.ldx, (int)chunk, (int)dy_affine) && p.p_per_split > 0 &&
                     (int64_t)p.splits * p.p_per_split >= p.P,
                 "row-table wgrad not legal here");
   if (box) {
-    TORCH_CHECK(wgrad_box_legal(p) && chunk == 8 && slab, "box wgrad not legal here (needs slab mode)");
-    const int64_t boxes = p.P / (p.Wo * (int64_t)wgrad_box_legal(p));
+    TORCH_CHECK(KSEL(h, wgrad_box_legal)(p) && chunk == 8 && slab, "box wgrad not legal here (needs slab mode)");
+    const int64_t boxes = p.P / (p.Wo * (int64_t)KSEL(h, wgrad_box_legal)(p));
     TORCH_CHECK(p.p_per_split > 0 && (int64_t)p.splits * p.p_per_split >= boxes, "box wgrad: split cover");
   }
   TORCH_CHECK(dy.numel() * 2 < 0xFFFFFF00ll && x.numel() * 2 < 0xFFFFFF00ll, "buffer extents must fit 32 bits");
@@ -320,24 +249,24 @@ void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& par
   p.xbytes = (unsigned)(x.numel() * 2);
   const int64_t nslab = slab ? (int64_t)p.splits * (box && p.Cin < 64 ? 4 : 1) : 1;   // narrow box: a slab per wave
   TORCH_CHECK(partial.numel() >= (int64_t)p.Cout * p.K * nslab, "wgrad accumulator too small");
-  conv_wgrad_launch(p, (int)chunk, cur_stream());
+  KSEL(h, conv_wgrad_launch)(p, (int)chunk, cur_stream());
 }
 
 // slab [splits][Cout][taps*Cin] of the box kernel -> grad; tmp: >= box_reduce_groups(splits) * Cout*taps*Cin floats
 void wgrad_box_reduce(const at::Tensor& slab, const at::Tensor& tmp, const at::Tensor& grad, int64_t splits,
                       int64_t Cout, int64_t taps, int64_t Cin, int64_t Cin_real, double scale, double beta) {
   const int64_t n = Cout * taps * Cin;
-  TORCH_CHECK(slab.numel() >= splits * n && tmp.numel() >= wgrad_box_reduce_groups((int)splits) * n && n % 4 == 0,
+  TORCH_CHECK(slab.numel() >= splits * n && tmp.numel() >= pva_bf16::wgrad_box_reduce_groups((int)splits) * n && n % 4 == 0,
               "box wgrad reduce: buffer sizes");
   TORCH_CHECK(grad.numel() >= Cout * taps * Cin_real, "box wgrad reduce: grad too small");
-  wgrad_box_reduce_launch(f32(slab), f32(tmp), f32(grad), (int)splits, (int)Cout, (int)taps, (int)Cin, (int)Cin_real,
+  pva_bf16::wgrad_box_reduce_launch(f32(slab), f32(tmp), f32(grad), (int)splits, (int)Cout, (int)taps, (int)Cin, (int)Cin_real,
                           (float)scale, (float)beta, cur_stream());
 }
 
 void wgrad_reduce(const at::Tensor& partial, const at::Tensor& grad, int64_t splits, int64_t Cout, int64_t taps,
                   int64_t Cin, int64_t Cin_real, double scale, double beta, int64_t slab) {
   TORCH_CHECK(!slab || partial.numel() >= splits * Cout * taps * Cin, "slab accumulator too small");
-  wgrad_reduce_launch(f32(partial), f32(grad), (int)splits, (int)Cout, (int)taps, (int)Cin, (int)Cin_real,
+  pva_bf16::wgrad_reduce_launch(f32(partial), f32(grad), (int)splits, (int)Cout, (int)taps, (int)Cin, (int)Cin_real,
                       (float)scale, (float)beta, (int)slab, cur_stream());
 }
 
@@ -360,29 +289,31 @@ void bn_finalize(const at::Tensor& part, int64_t tiles, int64_t C, int64_t count
   double* scr = nullptr;
   unsigned* ctr = nullptr;
   fin_buffers(fin, C, &scr, &ctr);
-  bn_finalize_launch(f32(part), (int)tiles, (int)C, count, f32(gamma), f32(beta), f32o(rm), f32o(rv), nb,
+  pva_bf16::bn_finalize_launch(f32(part), (int)tiles, (int)C, count, f32(gamma), f32(beta), f32o(rm), f32o(rv), nb,
                      (float)momentum, (float)eps, f32(smean), f32(srstd), f32(scale), f32(shift), cur_stream(), scr, ctr);
 }
 
 void bn_eval_affine(const at::Tensor& gamma, const at::Tensor& beta, const at::Tensor& rm, const at::Tensor& rv,
                     double eps, const at::Tensor& scale, const at::Tensor& shift) {
-  bn_eval_affine_launch((int)gamma.numel(), f32(gamma), f32(beta), f32(rm), f32(rv), (float)eps, f32(scale),
+  pva_bf16::bn_eval_affine_launch((int)gamma.numel(), f32(gamma), f32(beta), f32(rm), f32(rv), (float)eps, f32(scale),
                         f32(shift), cur_stream());
 }
 
 void bn_act(const at::Tensor& y, int64_t ldy, const at::Tensor& out, int64_t ldo, const at::Tensor& scale,
             const at::Tensor& shift, int64_t relu, int64_t M, int64_t C) {
+  const bool h = kind16(y);
   TORCH_CHECK(C % 8 == 0 && ldy % 8 == 0 && ldo % 8 == 0, "bn_act alignment");
-  bn_act_launch(bfp(y), (int)ldy, bfpm(out), (int)ldo, f32(scale), f32(shift), (int)relu, M, (int)C, cur_stream());
+  KSEL(h, bn_act_launch)(bfp(y), (int)ldy, bfpm(out), (int)ldo, f32(scale), f32(shift), (int)relu, M, (int)C, cur_stream());
 }
 
 void res_out(const at::Tensor& yc, const at::Tensor& sc, const at::Tensor& hc, const OptT& y1, const OptT& s1,
              const OptT& h1, const OptT& x, int64_t ldx, const at::Tensor& out, int64_t ldo, int64_t M, int64_t C,
              const OptT& mask) {
+  const bool h = kind16(yc);
   TORCH_CHECK(y1.has_value() || x.has_value(), "res_out needs a shortcut");
   TORCH_CHECK(!mask.has_value() || (mask->scalar_type() == at::kByte && mask->numel() >= M * (C / 8)),
               "res_out mask must be uint8 [M, C/8]");
-  res_out_launch(bfp(yc), f32(sc), f32(hc), bfo(y1), f32o(s1), f32o(h1), bfo(x), (int)ldx, bfpm(out), (int)ldo,
+  KSEL(h, res_out_launch)(bfp(yc), f32(sc), f32(hc), bfo(y1), f32o(s1), f32o(h1), bfo(x), (int)ldx, bfpm(out), (int)ldo,
                  mask.has_value() ? mask->data_ptr<uint8_t>() : nullptr, M, (int)C, cur_stream());
 }
 
@@ -398,7 +329,7 @@ static const void* mask_ptr(int64_t mode, const OptT& mo) {
 
 std::vector<int64_t> bn_bwd_blocks(int64_t M, int64_t C) {
   int rpb;
-  int b = bn_bwd_reduce_blocks(M, (int)C, &rpb);
+  int b = pva_bf16::bn_bwd_reduce_blocks(M, (int)C, &rpb);
   return {b, rpb};
 }
 
@@ -407,11 +338,12 @@ void bn_bwd_reduce(const at::Tensor& g, int64_t ldg, int64_t mask_mode, const Op
                    const OptT& mh, const OptT& y0, const OptT& mean0, const OptT& rstd0,
                    const OptT& y1, const OptT& mean1, const OptT& rstd1, int64_t M, int64_t C, int64_t blocks,
                    int64_t rpb, const at::Tensor& part, const OptT& dzout, int64_t lddz) {
+  const bool h = kind16(g);
   TORCH_CHECK(C % 8 == 0 && C <= 2048, "bn_bwd_reduce channel constraint");
   TORCH_CHECK(!dzout.has_value() || (lddz % 8 == 0 && dzout->size(0) >= M), "bn_bwd_reduce: dz output layout");
   TORCH_CHECK(!y0.has_value() || (mean0.has_value() && rstd0.has_value()), "y0 needs mean0/rstd0");
   TORCH_CHECK(mask_mode != 2 || y0.has_value(), "mask mode 2 reads y0");
-  bn_bwd_reduce_launch(bfp(g), (int)ldg, (int)mask_mode, mask_ptr(mask_mode, mo), (int)ldm, f32o(ms), f32o(mh), bfo(y0), f32o(mean0),
+  KSEL(h, bn_bwd_reduce_launch)(bfp(g), (int)ldg, (int)mask_mode, mask_ptr(mask_mode, mo), (int)ldm, f32o(ms), f32o(mh), bfo(y0), f32o(mean0),
                        f32o(rstd0), bfo(y1), f32o(mean1), f32o(rstd1), M, (int)C, (int)blocks, (int)rpb, f32(part),
                        bfom(dzout), (int)lddz, cur_stream());
 }
@@ -422,7 +354,7 @@ void bn_bwd_finalize(const at::Tensor& part, int64_t blocks, int64_t C, int64_t 
   double* scr = nullptr;
   unsigned* ctr = nullptr;
   fin_buffers(fin, C, &scr, &ctr);
-  bn_bwd_finalize_launch(f32(part), (int)blocks, (int)C, count, (int)which, f32(gamma), f32(mean), f32(rstd),
+  pva_bf16::bn_bwd_finalize_launch(f32(part), (int)blocks, (int)C, count, (int)which, f32(gamma), f32(mean), f32(rstd),
                          f32o(dgamma), f32o(dbeta), (float)beta_acc, f32(coef), cur_stream(), scr, ctr);
 }
 
@@ -431,9 +363,10 @@ void bn_bwd_apply(const at::Tensor& g, int64_t ldg, int64_t mask_mode, const Opt
                   const OptT& mh, const OptT& y0, const OptT& coef0, const OptT& dy0,
                   const OptT& y1, const OptT& coef1, const OptT& dy1, const OptT& dzout, int64_t lddz,
                   int64_t dz_accum, int64_t M, int64_t C) {
+  const bool h = kind16(g);
   TORCH_CHECK(y0.has_value() == coef0.has_value() && y0.has_value() == dy0.has_value(), "y0/coef0/dy0 go together");
   TORCH_CHECK(mask_mode != 2 || y0.has_value(), "mask mode 2 reads y0");
-  bn_bwd_apply_launch(bfp(g), (int)ldg, (int)mask_mode, mask_ptr(mask_mode, mo), (int)ldm, f32o(ms), f32o(mh), bfo(y0), f32o(coef0),
+  KSEL(h, bn_bwd_apply_launch)(bfp(g), (int)ldg, (int)mask_mode, mask_ptr(mask_mode, mo), (int)ldm, f32o(ms), f32o(mh), bfo(y0), f32o(coef0),
                       bfom(dy0), bfo(y1), f32o(coef1), bfom(dy1), bfom(dzout), (int)lddz, (int)dz_accum, M, (int)C,
                       cur_stream());
 }
@@ -442,12 +375,13 @@ void bn_bwd_apply(const at::Tensor& g, int64_t ldg, int64_t mask_mode, const Opt
 void stem_pool_fwd(const at::Tensor& y, const at::Tensor& scale, const at::Tensor& shift, const at::Tensor& out,
                    int64_t ldo, const at::Tensor& arg, int64_t NT_, int64_t H, int64_t W, int64_t Ho, int64_t Wo,
                    int64_t C, const OptT& ymax) {
+  const bool h = kind16(y);
   TORCH_CHECK(C % 8 == 0 && ldo % 8 == 0, "stem pool: channels / row stride must be multiples of 8");
   TORCH_CHECK(arg.numel() >= NT_ * Ho * Wo * C, "stem pool: argmax buffer too small");
   TORCH_CHECK(!ymax.has_value() || ymax->numel() >= NT_ * Ho * Wo * C, "stem pool: ymax buffer too small");
   TORCH_CHECK(NT_ * H * W < ((int64_t)1 << 31) && C <= 2048, "stem pool: position count exceeds int32");
   TORCH_CHECK(Ho == (H - 1) / 2 + 1 && Wo == (W - 1) / 2 + 1, "stem pool: 3x3/s2/p1 output dims");
-  stem_pool_fwd_launch(bfp(y), f32(scale), f32(shift), bfpm(out), arg.data_ptr<uint8_t>(), bfom(ymax), (int)NT_,
+  KSEL(h, stem_pool_fwd_launch)(bfp(y), f32(scale), f32(shift), bfpm(out), arg.data_ptr<uint8_t>(), bfom(ymax), (int)NT_,
                        (int)H, (int)W, (int)Ho, (int)Wo, (int)C, (int)ldo, cur_stream());
 }
 
@@ -455,35 +389,39 @@ void stem_pool_fwd(const at::Tensor& y, const at::Tensor& scale, const at::Tenso
 void stem_pool_bn_apply(const at::Tensor& dout, int64_t ldd, const at::Tensor& arg, const at::Tensor& y,
                         const at::Tensor& ms, const at::Tensor& mh, const at::Tensor& coef, const at::Tensor& dy,
                         int64_t NT_, int64_t H, int64_t W, int64_t Ho, int64_t Wo, int64_t C) {
+  const bool h = kind16(dout);
   TORCH_CHECK(C % 8 == 0 && ldd % 8 == 0 && C <= 2048, "stem pool bwd: channel layout");
   TORCH_CHECK(NT_ * H * W < ((int64_t)1 << 31), "stem pool bwd: position count exceeds int32");
   TORCH_CHECK(y.numel() >= NT_ * H * W * C && dy.numel() >= NT_ * H * W * C, "stem pool bwd: y/dy too small");
   TORCH_CHECK(arg.numel() >= NT_ * Ho * Wo * C && dout.dim() == 2 && dout.size(0) >= NT_ * Ho * Wo &&
               dout.size(1) >= C && dout.stride(0) == ldd, "stem pool bwd: pooled buffers / row stride");
   TORCH_CHECK(Ho == (H - 1) / 2 + 1 && Wo == (W - 1) / 2 + 1, "stem pool bwd: 3x3/s2/p1 output dims");
-  stem_pool_bn_apply_launch(bfp(dout), (int)ldd, arg.data_ptr<uint8_t>(), bfp(y), f32(ms), f32(mh), f32(coef), bfpm(dy),
+  KSEL(h, stem_pool_bn_apply_launch)(bfp(dout), (int)ldd, arg.data_ptr<uint8_t>(), bfp(y), f32(ms), f32(mh), f32(coef), bfpm(dy),
                             (int)NT_, (int)H, (int)W, (int)Ho, (int)Wo, (int)C, cur_stream());
 }
 
 void stem_pool_bwd(const at::Tensor& dout, int64_t ldd, const at::Tensor& arg, const at::Tensor& dact, int64_t NT_,
                    int64_t H, int64_t W, int64_t Ho, int64_t Wo, int64_t C) {
-  stem_pool_bwd_launch(bfp(dout), (int)ldd, arg.data_ptr<uint8_t>(), bfpm(dact), (int)NT_, (int)H, (int)W, (int)Ho,
+  const bool h = kind16(dout);
+  KSEL(h, stem_pool_bwd_launch)(bfp(dout), (int)ldd, arg.data_ptr<uint8_t>(), bfpm(dact), (int)NT_, (int)H, (int)W, (int)Ho,
                        (int)Wo, (int)C, cur_stream());
 }
 
 void avgpool_fwd(const at::Tensor& x, std::vector<int64_t> dims, std::vector<int64_t> k, const at::Tensor& out,
                  int64_t ldo, int64_t coff) {
+  const bool h = kind16(x);
   const int N = (int)dims[0], T = (int)dims[1], H = (int)dims[2], W = (int)dims[3], C = (int)dims[4];
   at::Tensor scratch;
   if (k[0] == T && k[1] == H && k[2] == W)   // global pool: per-split partial sums (deterministic)
-    scratch = at::empty({(int64_t)N * avgpool_global_splits(N, T * H * W) * C}, out.options());
-  avgpool_fwd_launch(bfp(x), N, T, H, W, C, (int)k[0], (int)k[1], (int)k[2], f32(out), (int)ldo, (int)coff,
+    scratch = at::empty({(int64_t)N * KSEL(h, avgpool_global_splits)(N, T * H * W) * C}, out.options());
+  KSEL(h, avgpool_fwd_launch)(bfp(x), N, T, H, W, C, (int)k[0], (int)k[1], (int)k[2], f32(out), (int)ldo, (int)coff,
                      scratch.defined() ? scratch.data_ptr<float>() : nullptr, cur_stream());
 }
 
 void avgpool_bwd(const at::Tensor& dout, int64_t ldo, int64_t coff, std::vector<int64_t> dims, std::vector<int64_t> k,
                  const at::Tensor& dx) {
-  avgpool_bwd_launch(f32(dout), (int)ldo, (int)coff, (int)dims[0], (int)dims[1], (int)dims[2], (int)dims[3],
+  const bool h = kind16(dx);
+  KSEL(h, avgpool_bwd_launch)(f32(dout), (int)ldo, (int)coff, (int)dims[0], (int)dims[1], (int)dims[2], (int)dims[3],
                      (int)dims[4], (int)k[0], (int)k[1], (int)k[2], bfpm(dx), cur_stream());
 }
 
@@ -495,23 +433,25 @@ void sgd_momentum(const at::Tensor& p, const at::Tensor& g, const at::Tensor& bu
   TORCH_CHECK(p.numel() == g.numel() && p.numel() == buf.numel(), "sgd buffers must match");
   int* fi = found_inf.has_value() ? found_inf->data_ptr<int>() : nullptr;
   const int* sk = skip_if.has_value() ? skip_if->data_ptr<int>() : nullptr;
-  sgd_momentum_launch(f32(p), f32(g), f32(buf), p.numel(), f32(lr), (float)momentum, (float)wd, (float)gscale,
+  pva_bf16::sgd_momentum_launch(f32(p), f32(g), f32(buf), p.numel(), f32(lr), (float)momentum, (float)wd, (float)gscale,
                       (int)first, fi, sk, cur_stream());
 }
 
 void nonfinite_check(const at::Tensor& g, double gscale, const at::Tensor& flag) {
   TORCH_CHECK(flag.scalar_type() == at::kInt, "flag must be int32");
-  nonfinite_check_launch(f32(g), g.numel(), (float)gscale, flag.data_ptr<int>(), cur_stream());
+  pva_bf16::nonfinite_check_launch(f32(g), g.numel(), (float)gscale, flag.data_ptr<int>(), cur_stream());
 }
 
 void pack_weights(const at::Tensor& master, const at::Tensor& fwd, const at::Tensor& dgr, const at::Tensor& descs,
                   int64_t ntensors) {
-  pack_weights_launch(f32(master), bfpm(fwd), bfpm(dgr), descs.data_ptr(), (int)ntensors, cur_stream());
+  const bool h = kind16(fwd);
+  KSEL(h, pack_weights_launch)(f32(master), bfpm(fwd), bfpm(dgr), descs.data_ptr(), (int)ntensors, cur_stream());
 }
 
 // frames: packed uint8 ; desc [B,10] int32 ; tidx [B,T] int32 ; out [B*T*S*S, 4] bf16
 void video_preprocess(const at::Tensor& frames, const at::Tensor& desc, const at::Tensor& tidx, int64_t T, int64_t S,
                       std::vector<double> mean, std::vector<double> std_, const at::Tensor& out, bool s2d) {
+  const bool h = kind16(out);
   TORCH_CHECK(!s2d || S % 2 == 0, "space-to-depth output needs an even crop");
   TORCH_CHECK(frames.scalar_type() == at::kByte, "frames must be uint8");
   TORCH_CHECK(desc.dim() == 2 && desc.size(1) == 10 && desc.scalar_type() == at::kInt, "desc [B,10] int32");
@@ -519,27 +459,29 @@ void video_preprocess(const at::Tensor& frames, const at::Tensor& desc, const at
   TORCH_CHECK(out.numel() >= desc.size(0) * T * S * S * 4, "output too small");
   const float m[3] = {(float)mean[0], (float)mean[1], (float)mean[2]};
   const float s[3] = {(float)std_[0], (float)std_[1], (float)std_[2]};
-  video_preprocess_launch(frames.data_ptr<uint8_t>(), desc.data_ptr<int>(), tidx.data_ptr<int>(), (int)desc.size(0),
+  KSEL(h, video_preprocess_launch)(frames.data_ptr<uint8_t>(), desc.data_ptr<int>(), tidx.data_ptr<int>(), (int)desc.size(0),
                           (int)T, (int)S, m, s, bfpm(out), s2d ? 1 : 0, cur_stream());
 }
 
 // space-to-depth stems: x [N*T*Hs*Ws, 16] bf16 ; wpack [Cout_pad16, kt*256] bf16
 void stem_fwd(const at::Tensor& x, const at::Tensor& wpack, const at::Tensor& y, const at::Tensor& stats,
               std::vector<int64_t> dims, int64_t Cout, int64_t kt) {
-  TORCH_CHECK(stem_s2d_supported((int)Cout, (int)kt), "unsupported stem");
+  const bool h = kind16(x);
+  TORCH_CHECK(KSEL(h, stem_s2d_supported)((int)Cout, (int)kt), "unsupported stem");
   TORCH_CHECK(x.size(1) == 16 && x.is_contiguous(), "stem input must be dense s2d [M,16]");
   const int N = dims[0], T = dims[1], Hs = dims[2], Ws = dims[3];
-  TORCH_CHECK(stats.numel() >= (int64_t)stem_tiles(Hs, Ws, N) * 2 * Cout, "stats too small");
-  stem_s2d_launch(0, bfp(x), bfp(wpack), bfpm(y), f32(stats), nullptr, nullptr, N, T, Hs, Ws, (int)Cout, (int)kt,
+  TORCH_CHECK(stats.numel() >= (int64_t)KSEL(h, stem_tiles)(Hs, Ws, N) * 2 * Cout, "stats too small");
+  KSEL(h, stem_s2d_launch)(0, bfp(x), bfp(wpack), bfpm(y), f32(stats), nullptr, nullptr, N, T, Hs, Ws, (int)Cout, (int)kt,
                   cur_stream());
 }
 
 void stem_wgrad(const at::Tensor& x, const at::Tensor& dy, const at::Tensor& acc, std::vector<int64_t> dims,
                 int64_t Cout, int64_t kt) {
-  TORCH_CHECK(stem_s2d_supported((int)Cout, (int)kt), "unsupported stem");
+  const bool h = kind16(x);
+  TORCH_CHECK(KSEL(h, stem_s2d_supported)((int)Cout, (int)kt), "unsupported stem");
   TORCH_CHECK(acc.numel() >= Cout * kt * 256, "accumulator too small");
   const int N = dims[0], T = dims[1], Hs = dims[2], Ws = dims[3];
-  stem_s2d_launch(1, bfp(x), nullptr, nullptr, nullptr, bfp(dy), f32(acc), N, T, Hs, Ws, (int)Cout, (int)kt,
+  KSEL(h, stem_s2d_launch)(1, bfp(x), nullptr, nullptr, nullptr, bfp(dy), f32(acc), N, T, Hs, Ws, (int)Cout, (int)kt,
                   cur_stream());
 }
 
@@ -560,7 +502,7 @@ void head_forward(const at::Tensor& feat, const at::Tensor& W, const OptT& b, do
   TORCH_CHECK(xm.numel() >= (int64_t)N * C && logits.numel() >= (int64_t)N * K, "head outputs too small");
   TORCH_CHECK(p_drop >= 0.0 && p_drop < 1.0, "dropout probability must be in [0, 1)");
   if (N == 0) return;
-  head_forward_launch(f32(feat), N, P, C, f32(W), f32o(b), K, (float)p_drop, (uint64_t)seed, seed_ptr(seed_dev),
+  pva_bf16::head_forward_launch(f32(feat), N, P, C, f32(W), f32o(b), K, (float)p_drop, (uint64_t)seed, seed_ptr(seed_dev),
                       f32(xm), f32(logits), cur_stream());
 }
 
@@ -573,7 +515,7 @@ void head_ce(const at::Tensor& logits, const OptT& labels, double gscale, const 
   TORCH_CHECK(!counts.has_value() || (counts->scalar_type() == at::kLong && counts->numel() >= 2), "counts int64 [2]");
   TORCH_CHECK(row_correct.scalar_type() == at::kInt && row_correct.numel() >= N && row_loss.numel() >= N, "row scratch");
   if (N == 0) return;
-  head_ce_launch(f32(logits), labels.has_value() ? labels->data_ptr<int64_t>() : nullptr, N, K, (float)gscale,
+  pva_bf16::head_ce_launch(f32(logits), labels.has_value() ? labels->data_ptr<int64_t>() : nullptr, N, K, (float)gscale,
                  f32o(dlogits), f32(row_loss), row_correct.data_ptr<int>(), f32o(loss),
                  counts.has_value() ? counts->data_ptr<int64_t>() : nullptr, (int)acc_counts, cur_stream());
 }
@@ -587,7 +529,7 @@ void head_backward(const at::Tensor& dlogits, const at::Tensor& xm, const at::Te
   TORCH_CHECK(scratch.numel() >= (int64_t)K * N + (int64_t)C * N + (int64_t)C * K, "head scratch too small");
   if (N == 0) return;
   float* sc = f32(scratch);
-  head_backward_launch(f32(dlogits), f32(xm), f32(W), N, (int)P, C, K, (float)p_drop, (uint64_t)seed,
+  pva_bf16::head_backward_launch(f32(dlogits), f32(xm), f32(W), N, (int)P, C, K, (float)p_drop, (uint64_t)seed,
                        seed_ptr(seed_dev), f32(dW),
                        f32o(db), (float)beta, f32o(dfeat), sc, sc + (int64_t)K * N, sc + (int64_t)K * N + (int64_t)C * N,
                        cur_stream());
@@ -599,11 +541,12 @@ void bnfold_fwd_stats(const at::Tensor& Wf, const at::Tensor& Ga, const at::Tens
                       const at::Tensor& beta, const OptT& rm, const OptT& rv, const OptT& nbt, double momentum,
                       double eps, const at::Tensor& smean, const at::Tensor& srstd, const at::Tensor& scale,
                       const at::Tensor& shift) {
+  const bool h = kind16(Wf);
   TORCH_CHECK(c % 8 == 0 && c <= 2048 && Wf.numel() >= C * c && Ga.numel() >= c * c && T.numel() >= C * c,
               "bnfold_fwd_stats shapes");
   TORCH_CHECK(sslab.numel() >= splits * c && s_out.numel() >= c, "bnfold colsum shapes");
   int64_t* nb = nbt.has_value() ? nbt->data_ptr<int64_t>() : nullptr;
-  bnfold_fwd_stats_launch(bfp(Wf), f32(Ga), f32(sslab), (int)splits, (int)C, (int)c, count, f32(T), f32(s_out),
+  KSEL(h, bnfold_fwd_stats_launch)(bfp(Wf), f32(Ga), f32(sslab), (int)splits, (int)C, (int)c, count, f32(T), f32(s_out),
                           f32(gamma), f32(beta), f32o(rm), f32o(rv), nb, (float)momentum, (float)eps, f32(smean),
                           f32(srstd), f32(scale), f32(shift), cur_stream());
 }
@@ -613,26 +556,27 @@ void bnfold_bwd(const at::Tensor& part, int64_t tiles, const at::Tensor& Wf, con
                 const at::Tensor& mean, const at::Tensor& rstd, const OptT& dgamma, const OptT& dbeta,
                 const at::Tensor& dW, double beta_acc, const at::Tensor& coef, const at::Tensor& W1t,
                 const at::Tensor& W2, const at::Tensor& bias) {
+  const bool h = kind16(Wf);
   TORCH_CHECK(c % 8 == 0 && Wf.numel() >= C * c && Wd.numel() >= C * c && G.numel() >= C * c && T.numel() >= C * c &&
               dW.numel() == C * c && coef.numel() >= 4 * C && W1t.numel() >= C * c && W2.numel() >= c * c &&
               bias.numel() >= 2 * c && part.numel() >= tiles * 3 * C, "bnfold_bwd shapes");
-  bnfold_bwd_launch(f32(part), (int)tiles, bfp(Wf), bfp(Wd), f32(G), f32(T), f32(s), (int)C, (int)c, count,
+  KSEL(h, bnfold_bwd_launch)(f32(part), (int)tiles, bfp(Wf), bfp(Wd), f32(G), f32(T), f32(s), (int)C, (int)c, count,
                     f32(gamma), f32(mean), f32(rstd), f32o(dgamma), f32o(dbeta), f32(dW), (float)beta_acc, f32(coef),
                     bfpm(W1t), bfpm(W2), f32(bias), cur_stream());
 }
 
 void head_seed_advance(const at::Tensor& seed_dev) {
   TORCH_CHECK(seed_dev.scalar_type() == at::kLong && seed_dev.numel() >= 1 && seed_dev.is_cuda(), "int64 [1] seed");
-  head_seed_advance_launch(reinterpret_cast<uint64_t*>(seed_dev.data_ptr<int64_t>()), cur_stream());
+  pva_bf16::head_seed_advance_launch(reinterpret_cast<uint64_t*>(seed_dev.data_ptr<int64_t>()), cur_stream());
 }
 
 void head_dropout_mask(const at::Tensor& out, double p_drop, int64_t seed) {
   TORCH_CHECK(out.scalar_type() == at::kByte, "mask must be uint8");
-  head_dropout_mask_launch(out.numel(), (float)p_drop, (uint64_t)seed, out.data_ptr<uint8_t>(), cur_stream());
+  pva_bf16::head_dropout_mask_launch(out.numel(), (float)p_drop, (uint64_t)seed, out.data_ptr<uint8_t>(), cur_stream());
 }
 
 void synth_frames(const at::Tensor& out, int64_t seed) {
-  synth_frames_launch(out.data_ptr<uint8_t>(), out.numel(), (uint32_t)seed, cur_stream());
+  pva_bf16::synth_frames_launch(out.data_ptr<uint8_t>(), out.numel(), (uint32_t)seed, cur_stream());
 }
 
 }  // namespace
@@ -650,12 +594,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("bnfold_fwd_stats", &bnfold_fwd_stats);
   m.def("bnfold_bwd", &bnfold_bwd);
   // launch-config helpers for the autotuner
-  m.def("conv_cfg_bm", [](int64_t cfg, int64_t N) { return (int64_t)conv_cfg_bm((int)cfg, (int)N); });
+  m.def("conv_cfg_bm", [](int64_t cfg, int64_t N) { return (int64_t)pva_bf16::conv_cfg_bm((int)cfg, (int)N); });
   m.def("conv_ut_legal", [](std::vector<int64_t> g, int64_t chunk, int64_t bk) {
     ConvParams q{};
     int* f = &q.M;
     for (int i = 0; i < 39 && i < (int)g.size(); ++i) f[i] = (int)g[i];
-    return (int64_t)conv_igemm_ut_legal(q, (int)chunk, (int)bk);
+    return (int64_t)pva_bf16::conv_igemm_ut_legal(q, (int)chunk, (int)bk);
   });
   m.def("wgrad_halo_legal", [](std::vector<int64_t> g, int64_t variant, int64_t affine) {
     TORCH_CHECK(g.size() == 23, "wgrad geometry must have 23 entries");
@@ -665,7 +609,7 @@ PYBIND11_MODULE(_C, m) {
     p.kt = g[12]; p.kh = g[13]; p.kw = g[14]; p.st = g[15]; p.sh = g[16]; p.sw = g[17];
     p.pt = g[18]; p.ph = g[19]; p.pw = g[20]; p.splits = g[21]; p.p_per_split = g[22];
     p.variant = (int)variant; p.affine = (int)affine;
-    return (int64_t)wgrad_halo_legal(p);
+    return (int64_t)pva_bf16::wgrad_halo_legal(p);
   });
   m.def("conv_pw_legal", [](std::vector<int64_t> g, int64_t chunk) {
     ConvParams q{};
@@ -678,10 +622,10 @@ PYBIND11_MODULE(_C, m) {
     };
     q.check = (dim_ok(q.Rt, q.ast, q.aot, q.dir, q.nt, q.Gt) && dim_ok(q.Rh, q.ash, q.aoh, q.dir, q.nh, q.Gh) &&
                dim_ok(q.Rw, q.asw, q.aow, q.dir, q.nw, q.Gw)) ? 0 : 1;
-    return (int64_t)conv_pw_legal(q, (int)chunk);
+    return (int64_t)pva_bf16::conv_pw_legal(q, (int)chunk);
   });
   m.def("wgrad_box_reduce", &wgrad_box_reduce);
-  m.def("box_reduce_groups", [](int64_t splits) { return (int64_t)wgrad_box_reduce_groups((int)splits); });
+  m.def("box_reduce_groups", [](int64_t splits) { return (int64_t)pva_bf16::wgrad_box_reduce_groups((int)splits); });
   m.def("wgrad_box_legal", [](std::vector<int64_t> g) {
     // [P, Cout, K, Cin, ldd, ldx, Ti, Hi, Wi, To, Ho, Wo, kt, kh, kw, st, sh, sw, pt, ph, pw]
     WgradParams q{};
@@ -689,39 +633,39 @@ PYBIND11_MODULE(_C, m) {
     q.Ti = g[6]; q.Hi = g[7]; q.Wi = g[8]; q.To = g[9]; q.Ho = g[10]; q.Wo = g[11];
     q.kt = g[12]; q.kh = g[13]; q.kw = g[14]; q.st = g[15]; q.sh = g[16]; q.sw = g[17];
     q.pt = g[18]; q.ph = g[19]; q.pw = g[20];
-    return (int64_t)wgrad_box_legal(q);
+    return (int64_t)pva_bf16::wgrad_box_legal(q);
   });
   m.def("conv_halo64p_legal", [](std::vector<int64_t> g, int64_t chunk) {
     ConvParams q{};
     int* f = &q.M;
     for (int i = 0; i < 39 && i < (int)g.size(); ++i) f[i] = (int)g[i];
-    return (int64_t)conv_halo64p_legal(q, (int)chunk);
+    return (int64_t)pva_bf16::conv_halo64p_legal(q, (int)chunk);
   });
   m.def("conv_halo_legal", [](std::vector<int64_t> g, int64_t chunk) {
     ConvParams q{};
     int* f = &q.M;
     for (int i = 0; i < 39 && i < (int)g.size(); ++i) f[i] = (int)g[i];
-    return (int64_t)conv_halo_legal(q, (int)chunk);
+    return (int64_t)pva_bf16::conv_halo_legal(q, (int)chunk);
   });
   m.def("conv_direct_legal", [](std::vector<int64_t> g, int64_t chunk) {
     ConvParams q{};
     int* f = &q.M;
     for (int i = 0; i < 39 && i < (int)g.size(); ++i) f[i] = (int)g[i];
-    return (int64_t)conv_direct_legal(q, (int)chunk);
+    return (int64_t)pva_bf16::conv_direct_legal(q, (int)chunk);
   });
   m.def("conv_igemm_epi", &conv_igemm_epi, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("accum"), py::arg("g"),
         py::arg("chunk"), py::arg("res"), py::arg("ldr"), py::arg("mask"), py::arg("y0"), py::arg("mean0"),
         py::arg("rstd0"), py::arg("y1"), py::arg("mean1"), py::arg("rstd1"), py::arg("part"),
         py::arg("msc") = py::none(), py::arg("msh") = py::none(), py::arg("cfg") = -1, py::arg("bias") = py::none());
   m.def("conv_m_tiles", &conv_m_tiles, py::arg("M"), py::arg("N"), py::arg("K") = 0, py::arg("Cg") = 0);
-  m.def("conv_set_bk", [](int64_t bk) { conv_igemm_set_bk((int)bk); });
-  m.def("conv_set_ut", [](int64_t mode) { conv_igemm_set_ut((int)mode); });
+  m.def("conv_set_bk", [](int64_t bk) { pva_bf16::conv_igemm_set_bk((int)bk); pva_f16::conv_igemm_set_bk((int)bk); });
+  m.def("conv_set_ut", [](int64_t mode) { pva_bf16::conv_igemm_set_ut((int)mode); pva_f16::conv_igemm_set_ut((int)mode); });
   m.def("wgrad_rt_legal", [](int64_t Cout, int64_t Cin, int64_t ldd, int64_t ldx, int64_t chunk) {
-    return wgrad_rt_legal((int)Cout, (int)Cin, (int)ldd, (int)ldx, (int)chunk, 0) != 0;
+    return pva_bf16::wgrad_rt_legal((int)Cout, (int)Cin, (int)ldd, (int)ldx, (int)chunk, 0) != 0;
   });
   m.def("wgrad_tile", &wgrad_tile, py::arg("Cout"), py::arg("K"), py::arg("variant") = -1);
   m.def("wgrad_narrow_legal", [](int64_t Cout, int64_t Cin, int64_t K) {
-    return (bool)wgrad_narrow_legal((int)Cout, (int)Cin, (int)K);
+    return (bool)pva_bf16::wgrad_narrow_legal((int)Cout, (int)Cin, (int)K);
   });
   m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("partial"), py::arg("scale"),
         py::arg("shift"), py::arg("affine"), py::arg("g"), py::arg("chunk"), py::arg("slab") = 0,
@@ -757,11 +701,11 @@ PYBIND11_MODULE(_C, m) {
         py::arg("skip_if") = py::none());
   m.def("nonfinite_check", &nonfinite_check);
   m.def("pack_weights", &pack_weights);
-  m.def("pack_desc_size", &pack_desc_size);
+  m.def("pack_desc_size", &pva_bf16::pack_desc_size);
   m.def("video_preprocess", &video_preprocess);
   m.def("synth_frames", &synth_frames);
-  m.def("stem_tiles", [](int64_t Ho, int64_t Wo, int64_t N) { return stem_tiles((int)Ho, (int)Wo, (int)N); });
-  m.def("stem_supported", [](int64_t Cout, int64_t kt) { return stem_s2d_supported((int)Cout, (int)kt); });
+  m.def("stem_tiles", [](int64_t Ho, int64_t Wo, int64_t N) { return pva_bf16::stem_tiles((int)Ho, (int)Wo, (int)N); });
+  m.def("stem_supported", [](int64_t Cout, int64_t kt) { return pva_bf16::stem_s2d_supported((int)Cout, (int)kt); });
   m.def("head_forward", &head_forward, py::arg("feat"), py::arg("W"), py::arg("b"), py::arg("p_drop"), py::arg("seed"),
         py::arg("xm"), py::arg("logits"), py::arg("seed_dev") = py::none());
   m.def("head_seed_advance", &head_seed_advance);
@@ -773,10 +717,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("stem_fwd", &stem_fwd);
   m.def("stem_wgrad", &stem_wgrad);
   m.def("stem_wgrad_convert", [](const at::Tensor& acc, const at::Tensor& grad, int64_t Cout, int64_t kt, double beta) {
-    stem_wgrad_convert_launch(f32(acc), f32(grad), (int)Cout, (int)kt, (float)beta, cur_stream());
+    pva_bf16::stem_wgrad_convert_launch(f32(acc), f32(grad), (int)Cout, (int)kt, (float)beta, cur_stream());
   });
   m.def("stem_pack", [](const at::Tensor& w, const at::Tensor& out, int64_t Cout, int64_t kt) {
-    stem_pack_launch(f32(w), bfpm(out), (int)Cout, (int)kt, cur_stream());
+    const bool h = kind16(out);
+    KSEL(h, stem_pack_launch)(f32(w), bfpm(out), (int)Cout, (int)kt, cur_stream());
   });
   register_clip_reader(m);
 }

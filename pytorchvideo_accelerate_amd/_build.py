@@ -1,8 +1,9 @@
 """Native build of the gfx950 extension (``pytorchvideo_accelerate_amd._C``).
 
 No hipify, no ``torch.utils.cpp_extension.CUDAExtension`` (which would run hipify on ROCm): every
-``csrc/kernels/*.hip`` file is compiled directly by ``hipcc --offload-arch=gfx950`` and linked with the
-pybind11 binding unit against libtorch.  Objects are cached by a hash of (source, headers, flags) so
+``csrc/kernels/*.hip`` file is compiled directly by ``hipcc --offload-arch=gfx950`` — twice, once per 16-bit
+compute type (``-DPVA_F16=0``: bf16 operands, namespace ``pva_bf16``; ``-DPVA_F16=1``: fp16 operands, namespace
+``pva_f16``; ``csrc/kernels/common.h``) — and linked with the pybind11 binding unit against libtorch.  Objects are cached by a hash of (source, headers, flags) so
 re-builds only recompile what changed.  The resulting ``_C*.so`` lives in-tree next to this file (so it
 travels to the GPU box with the repository snapshot).
 
@@ -49,11 +50,11 @@ def _headers_digest() -> str:
     return h.hexdigest()
 
 
-def _compile(src: str, flags: list, hdr: str, force: bool) -> str:
+def _compile(src: str, flags: list, hdr: str, force: bool, tag: str = "") -> str:
     with open(src, "rb") as fh:
         content = fh.read()
     key = hashlib.sha1(content + hdr.encode() + " ".join(flags).encode()).hexdigest()[:16]
-    obj = os.path.join(BUILD, os.path.basename(src) + "." + key + ".o")
+    obj = os.path.join(BUILD, os.path.basename(src) + tag + "." + key + ".o")
     if os.path.exists(obj) and not force:
         return obj
     cmd = [HIPCC] + flags + ["-c", src, "-o", obj + ".tmp"]
@@ -78,7 +79,8 @@ def build(jobs: int = 0, force: bool = False, verbose: bool = False) -> str:
     runtime = sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp")))
     jobs = jobs or min(16, os.cpu_count() or 4)
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-        futs = [ex.submit(_compile, s, kern_flags, hdr, force) for s in kernels]
+        futs = [ex.submit(_compile, s, kern_flags + [f"-DPVA_F16={h}"], hdr, force, (".f16" if h else ".bf16"))
+                for s in kernels for h in (0, 1)]
         futs += [ex.submit(_compile, s, bind_flags, hdr, force) for s in runtime]
         objs = [f.result() for f in futs]
     out = ext_path()

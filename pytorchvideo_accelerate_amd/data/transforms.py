@@ -100,9 +100,11 @@ class GpuClipBatch:
     """Runs the fused preprocess kernel for a batch of decoded clips (same source shape)."""
 
     def __init__(self, device, num_frames: int, crop: int, alpha: Optional[int], mean=MEAN, std=STD,
-                 s2d: bool = False):
+                 s2d: bool = False, dtype: torch.dtype = torch.bfloat16):
+        """``dtype``: the executor's 16-bit compute type (bf16, or fp16 for ``--mixed_precision fp16``)."""
         from ..ops._ext import require
         self.C = require()
+        self.dtype = dtype
         self.s2d = s2d  # space-to-depth output for the direct stem kernels (C = 16 at S/2 x S/2)
         self.device = torch.device(device)
         self.T, self.S, self.alpha = num_frames, crop, alpha
@@ -113,7 +115,7 @@ class GpuClipBatch:
     def _buf(self, key, shape):
         t = self._out.get(key)
         if t is None or tuple(t.shape) != tuple(shape):
-            t = torch.empty(shape, device=self.device, dtype=torch.bfloat16)
+            t = torch.empty(shape, device=self.device, dtype=self.dtype)
             self._out[key] = t
         return t
 

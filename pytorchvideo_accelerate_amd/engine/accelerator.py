@@ -61,9 +61,9 @@ class Accelerator:
         self.logging_dir = logging_dir
         self.bucket_mb = bucket_mb
         # Precision policy (what runs is what was asked for; recorded as ``compute_dtype``):
-        #  * bf16 / fp16 on a GPU -> the fused gfx950 kernels: bf16 MFMA compute, fp32 master weights and optimizer;
-        #    fp16 additionally runs the dynamic loss-scale state machine of the reference recipe (run_slowfast_r50.sh)
-        #    on top of bf16 compute (documented alias: the kernels have no fp16 variant);
+        #  * bf16 / fp16 on a GPU -> the fused gfx950 kernels in that dtype (bf16 or fp16 MFMA operands and
+        #    activations, fp32 accumulation, statistics, master weights and optimizer); fp16 also runs the dynamic
+        #    loss-scale state machine of the reference recipe (run_slowfast_r50.sh, GradScaler semantics);
         #  * "no" (the reference default, fp32 math) on a GPU -> the PyTorch fp32 module path, unless the fused
         #    kernels are requested explicitly with kernels="fused" (then bf16 compute, said so in compute_dtype);
         #  * CPU -> the PyTorch path.
@@ -76,7 +76,7 @@ class Accelerator:
                     print("note: --mixed_precision no requests fp32 math: running the PyTorch fp32 path; "
                           "--mixed_precision bf16 (or --kernels fused) selects the fused MI355X kernels", flush=True)
         if kernels == "fused":
-            self.compute_dtype = "bf16" if mixed_precision != "fp16" else "bf16+fp16-loss-scaling"
+            self.compute_dtype = "fp16" if mixed_precision == "fp16" else "bf16"
         else:
             self.compute_dtype = {"bf16": "bf16-autocast", "fp16": "fp16-autocast"}.get(mixed_precision, "fp32")
         self.kernels = kernels

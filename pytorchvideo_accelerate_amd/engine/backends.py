@@ -1,6 +1,6 @@
 """Execution back-ends behind one training-step interface.
 
-* :class:`FusedBackend` — the MI355X path: ``models/fused.FusedNet`` (gfx950 kernels, bf16) with the
+* :class:`FusedBackend` — the MI355X path: ``models/fused.FusedNet`` (gfx950 kernels, bf16 or fp16) with the
   bucketed RCCL gradient all-reduce of ``parallel/ddp.GradSync`` overlapped with the backward pass.
 * :class:`TorchBackend` — the reference PyTorch modules with autograd: CPU runs (``--cpu``, gloo DDP), fp32
   (``--mixed_precision no``) or autocast fp16/bf16 on GPU.  Gradients land in the same flat buffer
@@ -97,7 +97,8 @@ class FusedBackend:
         self.state = state
         self.device = state.device
         dp = state.world_size > 1
-        self.net = FusedNet(model, self.device, load_tuning=not dp)
+        cdt = torch.float16 if mixed_precision == "fp16" else torch.bfloat16
+        self.net = FusedNet(model, self.device, load_tuning=not dp, compute_dtype=cdt)
         if dp:   # identical autotuner choices on every rank
             self.net.tuner.agree = state.agree_times
             ts = self.net.tune_store
@@ -111,7 +112,7 @@ class FusedBackend:
         bounds = sorted(set(self.flat.span(p)[1] for p in self.flat.params))
         self.sync = GradSync(self.flat.grad, state, bucket_mb, boundaries=bounds)
         self.net.grad_hook = self.sync.progress if state.world_size > 1 else None
-        # fp16 requests get the dynamic loss-scale state machine (compute stays bf16 MFMA)
+        # fp16: fp16 kernels plus the dynamic loss-scale state machine (GradScaler semantics: fp16 has 5 exponent bits)
         self.scaler = FusedGradScaler() if mixed_precision == "fp16" else None
         self._training = True
         self.timer = None   # utils.profiling.StepTimer (optional)

@@ -152,7 +152,8 @@ def training_function(args: Namespace) -> dict:
         from ..data.loader import DeviceLoader, make_host_loader
         from ..data.transforms import GpuClipBatch
         prep = GpuClipBatch(acc.device, args.num_frames, args.crop_size,
-                            args.slowfast_alpha if args.is_slowfast else None, s2d=backend.net.input_s2d)
+                            args.slowfast_alpha if args.is_slowfast else None, s2d=backend.net.input_s2d,
+                            dtype=backend.net.cdt)
         train_loader = DeviceLoader(make_host_loader(train_ds, args.batch_size, args.num_workers, args.pin_memory),
                                     prep, acc.device)
         val_loader = DeviceLoader(make_host_loader(val_ds, args.batch_size, args.num_workers, args.pin_memory),

@@ -135,7 +135,7 @@ class _ConvBN:
         self.eng.mark(self.name + ".fwd")
         To, Ho, Wo = s.out_dims(x.T, x.H, x.W)
         M = x.N * To * Ho * Wo
-        y = self.eng.ws((self.name, "y", tag), (M, s.cout), torch.bfloat16)
+        y = self.eng.ws((self.name, "y", tag), (M, s.cout), self.eng.cdt)
         stats = None
         if train:  # sized for the smallest row tile (128); the launch writes ceil(M / BM) of them
             stats = self.eng.ws((self.name, "stats"), ((M + 127) // 128, 2, s.cout), torch.float32)
@@ -370,7 +370,7 @@ class _ConvBN:
             if g is None:
                 g = self._geo[key] = fwd_geometry(s, yb.N, yb.T, yb.H, yb.W, yb.ld, Co)
             stats = eng.ws((self.name, "stats"), ((yb.M + 127) // 128, 2, Co), torch.float32)
-            dummy = eng.ws(("nostore_y",), (1, 8), torch.bfloat16)
+            dummy = eng.ws(("nostore_y",), (1, 8), eng.cdt)
             tuner = eng.tuner
             aff = 2 if bxf.relu else 1
 
@@ -415,8 +415,8 @@ class _ConvBN:
         G = eng.scratch("fold_G", Co * c)
         self.wgrad(dz, yb, bxf, dest=G, beta=0.0)
         if getattr(self, "W1t", None) is None:
-            self.W1t = torch.empty(c, Co, device=eng.device, dtype=torch.bfloat16)
-            self.W2 = torch.empty(c, c, device=eng.device, dtype=torch.bfloat16)
+            self.W1t = torch.empty(c, Co, device=eng.device, dtype=eng.cdt)
+            self.W2 = torch.empty(c, c, device=eng.device, dtype=eng.cdt)
             self.fbias = torch.empty(2 * c, device=eng.device, dtype=torch.float32)   # [biasA | biasB]
         fg = eng.flat
         eng.mark(self.name + ".foldbwd")
@@ -467,8 +467,8 @@ class _ConvBN:
         G = eng.scratch("fold_G", Co * c)
         self.wgrad(dz, x, None, dest=G, beta=0.0)
         if getattr(self, "W1t", None) is None:
-            self.W1t = torch.empty(c, Co, device=eng.device, dtype=torch.bfloat16)
-            self.W2 = torch.empty(c, c, device=eng.device, dtype=torch.bfloat16)
+            self.W1t = torch.empty(c, Co, device=eng.device, dtype=eng.cdt)
+            self.W2 = torch.empty(c, c, device=eng.device, dtype=eng.cdt)
             self.fbias = torch.empty(2 * c, device=eng.device, dtype=torch.float32)   # [biasA | biasB]
         fg = eng.flat
         eng.mark(self.name + ".foldbwd")
@@ -586,8 +586,8 @@ class _ConvBN:
             C.bn_bwd_finalize(part, blocks, Cc, M, 1, other.bn.weight, other.mean, other.rstd,
                               fg.gview(other.bn.weight), fg.gview(other.bn.bias), eng.grad_beta, other.coef,
                               other.fin)
-        dy = eng.ws((self.name, "dy"), (M, Cc), torch.bfloat16)
-        dy1 = eng.ws((other.name, "dy"), (M, Cc), torch.bfloat16) if other is not None else None
+        dy = eng.ws((self.name, "dy"), (M, Cc), eng.cdt)
+        dy1 = eng.ws((other.name, "dy"), (M, Cc), eng.cdt) if other is not None else None
         eng.mark(self.name + ".bnapply")
         C.bn_bwd_apply(g.t, g.ld, mask_mode, mo_t, mo_ld,
                        None if mxf is None else mxf.scale, None if mxf is None else mxf.shift,
@@ -600,12 +600,12 @@ class _ConvBN:
         return a, b
 
 
-def to_s2d(x_ncthw: torch.Tensor) -> Act:
-    """NCTHW float clip -> space-to-depth stem input: 2x2 pixel blocks x RGB0 = 16 bf16 channels."""
+def to_s2d(x_ncthw: torch.Tensor, dtype: torch.dtype = torch.bfloat16) -> Act:
+    """NCTHW float clip -> space-to-depth stem input: 2x2 pixel blocks x RGB0 = 16 channels of ``dtype``."""
     N, C, T, H, W = x_ncthw.shape
     x = F.pad(x_ncthw, (0, 0, 0, 0, 0, 0, 0, 4 - C))                  # RGB0
     x = x.reshape(N, 4, T, H // 2, 2, W // 2, 2).permute(0, 2, 3, 5, 4, 6, 1)  # N,T,Hs,Ws,sy,sx,c
-    x = x.reshape(N * T * (H // 2) * (W // 2), 16).contiguous().to(torch.bfloat16)
+    x = x.reshape(N * T * (H // 2) * (W // 2), 16).contiguous().to(dtype)
     return Act(x, N, T, H // 2, W // 2)
 
 
@@ -626,7 +626,7 @@ class _Stem:
                     and eng.C.stem_supported(self.u.C, self.kt))
         if self.s2d:
             cpad = (self.u.C + 15) // 16 * 16
-            self.wpack = torch.zeros(cpad * self.kt * 256, device=eng.device, dtype=torch.bfloat16)
+            self.wpack = torch.zeros(cpad * self.kt * 256, device=eng.device, dtype=eng.cdt)
 
     def out_channels(self):
         return self.u.C
@@ -645,7 +645,7 @@ class _Stem:
         eng, C, u = self.eng, self.eng.C, self.u
         assert x.C == 16 and x.t.is_contiguous(), "s2d stem expects a dense [M, 16] space-to-depth input"
         M = x.M
-        y = eng.ws((u.name, "y", tag), (M, u.C), torch.bfloat16)
+        y = eng.ws((u.name, "y", tag), (M, u.C), eng.cdt)
         tiles = C.stem_tiles(x.H, x.W, x.N)
         stats = eng.ws((u.name, "stats"), (tiles, 2, u.C), torch.float32)
         eng.mark(u.name + ".fwd")
@@ -666,7 +666,7 @@ class _Stem:
         P = y.N * y.T * Ho * Wo
         arg = self.eng.ws((self.name, "arg"), (P, self.u.C), torch.uint8)
         # training: also the raw y at every window argmax — the BN-backward sums are then taken on the pooled grid
-        ymax = self.eng.ws((self.name, "ymax"), (P, self.u.C), torch.bfloat16) if train else None
+        ymax = self.eng.ws((self.name, "ymax"), (P, self.u.C), self.eng.cdt) if train else None
         self.eng.mark(self.name + ".pool")
         C.stem_pool_fwd(y.t, self.u.scale, self.u.shift, out, out.stride(0), arg, y.N * y.T, y.H, y.W, Ho, Wo,
                         self.u.C, ymax)
@@ -689,7 +689,7 @@ class _Stem:
         fg = eng.flat
         C.bn_bwd_finalize(part, blocks, u.C, y.M, 0, u.bn.weight, u.mean, u.rstd, fg.gview(u.bn.weight),
                           fg.gview(u.bn.bias), eng.grad_beta, u.coef, u.fin)
-        dyt = eng.ws((u.name, "dy"), (y.M, u.C), torch.bfloat16)
+        dyt = eng.ws((u.name, "dy"), (y.M, u.C), eng.cdt)
         eng.mark(self.name + ".poolbwd")
         C.stem_pool_bn_apply(dout.t, dout.ld, self.arg, y.t, u.scale, u.shift, u.coef, dyt, y.N * y.T, y.H, y.W,
                              dout.H, dout.W, u.C)
@@ -785,13 +785,13 @@ class _ResBlock:
         else:
             dyc, dy1 = self.c.bn_backward(dout, yc, 3, self.mask, None, other=self.one, other_y=y1)
         self.c.wgrad(dyc, yb, self.b.xf())
-        dab = eng.ws((self.name, "dab"), (yb.M, self.b.C), torch.bfloat16)
+        dab = eng.ws((self.name, "dab"), (yb.M, self.b.C), eng.cdt)
         # the dgrad epilogues apply the b / a ReLU masks and reduce their BN-backward sums (no separate pass)
         pb = self.c.dgrad(dyc, (yb.T, yb.H, yb.W), dab, False, bn=(self.b, yb))
         dyb, _ = self.b.bn_backward(Act(dab, yb.N, yb.T, yb.H, yb.W), yb, 0 if pb else 2, None,
                                     None if pb else self.b.xf(), pre=pb)
         self.b.wgrad(dyb, ya, self.a.xf())
-        daa = eng.ws((self.name, "daa"), (ya.M, self.a.C), torch.bfloat16)
+        daa = eng.ws((self.name, "daa"), (ya.M, self.a.C), eng.cdt)
         pa = self.b.dgrad(dyb, (ya.T, ya.H, ya.W), daa, False, bn=(self.a, ya))
         dya, _ = self.a.bn_backward(Act(daa, ya.N, ya.T, ya.H, ya.W), ya, 0 if pa else 2, None,
                                     None if pa else self.a.xf(), pre=pa)
@@ -820,7 +820,7 @@ class _ResBlock:
         fg = eng.flat
         res = None
         fold1 = self.fold1
-        dy1 = eng.ws((one.name, "dy"), (M, Cc), torch.bfloat16) if (one is not None and not fold1) else None
+        dy1 = eng.ws((one.name, "dy"), (M, Cc), eng.cdt) if (one is not None and not fold1) else None
         if pre is not None:
             # dout is already the masked dz; its partial sums came from the next unit's dgrad epilogue
             part, tiles = pre
@@ -836,7 +836,7 @@ class _ResBlock:
             dual = one is not None and not fold1
             dzb = None
             if one is not None and fold1:   # the folded branch1 needs dz itself: the same pass writes it
-                dzb = Act(eng.ws((self.name, "dz"), (M, Cc), torch.bfloat16), x.N, yb.T, yb.H, yb.W)
+                dzb = Act(eng.ws((self.name, "dz"), (M, Cc), eng.cdt), x.N, yb.T, yb.H, yb.W)
             C.bn_bwd_reduce(dout.t, dout.ld, 3, self.mask, Cc // 8, None, None, None, None, None,
                             y1.t if dual else None, one.mean if dual else None,
                             one.rstd if dual else None, M, Cc, blocks, rpb, part,
@@ -849,7 +849,7 @@ class _ResBlock:
             elif dzb is not None:
                 dz = dzb
             else:
-                dz = Act(eng.ws((self.name, "dz"), (M, Cc), torch.bfloat16), x.N, yb.T, yb.H, yb.W)
+                dz = Act(eng.ws((self.name, "dz"), (M, Cc), eng.cdt), x.N, yb.T, yb.H, yb.W)
         if one is not None and fold1:
             # branch1 first: it consumes the dz partials (`part`) before the conv_c dgrad epilogue reuses that scratch
             one.fold_branch1_backward(dz, part, tiles, x, dx, dx_accum)
@@ -864,11 +864,11 @@ class _ResBlock:
             else:
                 C.bn_bwd_apply(dout.t, dout.ld, 3, self.mask, Cc // 8, None, None, None, None, None, y1.t, one.coef,
                                dy1, dz.t, dz.ld, 0, M, Cc)
-        dab = eng.ws((self.name, "dab"), (yb.M, self.b.C), torch.bfloat16)
+        dab = eng.ws((self.name, "dab"), (yb.M, self.b.C), eng.cdt)
         pb = self.c.fold_backward(dz, part, tiles, yb, self.b, dab)
         dyb, _ = self.b.bn_backward(Act(dab, yb.N, yb.T, yb.H, yb.W), yb, 0, None, None, pre=pb)
         self.b.wgrad(dyb, ya, self.a.xf())
-        daa = eng.ws((self.name, "daa"), (ya.M, self.a.C), torch.bfloat16)
+        daa = eng.ws((self.name, "daa"), (ya.M, self.a.C), eng.cdt)
         pa = self.b.dgrad(dyb, (ya.T, ya.H, ya.W), daa, False, bn=(self.a, ya))
         dya, _ = self.a.bn_backward(Act(daa, ya.N, ya.T, ya.H, ya.W), ya, 0 if pa else 2, None,
                                     None if pa else self.a.xf(), pre=pa)
@@ -932,7 +932,7 @@ class _Stage:
                 o = out
             else:
                 T, H, W = b.out_dims(x.T, x.H, x.W)
-                o = eng.ws((b.name, "out", tag), (x.N * T * H * W, b.out_channels()), torch.bfloat16)
+                o = eng.ws((b.name, "out", tag), (x.N * T * H * W, b.out_channels()), eng.cdt)
             x = b.fwd(x, o, train, tag)
         return x
 
@@ -945,7 +945,7 @@ class _Stage:
                 tgt, acc = dx, dx_accum
             else:
                 xin = b.x
-                tgt, acc = eng.ws((b.name, "dx"), (xin.M, xin.C), torch.bfloat16), False
+                tgt, acc = eng.ws((b.name, "dx"), (xin.M, xin.C), eng.cdt), False
             pre = b.bwd(dout, tgt, acc, pre=pre, prev=self.blocks[i - 1] if i > 0 else None)
             b.eng_progress(b.flat_hi)
             if i > 0:
@@ -978,10 +978,14 @@ class FusedNet:
     """Executor bound to a reference ``Net`` (SlowFast or Slow ResNet3D) whose parameters it shares."""
 
     def __init__(self, model: R.Net, device: torch.device, stem_s2d: bool = True, deterministic: bool = False,
-                 load_tuning: bool = True):
+                 load_tuning: bool = True, compute_dtype: torch.dtype = torch.bfloat16):
         """``deterministic``: bitwise-reproducible gradients (slab wgrad reduction, generic stems; BN
         statistics are always reduced in a fixed order).  Costs a little speed.  ``load_tuning``: restore the
-        persistent autotuner table now (data parallelism restores rank 0's copy instead: ``FusedBackend``)."""
+        persistent autotuner table now (data parallelism restores rank 0's copy instead: ``FusedBackend``).
+        ``compute_dtype``: the 16-bit MFMA operand / activation type, bf16 or fp16 (``--mixed_precision fp16``: the
+        fp16 build of every kernel, csrc/kernels/common.h; fp32 accumulation, statistics and master weights)."""
+        assert compute_dtype in (torch.bfloat16, torch.float16), compute_dtype
+        self.cdt = compute_dtype
         self.C = require()
         self.deterministic = deterministic
         # fixed-order (slab) reduction for the weight-gradient launches whose results feed back into the step —
@@ -1007,7 +1011,7 @@ class FusedNet:
         self.tune_store = None
         if self.tuner.enabled:
             self.tune_store = TuneStore({"conv": self.tuner.cache, "eval": self._eval_tune, "wgrad": self.wtune},
-                                        TuneStore.build_ident(self.device, "bf16"))
+                                        TuneStore.build_ident(self.device, str(compute_dtype)))
             if load_tuning:
                 self.tune_store.load()
         self._ws: Dict = {}
@@ -1186,8 +1190,8 @@ class FusedNet:
             offs.append((fwd_n, dgr_n if nd else -1))
             fwd_n += (nf + 7) // 8 * 8
             dgr_n += (nd + 7) // 8 * 8
-        self.pack_fwd = torch.zeros(fwd_n, device=self.device, dtype=torch.bfloat16)
-        self.pack_dgr = torch.zeros(max(dgr_n, 8), device=self.device, dtype=torch.bfloat16)
+        self.pack_fwd = torch.zeros(fwd_n, device=self.device, dtype=self.cdt)
+        self.pack_dgr = torch.zeros(max(dgr_n, 8), device=self.device, dtype=self.cdt)
         import numpy as np
         dsz = self.C.pack_desc_size()
         assert dsz == 40
@@ -1238,10 +1242,10 @@ class FusedNet:
                     M = x.N * T * H * W
                     co = mod.out_channels()
                     if p == 0 and fuse is not None:
-                        cat = self.ws(("cat", si, tag), (M, co + fuse.u.C), torch.bfloat16)
+                        cat = self.ws(("cat", si, tag), (M, co + fuse.u.C), self.cdt)
                         out = cat[:, :co]
                     else:
-                        out = self.ws(("pout", si, p, tag), (M, co), torch.bfloat16)
+                        out = self.ws(("pout", si, p, tag), (M, co), self.cdt)
                     if ms and p == 1:
                         self.lane = 1
                         with torch.cuda.stream(side):
@@ -1392,7 +1396,7 @@ class FusedNet:
         coff = 0
         self.mark("head.poolbwd")
         for p, (o, k) in enumerate(zip(outs, ks)):
-            d = self.ws(("dlast", p), (o.M, o.C), torch.bfloat16)
+            d = self.ws(("dlast", p), (o.M, o.C), self.cdt)
             C.avgpool_bwd(gfeat, Ctot, coff, [o.N, o.T, o.H, o.W, o.C], list(k), d)
             douts.append(Act(d, o.N, o.T, o.H, o.W))
             coff += o.C
@@ -1430,7 +1434,7 @@ class FusedNet:
                                 self._progress(mod.flat_hi)
                         else:
                             xin = mod.blocks[0].x
-                            dx = self.ws(("dstage_in", si, p), (xin.M, xin.C), torch.bfloat16)
+                            dx = self.ws(("dstage_in", si, p), (xin.M, xin.C), self.cdt)
                             mod.bwd(douts[p], dx, False)
                             new[p] = Act(dx, xin.N, xin.T, xin.H, xin.W)
                     finally:
@@ -1450,5 +1454,5 @@ class FusedNet:
     def prepare_inputs(self, xs_ncthw: Sequence[torch.Tensor]) -> List[Act]:
         """NCTHW float clips (already normalised) -> stem input Acts (s2d or NDHWC RGB0)."""
         if self.input_s2d:
-            return [to_s2d(x.to(self.device)) for x in xs_ncthw]
-        return [Act.from_ncthw(x.to(self.device), c_pad=4) for x in xs_ncthw]
+            return [to_s2d(x.to(self.device), self.cdt) for x in xs_ncthw]
+        return [Act.from_ncthw(x.to(self.device), c_pad=4, dtype=self.cdt) for x in xs_ncthw]

@@ -51,12 +51,12 @@ class Act:
         return self.t.reshape(self.N, self.T, self.H, self.W, self.C).permute(0, 4, 1, 2, 3)
 
     @staticmethod
-    def from_ncthw(x: torch.Tensor, c_pad: Optional[int] = None) -> "Act":
+    def from_ncthw(x: torch.Tensor, c_pad: Optional[int] = None, dtype: torch.dtype = torch.bfloat16) -> "Act":
         N, C, T, H, W = x.shape
         y = x.permute(0, 2, 3, 4, 1)
         if c_pad is not None and c_pad > C:
             y = torch.nn.functional.pad(y, (0, c_pad - C))
-        y = y.contiguous().to(torch.bfloat16)
+        y = y.contiguous().to(dtype)
         return Act(y.reshape(N * T * H * W, y.shape[-1]), N, T, H, W)
 
 
@@ -92,8 +92,8 @@ class ConvSpec:
         return 2 * N * To * Ho * Wo * self.cout * self.cin * self.taps
 
 
-def pack_weight(w: torch.Tensor, spec: ConvSpec) -> Tuple[torch.Tensor, torch.Tensor]:
-    """fp32 [Cout, Cin, kt, kh, kw] -> (bf16 forward pack [Cout, taps, Cin_pad], dgrad pack [Cin, taps, Cout]).
+def pack_weight(w: torch.Tensor, spec: ConvSpec, dtype: torch.dtype = torch.bfloat16) -> Tuple[torch.Tensor, torch.Tensor]:
+    """fp32 [Cout, Cin, kt, kh, kw] -> (16-bit forward pack [Cout, taps, Cin_pad], dgrad pack [Cin, taps, Cout]).
 
     Host-side (torch) version used by tests and one-off packs; the training loop uses the multi-tensor
     ``pack_weights`` kernel (ops/optim.py).
@@ -103,7 +103,7 @@ def pack_weight(w: torch.Tensor, spec: ConvSpec) -> Tuple[torch.Tensor, torch.Te
     if spec.cin_pad > ci:
         wf = torch.nn.functional.pad(wf, (0, spec.cin_pad - ci))
     wd = w.reshape(co, ci, -1).permute(1, 2, 0)  # [Cin, taps, Cout]
-    return wf.contiguous().to(torch.bfloat16), wd.contiguous().to(torch.bfloat16)
+    return wf.contiguous().to(dtype), wd.contiguous().to(dtype)
 
 
 def fwd_geometry(spec: ConvSpec, N: int, T: int, H: int, W: int, ldx: int, ldy: int) -> list:
@@ -166,7 +166,7 @@ def conv_fwd(x: Act, wpack: torch.Tensor, spec: ConvSpec, out: Optional[torch.Te
     To, Ho, Wo = spec.out_dims(x.T, x.H, x.W)
     M = x.N * To * Ho * Wo
     if out is None:
-        out = torch.empty(M, spec.cout, device=x.t.device, dtype=torch.bfloat16)
+        out = torch.empty(M, spec.cout, device=x.t.device, dtype=x.t.dtype)
     affine = 0 if in_scale is None else (2 if in_relu else 1)
     g = fwd_geometry(spec, x.N, x.T, x.H, x.W, x.ld, out.stride(0))
     C.conv_igemm(x.t, wpack, out, stats, in_scale, in_shift, affine, 0, g, spec.chunk, cfg)
@@ -181,7 +181,7 @@ def conv_dgrad(dy: Act, wt_pack: torch.Tensor, spec: ConvSpec, in_dims: Triple, 
     assert dy.C == spec.cout and spec.cin % 8 == 0 and spec.cout % 8 == 0
     M = dy.N * Ti * Hi * Wi
     if out is None:
-        out = torch.empty(M, spec.cin, device=dy.t.device, dtype=torch.bfloat16)
+        out = torch.empty(M, spec.cin, device=dy.t.device, dtype=dy.t.dtype)
     for g in dgrad_phases(spec, dy.N, in_dims, (dy.T, dy.H, dy.W), dy.ld, out.stride(0)):
         if accum and g[28] == 0:
             continue

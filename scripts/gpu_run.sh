@@ -20,7 +20,11 @@ B=${BATCH:-160}
 fail() { tail -${2:-30} "$1"; exit 1; }
 
 t_smoke() { timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1 || fail $out/smoke.log; tail -1 $out/smoke.log; }
-t_tests() { timeout -k 10 1500 python -u -m pytest ${TESTS:-tests} -m gpu -x -v --timeout 300 --timeout-method thread > $out/tests.log 2>&1 || fail $out/tests.log 60; tail -2 $out/tests.log; }
+t_tests() {
+  # -s: the long tests print per-step progress, so a slow test is visibly alive (the runner kills silent commands)
+  timeout -k 10 1500 python -u -m pytest ${TESTS:-tests} -m gpu -x -v -s --timeout 300 --timeout-method thread > $out/tests.log 2>&1 || fail $out/tests.log 60
+  grep -E "passed|failed" $out/tests.log | tail -2
+}
 t_bench() { PVA_TUNE_LOG=1 timeout -k 10 400 python bench.py $BENCH_ARGS > $out/bench.json 2> $out/bench.err || fail $out/bench.err; cat $out/bench.json; }
 t_host() { timeout -k 10 400 python bench.py --source host $BENCH_ARGS > $out/bench_host.json 2> $out/bench_host.err || fail $out/bench_host.err; cat $out/bench_host.json; }
 t_fp16() { timeout -k 10 400 python bench.py --precision fp16 $BENCH_ARGS > $out/bench_fp16.json 2> $out/bench_fp16.err || fail $out/bench_fp16.err; cat $out/bench_fp16.json; }

@@ -73,7 +73,7 @@ def test_run_py_fused_gpu(tmp_path):
 
 @pytest.mark.parametrize("mp,kernels", [("fp16", "auto"), ("no", "fused"), ("no", "auto")])
 def test_run_py_precision_policy(tmp_path, mp, kernels):
-    """fp16 = fused kernels + dynamic loss scaling (scaler.pt saved/restored); "no" (the reference default, fp32
+    """fp16 = the fp16 fused kernels + dynamic loss scaling (scaler.pt saved/restored); "no" (the reference default, fp32
     math) runs the PyTorch fp32 path unless the fused kernels are asked for explicitly — and the precision that
     ran is recorded (history / tracker config ``compute_dtype``)."""
     import run
@@ -84,7 +84,7 @@ def test_run_py_precision_policy(tmp_path, mp, kernels):
     h = run.main(num_epochs=1, **kw)
     fused = mp == "fp16" or kernels == "fused"
     assert h["global_step"] == 2 and h["backend"] == ("fused" if fused else "torch")
-    assert h["compute_dtype"] == {"fp16": "bf16+fp16-loss-scaling", "no": "bf16" if fused else "fp32"}[mp]
+    assert h["compute_dtype"] == {"fp16": "fp16", "no": "bf16" if fused else "fp32"}[mp]
     assert (tmp_path / "o" / "epoch_0" / "scaler.pt").exists() == (mp == "fp16")
     if mp == "fp16":
         sd = torch.load(tmp_path / "o" / "epoch_0" / "scaler.pt", weights_only=True)
