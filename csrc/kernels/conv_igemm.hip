@@ -418,6 +418,59 @@ void conv_igemm_kernel(const ConvParams p) {
           for (int j = 0; j < TN; ++j) fb1[j] = *reinterpret_cast<const ev8_t*>(An + fb[1][j]);
         }
       }
+    } else if constexpr (glds_ut && NSTAGE >= 3 && BK == 32) {
+      // BK = 32 ring of NSTAGE buffers with the fragment reads of tile step+1 hoisted across the barrier: they are
+      // issued right after the barrier that publishes tile step+1 and land while the MFMAs of tile step run (two
+      // register sets for even / odd tiles, the loop unrolled by two so every fragment index is compile-time).
+      // Tiles step+2 (.. step+NSTAGE-2) stay in flight across each barrier (counted vmcnt, raw s_barrier);
+      // buffer (step+NSTAGE-1) % NSTAGE held tile step-1, whose reads every wave retired before this barrier.
+      ev8_t fa0[TM], fb0[TN], fa1[TM], fb1[TN];
+      auto rd = [&](const char* T, ev8_t (&ra)[TM], ev8_t (&rb)[TN]) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) ra[i] = *reinterpret_cast<const ev8_t*>(T + fa[0][i]);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) rb[j] = *reinterpret_cast<const ev8_t*>(T + fb[0][j]);
+      };
+      auto mm = [&](const ev8_t (&ra)[TM], const ev8_t (&rb)[TN]) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = PVA_MFMA16(rb[j], ra[i], acc[i][j], 0, 0, 0);
+      };
+      auto publish_next = [&](int step) {   // tile step+1 landed for every wave, tile step's reads retired
+        if (NSTAGE == 4 && step + 2 < nsteps) vm_wait_dyn<A_SLOTS, B_SLOTS>(nb_w);   // leave tile step+2
+        else vm_wait<0>();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (step + NSTAGE - 1 < nsteps) issue_dma((step + NSTAGE - 1) % NSTAGE);
+      };
+      if (NSTAGE == 4 && nsteps > 2) vm_wait_dyn<2 * A_SLOTS, 2 * B_SLOTS>(2 * nb_w);   // tile 0 (1, 2 in flight)
+      else if (nsteps > 1) vm_wait_dyn<A_SLOTS, B_SLOTS>(nb_w);
+      else vm_wait<0>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      rd(smem, fa0, fb0);
+      int step = 0;
+      for (; step + 1 < nsteps; step += 2) {
+        __builtin_amdgcn_sched_barrier(0);
+        publish_next(step);
+        rd(smem + ((step + 1) % NSTAGE) * TILE_BYTES, fa1, fb1);
+        __builtin_amdgcn_sched_barrier(0);
+        mm(fa0, fb0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (step + 2 < nsteps) {
+          publish_next(step + 1);
+          rd(smem + ((step + 2) % NSTAGE) * TILE_BYTES, fa0, fb0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        mm(fa1, fb1);
+      }
+      if (step < nsteps) {   // odd tile count: the last tile is in set 0
+        __builtin_amdgcn_sched_barrier(0);
+        mm(fa0, fb0);
+      }
     } else
     for (int step = 0; step < nsteps; ++step) {
       const int cur = step & 1;
