@@ -499,22 +499,35 @@ void conv_igemm_kernel(const ConvParams p) {
         A = smem + cur * TILE_BYTES;
       } else {
         __syncthreads();
-        if (step + 1 < nsteps) {
-          store_lds(cur ^ 1);
-          if (step + 2 < nsteps) load();
-        }
         A = smem + cur * TILE_BYTES;
       }
       if constexpr (glds_ut) {   // no register staging ring: room for the fragment double buffer
         mma_ktile<BK, TM, TN>(A, fa, fb, acc);
       } else {
+        // this tile's first-k-step fragments are read BEFORE the next tile is staged, so their LDS latency overlaps
+        // the staging work (global loads in, the consumer-side BN-ReLU of the A operand, ds_write) instead of the
+        // MFMAs waiting on it; the later k-steps' reads then overlap the first k-step's MFMAs
+        // (not for the 256x256 tile: its 128 accumulator registers leave no room, it would spill)
+        constexpr bool HOIST = BM * BN <= 256 * 128;
+        ev8_t af[TM], bfr[TN];
+        if constexpr (HOIST) {
+#pragma unroll
+          for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const ev8_t*>(A + fa[0][i]);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const ev8_t*>(A + fb[0][j]);
+        }
+        if (step + 1 < nsteps) {
+          store_lds(cur ^ 1);
+          if (step + 2 < nsteps) load();
+        }
 #pragma unroll
         for (int kk = 0; kk < BK / 32; ++kk) {
-          ev8_t af[TM], bfr[TN];
+          if (kk > 0 || !HOIST) {
 #pragma unroll
-          for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const ev8_t*>(A + fa[kk][i]);
+            for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const ev8_t*>(A + fa[kk][i]);
 #pragma unroll
-          for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const ev8_t*>(A + fb[kk][j]);
+            for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const ev8_t*>(A + fb[kk][j]);
+          }
 #pragma unroll
           for (int i = 0; i < TM; ++i)
 #pragma unroll

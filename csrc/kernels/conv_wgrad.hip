@@ -323,31 +323,39 @@ void conv_wgrad_kernel(const WgradParams p) {
     tb[j][0] = A_BYTES + img_off<BNW>(tr_row, cb);
     tb[j][1] = A_BYTES + img_off<BNW>(tr_row + 4, cb);
   }
+  auto frags = [&](const char* A, int kk, ev8_t (&af)[TM], ev8_t (&bfr)[TN]) {   // rows 32*kk.. of the stage
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      s16x4_t lo = tr_read(A + kk * 32 * BMW * 2 + ta[i][0]);
+      s16x4_t hi = tr_read(A + kk * 32 * BMW * 2 + ta[i][1]);
+      s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      af[i] = __builtin_bit_cast(ev8_t, v);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      s16x4_t lo = tr_read(A + kk * 32 * BNW * 2 + tb[j][0]);
+      s16x4_t hi = tr_read(A + kk * 32 * BNW * 2 + tb[j][1]);
+      s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      bfr[j] = __builtin_bit_cast(ev8_t, v);
+    }
+  };
   for (int step = 0; step < nsteps; ++step) {
     const int cur = step & 1;
     __syncthreads();
+    const char* A = smem + cur * TILE;
+    // the stage's first fragments are read BEFORE the next stage is staged: their LDS latency overlaps the
+    // staging work (the recomputed BN-ReLU of the im2col operand, ds_write), which the MFMAs otherwise waited out
+    // (not for the largest tiles, whose registers are already spoken for: there it spills)
+    constexpr bool HOIST = BMW * BNW <= 256 * 128 && !(CH == 4 && BNW == 256);
+    ev8_t af[TM], bfr[TN];
+    if constexpr (HOIST) frags(A, 0, af, bfr);
     if (step + 1 < nsteps) {
       store_lds(cur ^ 1);
       if (step + 2 < nsteps) load();
     }
-    const char* A = smem + cur * TILE;
 #pragma unroll
-    for (int kk = 0; kk < BP / 32; ++kk) {   // rows 32*kk.. of the stage: same swizzle (row bits 0-3)
-      ev8_t af[TM], bfr[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        s16x4_t lo = tr_read(A + kk * 32 * BMW * 2 + ta[i][0]);
-        s16x4_t hi = tr_read(A + kk * 32 * BMW * 2 + ta[i][1]);
-        s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        af[i] = __builtin_bit_cast(ev8_t, v);
-      }
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        s16x4_t lo = tr_read(A + kk * 32 * BNW * 2 + tb[j][0]);
-        s16x4_t hi = tr_read(A + kk * 32 * BNW * 2 + tb[j][1]);
-        s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        bfr[j] = __builtin_bit_cast(ev8_t, v);
-      }
+    for (int kk = 0; kk < BP / 32; ++kk) {
+      if (kk > 0 || !HOIST) frags(A, kk, af, bfr);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
