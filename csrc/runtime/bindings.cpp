@@ -270,15 +270,17 @@ void wgrad_reduce(const at::Tensor& partial, const at::Tensor& grad, int64_t spl
                       (float)scale, (float)beta, (int)slab, cur_stream());
 }
 
-// Two-level finalize workspace (bn_eltwise.hip): one float64 tensor = [256][2][C] partial doubles followed by
-// ceil(C/64) zero-initialised uint32 counters (kept zero by the kernels).  Absent: the single-level kernels.
+// Two-level finalize workspace (bn_eltwise.hip): one float64 tensor = [256][2][C] partial doubles at the front and
+// ceil(C/64) zero-initialised uint32 counters (kept zero by the kernels) in its LAST doubles, so one workspace sized
+// for the widest layer serves every narrower one (the executor keeps one per stream lane).  Absent: the
+// single-level kernels.
 inline int64_t fin_doubles(int64_t C) { return 256 * 2 * C + (C + 63) / 64; }
 static void fin_buffers(const OptT& fin, int64_t C, double** scr, unsigned** ctr) {
   if (!fin.has_value()) return;
   TORCH_CHECK(fin->scalar_type() == at::kDouble && fin->is_cuda() && fin->numel() >= fin_doubles(C),
               "finalize workspace: float64 [256*2*C + C/64] on the GPU");
   *scr = fin->data_ptr<double>();
-  *ctr = reinterpret_cast<unsigned*>(*scr + 256 * 2 * C);
+  *ctr = reinterpret_cast<unsigned*>(*scr + fin->numel() - (C + 63) / 64);
 }
 
 void bn_finalize(const at::Tensor& part, int64_t tiles, int64_t C, int64_t count, const at::Tensor& gamma,

@@ -115,8 +115,6 @@ class _ConvBN:
         self.scale = torch.ones(C, device=dev)
         self.shift = torch.zeros(C, device=dev)
         self.coef = torch.zeros(4 * C, device=dev)   # BN-backward coefficients (+ mean(dz) for BN folding)
-        # two-level finalize workspace (partial doubles + zeroed counters, kept zero by the kernels); one per unit
-        self.fin = torch.zeros(eng.C.fin_doubles(C), device=dev, dtype=torch.float64) if dev.type == "cuda" else None
         self._geo = {}
         self.wf = None  # bf16 forward pack view [Cout, taps*Cin_pad]
         self.wd = None  # bf16 dgrad pack view [Cin, taps*Cout]
@@ -124,6 +122,11 @@ class _ConvBN:
     @property
     def C(self):
         return self.spec.cout
+
+    @property
+    def fin(self):
+        """Two-level BN finalize workspace of the current stream lane (``FusedNet.fin_ws``)."""
+        return self.eng.fin_ws()
 
     def xf(self, relu=True) -> _Xf:
         return _Xf(self.scale, self.shift, relu)
@@ -1018,6 +1021,8 @@ class FusedNet:
         self._splits: Dict = {}
         self._bnb: Dict = {}
         self._scratch: Dict[Tuple, torch.Tensor] = {}
+        self._fin: Dict[int, torch.Tensor] = {}
+        self._cmax = 8
         self.grad_beta = 0.0
         self.lane = 0          # 0: main stream, 1: fast-pathway stream (per-lane scratch)
         self._side = None
@@ -1070,6 +1075,7 @@ class FusedNet:
                 self.units += p.units
             if fuse is not None:
                 self.units += fuse.units
+        self._cmax = max(u.C for u in self.units)
         # flat parameters in reverse execution order (head first)
         order = list(self.head.named_parameters(prefix="head"))
         for u in reversed(self.units):
@@ -1124,6 +1130,18 @@ class FusedNet:
         if t is None or tuple(t.shape) != tuple(shape) or t.dtype != dtype:
             t = torch.empty(shape, device=self.device, dtype=dtype)
             self._ws[key] = t
+        return t
+
+    def fin_ws(self) -> Optional[torch.Tensor]:
+        """Two-level BN finalize workspace (partial doubles + counters the kernels keep zero), ONE per stream lane
+        sized for the widest BatchNorm: the finalizes of a lane are stream-ordered, so every BN of the lane shares it
+        (one per unit held ~120 MB)."""
+        if self.device.type != "cuda":
+            return None
+        t = self._fin.get(self.lane)
+        if t is None:
+            t = self._fin[self.lane] = torch.zeros(self.C.fin_doubles(self._cmax), device=self.device,
+                                                   dtype=torch.float64)
         return t
 
     def scratch(self, key: str, numel: int, zero: bool = False) -> torch.Tensor:

@@ -7,6 +7,7 @@
 #   bench    bench.py $BENCH_ARGS (tuner log in bench.err)          host   bench.py --source host $BENCH_ARGS
 #   fp16     bench.py --precision fp16 $BENCH_ARGS
 #   ab       bench.py under each setting of $AB (";"-separated env assignments, e.g. AB="PVA_X=0;PVA_X=1")
+#   sweep    bench.py $BENCH_ARGS at every batch size of $SWEEP (memory / throughput sweep; stops at the first OOM)
 #   layers   serialised per-op profile at B=$BATCH (default 160) + roofline table
 #   trace    rocprofv3 kernel trace of 3 steps -> steady-state kernel table
 #   pmc      rocprofv3 PMC passes (one run each) over a bench step at B=$BATCH -> per-kernel summary
@@ -35,6 +36,12 @@ t_ab() {
     i=$((i+1))
     env $arm timeout -k 10 400 python bench.py $BENCH_ARGS > $out/ab$i.json 2> $out/ab$i.err || fail $out/ab$i.err
     echo "$arm: $(cat $out/ab$i.json)"
+  done
+}
+t_sweep() {
+  for b in $SWEEP; do
+    timeout -k 10 500 python bench.py --batch $b --steps ${STEPS:-8} --warmup 2 $BENCH_ARGS > $out/sweep_b$b.json 2> $out/sweep_b$b.err || { tail -3 $out/sweep_b$b.err; break; }
+    echo "B=$b $(cat $out/sweep_b$b.json)"
   done
 }
 t_layers() {
