@@ -235,6 +235,8 @@ def run(a):
         sync = GradSync(eng.flat.grad, st, a.bucket_mb, boundaries=bounds, first_mb=a.first_bucket_mb,
                         grad_dtype=gdt, timing=st.world_size > 1)
         eng.grad_hook = sync.progress if st.world_size > 1 else None   # (1 GPU: no buckets to launch)
+        sync.producers = eng.producer_streams   # RCCL: buckets issued from the sync's own comm stream
+        eng.grad_multi_stream = sync.multi_stream
         drank = st.rank if a.data_rank < 0 else a.data_rank
         gen = torch.Generator().manual_seed(1000 + drank)
         labels_all = torch.randint(0, a.classes, (64, B), generator=gen).to(dev)

@@ -112,6 +112,8 @@ class FusedBackend:
         bounds = sorted(set(self.flat.span(p)[1] for p in self.flat.params))
         self.sync = GradSync(self.flat.grad, state, bucket_mb, boundaries=bounds)
         self.net.grad_hook = self.sync.progress if state.world_size > 1 else None
+        self.sync.producers = self.net.producer_streams   # RCCL: buckets issued from the sync's own comm stream
+        self.net.grad_multi_stream = self.sync.multi_stream
         # fp16: fp16 kernels plus the dynamic loss-scale state machine (GradScaler semantics: fp16 has 5 exponent bits)
         self.scaler = FusedGradScaler() if mixed_precision == "fp16" else None
         self._training = True

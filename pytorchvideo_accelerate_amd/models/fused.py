@@ -1090,8 +1090,10 @@ class FusedNet:
         self.flat = FlatParams(named, self.device)
         self._build_packs()
         self.pack()
-        # backward progress reporting for overlapped gradient all-reduce (parallel/ddp.GradSync)
+        # backward progress reporting for overlapped gradient all-reduce (parallel/ddp.GradSync); grad_multi_stream:
+        # the sync waits on producer_streams() itself (its own comm stream), so reports need no stream joins
         self.grad_hook = None
+        self.grad_multi_stream = False
         self._head_hi = max(self.flat.span(p)[1] for p in self.head.parameters())
         for paths, fuse in self.stages:
             mods = list(paths) + ([fuse] if fuse is not None else [])
@@ -1115,10 +1117,23 @@ class FusedNet:
         p = self.prof or []
         return [(a, e0.elapsed_time(e1)) for (a, e0), (_, e1) in zip(p, p[1:])]
 
+    def producer_streams(self) -> List:
+        """Every stream that writes the flat gradient (the current one, the fast-pathway stream, the weight-gradient
+        streams): ``parallel/ddp.GradSync`` records an event on each before it launches a bucket."""
+        out = [torch.cuda.current_stream(self.device)]
+        if self._side is not None:
+            out.append(self._side)
+        out += [st for st in self._wst if st is not None]
+        return out
+
     def _progress(self, hi: int, force: bool = False):
-        """grad[:hi] is final on the current (main) stream.  During two-stream backward the per-block reports
-        are dropped: the stage's pathways finish in any order, so progress is reported once per stage after
-        the streams are joined (``force``)."""
+        """grad[:hi] is final once the work issued so far completes.  With a multi-stream gradient sync (its comm
+        stream waits on every producer stream) every block reports as soon as it is issued.  Otherwise, during
+        two-stream backward, the per-block reports are dropped (the stage's pathways finish in any order) and
+        progress is reported once per stage after the streams are joined (``force``)."""
+        if self.grad_hook is not None and self.grad_multi_stream:
+            self.grad_hook(hi)
+            return
         if self.grad_hook is not None and (force or not self._ms_bwd):
             if force:
                 self._join_wgrads()   # the bucket's weight gradients may still be in flight on the wgrad streams

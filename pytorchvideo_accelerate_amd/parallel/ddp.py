@@ -20,6 +20,13 @@ reference ``run.py:196-198,257``), all math-identical:
   DDP's ``_DEFAULT_FIRST_BUCKET_BYTES`` the first bucket is small (``first_mb``) so communication starts
   as soon as the head and the last residual unit are done.
 
+Framework-owned communication stream: the bucket's gradients are produced on several HIP streams (the
+slow-pathway stream, the fast-pathway stream and their weight-gradient streams).  ``producers`` (set by the executor)
+lists them; at each bucket launch an event is recorded on every producer and the comm stream waits on all of them
+before the collective is issued from it, so no compute stream ever waits for another one (or for the network) before
+``finish()`` — buckets can be reported per residual block even while both pathways and their weight-gradient streams
+are in flight.  Without ``producers`` (or for CPU gradients) the collective follows the current stream.
+
 Options beyond DDP's defaults: ``grad_dtype=torch.bfloat16`` all-reduces a bf16 copy of each bucket
 (half the xGMI bytes; the analogue of DDP's ``bf16_compress_hook``) and ``timing=True`` records, per
 step, every bucket's ready→reduced latency and the *exposed* communication time (how long the compute
@@ -27,7 +34,7 @@ stream waited in ``finish()``), exported by :meth:`stats`.
 """
 from __future__ import annotations
 
-from typing import Dict, List, Optional, Tuple
+from typing import Callable, Dict, List, Optional, Tuple
 
 import torch
 
@@ -66,6 +73,10 @@ class GradSync:
         # inside backward and serialise every bucket, so the gloo rehearsal runs untimed
         self.timing = timing and grad.is_cuda and state.backend == "nccl"
         self._comm_stream = torch.cuda.Stream(grad.device) if self.timing else None
+        # the framework's own communication stream and the executor's gradient-producing streams (GPU gradients:
+        # RCCL, and the gloo rehearsal of the same schedule on one GPU, whose CUDA work follows the issuing stream)
+        self.producers: Optional[Callable[[], List]] = None
+        self._cstream = torch.cuda.Stream(grad.device, priority=-1) if (self.enabled and grad.is_cuda) else None
         self._ev: List = []          # per step: (list of (ready, done) per bucket, (exp0, exp1))
         self._next = 0
         self._works = []
@@ -83,31 +94,47 @@ class GradSync:
         self._bev = []
         self.active = self.enabled and sync
 
-    def _event(self):
+    def _event(self, stream=None):
         e = torch.cuda.Event(enable_timing=True)
-        e.record()
+        e.record(stream)
         return e
+
+    @property
+    def multi_stream(self) -> bool:
+        """Whether bucket launches wait on every producing stream themselves (executor: report per block, no joins)."""
+        return self._cstream is not None and self.producers is not None
 
     def _launch(self, b: int):
         import torch.distributed as dist
         lo, hi = self.buckets[b]
         t = self.grad[lo:hi]
-        ready = self._event() if self.timing else None
-        if self.grad_dtype is not None:
-            if self._lowp is None:
-                self._lowp = torch.empty(self.grad.numel(), dtype=self.grad_dtype, device=self.grad.device)
-            low = self._lowp[lo:hi]
-            low.copy_(t)
-            comm = low
-        else:
-            comm = t
-        with trace_range(f"allreduce/bucket{b}"):
-            if self.state.backend == "nccl":
-                w = dist.all_reduce(comm, op=dist.ReduceOp.AVG, async_op=True)
-                post = None
+        cs = self._cstream if self.multi_stream else None
+        if cs is not None:   # the comm stream joins every producer at this point (events, no compute-stream wait)
+            for st in self.producers():
+                cs.wait_event(self._event(st))
+        ctx = torch.cuda.stream(cs) if cs is not None else None
+        if ctx is not None:
+            ctx.__enter__()
+        try:
+            ready = self._event() if self.timing else None
+            if self.grad_dtype is not None:
+                if self._lowp is None:
+                    self._lowp = torch.empty(self.grad.numel(), dtype=self.grad_dtype, device=self.grad.device)
+                low = self._lowp[lo:hi]
+                low.copy_(t)
+                comm = low
             else:
-                w = dist.all_reduce(comm, op=dist.ReduceOp.SUM, async_op=True)
-                post = "div"
+                comm = t
+            with trace_range(f"allreduce/bucket{b}"):
+                if self.state.backend == "nccl":
+                    w = dist.all_reduce(comm, op=dist.ReduceOp.AVG, async_op=True)
+                    post = None
+                else:
+                    w = dist.all_reduce(comm, op=dist.ReduceOp.SUM, async_op=True)
+                    post = "div"
+        finally:
+            if ctx is not None:
+                ctx.__exit__(None, None, None)
         self._works.append((w, t, comm, post))
         if self.timing:
             # the side stream waits for this collective only: its event marks the bucket's completion
@@ -133,7 +160,7 @@ class GradSync:
         e0 = self._event() if self.timing else None
         for b, (w, t, comm, post) in enumerate(self._works):
             trace_mark(f"allreduce/wait{b}")
-            w.wait()
+            w.wait()   # the CURRENT (compute) stream waits for the collective
             if post == "div":
                 comm.div_(self.state.world_size)
             if comm is not t:
