@@ -223,11 +223,16 @@ def run(a):
         model = R.create_slowfast(a.depth, a.classes)
         from pytorchvideo_accelerate_amd.ops.optim import FusedGradScaler
         assert not (a.graph and a.precision == "fp16"), "--graph replays no loss-scale check"
-        eng = FusedNet(model, dev, deterministic=a.deterministic,
+        eng = FusedNet(model, dev, deterministic=a.deterministic, load_tuning=st.world_size == 1,
                        compute_dtype=torch.float16 if a.precision == "fp16" else torch.bfloat16)
         scaler = FusedGradScaler() if a.precision == "fp16" else None
         if st.world_size > 1:
             eng.tuner.agree = st.agree_times
+            ts = eng.tune_store   # rank 0's persistent autotuner table, broadcast once (as engine/backends.py)
+            doc = st.broadcast_object(ts.read() if (ts is not None and st.rank == 0) else None)
+            if ts is not None:
+                ts.restore(doc)
+                ts.writer = st.rank == 0
         st.broadcast_tensors([eng.flat.data] + [b for b in model.buffers()])
         eng.pack()
         opt = FusedSGD(eng.flat, lr=a.lr, momentum=0.9, weight_decay=1e-4, after_step=eng.pack)

@@ -83,7 +83,10 @@ def test_fused_two_rank_shipped_default_config(tmp_path):
     """The shipped defaults exactly as bench.py / run.py run them (autotuner on and agreed across ranks, fold slabs
     on, two streams): the all-reduced gradient equals the mean of the single-rank gradients within the fp32-atomic
     noise of the leaf weight gradients (the production DP path checked on gradients, not only params)."""
-    err, spread = _dp_vs_singles(tmp_path, [], "dflt")
+    # The single-rank oracle runs restore the autotuner table the two-rank run agreed on and wrote (the persistent
+    # cache, as a re-run of the job would): kernel choices change fp32 summation orders, and this random-init network
+    # amplifies such differences chaotically (scripts/diag_chaos.py), so the comparison needs the same kernels.
+    err, spread = _dp_vs_singles(tmp_path, [], "dflt", PVA_TUNE_CACHE=str(tmp_path / "tune"))
     assert spread > 0.1, spread
     assert err < 2e-3, (err, spread)
 

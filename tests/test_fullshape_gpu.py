@@ -90,7 +90,9 @@ def test_fixed_batch_memorisation_tracks_fp32_oracle():
     and the fp32 PyTorch oracle side by side from the same weights: both memorise the batch (the loss falls well
     below its start) and the fused plateau (mean of the last ten losses) lies within a stated band of the oracle's,
     while the first steps track it closely.  (the plateau is judged against the oracle's own
-    trajectory, not a free threshold.)"""
+    trajectory, not a free threshold.)  Measured (profiles/r4_tests): the recipe overshoots at this batch (both rise
+    to ~90 by step 12, the fused run within 1-5 % of the oracle step for step until then), then both settle — fp32
+    oracle at 1.9-2.7, fused at 1.7-1.9 over the last ten steps."""
     torch.manual_seed(0)
     model = R.create_slowfast(50, 400, dropout_rate=0.0)
     oracle = copy.deepcopy(model).to(DEV).train()
