@@ -34,7 +34,7 @@ t_ab() {
   IFS=';' read -ra arms <<< "$AB"
   for arm in "${arms[@]}"; do
     i=$((i+1))
-    env $arm timeout -k 10 400 python bench.py $BENCH_ARGS > $out/ab$i.json 2> $out/ab$i.err || fail $out/ab$i.err
+    env PVA_TUNE_LOG=1 $arm timeout -k 10 400 python bench.py $BENCH_ARGS > $out/ab$i.json 2> $out/ab$i.err || fail $out/ab$i.err
     echo "$arm: $(cat $out/ab$i.json)"
   done
 }
