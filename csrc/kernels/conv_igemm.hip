@@ -201,8 +201,11 @@ void conv_igemm_kernel(const ConvParams p) {
     const int GHW = p.Gh * p.Gw, GTHW = p.Gt * GHW;
     // most negative tap offset (dgrad walks taps backwards): the no-check form adds taps as a >= 0 soffset
     const int tmin = p.dir < 0 ? -(((p.nt - 1) * p.Gh + (p.nh - 1)) * p.Gw + (p.nw - 1)) * p.ldx : 0;
-    int a_vo[A_SLOTS], sa[A_SLOTS];
+    int a_vo[A_SLOTS], sa[A_SLOTS], a2_vo[A_SLOTS];
     unsigned tmask[A_SLOTS];
+    const bool has2 = p.x2 != nullptr;   // K-concatenated second segment (ConvParams::x2)
+    const __amdgpu_buffer_rsrc_t x2r =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(has2 ? p.x2 : p.x), (short)0, (int)(has2 ? p.x2bytes : p.xbytes), 0x00020000);
 #pragma unroll
     for (int s = 0; s < A_SLOTS; ++s) {
       const int idx = tid + s * NT;
@@ -234,6 +237,17 @@ void conv_igemm_kernel(const ConvParams p) {
       // no-check: rows past M read a real (ignored) address — never rely on range checks there
       a_vo[s] = check ? off * 2 : (rv ? (off + tmin) * 2 : 0);
       sa[s] = lds_off<BK>(row, col);
+      // second K segment (x2): this row's lattice point mapped into x2, or out of range (zeros)
+      a2_vo[s] = (int)OOB;
+      if (has2 && rv) {
+        const int b = m / RTHW;
+        int r = m - b * RTHW;
+        const int qt = r / RHW; r -= qt * RHW;
+        const int qh = r / p.Rw; const int qw = r - qh * p.Rw;
+        if (qh % p.s2h == 0 && qw % p.s2w == 0)
+          a2_vo[s] = (((b * p.G2t + qt) * p.G2h + qh / p.s2h) * p.G2w + qw / p.s2w) * p.ldx2 * 2 +
+                     (glds_ut ? col ^ lds_swz<BK>(row) : col) * 16;
+      }
     }
     int b_vo[B_SLOTS], sb[B_SLOTS];
 #pragma unroll
@@ -245,11 +259,22 @@ void conv_igemm_kernel(const ConvParams p) {
       b_vo[s] = (idx < B_CHUNKS && n < p.Ngemm) ? (n * p.Kfull + bcol * 8) * 2 : 0;  // columns >= N: ignored
       sb[s] = lds_off<BK>(row, col);
     }
-    // uniform k cursor
+    // uniform k cursor (in2: inside the second segment)
     int kt_ = 0, kh_ = 0, kw_ = 0, t_ = 0, kb = 0, tapA = 0, tapW = 0;
+    bool in2 = false;
     auto retap = [&]() {
       tapA = p.dir * ((kt_ * p.Gh + kh_) * p.Gw + kw_) * p.ldx;
       tapW = (((p.bt0 + kt_ * p.bts) * p.kh + (p.bh0 + kh_ * p.bhs)) * p.kw + (p.bw0 + kw_ * p.bws)) * p.Cg;
+    };
+    auto kadv = [&]() {
+      kb += BK;
+      if (!in2 && kb == p.Cg) {
+        kb = 0;
+        ++t_;
+        if (++kw_ == p.nw) { kw_ = 0; if (++kh_ == p.nh) { kh_ = 0; ++kt_; } }
+        retap();
+        in2 = has2 && kt_ == p.nt;
+      }
     };
     retap();
     uint4 ra[A_SLOTS], rb[B_SLOTS];
@@ -259,27 +284,28 @@ void conv_igemm_kernel(const ConvParams p) {
       const int ta = tapA + kb;
       ra_c = kb;
       ra_valid = 0;
+      if (in2) {   // second segment: x2 rows (K-concatenated dgrad), weights from column k2off
 #pragma unroll
-      for (int s = 0; s < A_SLOTS; ++s) {
-        if (check) {
-          const bool v = (tmask[s] >> t_) & 1u;
-          ra[s] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, v ? a_vo[s] + ta * 2 : (int)OOB, 0, 0));
-          ra_valid |= (unsigned)v << s;
-        } else {
-          ra[s] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, a_vo[s], (ta - tmin) * 2, 0));
+        for (int s = 0; s < A_SLOTS; ++s)
+          ra[s] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+              x2r, a2_vo[s] == (int)OOB ? (int)OOB : a2_vo[s] + kb * 2, 0, 0));
+      } else {
+#pragma unroll
+        for (int s = 0; s < A_SLOTS; ++s) {
+          if (check) {
+            const bool v = (tmask[s] >> t_) & 1u;
+            ra[s] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, v ? a_vo[s] + ta * 2 : (int)OOB, 0, 0));
+            ra_valid |= (unsigned)v << s;
+          } else {
+            ra[s] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, a_vo[s], (ta - tmin) * 2, 0));
+          }
         }
       }
-      const int wso = (tapW + kb) * 2;
+      const int wso = ((in2 ? p.k2off : tapW) + kb) * 2;
 #pragma unroll
       for (int s = 0; s < B_SLOTS; ++s)
         rb[s] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wr, b_vo[s], wso, 0));
-      kb += BK;
-      if (kb == p.Cg) {
-        kb = 0;
-        ++t_;
-        if (++kw_ == p.nw) { kw_ = 0; if (++kh_ == p.nh) { kh_ = 0; ++kt_; } }
-        retap();
-      }
+      kadv();
     };
     auto store_lds = [&](int buf) {
       char* A = smem + buf * TILE_BYTES;
@@ -312,7 +338,7 @@ void conv_igemm_kernel(const ConvParams p) {
         *reinterpret_cast<uint4*>(B + sb[s]) = rb[s];
       }
     };
-    const int nsteps = (p.nt * p.nh * p.nw * p.Cg) / BK;
+    const int nsteps = (p.nt * p.nh * p.nw * p.Cg + (has2 ? p.Cg2 : 0)) / BK;
     __syncthreads();  // affine table ready
     // LDS-DMA staging (UT bit 4, no input affine): buffer_load ... lds writes each wave's 64 x 16 B straight
     // into LDS (lane-linear: the XOR swizzle moves to the source column), skipping the VGPR round trip and
@@ -325,27 +351,23 @@ void conv_igemm_kernel(const ConvParams p) {
 #pragma unroll
       for (int s = 0; s < A_SLOTS; ++s) {
         const int rs = __builtin_amdgcn_readfirstlane((s * NT + 64 * wid) / CPR);
-        if constexpr (check) {
+        if (in2) {
+          dma16(x2r, A + rs * BK * 2, a2_vo[s] == (int)OOB ? (int)OOB : a2_vo[s] + kb * 2, 0);
+        } else if constexpr (check) {
           const bool v = (tmask[s] >> t_) & 1u;
           dma16(xr, A + rs * BK * 2, v ? a_vo[s] + ta * 2 : (int)OOB, 0);
         } else {
           dma16(xr, A + rs * BK * 2, a_vo[s], (ta - tmin) * 2);
         }
       }
-      const int wso = (tapW + kb) * 2;
+      const int wso = ((in2 ? p.k2off : tapW) + kb) * 2;
 #pragma unroll
       for (int s = 0; s < B_SLOTS; ++s) {
         if (s * NT + 64 * wid >= B_CHUNKS) break;   // wave-uniform (B_CHUNKS is a multiple of 64)
         const int rs = __builtin_amdgcn_readfirstlane((s * NT + 64 * wid) / CPR);
         dma16(wr, B + rs * BK * 2, b_vo[s], wso);
       }
-      kb += BK;
-      if (kb == p.Cg) {
-        kb = 0;
-        ++t_;
-        if (++kw_ == p.nw) { kw_ = 0; if (++kh_ == p.nh) { kh_ = 0; ++kt_; } }
-        retap();
-      }
+      kadv();
     };
     // DMA instructions of one tile issued by this wave (A slots always; B slots only for waves whose rows exist)
     int nb_w = 0;
@@ -955,7 +977,7 @@ void conv_igemm_kernel(const ConvParams p) {
 static int g_ut_mode = 1;
 
 inline bool conv_ut_legal(const ConvParams& p, int ch, int bk) {
-  return ch == 8 && p.Cg % bk == 0 && p.nt * p.nh * p.nw <= 32;
+  return ch == 8 && p.Cg % bk == 0 && p.nt * p.nh * p.nw <= 32 && (p.x2 == nullptr || p.Cg2 % bk == 0);
 }
 
 template <int BM, int BN, int WM, int WN, int CH, int BK>

@@ -14,8 +14,11 @@ DEV = torch.device("cuda")
 
 
 def _ulp(ref: torch.Tensor, mant_bits: int = 7) -> torch.Tensor:
-    """One unit in the last place of a ``mant_bits``-bit significand (bf16: 7) at the magnitude of ``ref``."""
-    return torch.pow(2.0, torch.floor(torch.log2(ref.abs().clamp_min(2.0 ** -20))) - mant_bits)
+    """One unit in the last place of a ``mant_bits``-bit significand (bf16: 7) at the magnitude of ``ref`` — but never
+    below 1e-6: next to zero the fp32 cancellation in x/255 - mean (|x/255| ~ 0.5) already carries ~1e-7 absolute
+    error in the reference AND in the kernel (which normalises after interpolating), so a tiny output's last place is
+    noise in both."""
+    return torch.pow(2.0, torch.floor(torch.log2(ref.abs().clamp_min(2.0 ** -30))) - mant_bits).clamp_min(1e-6)
 
 
 def test_preprocess_kernel_matches_reference_transform():
