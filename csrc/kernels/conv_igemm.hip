@@ -133,10 +133,10 @@ void conv_igemm_kernel(const ConvParams p) {
   // stats slots, one per wave row (EPI 0: [BM/WM][2][BN]) or per wave (EPI 1: [NW][3][BN]); summed in a fixed
   // order, so the BN statistics are bitwise deterministic (no float atomics)
   constexpr int NWAVES = (BM / WM) * NWN;
-  constexpr int RED_FLOATS = EPI == 1 ? NWAVES * 3 * BN : (BM / WM) * 2 * BN;
+  constexpr int RED_FLOATS = EPI >= 1 ? NWAVES * 3 * BN : (BM / WM) * 2 * BN;
   float* red = reinterpret_cast<float*>(smem + MAIN_BYTES);
   float* bnp = red + RED_FLOATS;  // EPI: [6][BN] mean0 rstd0 mean1 rstd1 mask-scale mask-shift
-  float* aff = bnp + (EPI == 1 ? 6 * BN : 0);                            // [2][Cg] affine
+  float* aff = bnp + (EPI >= 1 ? 6 * BN : 0);                            // [2][Cg] affine
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / NWN, wn = wid % NWN;
@@ -147,7 +147,7 @@ void conv_igemm_kernel(const ConvParams p) {
   const int m0 = tile_m * BM, n0 = tile_n * BN;
 
   const bool do_stats = EPI == 0 && p.stats != nullptr;
-  const bool do_bstats = EPI == 1 && p.epart != nullptr;
+  const bool do_bstats = EPI >= 1 && p.epart != nullptr;
   const int affine = p.affine;
   if (do_bstats) {  // this tile's BN constants, read once here so the epilogue never waits on them
     for (int i = tid; i < BN; i += NT) {
@@ -706,7 +706,7 @@ void conv_igemm_kernel(const ConvParams p) {
       }
     }
   }
-  if constexpr (EPI == 1) __syncthreads();   // the fp32 staging below overwrites the k tiles
+  if constexpr (EPI >= 1) __syncthreads();   // the fp32 staging below overwrites the k tiles
 
   // ---- epilogue: D[n][m] fragment: lane holds channels n..n+3 of position m ----
   // EPI 0: direct fragment stores, cs = sum y, cq = sum y^2 (forward BN statistics)
@@ -790,7 +790,10 @@ void conv_igemm_kernel(const ConvParams p) {
       }
     }
   }
-  if constexpr (EPI == 1) {
+  if constexpr (EPI >= 1) {
+    // EPI 2 = the lean form (residual and / or ReLU bits and sum v only: no accumulate, no BN inputs, no bias —
+    // the identity unit's conv_a dgrad after a folded conv_c): fewer registers per row, so a whole slice's rows
+    // are in flight at once (one memory round trip per slice instead of two)
     // row-contiguous pass: each thread owns 8 consecutive channels (16-B global accesses) of every
     // RPP-th tile row: + old y, + residual, ReLU bits, store, backward-BN partial sums.  The fp32 tile is
     // staged through LDS (the k tiles are dead: the main loop ended with a barrier) in slices of SR rows.
@@ -805,11 +808,11 @@ void conv_igemm_kernel(const ConvParams p) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) { sv[e] = 0.f; s0[e] = 0.f; s1[e] = 0.f; }
     const bool nok = n < p.Ngemm;
-    const bool dual = p.ey1 != nullptr;
-    const bool masky = do_bstats && p.emsc != nullptr;
+    const bool dual = EPI == 1 && p.ey1 != nullptr;
+    const bool masky = EPI == 1 && do_bstats && p.emsc != nullptr;
     // rows whose loads are issued together (latency hiding); 2 for the 256x256 tile, whose 128 accumulator
     // registers per lane leave no room for more
-    constexpr int RB = BM * BN > 128 * 128 ? 2 : 4;
+    constexpr int RB = (EPI == 2 || BM * BN <= 128 * 128) ? 4 : 2;
 #pragma unroll   // compile-time slices: accumulators of staged slices are dead afterwards
     for (int r_lo = 0; r_lo < BM; r_lo += SR) {
     if (r_lo > 0) __syncthreads();   // the previous slice has been read
@@ -846,10 +849,10 @@ void conv_igemm_kernel(const ConvParams p) {
         lo[u] = lr[u] = l0[u] = l1[u] = uint4{0, 0, 0, 0};
         bits[u] = 0xffu;
         if (ok[u]) {
-          if (p.accum) lo[u] = *reinterpret_cast<const uint4*>(p.y + ps * p.ldy + n);
+          if (EPI == 1 && p.accum) lo[u] = *reinterpret_cast<const uint4*>(p.y + ps * p.ldy + n);
           if (p.eres) lr[u] = *reinterpret_cast<const uint4*>(p.eres + ps * p.ldr + n);
           if (p.emask) bits[u] = p.emask[ps * (p.Ngemm >> 3) + (n >> 3)];
-          if (do_bstats) {
+          if (EPI == 1 && do_bstats) {
             if (p.ey0) l0[u] = *reinterpret_cast<const uint4*>(p.ey0 + ps * p.Ngemm + n);
             if (dual) l1[u] = *reinterpret_cast<const uint4*>(p.ey1 + ps * p.Ngemm + n);
           }
@@ -872,7 +875,7 @@ void conv_igemm_kernel(const ConvParams p) {
           for (int e = 0; e < 8; ++e)
             if (!(a[e] * bnp[4 * BN + cg * 8 + e] + bnp[5 * BN + cg * 8 + e] > 0.f)) bits[u] &= ~(1u << e);
         }
-        if (p.ebias) {
+        if (EPI == 1 && p.ebias) {
           const f32x4_t b0 = *reinterpret_cast<const f32x4_t*>(p.ebias + n);
           const f32x4_t b1 = *reinterpret_cast<const f32x4_t*>(p.ebias + n + 4);
 #pragma unroll
@@ -1002,6 +1005,18 @@ void launch_cfg(const ConvParams& p, int ut_force, hipStream_t stream, bool dma 
   constexpr bool BIG = BM * BN > 128 * 128;
   if constexpr (BIG) {
     if (epi) {   // dgrad epilogue: never an input affine; the tuner only proposes the uniform-tap loader here
+      // lean epilogue (EPI 2): residual / ReLU bits / sum v only
+      const bool lean = !p.accum && !p.ey0 && !p.ey1 && !p.emsc && !p.ebias;
+      if (lean && ut) {
+        if (dma) {
+          if (p.check) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 2, 19>), grid, block, lds, stream, p);
+          else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 2, 17>), grid, block, lds, stream, p);
+        } else {
+          if (p.check) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 2, 3>), grid, block, lds, stream, p);
+          else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 2, 1>), grid, block, lds, stream, p);
+        }
+        return;
+      }
       if (ut && dma) {
         if (p.check) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 1, 19>), grid, block, lds, stream, p);
         else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 1, 17>), grid, block, lds, stream, p);
