@@ -228,13 +228,15 @@ class _ConvBN:
             C.wgrad_box_reduce(part, tmp, grad, nslab, s.cout, s.taps, s.cin_pad, s.cin, 1.0, beta_)
             return nslab
 
-        tkey = ("w", dy.M, dy.ld, x.ld, x.T, x.H, x.W, s.cout, K, s.chunk, aff, gram) + tuple(s.k) + tuple(s.stride)
+        tkey = ("w", dy.M, dy.ld, x.ld, x.T, x.H, x.W, s.cout, K, s.chunk, aff, gram, slab) + tuple(s.k) + tuple(
+            s.stride)
         cfg = eng.wtune.get(tkey)
         if cfg is None:
             cfg = -1
-            if eng.tuner.enabled and not slab:
+            if eng.tuner.enabled and not eng.deterministic:
                 # first use: time tile variant x split-K target on a scratch accumulator (atomic adds; the
-                # scratch content is irrelevant), keep the fastest
+                # scratch content is irrelevant), keep the fastest.  Slab launches (BN-folding Gram / G products
+                # under fold_slabs) are timed with their fixed-order reduction, whose cost grows with the split count
                 scratch = eng.scratch("wgrad_tune", s.cout * K)
                 cs_scr = eng.scratch("wgrad_tune_cs", 4096 * s.cout) if gram else None
                 cands, times = [], []
@@ -260,12 +262,12 @@ class _ConvBN:
                             continue
                         for tbi, bp in ((t, b) for t in range(3) for b in (0, 32)):
                             cands.append(16 | 2048 | (v & 3) | (64 if v >= 4 else 0) | (tbi << 2) | bp)
-                if C.wgrad_narrow_legal(s.cout, s.cin_pad, K) and s.chunk == 8:
+                if C.wgrad_narrow_legal(s.cout, s.cin_pad, K) and s.chunk == 8 and not slab:
                     cands += [c for c in (16 | 128 | (tbi << 2) for tbi in range(4))
                               if not (gram and geometry(c)[0] > 4096)]   # colsum slab holds 4096 splits
                 if not gram and box_wgrad_plan(s, dy.M, (dy.T, dy.H, dy.W), dy.ld, x.ld) is not None:
                     cands.append(16 | 1024)
-                if not gram:   # halo-staged kernel, two box sizes
+                if not gram and not slab:   # halo-staged kernel, two box sizes
                     from ..ops.conv import halo_wgrad_plan
                     for o in (0, 1):
                         plan = halo_wgrad_plan(s, dy.M, (dy.T, dy.H, dy.W), o)
@@ -281,6 +283,10 @@ class _ConvBN:
                 def trial(c):
                     if c & 1024:
                         box_run(c, gscr, 0.0)
+                    elif slab:
+                        part = eng.scratch("wgrad_tune_slab", geometry(c)[0] * s.cout * K)
+                        sp = launch(c, part, cs_scr)
+                        C.wgrad_reduce(part, gscr, sp, s.cout, s.taps, s.cin_pad, s.cin, 1.0, 0.0, 1)
                     else:
                         launch(c, scratch, cs_scr)
                 for c in cands:
