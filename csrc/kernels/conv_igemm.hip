@@ -201,11 +201,8 @@ void conv_igemm_kernel(const ConvParams p) {
     const int GHW = p.Gh * p.Gw, GTHW = p.Gt * GHW;
     // most negative tap offset (dgrad walks taps backwards): the no-check form adds taps as a >= 0 soffset
     const int tmin = p.dir < 0 ? -(((p.nt - 1) * p.Gh + (p.nh - 1)) * p.Gw + (p.nw - 1)) * p.ldx : 0;
-    int a_vo[A_SLOTS], sa[A_SLOTS], a2_vo[A_SLOTS];
+    int a_vo[A_SLOTS], sa[A_SLOTS];
     unsigned tmask[A_SLOTS];
-    const bool has2 = p.x2 != nullptr;   // K-concatenated second segment (ConvParams::x2)
-    const __amdgpu_buffer_rsrc_t x2r =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(has2 ? p.x2 : p.x), (short)0, (int)(has2 ? p.x2bytes : p.xbytes), 0x00020000);
 #pragma unroll
     for (int s = 0; s < A_SLOTS; ++s) {
       const int idx = tid + s * NT;
@@ -237,17 +234,6 @@ void conv_igemm_kernel(const ConvParams p) {
       // no-check: rows past M read a real (ignored) address — never rely on range checks there
       a_vo[s] = check ? off * 2 : (rv ? (off + tmin) * 2 : 0);
       sa[s] = lds_off<BK>(row, col);
-      // second K segment (x2): this row's lattice point mapped into x2, or out of range (zeros)
-      a2_vo[s] = (int)OOB;
-      if (has2 && rv) {
-        const int b = m / RTHW;
-        int r = m - b * RTHW;
-        const int qt = r / RHW; r -= qt * RHW;
-        const int qh = r / p.Rw; const int qw = r - qh * p.Rw;
-        if (qh % p.s2h == 0 && qw % p.s2w == 0)
-          a2_vo[s] = (((b * p.G2t + qt) * p.G2h + qh / p.s2h) * p.G2w + qw / p.s2w) * p.ldx2 * 2 +
-                     (glds_ut ? col ^ lds_swz<BK>(row) : col) * 16;
-      }
     }
     int b_vo[B_SLOTS], sb[B_SLOTS];
 #pragma unroll
@@ -259,22 +245,11 @@ void conv_igemm_kernel(const ConvParams p) {
       b_vo[s] = (idx < B_CHUNKS && n < p.Ngemm) ? (n * p.Kfull + bcol * 8) * 2 : 0;  // columns >= N: ignored
       sb[s] = lds_off<BK>(row, col);
     }
-    // uniform k cursor (in2: inside the second segment)
+    // uniform k cursor
     int kt_ = 0, kh_ = 0, kw_ = 0, t_ = 0, kb = 0, tapA = 0, tapW = 0;
-    bool in2 = false;
     auto retap = [&]() {
       tapA = p.dir * ((kt_ * p.Gh + kh_) * p.Gw + kw_) * p.ldx;
       tapW = (((p.bt0 + kt_ * p.bts) * p.kh + (p.bh0 + kh_ * p.bhs)) * p.kw + (p.bw0 + kw_ * p.bws)) * p.Cg;
-    };
-    auto kadv = [&]() {
-      kb += BK;
-      if (!in2 && kb == p.Cg) {
-        kb = 0;
-        ++t_;
-        if (++kw_ == p.nw) { kw_ = 0; if (++kh_ == p.nh) { kh_ = 0; ++kt_; } }
-        retap();
-        in2 = has2 && kt_ == p.nt;
-      }
     };
     retap();
     uint4 ra[A_SLOTS], rb[B_SLOTS];
@@ -284,28 +259,27 @@ void conv_igemm_kernel(const ConvParams p) {
       const int ta = tapA + kb;
       ra_c = kb;
       ra_valid = 0;
-      if (in2) {   // second segment: x2 rows (K-concatenated dgrad), weights from column k2off
 #pragma unroll
-        for (int s = 0; s < A_SLOTS; ++s)
-          ra[s] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
-              x2r, a2_vo[s] == (int)OOB ? (int)OOB : a2_vo[s] + kb * 2, 0, 0));
-      } else {
-#pragma unroll
-        for (int s = 0; s < A_SLOTS; ++s) {
-          if (check) {
-            const bool v = (tmask[s] >> t_) & 1u;
-            ra[s] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, v ? a_vo[s] + ta * 2 : (int)OOB, 0, 0));
-            ra_valid |= (unsigned)v << s;
-          } else {
-            ra[s] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, a_vo[s], (ta - tmin) * 2, 0));
-          }
+      for (int s = 0; s < A_SLOTS; ++s) {
+        if (check) {
+          const bool v = (tmask[s] >> t_) & 1u;
+          ra[s] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, v ? a_vo[s] + ta * 2 : (int)OOB, 0, 0));
+          ra_valid |= (unsigned)v << s;
+        } else {
+          ra[s] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, a_vo[s], (ta - tmin) * 2, 0));
         }
       }
-      const int wso = ((in2 ? p.k2off : tapW) + kb) * 2;
+      const int wso = (tapW + kb) * 2;
 #pragma unroll
       for (int s = 0; s < B_SLOTS; ++s)
         rb[s] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wr, b_vo[s], wso, 0));
-      kadv();
+      kb += BK;
+      if (kb == p.Cg) {
+        kb = 0;
+        ++t_;
+        if (++kw_ == p.nw) { kw_ = 0; if (++kh_ == p.nh) { kh_ = 0; ++kt_; } }
+        retap();
+      }
     };
     auto store_lds = [&](int buf) {
       char* A = smem + buf * TILE_BYTES;
@@ -338,7 +312,7 @@ void conv_igemm_kernel(const ConvParams p) {
         *reinterpret_cast<uint4*>(B + sb[s]) = rb[s];
       }
     };
-    const int nsteps = (p.nt * p.nh * p.nw * p.Cg + (has2 ? p.Cg2 : 0)) / BK;
+    const int nsteps = (p.nt * p.nh * p.nw * p.Cg) / BK;
     __syncthreads();  // affine table ready
     // LDS-DMA staging (UT bit 4, no input affine): buffer_load ... lds writes each wave's 64 x 16 B straight
     // into LDS (lane-linear: the XOR swizzle moves to the source column), skipping the VGPR round trip and
@@ -351,23 +325,27 @@ void conv_igemm_kernel(const ConvParams p) {
 #pragma unroll
       for (int s = 0; s < A_SLOTS; ++s) {
         const int rs = __builtin_amdgcn_readfirstlane((s * NT + 64 * wid) / CPR);
-        if (in2) {
-          dma16(x2r, A + rs * BK * 2, a2_vo[s] == (int)OOB ? (int)OOB : a2_vo[s] + kb * 2, 0);
-        } else if constexpr (check) {
+        if constexpr (check) {
           const bool v = (tmask[s] >> t_) & 1u;
           dma16(xr, A + rs * BK * 2, v ? a_vo[s] + ta * 2 : (int)OOB, 0);
         } else {
           dma16(xr, A + rs * BK * 2, a_vo[s], (ta - tmin) * 2);
         }
       }
-      const int wso = ((in2 ? p.k2off : tapW) + kb) * 2;
+      const int wso = (tapW + kb) * 2;
 #pragma unroll
       for (int s = 0; s < B_SLOTS; ++s) {
         if (s * NT + 64 * wid >= B_CHUNKS) break;   // wave-uniform (B_CHUNKS is a multiple of 64)
         const int rs = __builtin_amdgcn_readfirstlane((s * NT + 64 * wid) / CPR);
         dma16(wr, B + rs * BK * 2, b_vo[s], wso);
       }
-      kadv();
+      kb += BK;
+      if (kb == p.Cg) {
+        kb = 0;
+        ++t_;
+        if (++kw_ == p.nw) { kw_ = 0; if (++kh_ == p.nh) { kh_ = 0; ++kt_; } }
+        retap();
+      }
     };
     // DMA instructions of one tile issued by this wave (A slots always; B slots only for waves whose rows exist)
     int nb_w = 0;
@@ -440,59 +418,6 @@ void conv_igemm_kernel(const ConvParams p) {
           for (int j = 0; j < TN; ++j) fb1[j] = *reinterpret_cast<const ev8_t*>(An + fb[1][j]);
         }
       }
-    } else if constexpr (glds_ut && NSTAGE >= 3 && BK == 32) {
-      // BK = 32 ring of NSTAGE buffers with the fragment reads of tile step+1 hoisted across the barrier: they are
-      // issued right after the barrier that publishes tile step+1 and land while the MFMAs of tile step run (two
-      // register sets for even / odd tiles, the loop unrolled by two so every fragment index is compile-time).
-      // Tiles step+2 (.. step+NSTAGE-2) stay in flight across each barrier (counted vmcnt, raw s_barrier);
-      // buffer (step+NSTAGE-1) % NSTAGE held tile step-1, whose reads every wave retired before this barrier.
-      ev8_t fa0[TM], fb0[TN], fa1[TM], fb1[TN];
-      auto rd = [&](const char* T, ev8_t (&ra)[TM], ev8_t (&rb)[TN]) {
-#pragma unroll
-        for (int i = 0; i < TM; ++i) ra[i] = *reinterpret_cast<const ev8_t*>(T + fa[0][i]);
-#pragma unroll
-        for (int j = 0; j < TN; ++j) rb[j] = *reinterpret_cast<const ev8_t*>(T + fb[0][j]);
-      };
-      auto mm = [&](const ev8_t (&ra)[TM], const ev8_t (&rb)[TN]) {
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j) acc[i][j] = PVA_MFMA16(rb[j], ra[i], acc[i][j], 0, 0, 0);
-      };
-      auto publish_next = [&](int step) {   // tile step+1 landed for every wave, tile step's reads retired
-        if (NSTAGE == 4 && step + 2 < nsteps) vm_wait_dyn<A_SLOTS, B_SLOTS>(nb_w);   // leave tile step+2
-        else vm_wait<0>();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        if (step + NSTAGE - 1 < nsteps) issue_dma((step + NSTAGE - 1) % NSTAGE);
-      };
-      if (NSTAGE == 4 && nsteps > 2) vm_wait_dyn<2 * A_SLOTS, 2 * B_SLOTS>(2 * nb_w);   // tile 0 (1, 2 in flight)
-      else if (nsteps > 1) vm_wait_dyn<A_SLOTS, B_SLOTS>(nb_w);
-      else vm_wait<0>();
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      rd(smem, fa0, fb0);
-      int step = 0;
-      for (; step + 1 < nsteps; step += 2) {
-        __builtin_amdgcn_sched_barrier(0);
-        publish_next(step);
-        rd(smem + ((step + 1) % NSTAGE) * TILE_BYTES, fa1, fb1);
-        __builtin_amdgcn_sched_barrier(0);
-        mm(fa0, fb0);
-        __builtin_amdgcn_sched_barrier(0);
-        if (step + 2 < nsteps) {
-          publish_next(step + 1);
-          rd(smem + ((step + 2) % NSTAGE) * TILE_BYTES, fa0, fb0);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        mm(fa1, fb1);
-      }
-      if (step < nsteps) {   // odd tile count: the last tile is in set 0
-        __builtin_amdgcn_sched_barrier(0);
-        mm(fa0, fb0);
-      }
     } else
     for (int step = 0; step < nsteps; ++step) {
       const int cur = step & 1;
@@ -521,35 +446,22 @@ void conv_igemm_kernel(const ConvParams p) {
         A = smem + cur * TILE_BYTES;
       } else {
         __syncthreads();
+        if (step + 1 < nsteps) {
+          store_lds(cur ^ 1);
+          if (step + 2 < nsteps) load();
+        }
         A = smem + cur * TILE_BYTES;
       }
       if constexpr (glds_ut) {   // no register staging ring: room for the fragment double buffer
         mma_ktile<BK, TM, TN>(A, fa, fb, acc);
       } else {
-        // this tile's first-k-step fragments are read BEFORE the next tile is staged, so their LDS latency overlaps
-        // the staging work (global loads in, the consumer-side BN-ReLU of the A operand, ds_write) instead of the
-        // MFMAs waiting on it; the later k-steps' reads then overlap the first k-step's MFMAs
-        // (not for the 256x256 tile: its 128 accumulator registers leave no room, it would spill)
-        constexpr bool HOIST = BM * BN <= 256 * 128;
-        ev8_t af[TM], bfr[TN];
-        if constexpr (HOIST) {
-#pragma unroll
-          for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const ev8_t*>(A + fa[0][i]);
-#pragma unroll
-          for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const ev8_t*>(A + fb[0][j]);
-        }
-        if (step + 1 < nsteps) {
-          store_lds(cur ^ 1);
-          if (step + 2 < nsteps) load();
-        }
 #pragma unroll
         for (int kk = 0; kk < BK / 32; ++kk) {
-          if (kk > 0 || !HOIST) {
+          ev8_t af[TM], bfr[TN];
 #pragma unroll
-            for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const ev8_t*>(A + fa[kk][i]);
+          for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const ev8_t*>(A + fa[kk][i]);
 #pragma unroll
-            for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const ev8_t*>(A + fb[kk][j]);
-          }
+          for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const ev8_t*>(A + fb[kk][j]);
 #pragma unroll
           for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -980,7 +892,7 @@ void conv_igemm_kernel(const ConvParams p) {
 static int g_ut_mode = 1;
 
 inline bool conv_ut_legal(const ConvParams& p, int ch, int bk) {
-  return ch == 8 && p.Cg % bk == 0 && p.nt * p.nh * p.nw <= 32 && (p.x2 == nullptr || p.Cg2 % bk == 0);
+  return ch == 8 && p.Cg % bk == 0 && p.nt * p.nh * p.nw <= 32;
 }
 
 template <int BM, int BN, int WM, int WN, int CH, int BK>

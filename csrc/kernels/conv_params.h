@@ -66,15 +66,6 @@ struct ConvParams {
   // 1: statistics-only forward (EPI 0 with stats): the per-tile BN partial sums of the bf16-rounded output are
   // produced, the output itself is never stored (exact BN statistics of a folded conv, models/fused.py)
   int nostore;
-  // Optional second K segment: the one-launch dgrad of a residual unit's conv_a together with its 1x1 branch1 (the
-  // K-concatenated GEMM dX = [dY_a | dY_1] [W_a ; W_1]^T, so dX is written once instead of written and then
-  // accumulated into).  After the taps of x, Cg2 more k columns gather x2 (row stride ldx2, dims G2t x G2h x G2w) at
-  // the row-lattice point (b, qt, qh / s2h, qw / s2w) when qh % s2h == 0 and qw % s2w == 0, zeros elsewhere (the
-  // positions a strided branch1 never read).  That segment's weights start at column k2off of the packed row
-  // (Kfull = k2off + Cg2).  Uniform-tap loader only.
-  const uint16_t* x2;
-  int ldx2, Cg2, k2off, s2h, s2w, G2t, G2h, G2w;
-  unsigned x2bytes;
 };
 
 // Weight gradient: dW[n = cout][k = (tap, cin)] = sum_p dY[p][cout] * im2col(X)[p][k]

@@ -638,6 +638,49 @@ __global__ void wgrad_convert_kernel(float* __restrict__ accbuf, float* __restri
   }
 }
 
+// slab mode: 64 consecutive accumulator entries per block; wave w sums the slabs s = w, w + NW, ... (four running
+// partials, fixed order), the NW wave partials are combined in wave order through LDS.  Fixed order for a given
+// slab count, with 4*NW loads in flight per entry instead of one serial chain of `slabs` dependent adds (a 32x32
+// Gram of 4096 splits was a 16-wave, latency-bound pass).
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void wgrad_slab_reduce_kernel(const float* __restrict__ acc,
+                                                                    float* __restrict__ grad, int total_a, int taps,
+                                                                    int Cin, int Cin_real, float scale, float beta,
+                                                                    int slabs, int64_t ss) {
+  __shared__ float red[NW][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int a = blockIdx.x * 64 + lane;
+  float v = 0.f;
+  if (a < total_a) {
+    float t0 = 0.f, t1 = 0.f, t2 = 0.f, t3 = 0.f;
+    int s = w;
+    for (; s + 3 * NW < slabs; s += 4 * NW) {
+      t0 += acc[(int64_t)s * ss + a];
+      t1 += acc[(int64_t)(s + NW) * ss + a];
+      t2 += acc[(int64_t)(s + 2 * NW) * ss + a];
+      t3 += acc[(int64_t)(s + 3 * NW) * ss + a];
+    }
+    for (; s < slabs; s += NW) t0 += acc[(int64_t)s * ss + a];
+    v = (t0 + t1) + (t2 + t3);
+  }
+  if constexpr (NW > 1) {
+    red[w][lane] = v;
+    __syncthreads();
+    if (w != 0) return;
+#pragma unroll
+    for (int i = 1; i < NW; ++i) v += red[i][lane];
+  }
+  if (a >= total_a) return;
+  const int per_n = taps * Cin;
+  const int n = a / per_n;
+  const int rem = a - n * per_n;
+  const int tap = rem / Cin;
+  const int c = rem - tap * Cin;
+  if (c >= Cin_real) return;
+  const int o = (n * Cin_real + c) * taps + tap;
+  grad[o] = (beta == 0.f ? 0.f : beta * grad[o]) + scale * v;
+}
+
 }  // namespace
 
 // Shape-based tile choice: (BMW over cout, BNW over k).
@@ -719,6 +762,20 @@ void conv_wgrad_launch(const WgradParams& p, int chunk, hipStream_t stream) {
 void wgrad_reduce_launch(float* accbuf, float* grad, int splits, int Cout, int taps, int Cin, int Cin_real,
                          float scale, float beta, int slab, hipStream_t stream) {
   // atomic mode: one accumulator, re-zeroed here; slab mode: `splits` slabs fully overwritten by the kernel
+  if (slab && splits > 1) {
+    const int total_a = Cout * taps * Cin;
+    const dim3 grid((total_a + 63) / 64);
+    const int64_t ss = (int64_t)Cout * taps * Cin;
+#define PVA_SLAB_RED(NW) \
+    hipLaunchKernelGGL(wgrad_slab_reduce_kernel<NW>, grid, dim3(NW * 64), 0, stream, accbuf, grad, total_a, taps, Cin, \
+                       Cin_real, scale, beta, splits, ss)
+    if (splits >= 128) PVA_SLAB_RED(16);
+    else if (splits >= 32) PVA_SLAB_RED(8);
+    else if (splits >= 8) PVA_SLAB_RED(4);
+    else PVA_SLAB_RED(1);
+#undef PVA_SLAB_RED
+    return;
+  }
   const int total = Cout * taps * Cin_real;
   int blocks = std::min((total + 255) / 256, 4096);
   if (blocks < 1) blocks = 1;

@@ -107,32 +107,11 @@ static void check_pw(const ConvParams& p, int64_t chunk, int64_t cfg) {
   TORCH_CHECK(!p.emask || p.Ngemm % 8 == 0, "pointwise conv kernel: mask layout");
 }
 
-// second K segment (ConvParams::x2): g2 = [ldx2, Cg2, k2off, s2h, s2w, G2t, G2h, G2w]; uniform-tap configurations only
-static void set_x2(ConvParams& p, const OptT& x2, const std::vector<int64_t>& g2, int64_t chunk, int64_t cfg) {
-  if (!x2.has_value()) return;
-  TORCH_CHECK(g2.size() == 8, "second-segment geometry must have 8 entries");
-  p.x2 = bfp(*x2);
-  p.ldx2 = (int)g2[0]; p.Cg2 = (int)g2[1]; p.k2off = (int)g2[2]; p.s2h = (int)g2[3]; p.s2w = (int)g2[4];
-  p.G2t = (int)g2[5]; p.G2h = (int)g2[6]; p.G2w = (int)g2[7];
-  TORCH_CHECK(chunk == 8 && p.Cg2 % 32 == 0 && p.ldx2 % 8 == 0 && p.s2h > 0 && p.s2w > 0, "second segment layout");
-  TORCH_CHECK(p.Kfull == p.k2off + p.Cg2, "packed weight rows must hold both segments");
-  TORCH_CHECK(x2->numel() * 2 < 0xFFFFFF00ll && x2->numel() >= (int64_t)p.G2t * p.G2h * p.G2w * p.ldx2 / 1,
-              "second segment tensor extent");
-  p.x2bytes = (unsigned)(x2->numel() * 2);
-  TORCH_CHECK(cfg >= 0 && (cfg & 16) && !(cfg & (32 | 512 | 2048)) && ((cfg & 8) || (cfg & 256)),
-              "the K-concatenated dgrad runs on the uniform-tap loader only");
-  TORCH_CHECK(pva_bf16::conv_igemm_ut_legal(p, (int)chunk, (cfg & 4) ? 64 : 32) && p.Cg2 % ((cfg & 4) ? 64 : 32) == 0,
-              "uniform-tap loader not legal for this K-concatenated launch");
-}
-
 void conv_igemm(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, const OptT& stats,
                 const OptT& scale, const OptT& shift, int64_t affine, int64_t accum, std::vector<int64_t> g,
-                int64_t chunk, int64_t cfg, const OptT& bias, int64_t nostore, const OptT& x2,
-                std::vector<int64_t> g2) {
+                int64_t chunk, int64_t cfg, const OptT& bias, int64_t nostore) {
   const bool h = kind16(x);
   ConvParams p = conv_params(x, w, y, accum, g, chunk);
-  set_x2(p, x2, g2, chunk, cfg);
-  TORCH_CHECK(!x2.has_value() || (!affine && !stats.has_value() && !nostore), "K-concatenated launches are plain dgrads");
   p.nostore = (int)nostore;
   TORCH_CHECK(!nostore || (stats.has_value() && !accum && !bias.has_value()),
               "statistics-only forward needs stats and no accumulate / bias");
@@ -612,8 +591,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("trace_mark", [](const std::string& s) { roctxMarkA(s.c_str()); });
   m.def("conv_igemm", &conv_igemm, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("stats"), py::arg("scale"),
         py::arg("shift"), py::arg("affine"), py::arg("accum"), py::arg("g"), py::arg("chunk"), py::arg("cfg") = -1,
-        py::arg("bias") = py::none(), py::arg("nostore") = 0, py::arg("x2") = py::none(),
-        py::arg("g2") = std::vector<int64_t>{});
+        py::arg("bias") = py::none(), py::arg("nostore") = 0);
   m.def("conv_igemm_fres", &conv_igemm_fres);
   m.def("bnfold_fwd_stats", &bnfold_fwd_stats);
   m.def("bnfold_bwd", &bnfold_bwd);

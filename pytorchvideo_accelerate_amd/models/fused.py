@@ -564,41 +564,6 @@ class _ConvBN:
                          direct=bias is None)
         return None
 
-    def dgrad_cat_ok(self, one: "_ConvBN") -> bool:
-        """Whether this (stride-1) conv's dgrad and ``one``'s (1x1, temporal stride 1) can run as ONE K-concatenated
-        GEMM on the uniform-tap loader (both gathered channel counts multiples of 32)."""
-        s, s1 = self.spec, one.spec
-        return (self.eng.dgrad_cat and tuple(s.stride) == (1, 1, 1) and tuple(s1.k) == (1, 1, 1)
-                and s1.stride[0] == 1 and tuple(s1.pad) == (0, 0, 0) and s.cout % 32 == 0 and s1.cout % 32 == 0
-                and s.cin == s1.cin and s.cin % 8 == 0)
-
-    def dgrad_cat(self, dy: Act, in_dims, out: torch.Tensor, accum: bool, one: "_ConvBN", dy1: Act):
-        """dX = dgrad(self, dy) + dgrad(one, dy1) as ONE K-concatenated GEMM dX = [dY | dY_1] [W ; W_1]^T
-        (ConvParams::x2): this conv's taps, then branch1's 1x1 — at every s-th input position when it is strided,
-        zeros elsewhere.  dX is written once instead of written and then partly re-read and accumulated (the
-        stride-2 branch1 of each stage's first unit; VERDICT r3 next #1)."""
-        s, C = self.spec, self.eng.C
-        s1 = one.spec
-        self.eng.mark(self.name + ".dgrad")
-        key = ("dgc", dy.N, tuple(in_dims), dy.ld, out.stride(0), dy1.ld, (dy1.T, dy1.H, dy1.W))
-        geo = self._geo.get(key)
-        if geo is None:
-            ph = dgrad_phases(s, dy.N, tuple(in_dims), (dy.T, dy.H, dy.W), dy.ld, out.stride(0))
-            assert len(ph) == 1, "K-concatenated dgrad needs a single-phase (stride-1) first segment"
-            g = list(ph[0])
-            k2off = g[2]
-            g[2] = k2off + s1.cout
-            g2 = [dy1.ld, s1.cout, k2off, s1.stride[1], s1.stride[2], dy1.T, dy1.H, dy1.W]
-            geo = self._geo[key] = (g, g2)
-        g, g2 = geo
-        wcat = self.eng.wcat_of(self, one)
-        tuner = self.eng.tuner
-
-        def run(cfg, scratch):
-            C.conv_igemm(dy.t, wcat, tuner.scratch_like(out) if scratch else out, None, None, None, 0,
-                         1 if accum else 0, g, 8, cfg, None, 0, dy1.t, g2)
-        tuner.launch(("dgc", accum) + tuple(g) + tuple(g2), g, 8, run, ut_only=True, cg2=s1.cout)
-
     def bn_backward(self, g: Act, y: Act, mask_mode: int, mo: Optional[Act], mxf: Optional[_Xf],
                     dz_out: Optional[Act] = None, dz_accum: bool = False, other: Optional["_ConvBN"] = None,
                     other_y: Optional[Act] = None, pre=None) -> Tuple[Act, Optional[Act]]:
@@ -945,9 +910,6 @@ class _ResBlock:
         writing conv_a's first and accumulating branch1's second touches dx once in full plus once at those
         positions (the other order writes zeros at 3/4 of dx and then reads + rewrites all of it)."""
         x = self.x
-        if self.a.dgrad_cat_ok(self.one):   # one K-concatenated launch: dx written once
-            self.a.dgrad_cat(dya, (x.T, x.H, x.W), dx, dx_accum, self.one, dy1)
-            return None
         self.a.dgrad(dya, (x.T, x.H, x.W), dx, dx_accum)
         self.one.dgrad(dy1, (x.T, x.H, x.W), dx, True)
         return None
@@ -1086,10 +1048,6 @@ class FusedNet:
         self.bn_fold = os.environ.get("PVA_BN_FOLD", "1") != "0"
         self.fold_min_c = int(os.environ.get("PVA_BN_FOLD_MIN_C", "32"))
         self.bn_fold1 = self.bn_fold and os.environ.get("PVA_BN_FOLD1", "1") != '0'
-        # K-concatenated dgrad of a stage's first unit (conv_a + strided branch1 in one GEMM); PVA_DGRAD_CAT=0: two
-        # launches (conv_a writes dx, branch1 accumulates at its positions)
-        self.dgrad_cat = os.environ.get("PVA_DGRAD_CAT", "1") != "0"
-        self._wcat: Dict = {}
         # folds with fewer input channels than this take exact statistics from a statistics-only conv pass
         self.fold_exact_below = int(os.environ.get("PVA_BN_FOLD_EXACT_BELOW", "32"))
         blocks = list(model.blocks)
@@ -1288,23 +1246,9 @@ class FusedNet:
                 u.wd = self.pack_dgr[do:do + s.cin * s.taps * s.cout].view(s.cin, s.taps * s.cout)
         self.pack_desc = torch.from_numpy(rec.view(np.uint8).copy()).to(self.device)
 
-    def wcat_of(self, a: "_ConvBN", one: "_ConvBN") -> torch.Tensor:
-        """[Cin][taps_a*Cout_a + Cout_1] dgrad pack of a K-concatenated dgrad (refreshed by ``pack``)."""
-        k = (a.name, one.name)
-        t = self._wcat.get(k)
-        if t is None:
-            t = torch.empty(a.spec.cin, a.wd.shape[1] + one.wd.shape[1], device=self.device, dtype=self.cdt)
-            torch.cat([a.wd, one.wd], dim=1, out=t)
-            self._wcat[k] = (t, a, one)
-            return t
-        return t[0]
-
     def pack(self):
-        """Refresh the 16-bit packed weights from the fp32 master buffer (one multi-tensor launch + s2d stems, + the
-        K-concatenated dgrad packs)."""
+        """Refresh bf16 packed weights from the fp32 master buffer (one multi-tensor launch + s2d stems)."""
         self.C.pack_weights(self.flat.data, self.pack_fwd, self.pack_dgr, self.pack_desc, len(self.units))
-        for t, a, one in self._wcat.values():
-            torch.cat([a.wd, one.wd], dim=1, out=t)
         for paths, _ in self.stages:
             for m in paths:
                 if isinstance(m, _Stem):

@@ -288,8 +288,11 @@ def box_wgrad_slabs(spec: "ConvSpec", splits: int) -> int:
 def conv_wgrad(dy: Act, x: Act, spec: ConvSpec, grad: torch.Tensor, workspace: Optional[torch.Tensor] = None,
                in_scale: Optional[torch.Tensor] = None, in_shift: Optional[torch.Tensor] = None,
                in_relu: bool = True, scale: float = 1.0, beta: float = 0.0,
-               splits_pps: Optional[Tuple[int, int]] = None, variant: int = -1) -> torch.Tensor:
+               splits_pps: Optional[Tuple[int, int]] = None, variant: int = -1, slab: bool = False) -> torch.Tensor:
     """grad (fp32, [Cout, Cin, kt, kh, kw]) = beta*grad + scale * dW.
+
+    ``slab``: every split writes its own fp32 slab (no atomics) and the slabs are summed in a fixed order
+    (bitwise reproducible; the fused executor's deterministic mode and BN-fold products).
 
     ``variant``: -1 = heuristic tile; else bits 0-1 (+ bit 3 -> tiles 4-7) = tile (16x128, 32x128, 64x64, 128x64,
     128x128, 256x128, 128x256, 256x256), bit 2 = 64-position LDS stages (two MFMA k-steps per barrier);
@@ -323,14 +326,14 @@ def conv_wgrad(dy: Act, x: Act, spec: ConvSpec, grad: torch.Tensor, workspace: O
         assert plan is not None, "halo wgrad does not apply to this conv"
         splits_pps, variant = plan[:2], plan[2]
     splits, pps = splits_pps or wgrad_splits(P, spec.cout, K, variant=(variant & 11) if variant >= 0 else -1)
-    need = spec.cout * K
+    need = spec.cout * K * (splits if slab else 1)
     if workspace is None or workspace.numel() < need:
         workspace = torch.zeros(need, device=dy.t.device, dtype=torch.float32)  # kept zero by wgrad_reduce
     affine = 0 if in_scale is None else (2 if in_relu else 1)
     g = [P, spec.cout, K, spec.cin_pad, dy.ld, x.ld, x.T, x.H, x.W, dy.T, dy.H, dy.W,
          *spec.k, *spec.stride, *spec.pad, splits, pps]
-    C.conv_wgrad(dy.t, x.t, workspace, in_scale, in_shift, affine, g, spec.chunk, 0, variant)
-    C.wgrad_reduce(workspace, grad, splits, spec.cout, spec.taps, spec.cin_pad, spec.cin, scale, beta)
+    C.conv_wgrad(dy.t, x.t, workspace, in_scale, in_shift, affine, g, spec.chunk, int(slab), variant)
+    C.wgrad_reduce(workspace, grad, splits, spec.cout, spec.taps, spec.cin_pad, spec.cin, scale, beta, int(slab))
     return grad
 
 

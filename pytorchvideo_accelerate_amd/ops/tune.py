@@ -96,15 +96,10 @@ class ConvTuner:
 
     # ---------------------------------------------------------------- candidates
     def candidates(self, g: Sequence[int], chunk: int, aff: int = 0, epi: bool = False,
-                   direct: bool = True, pw: bool = True, halo: bool = True, ut_only: bool = False,
-                   cg2: int = 0) -> List[int]:
-        """``ut_only``: uniform-tap loader configurations only (the K-concatenated dgrad, whose second segment of
-        ``cg2`` channels that loader alone gathers)."""
+                   direct: bool = True, pw: bool = True, halo: bool = True) -> List[int]:
         N, Cg = g[1], g[3]
         K = g[28] * g[29] * g[30] * Cg
         out = []
-        if ut_only:
-            direct = pw = halo = False
         for v, bn in enumerate(TILE_BN):
             if bn > 16 and bn >= 2 * N:      # tile much wider than the output channels
                 continue
@@ -113,8 +108,8 @@ class ConvTuner:
             for bk in (32, 64):
                 if bk == 64 and (chunk != 8 or K < 64):
                     continue
-                uts = [] if ut_only else [False]
-                if chunk == 8 and self.C.conv_ut_legal(list(g), chunk, bk) and cg2 % bk == 0:
+                uts = [False]
+                if chunk == 8 and self.C.conv_ut_legal(list(g), chunk, bk):
                     uts.append(True)
                 for ut in uts:
                     out.append(cfg_word(v, bk, ut))
@@ -122,7 +117,7 @@ class ConvTuner:
                         out.append(cfg_word(v, bk, ut) | DMA)
         if N >= 256 and chunk == 8:   # 256x256 tile (UT loader only: the generic one is VALU-bound)
             for bk in (32, 64):
-                if self.C.conv_ut_legal(list(g), chunk, bk) and cg2 % bk == 0:
+                if self.C.conv_ut_legal(list(g), chunk, bk):
                     w = EXPLICIT | BIG | UT | (BK64 if bk == 64 else 0)
                     out.append(w)
                     if aff == 0 and self.dma:
@@ -156,8 +151,7 @@ class ConvTuner:
 
     # ---------------------------------------------------------------- launch
     def launch(self, key: Tuple, g: Sequence[int], chunk: int, run: Callable[[int, bool], None],
-               aff: int = 0, epi: bool = False, direct: bool = True, pw: bool = True, halo: bool = True,
-               ut_only: bool = False, cg2: int = 0) -> int:
+               aff: int = 0, epi: bool = False, direct: bool = True, pw: bool = True, halo: bool = True) -> int:
         """``run(cfg, scratch)`` performs the launch (into scratch outputs when ``scratch``).  Returns the
         configuration used for the real launch (-1 = kernel heuristic).  ``direct=False`` / ``pw=False``: the
         launch needs an epilogue the direct / pointwise kernel lacks (fused residual output, bias, statistics
@@ -165,23 +159,15 @@ class ConvTuner:
         cfg = self.cache.get(key)
         if cfg is None:
             self._pw_now = self.pw_kinds is None or (len(key) > 0 and key[0] in self.pw_kinds)
-            if self.enabled:
-                cfg = self._tune(g, chunk, run, aff, epi, direct, pw, halo, ut_only, cg2)
-            else:   # no tuning: the heuristic, or for uniform-tap-only launches the first legal configuration
-                cfg = -1
-                if ut_only:
-                    c = self.candidates(g, chunk, aff, epi, direct, pw, halo, ut_only, cg2)
-                    assert c, "no uniform-tap configuration for this launch"
-                    cfg = c[0]
+            cfg = self._tune(g, chunk, run, aff, epi, direct, pw, halo) if self.enabled else -1
             self._pw_now = True
             self.cache[key] = cfg
         run(cfg, False)
         return cfg
 
     def _tune(self, g: Sequence[int], chunk: int, run: Callable[[int, bool], None], aff: int = 0,
-              epi: bool = False, direct: bool = True, pw: bool = True, halo: bool = True, ut_only: bool = False,
-              cg2: int = 0) -> int:
-        cands = self.candidates(g, chunk, aff, epi, direct, pw, halo, ut_only, cg2)
+              epi: bool = False, direct: bool = True, pw: bool = True, halo: bool = True) -> int:
+        cands = self.candidates(g, chunk, aff, epi, direct, pw, halo)
         if len(cands) <= 1:
             return cands[0] if cands else -1
         self.tuned += 1

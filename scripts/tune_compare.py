@@ -32,8 +32,24 @@ def main():
     ap.add_argument("old")
     ap.add_argument("new")
     ap.add_argument("--family", default="", help="also list every configuration containing this substring")
+    ap.add_argument("--families", action="store_true",
+                    help="only the median new/old time ratio per configuration family (tile / loader / staging)")
     a = ap.parse_args()
     old, new = parse(a.old), parse(a.new)
+    if a.families:
+        import statistics
+        fam = collections.defaultdict(list)
+        for key, runs in new.items():
+            for i, (tn, _) in enumerate(runs):
+                if key not in old or i >= len(old[key]):
+                    continue
+                to = old[key][i][0]
+                for c in tn:
+                    if c in to:
+                        fam[re.sub(r"\d+(?=[a-z/]|$)", "", c) if not re.match(r"\d+x\d+", c) else c].append(tn[c] / to[c])
+        for f, v in sorted(fam.items()):
+            print(f"{f:26s} n={len(v):4d}  median new/old {statistics.median(v):.3f}")
+        return
     tot_o = tot_n = 0.0
     print(f"{'M':>9s} {'N':>5s} {'K':>5s} {'taps':>7s}  {'old best':>26s} {'us':>8s}  {'new best':>26s} {'us':>8s}  {'ratio':>6s}")
     for key, runs in new.items():

@@ -250,6 +250,31 @@ def test_conv_wgrad(case):
     assert rel_err(grad, 1.5 * w.grad) < 1e-2
 
 
+@pytest.mark.parametrize("splits", [3, 8, 40, 300])
+@pytest.mark.parametrize("case", [CASES[1], CASES[6], STEMS[1]])
+def test_conv_wgrad_slab_reduction(case, splits):
+    """Per-split slabs + the fixed-order slab reduction (every wave-count branch: 1, 4, 8, 16 waves per 64 entries;
+    padded input channels skipped) against PyTorch, with beta/scale, and bitwise equal run to run."""
+    x, w, spec = _mk(case, seed=5)
+    w.requires_grad_(True)
+    ref_y = torch.nn.functional.conv3d(x, w, None, spec.stride, spec.pad)
+    gy = torch.randn_like(ref_y).to(torch.bfloat16).float()
+    ref_y.backward(gy)
+    dy, xa = Act.from_ncthw(gy), Act.from_ncthw(x, spec.cin_pad)
+    pps = (dy.M + splits - 1) // splits
+    pps = (pps + 31) // 32 * 32
+    sp = ((dy.M + pps - 1) // pps, pps)
+    grad = torch.zeros_like(w)
+    conv_wgrad(dy, xa, spec, grad, splits_pps=sp, slab=True)
+    assert rel_err(grad, w.grad) < 1e-2
+    g2 = torch.full_like(w, 2.0)
+    conv_wgrad(dy, xa, spec, g2, splits_pps=sp, slab=True, scale=0.5, beta=1.0)
+    assert rel_err(g2, 2.0 + 0.5 * w.grad) < 1e-2
+    again = torch.zeros_like(w)
+    conv_wgrad(dy, xa, spec, again, splits_pps=sp, slab=True)
+    assert torch.equal(grad, again)
+
+
 @pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15])
 @pytest.mark.parametrize("case", [CASES[1], CASES[3], CASES[6], STEMS[1]])
 def test_conv_wgrad_tile_variants(case, variant):
@@ -603,42 +628,3 @@ def test_conv_wgrad_halo(case, affine, option):
     conv_wgrad(dy, Act.from_ncthw(x), spec, grad, in_scale=sc if affine else None,
                in_shift=sh if affine else None, variant=HALO | option)
     assert rel_err(grad, w.grad) < 1.5e-2
-
-
-@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("s1", [(1, 2, 2), (1, 1, 1)])
-def test_k_concatenated_dgrad(dt, s1):
-    """One-launch dgrad of conv_a (3,1,1) and a 1x1 branch1 (ConvParams::x2): dX = [dY_a | dY_1] [W_a ; W_1]^T with
-    the branch1 segment gathered at every s-th position (zeros elsewhere), every uniform-tap configuration, against the
-    sum of the two fp32 input gradients."""
-    from pytorchvideo_accelerate_amd.ops._ext import require
-    from pytorchvideo_accelerate_amd.ops.conv import dgrad_phases
-    from pytorchvideo_accelerate_amd.ops.tune import ConvTuner, describe
-    C = require()
-    g = torch.Generator().manual_seed(7)
-    N, Cin, Ca, C1, T, H, W = 2, 64, 64, 256, 4, 14, 14
-    sa = ConvSpec(Cin, Ca, (3, 1, 1), (1, 1, 1), (1, 0, 0))
-    sb = ConvSpec(Cin, C1, (1, 1, 1), s1, (0, 0, 0))
-    wa = (torch.randn(Ca, Cin, 3, 1, 1, generator=g) / 14).to(DEV).to(dt).float()
-    w1 = (torch.randn(C1, Cin, 1, 1, 1, generator=g) / 8).to(DEV).to(dt).float()
-    Ho, Wo = (H - 1) // s1[1] + 1, (W - 1) // s1[2] + 1
-    dya = torch.randn(N, Ca, T, H, W, generator=g).to(DEV).to(dt).float()
-    dy1 = torch.randn(N, C1, T, Ho, Wo, generator=g).to(DEV).to(dt).float()
-    shape = (N, Cin, T, H, W)
-    ref = (torch.nn.grad.conv3d_input(shape, wa, dya, 1, (1, 0, 0)) +
-           torch.nn.grad.conv3d_input(shape, w1, dy1, s1, 0))
-    _, wda = pack_weight(wa, sa, dt)
-    _, wd1 = pack_weight(w1, sb, dt)
-    wcat = torch.cat([wda.reshape(Cin, -1), wd1.reshape(Cin, -1)], dim=1).contiguous()
-    A, A1 = Act.from_ncthw(dya, dtype=dt), Act.from_ncthw(dy1, dtype=dt)
-    gg = list(dgrad_phases(sa, N, (T, H, W), (T, H, W), A.ld, Cin)[0])
-    k2off = gg[2]
-    gg[2] = k2off + C1
-    g2 = [A1.ld, C1, k2off, s1[1], s1[2], T, Ho, Wo]
-    cands = ConvTuner(C).candidates(gg, 8, ut_only=True, cg2=C1)
-    assert cands
-    for cfg in cands:
-        out = torch.full((N * T * H * W, Cin), float("nan"), device=DEV, dtype=dt)
-        C.conv_igemm(A.t, wcat, out, None, None, None, 0, 0, gg, 8, cfg, None, 0, A1.t, g2)
-        got = out.float().view(N, T, H, W, Cin).permute(0, 4, 1, 2, 3)
-        assert rel_err(got, ref) < 1e-2, describe(cfg)
