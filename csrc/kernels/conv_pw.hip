@@ -27,15 +27,22 @@ inline int pw_ks(int K) {
 // rows per workgroup of a pointwise launch configuration (cfg bits 0-1)
 int conv_pw_rows(int cfg) { return 1024 << (cfg & 3); }
 
-// 1 when the geometry is a dense 1x1x1 unit-stride unpadded GEMM the pointwise kernel can run
+// 1 when the geometry is a dense 1x1x1 unit-stride unpadded GEMM the pointwise kernel can run, or a (kt,1,1)
+// temporal conv at unit stride (forward, or the stride-1 dgrad gathering backwards) whose taps are visited in
+// weight order: K = kt x Cg <= 256, clip slices of >= 32 pixels (a 64-row tile crosses at most two)
 int conv_pw_legal(const ConvParams& p, int chunk) {
   if (chunk != 8) return 0;
-  if (p.nt != 1 || p.nh != 1 || p.nw != 1 || p.check) return 0;
-  if (p.ast != 1 || p.ash != 1 || p.asw != 1 || p.aot != 0 || p.aoh != 0 || p.aow != 0) return 0;
+  if (p.nh != 1 || p.nw != 1) return 0;
+  if (p.ast != 1 || p.ash != 1 || p.asw != 1 || p.aoh != 0 || p.aow != 0) return 0;
   if (p.Gt != p.Rt || p.Gh != p.Rh || p.Gw != p.Rw) return 0;
   if (p.ost != 1 || p.osh != 1 || p.osw != 1 || p.ort != 0 || p.orh != 0 || p.orw != 0) return 0;
   if (p.Ot != p.Rt || p.Oh != p.Rh || p.Ow != p.Rw) return 0;
-  if (p.Kfull != p.Cg || p.Cg % 8 != 0 || p.Cg > 256 || p.Ngemm % 32 != 0) return 0;
+  if (p.nt == 1) {
+    if (p.check || p.aot != 0) return 0;
+  } else {
+    if (p.bt0 != 0 || p.bts != 1 || (p.dir != 1 && p.dir != -1) || p.Rh * p.Rw < 32 || p.Rt < 2) return 0;
+  }
+  if (p.Kfull != p.nt * p.Cg || p.Cg % 8 != 0 || p.Kfull > 256 || p.Ngemm % 32 != 0) return 0;
   if (p.ldx % 8 != 0 || p.ldy % 8 != 0) return 0;
   return 1;
 }
@@ -55,7 +62,7 @@ static int pw_group_chunks(int N, int ks, int nslot, int aff_bytes) {
 void conv_pw_launch(const ConvParams& p, int cfg, hipStream_t st) {
   const bool ep2 = !p.fres && (p.eres || p.emask || p.epart);
   const int ep = p.fres ? 1 : (ep2 ? 2 : 0);
-  const int ks = pw_ks(p.Cg);
+  const int ks = pw_ks(p.Kfull);
   // per-wave statistic slots [8 waves][statistics] per channel (none for the residual output)
   const int nslot = ep == 1 ? 0 : (ep == 2 ? 3 : 2) * 8;
   const int aff_bytes = p.affine ? 2 * p.Cg * 4 : 0;

@@ -101,13 +101,13 @@ struct Pre {
 // buffer descriptors / branches) only for its own streams, so the ring can be deeper
 constexpr int OP_OLD = 1, OP_RES = 2, OP_Y0 = 4, OP_Y1 = 8, OP_MASK = 16, OP_MSC = 32;
 
-template <int KS, int TM, int EP, int AFF, bool NTS, int OPS, int PD, int CPI>
+template <int KS, int TM, int EP, int AFF, bool NTS, int OPS, int PD, int CPI, bool TP>
 __global__ __launch_bounds__(PW_THREADS) void conv_pw_kernel(const ConvParams p, int rpb, int gch) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NST = EP == 2 ? 3 : 2;
   constexpr int NSLOT = EP == 1 ? 0 : NST * PW_WAVES;   // per-wave statistic slots (= conv_pw.hip)
   constexpr int MT = 16 * TM;   // PD: prefetch ring depth (chunks)
-  const int N = p.Ngemm, K = p.Cg;
+  const int N = p.Ngemm, K = p.Kfull, Ca = p.Cg;   // K = taps x Ca (1x1: K = Ca)
   // output-channel group of this workgroup (weights of wide convs do not fit LDS at once: the row range
   // is walked once per group of gch 32-channel chunks; the XCD remap puts the groups of one row range on
   // the same XCD, so its activations are re-read from that L2)
@@ -120,7 +120,7 @@ __global__ __launch_bounds__(PW_THREADS) void conv_pw_kernel(const ConvParams p,
   const int wimg = nch * 2 * KS * 1024;
   float* st_lds = reinterpret_cast<float*>(smem + wimg);   // [PW_WAVES][NST][NG] per-wave statistics
   float* cst = st_lds + NSLOT * NG;                         // [4][NG] per-channel epilogue constants
-  float* affs = cst + 4 * NG;                               // [2][K] input affine
+  float* affs = cst + 4 * NG;                               // [2][Ca] input affine (per gathered channel)
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int rho = lane & 15, g = lane >> 4;
   // this wave's statistic slots: every (statistic, channel) address is updated by one lane of one wave, in
@@ -145,7 +145,7 @@ __global__ __launch_bounds__(PW_THREADS) void conv_pw_kernel(const ConvParams p,
   if (do_stats)
     for (int i = tid; i < NSLOT * NG; i += PW_THREADS) st_lds[i] = 0.f;
   if (AFF)
-    for (int i = tid; i < K; i += PW_THREADS) { affs[i] = p.in_scale[i]; affs[K + i] = p.in_shift[i]; }
+    for (int i = tid; i < Ca; i += PW_THREADS) { affs[i] = p.in_scale[i]; affs[Ca + i] = p.in_shift[i]; }
   // EP 1: fsc fsh rsc rsh ; EP 0 / 2: bias (0 when absent), mask-affine scale and shift
   for (int i = tid; i < NG; i += PW_THREADS) {
     const int n = nb0 + i;
@@ -209,12 +209,51 @@ __global__ __launch_bounds__(PW_THREADS) void conv_pw_kernel(const ConvParams p,
   const int tstride = PW_WAVES * MT;
   const int mfirst = row0 + wid * MT;
   const int ntw = mfirst < row_end ? (row_end - mfirst + tstride - 1) / tstride : 0;
-  // this lane's activation offsets within a row (k past K -> out of bounds -> zero)
+  // this lane's activation offsets within a row (k past K -> out of bounds -> zero).  Temporal taps (kt,1,1),
+  // unit stride (fwd, or the stride-1 dgrad gathering backwards): k = 32 s + 8 g is tap j = k / Ca, channel
+  // k % Ca, read from the row (t + aot + dir j) of the same clip and pixel — a whole-row delta of
+  // (aot + dir j) * H * W rows; taps leaving the clip read zero (padding).  Tap rows may lie outside this
+  // workgroup's row range, so they go through a resource over the whole tensor.
+  constexpr bool taps = TP;   // (launch_ks: p.nt > 1)
+  const int HW = p.Rh * p.Rw;
   uint32_t xk[KS];
+  int kc[KS], tdel[KS], rdel[KS];
 #pragma unroll
-  for (int s = 0; s < KS; ++s) xk[s] = 32 * s + 8 * g < K ? (32 * s + 8 * g) * 2 : OOB;
+  for (int s = 0; s < KS; ++s) {
+    const int k0 = 32 * s + 8 * g;
+    const int j = k0 / Ca;
+    kc[s] = k0 - j * Ca;
+    tdel[s] = p.aot + p.dir * j;
+    rdel[s] = tdel[s] * HW * xb;
+    xk[s] = k0 < K ? (taps ? kc[s] : k0) * 2 : OOB;
+  }
+  const __amdgpu_buffer_rsrc_t xall = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, (int)p.xbytes,
+                                                                        0x00020000);
   uint4 araw[TM][KS];
+  unsigned amask = 0;   // taps: (row i, chunk s) inside the clip -> bit i * KS + s
   auto load_a = [&](int m0) {
+    if constexpr (taps) {
+      const int q0 = m0 / HW;
+      const int rem0 = m0 - q0 * HW;
+      const int t0 = q0 % p.Rt;
+      amask = 0;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int pos = rem0 + 16 * i + rho;   // < HW + 64 <= 3 HW (host: HW >= 32): at most two slice steps
+        int tr = t0 + (pos >= HW ? 1 : 0) + (pos >= 2 * HW ? 1 : 0);
+        if (tr >= p.Rt) tr -= p.Rt;
+        const int base = (m0 + 16 * i + rho) * xb;
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          const int tt = tr + tdel[s];
+          const bool v = xk[s] != OOB && tt >= 0 && tt < p.Gt;
+          araw[i][s] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+              xall, v ? (uint32_t)(base + rdel[s]) + xk[s] : OOB, 0, 0));
+          amask |= (v ? 1u : 0u) << (i * KS + s);
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const uint32_t ro = (uint32_t)(m0 - row0 + 16 * i + rho) * xb;
@@ -270,13 +309,14 @@ __global__ __launch_bounds__(PW_THREADS) void conv_pw_kernel(const ConvParams p,
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
           uint4 v = araw[i][s];
-          if (AFF && xk[s] != OOB && !(tail && m0 + 16 * i + rho >= row_end)) {   // (padding stays zero)
-            const int k0 = 32 * s + 8 * g;
+          const bool live = taps ? ((amask >> (i * KS + s)) & 1u) != 0 : xk[s] != OOB;
+          if (AFF && live && !(tail && m0 + 16 * i + rho >= row_end)) {   // (padding stays zero)
+            const int k0 = taps ? kc[s] : 32 * s + 8 * g;
             float f[8];
             unpack8(v, f);
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
-              const float z = __builtin_fmaf(f[e], affs[k0 + e], affs[K + k0 + e]);
+              const float z = __builtin_fmaf(f[e], affs[k0 + e], affs[Ca + k0 + e]);
               f[e] = AFF == 2 ? fmaxf(z, 0.f) : z;
             }
             v = pack8_fast(f);
@@ -446,7 +486,7 @@ __global__ __launch_bounds__(PW_THREADS) void conv_pw_kernel(const ConvParams p,
   }
 }
 
-template <int KS, int TM, int EP, int AFF, int OPS, int PD>
+template <int KS, int TM, int EP, int AFF, int OPS, int PD, bool TP>
 void launch_one(const ConvParams& p, int rpb, int gch, size_t lds, hipStream_t st) {
   // non-temporal (streaming) output stores for the BN-folded residual output, whose 16-B rows are never
   // re-read while L2-resident (measured +8 % on the res2 shape, scripts/pw_probe.py); the other epilogues
@@ -457,32 +497,32 @@ void launch_one(const ConvParams& p, int rpb, int gch, size_t lds, hipStream_t s
   const dim3 grid(((p.M + rpb - 1) / rpb) * ngrp), block(PW_THREADS);
   if constexpr (KS == 1) {
     if (gch < 2) {
-      hipLaunchKernelGGL((conv_pw_kernel<KS, TM, EP, AFF, EP == 1, OPS, PD, 1>), grid, block, lds, st, p, rpb, gch);
+      hipLaunchKernelGGL((conv_pw_kernel<KS, TM, EP, AFF, EP == 1, OPS, PD, 1, TP>), grid, block, lds, st, p, rpb, gch);
       return;
     }
   }
-  hipLaunchKernelGGL((conv_pw_kernel<KS, (TM > 1 ? TM / 2 : 1), EP, AFF, EP == 1, OPS, PD, 2>), grid, block, lds,
+  hipLaunchKernelGGL((conv_pw_kernel<KS, (TM > 1 ? TM / 2 : 1), EP, AFF, EP == 1, OPS, PD, 2, TP>), grid, block, lds,
                      st, p, rpb, gch);
 }
 
-template <int KS, int TM, int EP, int OPS, int PD>
+template <int KS, int TM, int EP, int OPS, int PD, bool TP>
 void launch_aff(const ConvParams& p, int rpb, int gch, size_t lds, hipStream_t st) {
   switch (EP == 2 ? 0 : p.affine) {
-    case 0: launch_one<KS, TM, EP, 0, OPS, PD>(p, rpb, gch, lds, st); break;
-    case 1: launch_one<KS, TM, EP, 1, OPS, PD>(p, rpb, gch, lds, st); break;
-    default: launch_one<KS, TM, EP, 2, OPS, PD>(p, rpb, gch, lds, st); break;
+    case 0: launch_one<KS, TM, EP, 0, OPS, PD, TP>(p, rpb, gch, lds, st); break;
+    case 1: launch_one<KS, TM, EP, 1, OPS, PD, TP>(p, rpb, gch, lds, st); break;
+    default: launch_one<KS, TM, EP, 2, OPS, PD, TP>(p, rpb, gch, lds, st); break;
   }
 }
 
 // backward-BN epilogue: tile rows and ring depth sized by the 16-B operand streams an instantiation
 // carries (a lane holds TM * 16 B per stream per ring stage)
-template <int KS, int OPS>
+template <int KS, int OPS, bool TP>
 void launch_ep2(const ConvParams& p, int rpb, int gch, size_t lds, hipStream_t st) {
   constexpr int nops = ((OPS >> 0) & 1) + ((OPS >> 1) & 1) + ((OPS >> 2) & 1) + ((OPS >> 3) & 1);
   constexpr int TM0 = nops <= 1 ? 4 : 2;
   constexpr int TM = KS <= 2 ? TM0 : KS == 4 ? 2 : TM0 / 2;
   constexpr int PD = nops <= 2 ? 3 : 2;
-  launch_one<KS, TM, 2, 0, OPS, PD>(p, rpb, gch, lds, st);
+  launch_one<KS, TM, 2, 0, OPS, PD, TP>(p, rpb, gch, lds, st);
 }
 
 // the operand-stream combinations the dgrad epilogues produce (models/fused.py): the BN path (ReLU from
@@ -498,30 +538,40 @@ constexpr int EP2_OPS[] = {
     OP_MASK | OP_Y0 | OP_Y1 | OP_RES | OP_OLD};
 constexpr int N_EP2_OPS = sizeof(EP2_OPS) / sizeof(EP2_OPS[0]);
 
-template <int KS, int I = 0>
+template <int KS, bool TP, int I = 0>
 bool launch_ep2_ops(const ConvParams& p, int ops, int rpb, int gch, size_t lds, hipStream_t st) {
   if constexpr (I < N_EP2_OPS) {
     if (ops == EP2_OPS[I]) {
-      launch_ep2<KS, EP2_OPS[I]>(p, rpb, gch, lds, st);
+      launch_ep2<KS, EP2_OPS[I], TP>(p, rpb, gch, lds, st);
       return true;
     }
-    return launch_ep2_ops<KS, I + 1>(p, ops, rpb, gch, lds, st);
+    return launch_ep2_ops<KS, TP, I + 1>(p, ops, rpb, gch, lds, st);
   } else {
     return false;
   }
 }
 
-// forward epilogues: 64-row tiles (32 at K > 128), 3-deep ring; false: no instantiation for `ops`
-template <int KS>
-bool launch_ks(const ConvParams& p, int ep, int ops, int rpb, int gch, size_t lds, hipStream_t st) {
+// forward epilogues: 64-row tiles (32 at K > 128), 3-deep ring; false: no instantiation for `ops`.  TP: the
+// temporal-tap loader (no residual-output epilogue: that one belongs to the 1x1 conv_c)
+template <int KS, bool TP>
+bool launch_ks_tp(const ConvParams& p, int ep, int ops, int rpb, int gch, size_t lds, hipStream_t st) {
   constexpr int TMF = KS <= 4 ? 4 : 2;
-  if (ep == 1) { launch_aff<KS, TMF, 1, OP_RES, 3>(p, rpb, gch, lds, st); return true; }
+  if (ep == 1) {
+    if constexpr (TP) return false;
+    else { launch_aff<KS, TMF, 1, OP_RES, 3, false>(p, rpb, gch, lds, st); return true; }
+  }
   if (ep == 0) {
-    if (ops & OP_OLD) launch_aff<KS, TMF, 0, OP_OLD, 3>(p, rpb, gch, lds, st);
-    else launch_aff<KS, TMF, 0, 0, 3>(p, rpb, gch, lds, st);
+    if (ops & OP_OLD) launch_aff<KS, TMF, 0, OP_OLD, 3, TP>(p, rpb, gch, lds, st);
+    else launch_aff<KS, TMF, 0, 0, 3, TP>(p, rpb, gch, lds, st);
     return true;
   }
-  return launch_ep2_ops<KS>(p, ops, rpb, gch, lds, st);
+  return launch_ep2_ops<KS, TP>(p, ops, rpb, gch, lds, st);
+}
+
+template <int KS>
+bool launch_ks(const ConvParams& p, int ep, int ops, int rpb, int gch, size_t lds, hipStream_t st) {
+  return p.nt > 1 ? launch_ks_tp<KS, true>(p, ep, ops, rpb, gch, lds, st)
+                  : launch_ks_tp<KS, false>(p, ep, ops, rpb, gch, lds, st);
 }
 
 }  // namespace

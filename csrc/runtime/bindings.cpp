@@ -103,6 +103,7 @@ static void check_pw(const ConvParams& p, int64_t chunk, int64_t cfg) {
   }
   if (cfg < 0 || !(cfg & 16) || !(cfg & 512)) return;
   TORCH_CHECK(pva_bf16::conv_pw_legal(p, (int)chunk), "pointwise conv kernel selected for an unsupported geometry");
+  TORCH_CHECK(p.nt == 1 || p.xbytes < 0x80000000u, "temporal pointwise conv: input must stay under 2 GiB");
   TORCH_CHECK(!p.eres || p.ldr % 8 == 0, "pointwise conv kernel: residual row stride must be a multiple of 8");
   TORCH_CHECK(!p.emask || p.Ngemm % 8 == 0, "pointwise conv kernel: mask layout");
 }

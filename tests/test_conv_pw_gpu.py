@@ -187,3 +187,105 @@ def test_pw_legality():
     assert not C.conv_pw_legal(list(fwd_geometry(n16, 1, 2, 8, 8, 64, 16)), 8)
     ok = ConvSpec(64, 256, (1, 1, 1))
     assert C.conv_pw_legal(list(fwd_geometry(ok, 1, 2, 8, 8, 64, 256)), 8)
+
+
+def _rows(t):   # [N, C, T, H, W] -> rows [N*T*H*W, C]
+    return t.permute(0, 2, 3, 4, 1).reshape(-1, t.shape[1])
+
+
+# temporal (kt,1,1) unit-stride convs on the pointwise kernel's temporal-tap loader: (N, T, H, W), Cin, Cout, kt
+TEMPORAL = [((2, 4, 6, 7), 32, 32, 3), ((1, 8, 7, 7), 64, 64, 3), ((2, 3, 8, 8), 16, 32, 5), ((1, 5, 6, 6), 8, 96, 3),
+            ((1, 4, 7, 9), 64, 128, 3)]
+
+
+@pytest.mark.parametrize("case", TEMPORAL)
+@pytest.mark.parametrize("aff", [0, 2])
+def test_pw_temporal_forward(case, aff):
+    """(kt,1,1) conv with temporal zero padding (taps leaving the clip read zero, also under the input BN-ReLU),
+    accumulate + bias, forward BN partial sums, against PyTorch conv3d in float64."""
+    C = _C()
+    (N, T, H, W), ci, co, kt = case
+    M = N * T * H * W
+    g = torch.Generator().manual_seed(ci + co + kt + aff)
+    spec = ConvSpec(ci, co, (kt, 1, 1), (1, 1, 1), (kt // 2, 0, 0))
+    w = torch.randn(co, ci, kt, 1, 1, generator=g) * (2.0 / (ci * kt)) ** 0.5
+    wf, _ = pack_weight(w.to(DEV), spec)
+    x = torch.randn(M, ci, generator=g).to(torch.bfloat16).to(DEV)
+    sc = (torch.rand(ci, generator=g) + 0.5).to(DEV)
+    sh = (torch.randn(ci, generator=g) * 0.3).to(DEV)
+    bias = (torch.randn(co, generator=g) * 0.2).to(DEV)
+    xin = x.double() if not aff else torch.relu(x.float() * sc + sh).to(torch.bfloat16).double()
+    xin = xin.view(N, T, H, W, ci).permute(0, 4, 1, 2, 3)
+    ref0 = _rows(torch.nn.functional.conv3d(xin, w.to(torch.bfloat16).double().to(DEV), None, 1, (kt // 2, 0, 0)))
+    geo = fwd_geometry(spec, N, T, H, W, ci, co)
+    assert C.conv_pw_legal(list(geo), 8)
+    for cfg in _cfgs():
+        for accum, use_bias in ((0, False), (1, True)):
+            y = torch.randn(M, co, generator=g).to(torch.bfloat16).to(DEV)
+            old = y.clone()
+            rows = C.conv_cfg_bm(cfg, co)
+            stats = torch.full(((M + rows - 1) // rows, 2, co), float("nan"), device=DEV)
+            C.conv_igemm(x, wf, y, stats, sc if aff else None, sh if aff else None, aff, accum, list(geo), 8, cfg,
+                         bias if use_bias else None)
+            torch.cuda.synchronize()
+            ref = ref0 + (bias.double() if use_bias else 0) + (old.double() if accum else 0)
+            assert _rel(y, ref) < 8e-3, (cfg, accum)
+            q = y.double()
+            s = stats.double().sum(0)
+            assert _rel(s[0], q.sum(0)) < 1e-4 and _rel(s[1], (q * q).sum(0)) < 1e-4, cfg
+
+
+@pytest.mark.parametrize("case", TEMPORAL)
+@pytest.mark.parametrize("mode", ["res_mask_dual_accum", "plain"])
+def test_pw_temporal_dgrad(case, mode):
+    """dgrad of a (kt,1,1) stride-1 conv (taps gathered backwards) with the backward-BN epilogue, against
+    torch.nn.grad.conv3d_input in float64."""
+    C = _C()
+    (N, T, H, W), ci, co, kt = case
+    if ci % 32 or kt * co > 256:
+        pytest.skip("not a pointwise-kernel dgrad geometry (N % 32 / K > 256)")
+    M = N * T * H * W
+    g = torch.Generator().manual_seed(3 * ci + co + kt + len(mode))
+    spec = ConvSpec(ci, co, (kt, 1, 1), (1, 1, 1), (kt // 2, 0, 0))
+    w = torch.randn(co, ci, kt, 1, 1, generator=g) * (2.0 / (ci * kt)) ** 0.5
+    _, wd = pack_weight(w.to(DEV), spec)
+    dy = torch.randn(M, co, generator=g).to(torch.bfloat16).to(DEV)
+    bf = lambda *s: torch.randn(*s, generator=g).to(torch.bfloat16).to(DEV)
+    res, old, y0, y1 = bf(M, ci), bf(M, ci), bf(M, ci) * 2 + 0.5, bf(M, ci)
+    mask = torch.rand(M, ci, generator=g).to(DEV) > 0.4
+    mean0, rstd0 = (torch.randn(ci, generator=g) * 0.3).to(DEV), (torch.rand(ci, generator=g) + 0.5).to(DEV)
+    mean1, rstd1 = (torch.randn(ci, generator=g) * 0.3).to(DEV), (torch.rand(ci, generator=g) + 0.5).to(DEV)
+    geo = dgrad_phases(spec, N, (T, H, W), (T, H, W), co, ci)
+    assert len(geo) == 1 and C.conv_pw_legal(list(geo[0]), 8)
+    dyn = dy.double().view(N, T, H, W, co).permute(0, 4, 1, 2, 3)
+    dx = _rows(torch.nn.grad.conv3d_input((N, ci, T, H, W), w.to(torch.bfloat16).double().to(DEV), dyn, 1,
+                                          (kt // 2, 0, 0)))
+    for cfg in _cfgs():
+        rows = C.conv_cfg_bm(cfg, ci)
+        part = torch.full(((M + rows - 1) // rows, 3, ci), float("nan"), device=DEV)
+        out = old.clone()
+        if mode == "res_mask_dual_accum":
+            C.conv_igemm_epi(dy, wd, out, 1, list(geo[0]), 8, res, ci, _bits(mask), y0, mean0, rstd0, y1, mean1,
+                             rstd1, part, None, None, cfg)
+            v = (dx + old.double() + res.double()) * mask
+        else:
+            C.conv_igemm_epi(dy, wd, out, 0, list(geo[0]), 8, None, 0, None, None, None, None, None, None, None,
+                             part, None, None, cfg)
+            v = dx
+        torch.cuda.synchronize()
+        assert _rel(out, v) < 1e-2, (cfg, mode)
+        assert _rel(part.double().sum(0)[0], out.double().sum(0)) < 1e-4, cfg
+
+
+def test_pw_temporal_legality():
+    C = _C()
+    t3 = ConvSpec(32, 32, (3, 1, 1), (1, 1, 1), (1, 0, 0))
+    assert C.conv_pw_legal(list(fwd_geometry(t3, 2, 4, 6, 7, 32, 32)), 8)
+    assert C.conv_pw_legal(list(dgrad_phases(t3, 2, (4, 6, 7), (4, 6, 7), 32, 32)[0]), 8)
+    assert not C.conv_pw_legal(list(fwd_geometry(t3, 2, 4, 5, 5, 32, 32)), 8)       # slices < 32 pixels
+    deep = ConvSpec(128, 32, (3, 1, 1), (1, 1, 1), (1, 0, 0))                       # K = 384
+    assert not C.conv_pw_legal(list(fwd_geometry(deep, 1, 4, 8, 8, 128, 32)), 8)
+    st2 = ConvSpec(32, 32, (3, 1, 1), (2, 1, 1), (1, 0, 0))                         # temporal stride
+    assert not C.conv_pw_legal(list(fwd_geometry(st2, 1, 4, 8, 8, 32, 32)), 8)
+    sp = ConvSpec(32, 32, (1, 3, 3), (1, 1, 1), (0, 1, 1))                          # spatial taps
+    assert not C.conv_pw_legal(list(fwd_geometry(sp, 1, 4, 8, 8, 32, 32)), 8)
