@@ -41,7 +41,7 @@ t_ab() {
 t_sweep() {
   for b in $SWEEP; do
     timeout -k 10 500 python bench.py --batch $b --steps ${STEPS:-8} --warmup 2 $BENCH_ARGS > $out/sweep_b$b.json 2> $out/sweep_b$b.err || { tail -3 $out/sweep_b$b.err; break; }
-    echo "B=$b $(cat $out/sweep_b$b.json)"
+    echo "B=$b $(python3 -c "import json; d=json.load(open('$out/sweep_b$b.json')); print(d['value'], 'clips/s', d['ms_per_step'], 'ms', d['config'].get('peak_mem_gb'), 'GB')")"
   done
 }
 t_layers() {
@@ -63,7 +63,8 @@ t_pmc() {
     i=$((i+1))
     timeout -k 10 420 rocprofv3 --pmc $P --kernel-trace --output-format csv -d $out/pmc/p$i -o p -- python3 bench.py --steps 2 --warmup 1 --batch $B > $out/pmc_p$i.log 2>&1 || fail $out/pmc_p$i.log 5
   done
-  python3 scripts/pmc_step_summary.py $out/pmc > $out/pmc_summary_b$B.txt && head -30 $out/pmc_summary_b$B.txt
+  # raw per-dispatch CSVs are large (gpurun copies back at most 64 MiB): keep the summary only
+  python3 scripts/pmc_step_summary.py $out/pmc > $out/pmc_summary_b$B.txt && rm -rf $out/pmc && head -30 $out/pmc_summary_b$B.txt
 }
 t_runpy() {
   timeout -k 10 600 python -u run.py --synthetic --is_slowfast --num_frames 32 --sampling_rate 2 --crop_size 224 \
