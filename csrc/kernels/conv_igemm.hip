@@ -42,8 +42,10 @@ __host__ __device__ constexpr int main_lds_bytes(int BM, int BN, int BK, int EPI
 
 __host__ __device__ constexpr int dma_stages(int BM, int BN, int BK, bool dma) {
   // the 256x256 tile runs one workgroup per CU anyway: at BK = 32 a 4-buffer ring (128 KB, two tiles in flight
-  // across each barrier) fits beside its epilogue/statistics area
-  return (dma && BM * BN > 128 * 128 && 4 * (BM + BN) * BK * 2 <= 128 * 1024) ? 4
+  // across each barrier) fits beside its epilogue/statistics area.  The 4-wave 256x128 tile keeps two
+  // workgroups per CU (<= 80 KB each: a 3-buffer ring at BK = 32)
+  return (dma && BM * BN == 256 * 128) ? (3 * (BM + BN) * BK * 2 <= 80 * 1024 ? 3 : 2)
+         : (dma && BM * BN > 128 * 128 && 4 * (BM + BN) * BK * 2 <= 128 * 1024) ? 4
          : (dma && 3 * (BM + BN) * BK * 2 <= 96 * 1024) ? 3 : 2;
 }
 
@@ -112,7 +114,8 @@ __device__ __forceinline__ void mma_ktile(const char* A, const int (&fa)[BK / 32
 }
 
 template <int BM, int BN, int WM, int WN, int CH, int BK, int EPI, int UT>
-__global__ __launch_bounds__((BM / WM) * (BN / WN) * 64)
+// the 4-wave 256x128 tile runs two workgroups per CU: at most 256 VGPRs (two waves per SIMD)
+__global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, (BM * BN == 256 * 128) ? 2 : 1)
 void conv_igemm_kernel(const ConvParams p) {
   constexpr int NWN = BN / WN;
   constexpr int NT = (BM / WM) * NWN * 64;
@@ -999,6 +1002,9 @@ void launch_variant(int v, const ConvParams& p, int ut_force, hipStream_t stream
     case 4:
       if constexpr (CH == 8) launch_cfg<256, 256, 128, 64, CH, BK>(p, ut_force, stream, dma);
       break;
+    case 5:   // 256x128 of 4 waves (128x64 each, as the 256x256 tile's): two independent workgroups per CU
+      if constexpr (CH == 8) launch_cfg<256, 128, 128, 64, CH, BK>(p, ut_force, stream, dma);
+      break;
     default: launch_cfg<256, 16, 64, 16, CH, BK>(p, ut_force, stream, dma); break;
   }
 }
@@ -1016,7 +1022,7 @@ static int pick_variant(int M, int N) {
 // uniform-tap loader (bit 3), bit 4 set = explicit (else the built-in heuristic), bit 5 = the narrow
 // direct-to-register kernel of conv_direct.hip (bit 6: 2048 rows per workgroup, else 512), bit 7 = LDS-DMA
 // staging of the uniform-tap loader (launches without an input affine), bit 8 = 256x256 tile of 8 waves
-// (overrides bits 0-1; forward / plain dgrad only).  -1 = heuristic.
+// (bit 0 with it: the 256x128 tile of 4 waves instead; overrides the tile bits).  -1 = heuristic.
 int conv_direct_rows(int cfg);
 void conv_direct_launch(const ConvParams& p, int cfg, hipStream_t s);
 // bit 9 = the streaming pointwise kernel of conv_pw.hip (dense 1x1x1 GEMMs; bits 0-1: 1024 << v rows per
@@ -1070,7 +1076,7 @@ void conv_igemm_launch(const ConvParams& p, int chunk, hipStream_t stream, int c
     return;
   }
   if (cfg >= 0 && (cfg & 16)) {
-    v = (cfg & 256) ? 4 : (cfg & 3);
+    v = (cfg & 256) ? 4 + (cfg & 1) : (cfg & 3);
     bk = (cfg & 4) ? 64 : 32;
     ut_force = (cfg >> 3) & 1;
     dma = (cfg & 128) != 0;   // LDS-DMA staging (uniform-tap loader, no input affine)

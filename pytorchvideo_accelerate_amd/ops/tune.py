@@ -36,7 +36,8 @@ DIRECT = 32           # narrow direct-to-register kernel (csrc/kernels/conv_dire
 DIRECT_2K = 64        #   with 2048 rows per workgroup (else 512)
 DMA = 128             # uniform-tap loader staged by LDS-DMA (buffer_load ... lds); launches without input affine
 DIRECT_HALF = 1024    #   (with DIRECT) half the row groups in flight per wave: fewer VGPRs, more waves per SIMD
-BIG = 256             # 256x256 tile of 8 waves (N >= 256; the backward-BN epilogue in 64-row slices)
+BIG = 256             # 256x256 tile of 8 waves (N >= 256; the backward-BN epilogue in 64-row slices);
+BIG_HALF = 1          #   with bit 0: the 256x128 tile of 4 waves (N >= 128; two independent workgroups per CU)
 PW = 512              # streaming pointwise kernel (csrc/kernels/conv_pw.hip): dense 1x1x1 GEMMs, K <= 256,
 PW_ROWS = (1024, 2048, 4096)   # N % 32 == 0, weights in LDS; bits 0-1 select the rows per workgroup,
 PW_SOLO = 4                     # bit 2 one workgroup per CU
@@ -61,7 +62,8 @@ def describe(cfg: int) -> str:
     if cfg & DIRECT:
         return "direct%d%s" % (2048 if cfg & DIRECT_2K else 512, "/rt2" if cfg & DIRECT_HALF else "")
     if cfg & BIG:
-        return "256x256/bk%d%s%s" % (64 if cfg & BK64 else 32, "/ut" if cfg & UT else "", "/dma" if cfg & DMA else "")
+        return "256x%d/bk%d%s%s" % (128 if cfg & BIG_HALF else 256, 64 if cfg & BK64 else 32, "/ut" if cfg & UT else "",
+                                    "/dma" if cfg & DMA else "")
     return "%dx%d/bk%d%s%s" % (TILE_BM[cfg & 3], TILE_BN[cfg & 3], 64 if cfg & BK64 else 32, "/ut" if cfg & UT else "",
                                "/dma" if cfg & DMA else "")
 
@@ -78,6 +80,7 @@ class ConvTuner:
         self.dma = os.environ.get("PVA_CONV_DMA", "1") != "0"
         self.pw = os.environ.get("PVA_CONV_PW", "1") != "0"
         self.halo = os.environ.get("PVA_CONV_HALO", "1") != "0"
+        self.big_half = os.environ.get("PVA_CONV_BIG_HALF", "0") != "0"
         # debugging aid: PVA_PW_KINDS=f,fres,er,... restricts the pointwise kernel to launches whose key
         # starts with one of these kinds (models/fused.py: f fres fw2 eb er d)
         kinds = os.environ.get("PVA_PW_KINDS")
@@ -115,13 +118,15 @@ class ConvTuner:
                     out.append(cfg_word(v, bk, ut))
                     if ut and aff == 0 and self.dma:
                         out.append(cfg_word(v, bk, ut) | DMA)
-        if N >= 256 and chunk == 8:   # 256x256 tile (UT loader only: the generic one is VALU-bound)
-            for bk in (32, 64):
-                if self.C.conv_ut_legal(list(g), chunk, bk):
-                    w = EXPLICIT | BIG | UT | (BK64 if bk == 64 else 0)
-                    out.append(w)
-                    if aff == 0 and self.dma:
-                        out.append(w | DMA)
+        if N >= 128 and chunk == 8:   # 256x256 / 256x128 tiles (UT loader only: the generic one is VALU-bound)
+            halves = (0, BIG_HALF) if self.big_half else (0,)
+            for half in (h for h in halves if N >= (128 if h else 256)):
+                for bk in (32, 64):
+                    if self.C.conv_ut_legal(list(g), chunk, bk):
+                        w = EXPLICIT | BIG | half | UT | (BK64 if bk == 64 else 0)
+                        out.append(w)
+                        if aff == 0 and self.dma:
+                            out.append(w | DMA)
         if direct and self.direct and self.C.conv_direct_legal(list(g), chunk):
             out += [EXPLICIT | DIRECT | r | h for r in (0, DIRECT_2K) for h in (0, DIRECT_HALF)]
         if halo and self.halo and (aff == 0 or not epi):
