@@ -80,7 +80,7 @@ class ConvTuner:
         self.dma = os.environ.get("PVA_CONV_DMA", "1") != "0"
         self.pw = os.environ.get("PVA_CONV_PW", "1") != "0"
         self.halo = os.environ.get("PVA_CONV_HALO", "1") != "0"
-        self.big_half = os.environ.get("PVA_CONV_BIG_HALF", "0") != "0"
+        self.big_half = os.environ.get("PVA_CONV_BIG_HALF", "1") != "0"
         # debugging aid: PVA_PW_KINDS=f,fres,er,... restricts the pointwise kernel to launches whose key
         # starts with one of these kinds (models/fused.py: f fres fw2 eb er d)
         kinds = os.environ.get("PVA_PW_KINDS")
