@@ -20,7 +20,6 @@
 //   * Linear workgroup ids go through the bijective XCD remap so the n-tiles of one m-tile share an L2.
 #include "common.h"
 #include "conv_params.h"
-#include <cstdlib>
 #include <type_traits>
 
 PVA_NS_BEGIN
@@ -201,7 +200,6 @@ void conv_igemm_kernel(const ConvParams p) {
     constexpr bool check = (UT >> 1) & 1;
     constexpr int uaff = (UT >> 2) & 3;
     constexpr bool glds_ut = (UT >> 4) & 1;
-    constexpr bool late = (UT >> 5) & 1;   // BK=64 two-buffer loop: second-half fragments read at the loop top
     static_assert(!glds_ut || uaff == 0, "LDS-DMA staging cannot transform the A operand");
     const int GHW = p.Gh * p.Gw, GTHW = p.Gt * GHW;
     // most negative tap offset (dgrad walks taps backwards): the no-check form adds taps as a >= 0 soffset
@@ -369,54 +367,7 @@ void conv_igemm_kernel(const ConvParams p) {
       store_lds(0);
       if (nsteps > 1) load();
     }
-    if constexpr (glds_ut && NSTAGE == 2 && BK == 64 && late) {
-      // as below, but the second-half fragments of tile step are read at the top of iteration step (issued ahead
-      // of the first-half MFMAs, which only need the first-half fragments read one barrier earlier) instead of at
-      // the bottom of iteration step-1: the loop-top lgkmcnt no longer waits on reads issued just before it
-      ev8_t fa0[TM], fb0[TN], fa1[TM], fb1[TN];
-      vm_wait<0>();
-      __syncthreads();   // tile 0 landed
-      if (nsteps > 1) issue_dma(1);
-#pragma unroll
-      for (int i = 0; i < TM; ++i) fa0[i] = *reinterpret_cast<const ev8_t*>(smem + fa[0][i]);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) fb0[j] = *reinterpret_cast<const ev8_t*>(smem + fb[0][j]);
-      for (int step = 0; step < nsteps; ++step) {
-        const int cur = step & 1;
-        const char* Ac = smem + cur * TILE_BYTES;
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int i = 0; i < TM; ++i) fa1[i] = *reinterpret_cast<const ev8_t*>(Ac + fa[1][i]);
-#pragma unroll
-        for (int j = 0; j < TN; ++j) fb1[j] = *reinterpret_cast<const ev8_t*>(Ac + fb[1][j]);
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = PVA_MFMA16(fb0[j], fa0[i], acc[i][j], 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
-        vm_wait<0>();   // this wave's DMA of tile step+1
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's reads of tile step
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        const bool more = step + 1 < nsteps;
-        if (step + 2 < nsteps) issue_dma(cur);
-        if (more) {
-          const char* An = smem + (cur ^ 1) * TILE_BYTES;
-#pragma unroll
-          for (int i = 0; i < TM; ++i) fa0[i] = *reinterpret_cast<const ev8_t*>(An + fa[0][i]);
-#pragma unroll
-          for (int j = 0; j < TN; ++j) fb0[j] = *reinterpret_cast<const ev8_t*>(An + fb[0][j]);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = PVA_MFMA16(fb1[j], fa1[i], acc[i][j], 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    } else if constexpr (glds_ut && NSTAGE == 2 && BK == 64) {
+    if constexpr (glds_ut && NSTAGE == 2 && BK == 64) {
       // 2 buffers x 2 MFMA k-steps, software-pipelined across the barrier: the barrier sits between the two
       // k-steps of a tile, where (a) this tile's second-half fragments are already in registers, so every read
       // of the tile is done and its buffer can take the DMA of tile step+2, and (b) tile step+1 has landed, so
@@ -943,16 +894,6 @@ void conv_igemm_kernel(const ConvParams p) {
 // uniform-tap loader use: 0 never, 1 where it measured faster (default), 2 whenever legal
 static int g_ut_mode = 1;
 
-// big-tile BK=64 LDS-DMA loop with the second-half fragments read at the loop top (UT word bit 5);
-// PVA_CONV_LATE=0 restores the bottom-of-loop reads
-static bool late_frags() {
-  static const int v = [] {
-    const char* e = std::getenv("PVA_CONV_LATE");
-    return e ? std::atoi(e) : 0;
-  }();
-  return v != 0;
-}
-
 inline bool conv_ut_legal(const ConvParams& p, int ch, int bk) {
   return ch == 8 && p.Cg % bk == 0 && p.nt * p.nh * p.nw <= 32;
 }
@@ -982,13 +923,6 @@ void launch_cfg(const ConvParams& p, int ut_force, hipStream_t stream, bool dma 
       // lean epilogue (EPI 2): residual / ReLU bits / sum v only
       const bool lean = !p.accum && !p.ey0 && !p.ey1 && !p.emsc && !p.ebias;
       if (lean && ut) {
-        if constexpr (BK == 64) {
-          if (dma && late_frags()) {
-            if (p.check) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 2, 51>), grid, block, lds, stream, p);
-            else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 2, 49>), grid, block, lds, stream, p);
-            return;
-          }
-        }
         if (dma) {
           if (p.check) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 2, 19>), grid, block, lds, stream, p);
           else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 2, 17>), grid, block, lds, stream, p);
@@ -997,13 +931,6 @@ void launch_cfg(const ConvParams& p, int ut_force, hipStream_t stream, bool dma 
           else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 2, 1>), grid, block, lds, stream, p);
         }
         return;
-      }
-      if constexpr (BK == 64) {
-        if (ut && dma && late_frags()) {
-          if (p.check) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 1, 51>), grid, block, lds, stream, p);
-          else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 1, 49>), grid, block, lds, stream, p);
-          return;
-        }
       }
       if (ut && dma) {
         if (p.check) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 1, 19>), grid, block, lds, stream, p);
@@ -1016,13 +943,6 @@ void launch_cfg(const ConvParams& p, int ut_force, hipStream_t stream, bool dma 
         hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 1, 0>), grid, block, lds, stream, p);
       }
       return;
-    }
-    if constexpr (BK == 64) {
-      if (ut && dma && !p.affine && late_frags()) {
-        if (p.check) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 0, 51>), grid, block, lds, stream, p);
-        else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 0, 49>), grid, block, lds, stream, p);
-        return;
-      }
     }
     if (ut && dma && !p.affine) {
       if (p.check) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 0, 19>), grid, block, lds, stream, p);
