@@ -28,7 +28,7 @@ t_tests() {
 }
 t_bench() { PVA_TUNE_LOG=1 timeout -k 10 400 python bench.py $BENCH_ARGS > $out/bench.json 2> $out/bench.err || fail $out/bench.err; cat $out/bench.json; }
 t_host() { timeout -k 10 400 python bench.py --source host $BENCH_ARGS > $out/bench_host.json 2> $out/bench_host.err || fail $out/bench_host.err; cat $out/bench_host.json; }
-t_fp16() { timeout -k 10 400 python bench.py --precision fp16 $BENCH_ARGS > $out/bench_fp16.json 2> $out/bench_fp16.err || fail $out/bench_fp16.err; cat $out/bench_fp16.json; }
+t_fp16() { PVA_TUNE_LOG=1 timeout -k 10 400 python bench.py --precision fp16 $BENCH_ARGS > $out/bench_fp16.json 2> $out/bench_fp16.err || fail $out/bench_fp16.err; cat $out/bench_fp16.json; }
 t_ab() {
   local i=0
   IFS=';' read -ra arms <<< "$AB"
