@@ -235,15 +235,18 @@ def test_pw_temporal_forward(case, aff):
             assert _rel(s[0], q.sum(0)) < 1e-4 and _rel(s[1], (q * q).sum(0)) < 1e-4, cfg
 
 
-@pytest.mark.parametrize("case", TEMPORAL)
+# dgrad geometries the kernel takes: N = Cin % 32 == 0, K = kt x Cout <= 256
+TEMPORAL_DGRAD = [((2, 4, 6, 7), 32, 32, 3), ((1, 8, 7, 7), 64, 64, 3), ((2, 4, 8, 8), 64, 32, 5),
+                  ((1, 6, 6, 6), 128, 64, 3)]
+
+
+@pytest.mark.parametrize("case", TEMPORAL_DGRAD)
 @pytest.mark.parametrize("mode", ["res_mask_dual_accum", "plain"])
 def test_pw_temporal_dgrad(case, mode):
     """dgrad of a (kt,1,1) stride-1 conv (taps gathered backwards) with the backward-BN epilogue, against
     torch.nn.grad.conv3d_input in float64."""
     C = _C()
     (N, T, H, W), ci, co, kt = case
-    if ci % 32 or kt * co > 256:
-        pytest.skip("not a pointwise-kernel dgrad geometry (N % 32 / K > 256)")
     M = N * T * H * W
     g = torch.Generator().manual_seed(3 * ci + co + kt + len(mode))
     spec = ConvSpec(ci, co, (kt, 1, 1), (1, 1, 1), (kt // 2, 0, 0))
