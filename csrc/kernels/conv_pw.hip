@@ -42,9 +42,7 @@ int conv_pw_legal(const ConvParams& p, int chunk) {
   } else {
     if (p.bt0 != 0 || p.bts != 1 || (p.dir != 1 && p.dir != -1) || p.Rh * p.Rw < 32 || p.Rt < 2) return 0;
   }
-  // N: whole 32-channel chunks, or one partial chunk of 8 / 16 channels (the fast pathway's narrow conv_a)
-  if (p.Kfull != p.nt * p.Cg || p.Cg % 8 != 0 || p.Kfull > 256) return 0;
-  if (p.Ngemm % 32 != 0 && p.Ngemm != 8 && p.Ngemm != 16) return 0;
+  if (p.Kfull != p.nt * p.Cg || p.Cg % 8 != 0 || p.Kfull > 256 || p.Ngemm % 32 != 0) return 0;
   if (p.ldx % 8 != 0 || p.ldy % 8 != 0) return 0;
   return 1;
 }
@@ -52,7 +50,7 @@ int conv_pw_legal(const ConvParams& p, int chunk) {
 // 32-channel chunks per output-channel group: the largest group whose weight image, statistics and epilogue
 // constants fit the LDS budget, then balanced over the groups (equal work per workgroup)
 static int pw_group_chunks(int N, int ks, int nslot, int aff_bytes) {
-  const int nch = (N + 31) / 32;
+  const int nch = N / 32;
   const int per_chunk = 2 * ks * 1024 + (nslot + 4) * 32 * 4;
   int gmax = std::max(1, (PW_LDS - aff_bytes) / per_chunk);
   if (gmax >= 2) gmax &= ~1;   // even groups: chunk pairs stay aligned to 128-B lines

@@ -111,12 +111,11 @@ __global__ __launch_bounds__(PW_THREADS) void conv_pw_kernel(const ConvParams p,
   // output-channel group of this workgroup (weights of wide convs do not fit LDS at once: the row range
   // is walked once per group of gch 32-channel chunks; the XCD remap puts the groups of one row range on
   // the same XCD, so its activations are re-read from that L2)
-  const int nchunks = (N + 31) >> 5;   // N = 8 / 16: one partial chunk (channels >= N: zero weights, no stores)
-  const int ngrp = (nchunks + gch - 1) / gch;
+  const int ngrp = ((N >> 5) + gch - 1) / gch;
   const int L = xcd_remap(blockIdx.x, gridDim.x);
   const int grp = L % ngrp, rblk = L / ngrp;
   const int cbase = grp * gch;                              // first chunk of the group
-  const int nch = min(gch, nchunks - cbase);                // chunks in this group
+  const int nch = min(gch, (N >> 5) - cbase);               // chunks in this group
   const int NG = nch * 32, nb0 = cbase * 32;                // group channels, first channel
   const int wimg = nch * 2 * KS * 1024;
   float* st_lds = reinterpret_cast<float*>(smem + wimg);   // [PW_WAVES][NST][NG] per-wave statistics
@@ -139,7 +138,7 @@ __global__ __launch_bounds__(PW_THREADS) void conv_pw_kernel(const ConvParams p,
     const int n = nb0 + 32 * c + 8 * (r >> 2) + 4 * h + (r & 3);
     const int k0 = 32 * s + 8 * (l >> 4);
     uint4 v = uint4{0, 0, 0, 0};
-    if (k0 < K && n < N) v = *reinterpret_cast<const uint4*>(p.w + (int64_t)n * p.Kfull + k0);
+    if (k0 < K) v = *reinterpret_cast<const uint4*>(p.w + (int64_t)n * p.Kfull + k0);
     *reinterpret_cast<uint4*>(smem + (int64_t)u * 16) = v;
   }
   const bool do_stats = (EP == 0 && p.stats != nullptr) || (EP == 2 && p.epart != nullptr);
@@ -150,10 +149,6 @@ __global__ __launch_bounds__(PW_THREADS) void conv_pw_kernel(const ConvParams p,
   // EP 1: fsc fsh rsc rsh ; EP 0 / 2: bias (0 when absent), mask-affine scale and shift
   for (int i = tid; i < NG; i += PW_THREADS) {
     const int n = nb0 + i;
-    if (n >= N) {   // the partial chunk of a narrow conv
-      cst[i] = 0.f; cst[NG + i] = 0.f; cst[2 * NG + i] = 0.f; cst[3 * NG + i] = 0.f;
-      continue;
-    }
     if (EP == 1) {
       cst[i] = p.fsc[n]; cst[NG + i] = p.fsh[n];
       cst[2 * NG + i] = p.rsc ? p.rsc[n] : 1.f; cst[3 * NG + i] = p.rsh ? p.rsh[n] : 0.f;
@@ -271,14 +266,13 @@ __global__ __launch_bounds__(PW_THREADS) void conv_pw_kernel(const ConvParams p,
   // row r's offsets (rows relative to row0; this lane's 8 channels 8g.. folded in)
   auto prefetch1 = [&](int m0, int c, Pre<TM>& Q) {
     const int nc = nb0 + 32 * c;   // chunk's first channel (uniform)
-    const bool nlive = nc + 8 * g < N;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const uint32_t r = (uint32_t)(m0 - row0 + 16 * i + rho);
       Q.old[i] = Q.res[i] = Q.y0[i] = Q.y1[i] = uint4{0, 0, 0, 0};
       Q.bits[i] = 0xffu;
       if constexpr (EP != 1 && (OPS & OP_OLD))
-        Q.old[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(yr, nlive ? r * yb + 16 * g + nc * 2 : OOB, 0, 0));
+        Q.old[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(yr, r * yb + 16 * g + nc * 2, 0, 0));
       if constexpr (EP != 0 && (OPS & OP_RES))
         Q.res[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(resr, r * rb + 16 * g, nc * 2, 0));
       if constexpr (EP == 2) {
@@ -344,7 +338,6 @@ __global__ __launch_bounds__(PW_THREADS) void conv_pw_kernel(const ConvParams p,
         if (c >= nch) break;
         const int nl = 32 * c + 8 * g;   // this lane's 8 output channels (group-local)
         const int nc = nb0 + 32 * c;     // chunk's first channel
-        const bool nlive = nb0 + nl < N;   // (narrow convs: lanes past N store nothing)
         // ---- MFMAs: D = W X^T, lane gets channels n..n+3 (half 0) and n+4..n+7 (half 1) of its position
         f32x4_t acc[TM][2];
 #pragma unroll
@@ -387,7 +380,7 @@ __global__ __launch_bounds__(PW_THREADS) void conv_pw_kernel(const ConvParams p,
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] = fmaxf(__builtin_fmaf(v[e], cb[e], c2[e]) + rr[e], 0.f);
             const uint4 pk = pack8_fast(v);
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, pk), yr, nlive ? r * yb + 16 * g + nc * 2 : OOB, 0,
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, pk), yr, r * yb + 16 * g + nc * 2, 0,
                                                    ST_AUX);
             const uint32_t w4[4] = {pk.x, pk.y, pk.z, pk.w};
             unsigned bits = 0;
@@ -396,7 +389,7 @@ __global__ __launch_bounds__(PW_THREADS) void conv_pw_kernel(const ConvParams p,
               bits |= ((w4[e] & 0x7fffu) != 0 && !(w4[e] & 0x8000u)) ? 1u << (2 * e) : 0u;
               bits |= ((w4[e] & 0x7fff0000u) != 0 && !(w4[e] & 0x80000000u)) ? 1u << (2 * e + 1) : 0u;
             }
-            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)bits, mor, nlive ? r * mrow + g + (nc >> 3) : OOB, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)bits, mor, r * mrow + g + (nc >> 3), 0, 0);
           } else if (EP == 0) {
             float o[8];
             unpack8(E.old[i], o);
@@ -406,7 +399,7 @@ __global__ __launch_bounds__(PW_THREADS) void conv_pw_kernel(const ConvParams p,
 #pragma unroll
               for (int e = 0; e < 8; ++e) v[e] = 0.f;
             const uint4 pk = pack8_fast(v);
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, pk), yr, nlive ? r * yb + 16 * g + nc * 2 : OOB, 0,
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, pk), yr, r * yb + 16 * g + nc * 2, 0,
                                                    ST_AUX);
             if (do_stats) {
               float q[8];
@@ -433,7 +426,7 @@ __global__ __launch_bounds__(PW_THREADS) void conv_pw_kernel(const ConvParams p,
               v[e] = __uint_as_float(__float_as_uint(v[e] + o[e] + rr[e] + cb[e]) & keep);
             }
             const uint4 pk = pack8_fast(v);
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, pk), yr, nlive ? r * yb + 16 * g + nc * 2 : OOB, 0,
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, pk), yr, r * yb + 16 * g + nc * 2, 0,
                                                    ST_AUX);
             if (do_stats) {
               float q[8], y1[8];
@@ -488,7 +481,6 @@ __global__ __launch_bounds__(PW_THREADS) void conv_pw_kernel(const ConvParams p,
       for (int w = 0; w < PW_WAVES; ++w) s0 += st_lds[w * NST * NG + nl];
       v = have ? (v - mean[n] * s0) * rstd[n] : 0.f;
     }
-    if (n >= N) continue;
     if (EP == 2) p.epart[((int64_t)rblk * 3 + k) * N + n] = v;
     else p.stats[((int64_t)rblk * 2 + k) * N + n] = v;
   }
@@ -501,7 +493,7 @@ void launch_one(const ConvParams& p, int rpb, int gch, size_t lds, hipStream_t s
   // measured 1-3 % slower with them.  TM is the tile height at one chunk per iteration: chunk pairs halve
   // it, keeping the registers of a ring stage.  One-chunk groups (N = 32) run the single-chunk variant at
   // KS = 1 (the fast pathway's layers) and the pair variant (half a pair idle) otherwise.
-  const int ngrp = (((p.Ngemm + 31) >> 5) + gch - 1) / gch;
+  const int ngrp = ((p.Ngemm >> 5) + gch - 1) / gch;
   const dim3 grid(((p.M + rpb - 1) / rpb) * ngrp), block(PW_THREADS);
   if constexpr (KS == 1) {
     if (gch < 2) {

@@ -35,8 +35,7 @@ def _bits(mask):
 # (M as (N, T, H, W), Cin, Cout, extra input / output row padding)
 FWD = [((2, 3, 7, 9), 64, 256, 0, 0), ((1, 4, 10, 10), 128, 512, 16, 8), ((3, 1, 11, 13), 8, 32, 8, 0),
        ((2, 2, 9, 9), 80, 256, 0, 16), ((1, 2, 15, 15), 256, 64, 0, 0), ((1, 1, 33, 31), 200, 96, 8, 0),
-       ((2, 4, 8, 8), 32, 128, 0, 0), ((1, 2, 7, 9), 256, 1024, 0, 0), ((1, 3, 5, 7), 64, 2048, 0, 0),
-       ((2, 3, 7, 9), 64, 16, 0, 0), ((1, 4, 10, 10), 32, 8, 8, 8)]   # narrow N: one partial chunk
+       ((2, 4, 8, 8), 32, 128, 0, 0), ((1, 2, 7, 9), 256, 1024, 0, 0), ((1, 3, 5, 7), 64, 2048, 0, 0)]
 
 
 @pytest.mark.parametrize("case", FWD)
@@ -117,8 +116,7 @@ def test_pw_fres(identity, shape):
 
 
 @pytest.mark.parametrize("shape", [((2, 3, 7, 9), 256, 64), ((1, 2, 10, 10), 64, 256), ((2, 2, 9, 7), 512, 128),
-                                   ((1, 1, 13, 13), 32, 24), ((1, 2, 7, 9), 1024, 256), ((2, 3, 7, 9), 16, 64),
-                                   ((1, 2, 10, 10), 8, 32)])
+                                   ((1, 1, 13, 13), 32, 24), ((1, 2, 7, 9), 1024, 256)])
 @pytest.mark.parametrize("mode", ["res_mask_dual_accum", "bnmask_bias", "plain"])
 def test_pw_dgrad_epilogue(shape, mode):
     """dx = dy W for a 1x1 conv Ci -> Co (K = Co, N = Ci) with the backward-BN epilogue."""
@@ -185,10 +183,8 @@ def test_pw_legality():
     assert C.conv_pw_legal(list(fwd_geometry(big, 1, 2, 8, 8, 256, 1024)), 8)
     deep = ConvSpec(512, 256, (1, 1, 1))   # K > 256
     assert not C.conv_pw_legal(list(fwd_geometry(deep, 1, 2, 8, 8, 512, 256)), 8)
-    n24 = ConvSpec(64, 24, (1, 1, 1))      # N % 32 != 0 and not one 8 / 16-channel partial chunk
-    assert not C.conv_pw_legal(list(fwd_geometry(n24, 1, 2, 8, 8, 64, 24)), 8)
-    for n in (8, 16):                      # narrow: one partial chunk
-        assert C.conv_pw_legal(list(fwd_geometry(ConvSpec(64, n, (1, 1, 1)), 1, 2, 8, 8, 64, n)), 8)
+    n16 = ConvSpec(64, 16, (1, 1, 1))      # N % 32 != 0
+    assert not C.conv_pw_legal(list(fwd_geometry(n16, 1, 2, 8, 8, 64, 16)), 8)
     ok = ConvSpec(64, 256, (1, 1, 1))
     assert C.conv_pw_legal(list(fwd_geometry(ok, 1, 2, 8, 8, 64, 256)), 8)
 
@@ -199,7 +195,7 @@ def _rows(t):   # [N, C, T, H, W] -> rows [N*T*H*W, C]
 
 # temporal (kt,1,1) unit-stride convs on the pointwise kernel's temporal-tap loader: (N, T, H, W), Cin, Cout, kt
 TEMPORAL = [((2, 4, 6, 7), 32, 32, 3), ((1, 8, 7, 7), 64, 64, 3), ((2, 3, 8, 8), 16, 32, 5), ((1, 5, 6, 6), 8, 96, 3),
-            ((1, 4, 7, 9), 64, 128, 3), ((2, 4, 8, 8), 32, 8, 3), ((1, 4, 7, 7), 64, 16, 3)]   # (fast conv_a: N 8 / 16)
+            ((1, 4, 7, 9), 64, 128, 3)]
 
 
 @pytest.mark.parametrize("case", TEMPORAL)
