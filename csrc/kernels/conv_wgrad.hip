@@ -638,29 +638,31 @@ __global__ void wgrad_convert_kernel(float* __restrict__ accbuf, float* __restri
   }
 }
 
-// slab mode: 64 consecutive accumulator entries per block; wave w sums the slabs s = w, w + NW, ... (four running
-// partials, fixed order), the NW wave partials are combined in wave order through LDS.  Fixed order for a given
-// slab count, with 4*NW loads in flight per entry instead of one serial chain of `slabs` dependent adds (a 32x32
-// Gram of 4096 splits was a 16-wave, latency-bound pass).
+// slab mode: 256 consecutive accumulator entries per block (4 per lane, 16-B loads); wave w sums the slabs
+// s = w, w + NW, ... (four running partials, fixed order), the NW wave partials are combined in wave order through
+// LDS.  Fixed order for a given slab count, 4*NW 16-B loads in flight per lane (one float per lane per load ran
+// these at ~0.5 TB/s: the BN-fold G products reduce up to 4096 slabs).
 template <int NW>
 __global__ __launch_bounds__(NW * 64) void wgrad_slab_reduce_kernel(const float* __restrict__ acc,
                                                                     float* __restrict__ grad, int total_a, int taps,
                                                                     int Cin, int Cin_real, float scale, float beta,
                                                                     int slabs, int64_t ss) {
-  __shared__ float red[NW][64];
+  __shared__ f32x4_t red[NW][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int a = blockIdx.x * 64 + lane;
-  float v = 0.f;
+  const int a = (blockIdx.x * 64 + lane) * 4;   // total_a and ss are multiples of 4 (Cin % 8 == 0)
+  f32x4_t v = {0.f, 0.f, 0.f, 0.f};
   if (a < total_a) {
-    float t0 = 0.f, t1 = 0.f, t2 = 0.f, t3 = 0.f;
+    const f32x4_t* base = reinterpret_cast<const f32x4_t*>(acc + a);
+    const int64_t s4 = ss >> 2;
+    f32x4_t t0 = v, t1 = v, t2 = v, t3 = v;
     int s = w;
     for (; s + 3 * NW < slabs; s += 4 * NW) {
-      t0 += acc[(int64_t)s * ss + a];
-      t1 += acc[(int64_t)(s + NW) * ss + a];
-      t2 += acc[(int64_t)(s + 2 * NW) * ss + a];
-      t3 += acc[(int64_t)(s + 3 * NW) * ss + a];
+      t0 += base[(int64_t)s * s4];
+      t1 += base[(int64_t)(s + NW) * s4];
+      t2 += base[(int64_t)(s + 2 * NW) * s4];
+      t3 += base[(int64_t)(s + 3 * NW) * s4];
     }
-    for (; s < slabs; s += NW) t0 += acc[(int64_t)s * ss + a];
+    for (; s < slabs; s += NW) t0 += base[(int64_t)s * s4];
     v = (t0 + t1) + (t2 + t3);
   }
   if constexpr (NW > 1) {
@@ -675,10 +677,13 @@ __global__ __launch_bounds__(NW * 64) void wgrad_slab_reduce_kernel(const float*
   const int n = a / per_n;
   const int rem = a - n * per_n;
   const int tap = rem / Cin;
-  const int c = rem - tap * Cin;
-  if (c >= Cin_real) return;
-  const int o = (n * Cin_real + c) * taps + tap;
-  grad[o] = (beta == 0.f ? 0.f : beta * grad[o]) + scale * v;
+  const int c = rem - tap * Cin;   // 4 consecutive channels of one (n, tap)
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    if (c + e >= Cin_real) break;
+    const int o = (n * Cin_real + c + e) * taps + tap;
+    grad[o] = (beta == 0.f ? 0.f : beta * grad[o]) + scale * v[e];
+  }
 }
 
 }  // namespace
@@ -762,9 +767,9 @@ void conv_wgrad_launch(const WgradParams& p, int chunk, hipStream_t stream) {
 void wgrad_reduce_launch(float* accbuf, float* grad, int splits, int Cout, int taps, int Cin, int Cin_real,
                          float scale, float beta, int slab, hipStream_t stream) {
   // atomic mode: one accumulator, re-zeroed here; slab mode: `splits` slabs fully overwritten by the kernel
-  if (slab && splits > 1) {
+  if (slab && splits > 1 && Cin % 4 == 0) {   // (Cin % 4 != 0: the per-element pass below sums the slabs)
     const int total_a = Cout * taps * Cin;
-    const dim3 grid((total_a + 63) / 64);
+    const dim3 grid((total_a / 4 + 63) / 64);
     const int64_t ss = (int64_t)Cout * taps * Cin;
 #define PVA_SLAB_RED(NW) \
     hipLaunchKernelGGL(wgrad_slab_reduce_kernel<NW>, grid, dim3(NW * 64), 0, stream, accbuf, grad, total_a, taps, Cin, \
