@@ -1040,13 +1040,12 @@ class FusedNet:
         self._ms_ok = (not deterministic and torch.device(device).type == "cuda"
                        and os.environ.get("PVA_STREAMS", "1") != "0")
         # BN folding of the 1x1 conv_c (never materialise its output); units whose conv_c input has at least
-        # fold_min_c channels (default: the slow pathway, where the Gram matrices run at MFMA speed).  Narrow
-        # (fast-pathway) folds take exact statistics from a statistics-only conv pass (Gram-derived variances
-        # E[y^2] - E[y]^2 over fp32-atomic sums were not reproducible there: scripts/diag_ms_fold.py); with that
-        # pass, folding them too measures even with not folding (1034 vs 1030 clips/s, round-2 runner gpu_r2_exact.sh, git 3ce07ef),
-        # so it stays opt-in (PVA_BN_FOLD_MIN_C=8).
+        # fold_min_c channels.  Narrow (fast-pathway) folds take exact statistics from a statistics-only conv pass
+        # (Gram-derived variances E[y^2] - E[y]^2 over fp32-atomic sums were not reproducible there:
+        # scripts/diag_ms_fold.py).  Measured (profiles/r4_fold): min C 32 / 16 / 8 -> 1182.4 / 1192.5 / 1190.6
+        # clips/s once the fold's slab reductions were parallel, so the fast res3+ units fold too (default 16).
         self.bn_fold = os.environ.get("PVA_BN_FOLD", "1") != "0"
-        self.fold_min_c = int(os.environ.get("PVA_BN_FOLD_MIN_C", "32"))
+        self.fold_min_c = int(os.environ.get("PVA_BN_FOLD_MIN_C", "16"))
         self.bn_fold1 = self.bn_fold and os.environ.get("PVA_BN_FOLD1", "1") != '0'
         # folds with fewer input channels than this take exact statistics from a statistics-only conv pass
         self.fold_exact_below = int(os.environ.get("PVA_BN_FOLD_EXACT_BELOW", "32"))
