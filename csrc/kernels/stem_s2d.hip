@@ -491,120 +491,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void s
       }
 }
 
-// Two frame pairs per step (output frames t0..t0+3) for the Cout == 8 temporal stem's weight gradient: the pairs'
-// input windows overlap in KT - 1 frames, so every input fragment read from LDS feeds the MFMA of both pairs where
-// both windows hold it (window frame f is tap f of pair a and tap f - 2 of pair b): 2 (KT + 3) fragment reads per 2
-// (KT + 1) MFMA pairs instead of one read per MFMA (the pair kernel is LDS-read-bound: one 1 KB read per 16-cycle
-// MFMA per wave).  8 waves: wave w owns spatial taps (bh = w & 3, bw = 2 (w >> 2) + 0..1) of every window frame.
-// One workgroup per CU (12 frame slots + 4 dY tiles: 102 KB), two waves per SIMD as with two pair workgroups.
-__device__ __forceinline__ void dma_patch512(__amdgpu_buffer_rsrc_t r, const StemParams& p, int ti, int hs0, int ws0,
-                                             char* slot) {
-  const int tid = threadIdx.x, w = tid >> 6;
-  if (w == 7) return;   // chunks 448.. do not exist (wave-uniform)
-  const int pos = pswz(tid >> 1), half = tid & 1;
-  const int r_ = pos / PW, c_ = pos - r_ * PW;
-  const int hs = hs0 + r_ - 2, ws = ws0 + c_ - 2;
-  const bool ok = pos < PH * PW && ti >= 0 && ti < p.T && (unsigned)hs < (unsigned)p.Hs && (unsigned)ws < (unsigned)p.Ws;
-  const uint32_t vo = ok ? (uint32_t)((((ti * p.Hs + hs) * p.Ws + ws) * 16 + half * 8) * 2) : OOB;
-  dma16(r, slot + w * 64 * 16, vo);
-}
-
-template <int KT>
-__global__ __launch_bounds__(512) void stem_wgrad_quad_kernel(const StemParams p) {
-  constexpr int TAPS = KT * 16;
-  constexpr int J = KT + 1;        // window frames of one pair
-  constexpr int F = J + 2;         // window frames of two pairs
-  constexpr int SLOTS = F + 4;     // + the next step's four new frames
-  constexpr int DYB = TH * TW * 16 * 2;   // dY tile of one pair [128 pos][16]
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* dyt = smem + SLOTS * SLOT_BYTES;  // [2 step parities][2 pairs] dY tiles
-
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int g = lane >> 4, li = lane & 15;
-  const int bh = w & 3, s0 = 2 * (w >> 2);
-  int b = blockIdx.x;
-  const int tw = b % p.tiles_w; b /= p.tiles_w;
-  const int th = b % p.tiles_h;
-  const int n = b / p.tiles_h;
-  const int ho0 = th * TH, wo0 = tw * TW;
-  const __amdgpu_buffer_rsrc_t xr =
-      clip_rsrc(p.x + (int64_t)n * p.T * p.Hs * p.Ws * 16, (uint32_t)(p.T * p.Hs * p.Ws * 32));
-  const __amdgpu_buffer_rsrc_t yr =
-      clip_rsrc(p.dy + (int64_t)n * p.To * p.Ho * p.Wo * 8, (uint32_t)(p.To * p.Ho * p.Wo * 16));
-  // dY chunk of this lane: pair (tid >> 8) of the step, position (tid >> 1) & 127, frame + (tid & 1)
-  const int dpos = pswz((tid >> 1) & 127), dfh = tid & 1, dpair = tid >> 8;
-  const int dho = ho0 + dpos / TW, dwo = wo0 + dpos % TW;
-  const bool dok = dho < p.Ho && dwo < p.Wo;
-  auto dma_dy = [&](int t0, char* buf) {
-    const int to = t0 + 2 * dpair + dfh;
-    const uint32_t vo = dok && to < p.To ? (uint32_t)((((to * p.Ho + dho) * p.Wo + dwo) * 8) * 2) : OOB;
-    dma16(yr, buf + w * 64 * 16, vo);
-  };
-
-  f32x4_t acc[J][2];
-#pragma unroll
-  for (int j = 0; j < J; ++j)
-#pragma unroll
-    for (int s = 0; s < 2; ++s) acc[j][s] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-  for (int f = 0; f < F; ++f) dma_patch512(xr, p, f - p.pt, ho0, wo0, smem + f * SLOT_BYTES);
-  dma_dy(0, dyt);
-  __syncthreads();
-  const int rq = li >> 2, cb = (li & 3) * 8;
-  for (int t0 = 0; t0 < p.To; t0 += 4) {
-    const char* da = dyt + ((t0 >> 2) & 1) * 2 * DYB;
-    const char* db = da + DYB;
-    if (t0 + 4 < p.To) {
-      const int tn = t0 - p.pt + F;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) dma_patch512(xr, p, tn + k, ho0, wo0, smem + ((t0 + F + k) % SLOTS) * SLOT_BYTES);
-      dma_dy(t0 + 4, dyt + (((t0 >> 2) + 1) & 1) * 2 * DYB);
-    }
-    const bool has_b = t0 + 2 < p.To;   // (wave-uniform)
-#pragma unroll
-    for (int kstep = 0; kstep < TH * TW / 32; ++kstep) {
-      const int hh = 2 * kstep + (g >> 1);
-      const int wq = 8 * (g & 1) + rq;
-      const int dp = hh * TW + wq;
-      ev8_t aa, ab;
-      {
-        s16x4_t lo = trr(da + pswz(dp) * 32 + cb), hi = trr(da + pswz(dp + 4) * 32 + cb);
-        s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        aa = __builtin_bit_cast(ev8_t, v);
-        lo = trr(db + pswz(dp) * 32 + cb);
-        hi = trr(db + pswz(dp + 4) * 32 + cb);
-        s16x8_t u = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        ab = __builtin_bit_cast(ev8_t, u);
-      }
-#pragma unroll
-      for (int f = 0; f < F; ++f) {
-        const char* slot = smem + ((t0 + f) % SLOTS) * SLOT_BYTES;
-#pragma unroll
-        for (int si = 0; si < 2; ++si) {
-          const int ip = (hh + bh) * PW + (wq + s0 + si);
-          s16x4_t lo = trr(slot + pswz(ip) * POSB + cb), hi = trr(slot + pswz(ip + 4) * POSB + cb);
-          s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-          const ev8_t xb = __builtin_bit_cast(ev8_t, v);
-          if (f < J) acc[f][si] = PVA_MFMA16(aa, xb, acc[f][si], 0, 0, 0);
-          if (f >= 2 && has_b) acc[f - 2][si] = PVA_MFMA16(ab, xb, acc[f - 2][si], 0, 0, 0);
-        }
-      }
-    }
-    __syncthreads();  // next frames / dY tiles landed; this step's first four window slots and dY tiles are free
-  }
-  // dW[co][dt][tap] = rows 0-7 of acc[dt] (lanes g < 2) + rows 8-15 of acc[dt + 1] (lanes g >= 2)
-#pragma unroll
-  for (int dt = 0; dt < KT; ++dt)
-#pragma unroll
-    for (int si = 0; si < 2; ++si)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float v = g < 2 ? acc[dt][si][r] : acc[dt + 1][si][r];
-        v += __shfl_xor(v, 32, 64);
-        if (g < 2) atomicAdd(p.dw + (int64_t)(4 * g + r) * TAPS * 16 + (dt * 16 + 4 * bh + s0 + si) * 16 + li, v);
-      }
-}
-
 // dW (s2d accumulator [Cout][kt][4][4][sy][sx][c4]) -> grad [Cout][3][kt][7][7] ; re-zeroes the accumulator
 __global__ void stem_wgrad_convert_kernel(float* __restrict__ acc, float* __restrict__ grad, int Cout, int kt,
                                           float beta) {
@@ -663,12 +549,6 @@ void launch_fwd_pair(const StemParams& p, hipStream_t s) {
 }
 
 template <int KT>
-void launch_wgrad_quad(const StemParams& p, hipStream_t s) {
-  const size_t lds = (KT + 7) * SLOT_BYTES + 4 * TH * TW * 16 * 2;
-  hipLaunchKernelGGL((stem_wgrad_quad_kernel<KT>), dim3(p.N * p.tiles_h * p.tiles_w), dim3(512), lds, s, p);
-}
-
-template <int KT>
 void launch_wgrad_pair(const StemParams& p, hipStream_t s) {
   const size_t lds = (KT + 3) * SLOT_BYTES + 2 * TH * TW * 16 * 2;
   hipLaunchKernelGGL((stem_wgrad_pair_kernel<KT>), dim3(p.N * p.tiles_h * p.tiles_w), dim3(256), lds, s, p);
@@ -682,12 +562,6 @@ int stem_tiles(int Ho, int Wo, int N) { return N * ((Ho + TH - 1) / TH) * ((Wo +
 // (read per launch — two launches per step — so tests can switch kernels within one process)
 static bool stem_pair_enabled() {
   const char* e = getenv("PVA_STEM_PAIR");
-  return !(e && e[0] == '0');
-}
-
-// the two-pair weight-gradient kernel of the fast stem (PVA_STEM_QUAD=0: the pair kernel)
-static bool stem_quad_enabled() {
-  const char* e = getenv("PVA_STEM_QUAD");
   return !(e && e[0] == '0');
 }
 
@@ -706,8 +580,7 @@ void stem_s2d_launch(int mode, const uint16_t* x, const uint16_t* w, uint16_t* y
     else if (kt == 5 && Cout <= 16) launch_fwd<5, 1>(p, s);
     else if (kt == 1 && Cout <= 64) launch_fwd<1, 4>(p, s);
   } else {
-    if (pair && stem_quad_enabled()) launch_wgrad_quad<5>(p, s);
-    else if (pair) launch_wgrad_pair<5>(p, s);
+    if (pair) launch_wgrad_pair<5>(p, s);
     else if (kt == 5 && Cout <= 16) launch_wgrad<5, 1>(p, s);
     else if (kt == 1 && Cout <= 64) launch_wgrad<1, 4>(p, s);
   }

@@ -1,5 +1,6 @@
 """Fast-stem (k(5,7,7), Cout 8) s2d kernels at the B=160 SlowFast-R50 shape: forward and weight gradient, per kernel
-variant (PVA_STEM_PAIR / PVA_STEM_QUAD are read per launch).
+variant (PVA_STEM_PAIR is read per launch).  Round 4 also timed a two-pair weight-gradient kernel here (8 waves,
+12-frame ring, each LDS fragment feeding both pairs): 2412 vs 1956 us for the pair kernel — removed.
     python scripts/stem_bench.py [--batch 160] [--iters 10]
 """
 import argparse
@@ -42,8 +43,8 @@ def main():
     acc = torch.zeros(cout * kt * 256, device=dev)
     flop = 2.0 * M * cout * 3 * kt * 49
     ref = None
-    for pair, quad in (("0", "0"), ("1", "0"), ("1", "1")):
-        os.environ["PVA_STEM_PAIR"], os.environ["PVA_STEM_QUAD"] = pair, quad
+    for pair in ("0", "1", "0", "1"):   # twice each: the first launches of a process run at lower clocks
+        os.environ["PVA_STEM_PAIR"] = pair
         tf = timeit(lambda: C.stem_fwd(xs, wp, y, stats, [N, T, Hs, Hs], cout, kt), a.iters)
         acc.zero_()
         tw = timeit(lambda: C.stem_wgrad(xs, dy, acc, [N, T, Hs, Hs], cout, kt), a.iters)
@@ -53,7 +54,7 @@ def main():
         if ref is None:
             ref = acc.clone()
         err = ((acc - ref).norm() / ref.norm()).item()
-        print(f"pair={pair} quad={quad}: fwd {tf:8.1f} us ({flop / tf / 1e6:6.1f} TF/s)  wgrad {tw:8.1f} us "
+        print(f"pair={pair}: fwd {tf:8.1f} us ({flop / tf / 1e6:6.1f} TF/s)  wgrad {tw:8.1f} us "
               f"({flop / tw / 1e6:6.1f} TF/s)  wgrad rel-diff vs one-frame kernel {err:.2e}", flush=True)
 
 
