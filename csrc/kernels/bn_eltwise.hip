@@ -95,18 +95,6 @@ __device__ __forceinline__ bool fin_reduce_and_elect(const float* __restrict__ p
   if (c < C) {
     double a4[4] = {0.0, 0.0, 0.0, 0.0}, b4[4] = {0.0, 0.0, 0.0, 0.0};
     int t = t0 + tl;
-    // sixteen rows per tile lane in flight: a workgroup's 64 tiles are one round trip (these run beside streaming
-    // kernels, where each dependent round trip costs microseconds; four in flight measured ~40 us per finalize)
-    for (; t + 60 < t1; t += 64) {
-      float fa[16], fb[16];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        fa[u] = part[((int64_t)(t + 4 * u) * K + k0) * C + c];
-        fb[u] = part[((int64_t)(t + 4 * u) * K + k1) * C + c];
-      }
-#pragma unroll
-      for (int u = 0; u < 16; ++u) { a4[u & 3] += fa[u]; b4[u & 3] += fb[u]; }
-    }
     for (; t + 12 < t1; t += 16) {
       float fa[4], fb[4];
 #pragma unroll
@@ -147,16 +135,6 @@ __device__ __forceinline__ bool fin_reduce_and_elect(const float* __restrict__ p
   if (c < C) {
     double a4[4] = {0.0, 0.0, 0.0, 0.0}, b4[4] = {0.0, 0.0, 0.0, 0.0};
     int r = tl;
-    for (; r + 60 < S; r += 64) {
-      double fa[16], fb[16];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        fa[u] = __builtin_nontemporal_load(scratch + ((int64_t)(r + 4 * u) * 2) * C + c);
-        fb[u] = __builtin_nontemporal_load(scratch + ((int64_t)(r + 4 * u) * 2 + 1) * C + c);
-      }
-#pragma unroll
-      for (int u = 0; u < 16; ++u) { a4[u & 3] += fa[u]; b4[u & 3] += fb[u]; }
-    }
     for (; r + 12 < S; r += 16) {
       double fa[4], fb[4];
 #pragma unroll
