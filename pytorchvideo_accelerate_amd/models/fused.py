@@ -293,7 +293,7 @@ class _ConvBN:
                     trial(c)
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     e0.record()
-                    for _ in range(3):
+                    for _ in range(eng.tuner.reps):
                         trial(c)
                     e1.record()
                     e1.synchronize()
@@ -304,7 +304,7 @@ class _ConvBN:
                 if eng.tuner.log:
                     import sys
                     print("wtune %s%s P=%d Cout=%d K=%d: " % (self.name, ".gram" if gram else "", dy.M, s.cout, K)
-                          + " ".join("%d=%.1fus" % (c, 1e3 * t / 3) for c, t in zip(cands, times))
+                          + " ".join("%d=%.1fus" % (c, 1e3 * t / eng.tuner.reps) for c, t in zip(cands, times))
                           + " -> %d" % cfg, file=sys.stderr, flush=True)
             eng.wtune[tkey] = cfg
         # off the critical path: a weight gradient that lands in the flat buffer runs on the lane's wgrad

@@ -89,7 +89,7 @@ class ConvTuner:
         self.pw_only: Optional[int] = None   # debugging aid: allow the pointwise kernel on the n-th PW-legal tuning only
         self._pw_seen = 0
         self.log = os.environ.get("PVA_TUNE_LOG", "0") != "0"
-        self.reps = reps
+        self.reps = int(os.environ.get("PVA_TUNE_REPS", reps))   # timed launches per candidate
         self.tuned = 0          # geometries timed by this process (conv + weight-gradient tunings)
         self.cache: Dict[Tuple, int] = {}
         self._scratch: Dict[Tuple, torch.Tensor] = {}
