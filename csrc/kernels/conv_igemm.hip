@@ -1061,7 +1061,6 @@ void conv_igemm_launch(const ConvParams& p, int chunk, hipStream_t stream, int c
   if ((p.eres || p.emask || p.epart || p.fres) && chunk != 8) return;  // host binding rejects this combination
   int v, bk, ut_force;
   bool dma = false;
-  if (p.nostore && cfg >= 0 && (cfg & 16) && (cfg & 512)) cfg = -1;   // the pointwise kernel always stores
   if (cfg >= 0 && (cfg & 16) && (cfg & 2048)) {  // halo-staged 3x3 kernel (legality checked by the bindings)
     conv_halo_launch(p, cfg, stream);
     return;

@@ -142,6 +142,7 @@ __global__ __launch_bounds__(PW_THREADS) void conv_pw_kernel(const ConvParams p,
     *reinterpret_cast<uint4*>(smem + (int64_t)u * 16) = v;
   }
   const bool do_stats = (EP == 0 && p.stats != nullptr) || (EP == 2 && p.epart != nullptr);
+  const bool nostore = EP == 0 && p.nostore != 0;
   if (do_stats)
     for (int i = tid; i < NSLOT * NG; i += PW_THREADS) st_lds[i] = 0.f;
   if (AFF)
@@ -399,8 +400,9 @@ __global__ __launch_bounds__(PW_THREADS) void conv_pw_kernel(const ConvParams p,
 #pragma unroll
               for (int e = 0; e < 8; ++e) v[e] = 0.f;
             const uint4 pk = pack8_fast(v);
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, pk), yr, r * yb + 16 * g + nc * 2, 0,
-                                                   ST_AUX);
+            if (!nostore)   // (statistics-only pass of a narrow BN fold: the output is never stored)
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, pk), yr, r * yb + 16 * g + nc * 2, 0,
+                                                     ST_AUX);
             if (do_stats) {
               float q[8];
               unpack8(pk, q);

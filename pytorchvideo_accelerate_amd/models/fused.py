@@ -386,7 +386,7 @@ class _ConvBN:
             def run(cfg, scratch):
                 C.conv_igemm(yb.t, self.wf, dummy, tuner.scratch_like(stats) if scratch else stats, bxf.scale,
                              bxf.shift, aff, 0, g, s.chunk, cfg, None, 1)
-            cfg = tuner.launch(("fst", aff) + tuple(g), g, s.chunk, run, aff=aff, direct=False, pw=False)
+            cfg = tuner.launch(("fst", aff) + tuple(g), g, s.chunk, run, aff=aff, direct=False)
             tiles = (yb.M + tuner.bm(cfg, Co) - 1) // tuner.bm(cfg, Co)
             C.bn_finalize(stats, tiles, Co, yb.M, bn.weight, bn.bias, bn.running_mean, bn.running_var,
                           bn.num_batches_tracked, bn.momentum if bn.momentum is not None else 0.1, bn.eps,

@@ -292,3 +292,32 @@ def test_pw_temporal_legality():
     assert not C.conv_pw_legal(list(fwd_geometry(st2, 1, 4, 8, 8, 32, 32)), 8)
     sp = ConvSpec(32, 32, (1, 3, 3), (1, 1, 1), (0, 1, 1))                          # spatial taps
     assert not C.conv_pw_legal(list(fwd_geometry(sp, 1, 4, 8, 8, 32, 32)), 8)
+
+
+@pytest.mark.parametrize("case", [FWD[0], FWD[2], FWD[6]])
+def test_pw_statistics_only(case):
+    """nostore (the narrow BN fold's exact-statistics pass): the same per-tile BN partial sums as a storing launch,
+    and nothing written."""
+    C = _C()
+    (N, T, H, W), ci, co, _, _ = case
+    M = N * T * H * W
+    g = torch.Generator().manual_seed(ci + co)
+    spec = ConvSpec(ci, co, (1, 1, 1))
+    w = torch.randn(co, ci, 1, 1, 1, generator=g) * (2.0 / ci) ** 0.5
+    wf, _ = pack_weight(w.to(DEV), spec)
+    x = torch.randn(M, ci, generator=g).to(torch.bfloat16).to(DEV)
+    sc = (torch.rand(ci, generator=g) + 0.5).to(DEV)
+    sh = (torch.randn(ci, generator=g) * 0.3).to(DEV)
+    geo = fwd_geometry(spec, N, T, H, W, ci, co)
+    for cfg in _cfgs():
+        rows = C.conv_cfg_bm(cfg, co)
+        tiles = (M + rows - 1) // rows
+        y = torch.empty(M, co, device=DEV, dtype=torch.bfloat16)
+        ref = torch.full((tiles, 2, co), float("nan"), device=DEV)
+        C.conv_igemm(x, wf, y, ref, sc, sh, 2, 0, list(geo), 8, cfg, None, 0)
+        dummy = torch.zeros(1, 8, device=DEV, dtype=torch.bfloat16)
+        got = torch.full((tiles, 2, co), float("nan"), device=DEV)
+        C.conv_igemm(x, wf, dummy, got, sc, sh, 2, 0, list(geo), 8, cfg, None, 1)
+        torch.cuda.synchronize()
+        assert torch.equal(got, ref), cfg
+        assert torch.all(dummy == 0)
