@@ -1005,9 +1005,6 @@ void launch_variant(int v, const ConvParams& p, int ut_force, hipStream_t stream
     case 5:   // 256x128 of 4 waves (128x64 each, as the 256x256 tile's): two independent workgroups per CU
       if constexpr (CH == 8) launch_cfg<256, 128, 128, 64, CH, BK>(p, ut_force, stream, dma);
       break;
-    case 6:   // 128x256 of 4 waves (64x128 each): the same, for wide outputs with fewer rows
-      if constexpr (CH == 8) launch_cfg<128, 256, 64, 128, CH, BK>(p, ut_force, stream, dma);
-      break;
     default: launch_cfg<256, 16, 64, 16, CH, BK>(p, ut_force, stream, dma); break;
   }
 }
@@ -1025,7 +1022,7 @@ static int pick_variant(int M, int N) {
 // uniform-tap loader (bit 3), bit 4 set = explicit (else the built-in heuristic), bit 5 = the narrow
 // direct-to-register kernel of conv_direct.hip (bit 6: 2048 rows per workgroup, else 512), bit 7 = LDS-DMA
 // staging of the uniform-tap loader (launches without an input affine), bit 8 = 256x256 tile of 8 waves
-// (bit 0 with it: the 256x128 tile of 4 waves, bit 1: the 128x256 tile of 4 waves; overrides the tile bits).
+// (bit 0 with it: the 256x128 tile of 4 waves instead; overrides the tile bits).  -1 = heuristic.
 int conv_direct_rows(int cfg);
 void conv_direct_launch(const ConvParams& p, int cfg, hipStream_t s);
 // bit 9 = the streaming pointwise kernel of conv_pw.hip (dense 1x1x1 GEMMs; bits 0-1: 1024 << v rows per
@@ -1041,7 +1038,7 @@ int conv_cfg_bm(int cfg, int N) {
   if (cfg >= 0 && (cfg & 16) && (cfg & 2048)) return cfg >> 12;
   if (cfg >= 0 && (cfg & 16) && (cfg & 512)) return conv_pw_rows(cfg);
   if (cfg >= 0 && (cfg & 16) && (cfg & 32)) return conv_direct_rows(cfg);
-  if (cfg >= 0 && (cfg & 16) && (cfg & 256)) return (cfg & 2) ? 128 : 256;   // 256x256 / 256x128 / 128x256 tiles
+  if (cfg >= 0 && (cfg & 16) && (cfg & 256)) return 256;   // 256x256 tile
   const int v = (cfg >= 0 && (cfg & 16)) ? (cfg & 3) : pick_variant(0, N);
   return v <= 1 ? 128 : 256;
 }
@@ -1078,7 +1075,7 @@ void conv_igemm_launch(const ConvParams& p, int chunk, hipStream_t stream, int c
     return;
   }
   if (cfg >= 0 && (cfg & 16)) {
-    v = (cfg & 256) ? 4 + (cfg & 3) : (cfg & 3);
+    v = (cfg & 256) ? 4 + (cfg & 1) : (cfg & 3);
     bk = (cfg & 4) ? 64 : 32;
     ut_force = (cfg >> 3) & 1;
     dma = (cfg & 128) != 0;   // LDS-DMA staging (uniform-tap loader, no input affine)

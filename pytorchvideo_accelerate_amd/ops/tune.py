@@ -38,7 +38,6 @@ DMA = 128             # uniform-tap loader staged by LDS-DMA (buffer_load ... ld
 DIRECT_HALF = 1024    #   (with DIRECT) half the row groups in flight per wave: fewer VGPRs, more waves per SIMD
 BIG = 256             # 256x256 tile of 8 waves (N >= 256; the backward-BN epilogue in 64-row slices);
 BIG_HALF = 1          #   with bit 0: the 256x128 tile of 4 waves (N >= 128; two independent workgroups per CU)
-BIG_WIDE = 2          #   with bit 1: the 128x256 tile of 4 waves (N >= 256)
 PW = 512              # streaming pointwise kernel (csrc/kernels/conv_pw.hip): dense 1x1x1 GEMMs, K <= 256,
 PW_ROWS = (1024, 2048, 4096)   # N % 32 == 0, weights in LDS; bits 0-1 select the rows per workgroup,
 PW_SOLO = 4                     # bit 2 one workgroup per CU
@@ -63,8 +62,8 @@ def describe(cfg: int) -> str:
     if cfg & DIRECT:
         return "direct%d%s" % (2048 if cfg & DIRECT_2K else 512, "/rt2" if cfg & DIRECT_HALF else "")
     if cfg & BIG:
-        tile = "256x128" if cfg & BIG_HALF else ("128x256" if cfg & BIG_WIDE else "256x256")
-        return "%s/bk%d%s%s" % (tile, 64 if cfg & BK64 else 32, "/ut" if cfg & UT else "", "/dma" if cfg & DMA else "")
+        return "256x%d/bk%d%s%s" % (128 if cfg & BIG_HALF else 256, 64 if cfg & BK64 else 32, "/ut" if cfg & UT else "",
+                                    "/dma" if cfg & DMA else "")
     return "%dx%d/bk%d%s%s" % (TILE_BM[cfg & 3], TILE_BN[cfg & 3], 64 if cfg & BK64 else 32, "/ut" if cfg & UT else "",
                                "/dma" if cfg & DMA else "")
 
@@ -82,7 +81,6 @@ class ConvTuner:
         self.pw = os.environ.get("PVA_CONV_PW", "1") != "0"
         self.halo = os.environ.get("PVA_CONV_HALO", "1") != "0"
         self.big_half = os.environ.get("PVA_CONV_BIG_HALF", "1") != "0"
-        self.big_wide = os.environ.get("PVA_CONV_BIG_WIDE", "0") != "0"
         # debugging aid: PVA_PW_KINDS=f,fres,er,... restricts the pointwise kernel to launches whose key
         # starts with one of these kinds (models/fused.py: f fres fw2 eb er d)
         kinds = os.environ.get("PVA_PW_KINDS")
@@ -121,8 +119,8 @@ class ConvTuner:
                     if ut and aff == 0 and self.dma:
                         out.append(cfg_word(v, bk, ut) | DMA)
         if N >= 128 and chunk == 8:   # 256x256 / 256x128 tiles (UT loader only: the generic one is VALU-bound)
-            halves = ((0, BIG_HALF) if self.big_half else (0,)) + ((BIG_WIDE,) if self.big_wide else ())
-            for half in (h for h in halves if N >= (128 if h == BIG_HALF else 256)):
+            halves = (0, BIG_HALF) if self.big_half else (0,)
+            for half in (h for h in halves if N >= (128 if h else 256)):
                 for bk in (32, 64):
                     if self.C.conv_ut_legal(list(g), chunk, bk):
                         w = EXPLICIT | BIG | half | UT | (BK64 if bk == 64 else 0)
