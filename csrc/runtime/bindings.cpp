@@ -584,8 +584,13 @@ void synth_frames(const at::Tensor& out, int64_t seed) {
 
 }  // namespace
 
+// generated per build by _build.py (build/obj/build_id.<id>.cpp): "PVA_BUILD_ID:" + the source-tree hash
+extern "C" const char pva_build_id_str[];
+
 PYBIND11_MODULE(_C, m) {
   m.doc() = "gfx950 HIP kernels for pytorchvideo_accelerate_amd";
+  // provenance: hash of (csrc sources, headers, compile flags) this binary was linked from (_build.tree_id)
+  m.def("build_id", []() { return std::string(pva_build_id_str + 13); });
   // ROCTx ranges / marks (host timeline; recorded by rocprofv3 --marker-trace, no-ops without a tool attached)
   m.def("range_push", [](const std::string& s) { return (int64_t)roctxRangePushA(s.c_str()); });
   m.def("range_pop", []() { return (int64_t)roctxRangePop(); });

@@ -4,7 +4,9 @@ No hipify, no ``torch.utils.cpp_extension.CUDAExtension`` (which would run hipif
 ``csrc/kernels/*.hip`` file is compiled directly by ``hipcc --offload-arch=gfx950`` — twice, once per 16-bit
 compute type (``-DPVA_F16=0``: bf16 operands, namespace ``pva_bf16``; ``-DPVA_F16=1``: fp16 operands, namespace
 ``pva_f16``; ``csrc/kernels/common.h``) — and linked with the pybind11 binding unit against libtorch.  Objects are cached by a hash of (source, headers, flags) so
-re-builds only recompile what changed.  The resulting ``_C*.so`` lives in-tree next to this file (so it
+re-builds only recompile what changed.  The binary carries the build id of the tree it was linked from
+(``tree_id``: sources, headers, flags; ``_C.build_id()``); ``build()`` relinks whenever it differs and the loader
+(``ops/_ext.py``) refuses a stale binary.  The resulting ``_C*.so`` lives in-tree next to this file (so it
 travels to the GPU box with the repository snapshot).
 
     python -m pytorchvideo_accelerate_amd._build [--jobs N] [--force]
@@ -18,7 +20,9 @@ import hashlib
 import os
 import subprocess
 import sys
+import re
 import sysconfig
+from typing import Optional, Tuple
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(PKG_DIR)
@@ -42,19 +46,62 @@ def _torch_paths():
     return root, inc, os.path.join(root, "lib"), int(torch._C._GLIBCXX_USE_CXX11_ABI)
 
 
-def _headers_digest() -> str:
+def _headers_digest(csrc: str = CSRC) -> str:
     h = hashlib.sha1()
-    for f in sorted(glob.glob(os.path.join(CSRC, "**", "*.h"), recursive=True)):
+    for f in sorted(glob.glob(os.path.join(csrc, "**", "*.h"), recursive=True)):
         with open(f, "rb") as fh:
             h.update(fh.read())
     return h.hexdigest()
 
 
-def _compile(src: str, flags: list, hdr: str, force: bool, tag: str = "") -> str:
+# compile flags that change the generated code (include paths excluded: they do not)
+FLAGS_SIG = "-O3 -std=c++17 -ffp-contract=fast PVA_F16=0,1 arch=" + ARCH
+ID_MARK = b"PVA_BUILD_ID:"
+_ID_RE = re.compile(re.escape(ID_MARK) + rb"([0-9a-f]{40})")
+
+
+def tree_id(csrc: str = CSRC) -> str:
+    """Build id of a source tree: sha1 over every csrc source/header (relative path + bytes) and the flags.
+    Compiled into the extension (``_C.build_id()``), so a binary can be checked against the tree it ships with."""
+    h = hashlib.sha1(FLAGS_SIG.encode())
+    files = []
+    for ext in ("*.hip", "*.h", "*.cpp"):
+        files += glob.glob(os.path.join(csrc, "**", ext), recursive=True)
+    for f in sorted(files, key=lambda f: os.path.relpath(f, csrc)):
+        h.update(os.path.relpath(f, csrc).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+        h.update(b"\0")
+    return h.hexdigest()
+
+
+def embedded_id(so_path: str) -> Optional[str]:
+    """The build id compiled into a built ``_C*.so`` (read from the file, without importing it), or None."""
+    try:
+        with open(so_path, "rb") as fh:
+            m = _ID_RE.search(fh.read())
+    except OSError:
+        return None
+    return m.group(1).decode() if m else None
+
+
+def check(so_path: Optional[str] = None, csrc: Optional[str] = None) -> Tuple[bool, Optional[str], Optional[str]]:
+    """(up to date, embedded id, tree id).  Without a source tree next to the package nothing can be compared:
+    that counts as up to date (an installed copy)."""
+    so_path = so_path or ext_path()
+    csrc = csrc or CSRC
+    emb = embedded_id(so_path)
+    if not os.path.isdir(csrc):
+        return emb is not None, emb, None
+    want = tree_id(csrc)
+    return emb == want, emb, want
+
+
+def _compile(src: str, flags: list, hdr: str, force: bool, tag: str = "", build_dir: str = BUILD) -> str:
     with open(src, "rb") as fh:
         content = fh.read()
     key = hashlib.sha1(content + hdr.encode() + " ".join(flags).encode()).hexdigest()[:16]
-    obj = os.path.join(BUILD, os.path.basename(src) + tag + "." + key + ".o")
+    obj = os.path.join(build_dir, os.path.basename(src) + tag + "." + key + ".o")
     if os.path.exists(obj) and not force:
         return obj
     cmd = [HIPCC] + flags + ["-c", src, "-o", obj + ".tmp"]
@@ -65,8 +112,11 @@ def _compile(src: str, flags: list, hdr: str, force: bool, tag: str = "") -> str
     return obj
 
 
-def build(jobs: int = 0, force: bool = False, verbose: bool = False) -> str:
-    os.makedirs(BUILD, exist_ok=True)
+def build(jobs: int = 0, force: bool = False, verbose: bool = False, csrc: str = CSRC, build_dir: str = BUILD,
+          out: Optional[str] = None) -> str:
+    """Compile (object cache keyed by content) and relink whenever the binary's embedded build id differs from
+    the tree's — never trusts a side file.  ``csrc`` / ``build_dir`` / ``out`` let a test build a copy of the tree."""
+    os.makedirs(build_dir, exist_ok=True)
     _, tinc, tlib, abi = _torch_paths()
     pyinc = sysconfig.get_paths()["include"]
     common = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
@@ -74,32 +124,37 @@ def build(jobs: int = 0, force: bool = False, verbose: bool = False) -> str:
     kern_flags = common + ["-ffp-contract=fast"]
     bind_flags = common + ["-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H", "-DUSE_ROCM=1",
                            "-D__HIP_PLATFORM_AMD__=1", f"-I{pyinc}"] + [f"-I{p}" for p in tinc]
-    hdr = _headers_digest()
-    kernels = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
-    runtime = sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp")))
+    out = out or ext_path()
+    bid = tree_id(csrc)
+    if os.path.exists(out) and not force and embedded_id(out) == bid:
+        return out
+    hdr = _headers_digest(csrc)
+    kernels = sorted(glob.glob(os.path.join(csrc, "kernels", "*.hip")))
+    runtime = sorted(glob.glob(os.path.join(csrc, "runtime", "*.cpp")))
+    id_src = os.path.join(build_dir, f"build_id.{bid}.cpp")
+    if not os.path.exists(id_src):
+        with open(id_src + ".tmp", "w") as fh:
+            fh.write('extern "C" const char pva_build_id_str[] = "%s%s";\n' % (ID_MARK.decode(), bid))
+        os.replace(id_src + ".tmp", id_src)
     jobs = jobs or min(16, os.cpu_count() or 4)
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-        futs = [ex.submit(_compile, s, kern_flags + [f"-DPVA_F16={h}"], hdr, force, (".f16" if h else ".bf16"))
+        futs = [ex.submit(_compile, s, kern_flags + [f"-DPVA_F16={h}"], hdr, force, (".f16" if h else ".bf16"), build_dir)
                 for s in kernels for h in (0, 1)]
-        futs += [ex.submit(_compile, s, bind_flags, hdr, force) for s in runtime]
+        futs += [ex.submit(_compile, s, bind_flags, hdr, force, "", build_dir) for s in runtime]
+        futs.append(ex.submit(_compile, id_src, common, "", force, "", build_dir))
         objs = [f.result() for f in futs]
-    out = ext_path()
     libs = ["-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
             f"-L{ROCM_LIB}", f"-Wl,-rpath,{ROCM_LIB}", "-lrocprofiler-sdk-roctx"]   # ROCTx ranges
-    stamp = hashlib.sha1(" ".join(objs).encode()).hexdigest()
-    stamp_file = out + ".stamp"
-    if os.path.exists(out) and not force and os.path.exists(stamp_file) and open(stamp_file).read() == stamp:
-        return out
     cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}"] + objs + [f"-L{tlib}", f"-Wl,-rpath,{tlib}"] + libs + [
         "-o", out + ".tmp"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
     os.replace(out + ".tmp", out)
-    with open(stamp_file, "w") as fh:
-        fh.write(stamp)
+    if embedded_id(out) != bid:
+        raise RuntimeError(f"linked {out} but its embedded build id is not {bid}")
     if verbose:
-        print("built", out)
+        print("built", out, "build id", bid)
     return out
 
 

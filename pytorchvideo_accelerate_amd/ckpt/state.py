@@ -122,6 +122,8 @@ def save_state(output_dir: str, model: torch.nn.Module, optimizers: Sequence = (
         if old is not None:
             shutil.rmtree(old, ignore_errors=True)
     barrier()
+    if not is_main:   # a node that does not share the main process's filesystem (accelerate: every rank creates it)
+        os.makedirs(output_dir, exist_ok=True)
     _atomic_torch_save(rng_state(step), os.path.join(output_dir, f"random_states_{rank}.pkl"))
     barrier()
     if is_main:

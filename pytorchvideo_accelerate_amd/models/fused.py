@@ -1000,7 +1000,10 @@ class FusedNet:
         # fixed-order (slab) reduction for the weight-gradient launches whose results feed back into the step —
         # the BN-fold Gram matrices (forward statistics) and G = dz^T act (backward coefficients) — while the
         # leaf weight gradients keep their fp32 atomics: the loss and the dgrad chain are then reproducible
-        # run to run and only the weight gradients carry atomic-order noise (~1e-6).  Without it that noise
+        # run to run *for the same tuned launch configurations* (the slab count of a Gram / G launch is an
+        # autotuner choice, and with it the summation order: two processes agree bitwise only when they share the
+        # persisted tune table, ops/tune.py TuneStore, or run deterministic=True, which fixes the split heuristic)
+        # and only the weight gradients carry atomic-order noise (~1e-6).  Without it that noise
         # flips ReLU masks and the random-init network's chaotic backward decorrelates two runs' gradients
         # (cosine ~0.65 at B=4-32: scripts/diag_ms_race.py).  On by default (only the few Gram / G launches pay the
         # slab reduction); PVA_FOLD_SLABS=0 turns it off; implied by ``deterministic``.

@@ -14,7 +14,7 @@ the same order, so the result does not depend on the choice.
 Disabled by ``PVA_AUTOTUNE=0`` and in deterministic mode (the built-in heuristic is used instead).
 
 Tuned choices persist across processes (:class:`TuneStore`): a JSON table under ``~/.cache/pva/`` (or
-``$PVA_TUNE_CACHE``; ``PVA_TUNE_CACHE=0`` disables it) whose file name hashes the extension's build stamp, the
+``$PVA_TUNE_CACHE``; ``PVA_TUNE_CACHE=0`` disables it) whose file name hashes the extension's embedded build id, the planner sources, the
 device name, the HIP version, the compute dtype and the kernel-selection knobs — a rebuilt ``.so`` or another GPU
 gets a fresh table.  Under data parallelism rank 0 reads it and broadcasts it (one collective), and only rank 0
 writes it back.
@@ -224,14 +224,19 @@ class TuneStore:
     def build_ident(device, dtype: str) -> Dict[str, str]:
         from .. import _build
         import torch as _t
-        stamp = ""
-        try:
-            with open(_build.ext_path() + ".stamp") as f:
-                stamp = f.read().strip()
-        except OSError:
-            pass
+        so = _build.embedded_id(_build.ext_path()) or ""
+        # the Python side interprets cached cfg words (split heuristics, legality filters): a change there must
+        # invalidate the table too, not only a rebuilt binary
+        h = hashlib.sha1()
+        pkg = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        for rel in ("ops/tune.py", "ops/conv.py", "models/fused.py"):
+            try:
+                with open(os.path.join(pkg, rel), "rb") as f:
+                    h.update(f.read())
+            except OSError:
+                pass
         name = _t.cuda.get_device_name(device) if _t.device(device).type == "cuda" else "cpu"
-        return {"so": stamp, "device": name, "hip": str(_t.version.hip), "dtype": dtype}
+        return {"so": so, "py": h.hexdigest()[:16], "device": name, "hip": str(_t.version.hip), "dtype": dtype}
 
     def _count(self) -> int:
         return sum(len(t) for t in self.tables.values())

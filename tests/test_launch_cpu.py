@@ -2,6 +2,8 @@
 import os
 import socket
 import subprocess
+
+import pytest
 import sys
 
 from pytorchvideo_accelerate_amd import launch
@@ -78,11 +80,14 @@ def test_fault_injection_elastic_restart_auto_resume(tmp_path):
     assert (out / "step_4" / "model.safetensors").exists()  # 2 epochs x 2 global steps; final save
 
 
-def test_crash_inside_checkpoint_save_restarts_from_previous(tmp_path):
+@pytest.mark.parametrize("nproc", [1, 2])
+def test_crash_inside_checkpoint_save_restarts_from_previous(tmp_path, nproc):
     """The elastic agent restarts a run whose step-4 save died half-way; --auto_resume continues from the complete
-    step_2 checkpoint (not the partial step_4.tmp) and the run finishes."""
+    step_2 checkpoint (not the partial step_4.tmp) and the run finishes.  With 2 ranks only the main process
+    crashes (it alone writes the shared files) while rank 1 waits in the save's barrier: the agent tears the whole
+    group down on the main process's exit (no collective timeout) and restarts it."""
     out = tmp_path / "out"
-    cmd = [sys.executable, "-m", "pytorchvideo_accelerate_amd.launch", "--cpu", "--num_processes", "1",
+    cmd = [sys.executable, "-m", "pytorchvideo_accelerate_amd.launch", "--cpu", "--num_processes", str(nproc),
            "--max_restarts", "1", "--monitor_interval", "1", "--main_process_port", str(_port()), "--auto_resume",
            os.path.join(REPO, "run.py"), "--synthetic", "--synthetic_videos", "8", "--synthetic_classes", "3",
            "--num_frames", "8", "--crop_size", "64", "--batch_size", "2", "--num_workers", "0", "--num_epochs", "2",
@@ -95,4 +100,4 @@ def test_crash_inside_checkpoint_save_restarts_from_previous(tmp_path):
     assert r.returncode == 0, log
     assert "injected fault while saving" in log and "Resumed from checkpoint" in log and "step_2" in log, log
     assert (out / ".save_fault_injected_0").exists()
-    assert (out / "step_8" / ".pva_complete").exists() and not (out / "step_4.tmp").exists()
+    assert (out / f"step_{8 // nproc}" / ".pva_complete").exists() and not (out / "step_4.tmp").exists()
