@@ -226,7 +226,7 @@ def run(a):
         eng = FusedNet(model, dev, deterministic=a.deterministic, load_tuning=st.world_size == 1,
                        compute_dtype=torch.float16 if a.precision == "fp16" else torch.bfloat16)
         scaler = FusedGradScaler() if a.precision == "fp16" else None
-        if st.world_size > 1:
+        if st.multi:
             eng.tuner.agree = st.agree_times
             ts = eng.tune_store   # rank 0's persistent autotuner table, broadcast once (as engine/backends.py)
             doc = st.broadcast_object(ts.read() if (ts is not None and st.rank == 0) else None)
@@ -238,8 +238,8 @@ def run(a):
         opt = FusedSGD(eng.flat, lr=a.lr, momentum=0.9, weight_decay=1e-4, after_step=eng.pack)
         bounds = sorted(set(eng.flat.span(p)[1] for p in eng.flat.params))
         sync = GradSync(eng.flat.grad, st, a.bucket_mb, boundaries=bounds, first_mb=a.first_bucket_mb,
-                        grad_dtype=gdt, timing=st.world_size > 1)
-        eng.grad_hook = sync.progress if st.world_size > 1 else None   # (1 GPU: no buckets to launch)
+                        grad_dtype=gdt, timing=st.multi)
+        eng.grad_hook = sync.progress if st.multi else None   # (1 GPU: no buckets to launch)
         sync.producers = eng.producer_streams   # RCCL: buckets issued from the sync's own comm stream
         eng.grad_multi_stream = sync.multi_stream
         drank = st.rank if a.data_rank < 0 else a.data_rank
@@ -373,7 +373,7 @@ def run(a):
     if a.dump:
         dump["params"] = opt.flat.data.clone()
         gathered = [torch.zeros_like(dump["params"]) for _ in range(st.world_size)]
-        if st.world_size > 1:
+        if st.multi:
             import torch.distributed as dist
             dist.all_gather(gathered, dump["params"])
         else:
@@ -410,6 +410,7 @@ def run(a):
                        "global_batch": B * a.grad_accum * st.world_size,
                        "per_gpu_batch": B, "grad_accum": a.grad_accum, "seq_len": a.frames,
                        "parallelism": f"dp{st.world_size}", "backend": st.backend or "none",
+                       "forced_sync": st.forced,
                        "grad_dtype": a.grad_dtype, "classes": a.classes, "hip_graph": bool(gstep is not None),
                        "deterministic": a.deterministic, "source": a.source,
                        "final_loss": round(float(loss), 4) if loss is not None else None,

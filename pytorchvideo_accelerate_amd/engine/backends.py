@@ -96,7 +96,7 @@ class FusedBackend:
         from ..ops.optim import FusedGradScaler
         self.state = state
         self.device = state.device
-        dp = state.world_size > 1
+        dp = state.multi
         cdt = torch.float16 if mixed_precision == "fp16" else torch.bfloat16
         self.net = FusedNet(model, self.device, load_tuning=not dp, compute_dtype=cdt)
         if dp:   # identical autotuner choices on every rank
@@ -111,7 +111,7 @@ class FusedBackend:
         self.flat = self.net.flat
         bounds = sorted(set(self.flat.span(p)[1] for p in self.flat.params))
         self.sync = GradSync(self.flat.grad, state, bucket_mb, boundaries=bounds)
-        self.net.grad_hook = self.sync.progress if state.world_size > 1 else None
+        self.net.grad_hook = self.sync.progress if state.multi else None
         self.sync.producers = self.net.producer_streams   # RCCL: buckets issued from the sync's own comm stream
         self.net.grad_multi_stream = self.sync.multi_stream
         # fp16: fp16 kernels plus the dynamic loss-scale state machine (GradScaler semantics: fp16 has 5 exponent bits)

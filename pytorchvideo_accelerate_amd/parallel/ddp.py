@@ -48,7 +48,7 @@ class GradSync:
                  grad_dtype: Optional[torch.dtype] = None, timing: bool = False):
         self.grad = grad
         self.state = state
-        self.enabled = state.world_size > 1 and state.initialized
+        self.enabled = state.multi
         n = grad.numel()
         cap = max(1, int(bucket_mb * (1 << 20) / grad.element_size()))
         first = cap if first_mb is None else max(1, int(first_mb * (1 << 20) / grad.element_size()))

@@ -6,6 +6,10 @@ Mirrors what the reference gets from ``accelerate`` (SURVEY.md D1/D2/D10/D13/D14
   ``WORLD_SIZE``, ``MASTER_ADDR``, ``MASTER_PORT``); with ``LOCAL_RANK`` set and a GPU present it
   initialises the ``nccl`` backend (RCCL on ROCm) and binds ``cuda:LOCAL_RANK``; on CPU with
   world > 1 it uses ``gloo``; otherwise it is single-process (``distributed_type == "NO"``).
+* ``PVA_FORCE_GRADSYNC=1`` initialises the process group even at world size 1 (``multi`` is then true): every
+  collective, the gradient all-reduce included, runs through the real backend — RCCL's code paths (``ReduceOp.AVG``,
+  ``barrier(device_ids)``, ``all_gather_into_tensor``, the comm-stream bucket schedule) executed on a 1-GPU box
+  (SURVEY.md §4.3 item 4).
 * ``broadcast_module`` (rank-0 params + buffers, coalesced into one flat buffer per dtype),
   ``all_gather_cat`` (``accelerator.gather``), ``all_reduce_`` (AVG on RCCL, SUM/W on gloo), barrier.
 """
@@ -27,6 +31,7 @@ class DistState:
     backend: Optional[str] = None
     device: torch.device = torch.device("cpu")
     distributed_type: str = "NO"
+    forced: bool = False      # PVA_FORCE_GRADSYNC=1: a process group (and every collective) even at world size 1
 
     @property
     def is_main_process(self) -> bool:
@@ -36,6 +41,11 @@ class DistState:
     def initialized(self) -> bool:
         return dist.is_available() and dist.is_initialized()
 
+    @property
+    def multi(self) -> bool:
+        """Collectives are live: a process group with more than one rank, or a forced single-rank group."""
+        return self.initialized and (self.world_size > 1 or self.forced)
+
     @classmethod
     def from_env(cls, cpu: bool = False, timeout_s: int = 1800) -> "DistState":
         ws = int(os.environ.get("WORLD_SIZE", "1"))
@@ -43,15 +53,17 @@ class DistState:
         lr = int(os.environ.get("LOCAL_RANK", "0"))
         use_gpu = (not cpu) and torch.cuda.is_available()
         st = cls(rank=rank, world_size=ws, local_rank=lr)
+        st.forced = os.environ.get("PVA_FORCE_GRADSYNC", "0") == "1"
         if use_gpu:
             ndev = torch.cuda.device_count()
             st.device = torch.device("cuda", lr % max(ndev, 1))
             torch.cuda.set_device(st.device)
-        if ws > 1:
+        if ws > 1 or st.forced:
             # PVA_DIST_BACKEND=gloo on a GPU: several ranks may share one device (1-GPU rehearsal of the
             # multi-rank path; RCCL refuses duplicate devices).  Default on GPU: nccl (= RCCL on ROCm).
             st.backend = os.environ.get("PVA_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
-            st.distributed_type = "MULTI_GPU" if use_gpu else "MULTI_CPU"
+            if ws > 1:
+                st.distributed_type = "MULTI_GPU" if use_gpu else "MULTI_CPU"
             if not dist.is_initialized():
                 os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
                 os.environ.setdefault("MASTER_PORT", "29500")
@@ -77,7 +89,7 @@ class DistState:
 
     # -------------------------------------------------------------- collectives
     def barrier(self):
-        if self.initialized and self.world_size > 1:
+        if self.multi:
             if self.backend == "nccl":
                 dist.barrier(device_ids=[self.device.index])
             else:
@@ -87,7 +99,7 @@ class DistState:
         """Autotuner consensus: every rank times the same candidate list; all pick the argmin of the
         per-candidate MAX over ranks (the slowest rank bounds a data-parallel step), so every rank runs
         identical kernels."""
-        if not (self.initialized and self.world_size > 1) or not times:
+        if not self.multi or not times:
             return times
         dev = self.device if self.backend == "nccl" else torch.device("cpu")
         t = torch.tensor(times, dtype=torch.float64, device=dev)
@@ -95,7 +107,7 @@ class DistState:
         return t.cpu().tolist()
 
     def all_reduce_(self, t: torch.Tensor, op: str = "avg") -> torch.Tensor:
-        if not (self.initialized and self.world_size > 1):
+        if not self.multi:
             return t
         if op == "avg":
             if self.backend == "nccl":
@@ -113,7 +125,7 @@ class DistState:
 
     def all_gather_cat(self, t: torch.Tensor) -> torch.Tensor:
         """``accelerator.gather``: concatenate every rank's tensor along dim 0 (equal shapes)."""
-        if not (self.initialized and self.world_size > 1):
+        if not self.multi:
             return t
         t = t.contiguous()
         if self.backend == "nccl":
@@ -126,7 +138,7 @@ class DistState:
 
     def broadcast_tensors(self, tensors: List[torch.Tensor], src: int = 0):
         """Coalesced broadcast (one flat buffer per dtype) of rank ``src``'s tensors, in place."""
-        if not (self.initialized and self.world_size > 1) or not tensors:
+        if not self.multi or not tensors:
             return
         by_dtype = {}
         for t in tensors:
@@ -146,7 +158,7 @@ class DistState:
         self.broadcast_tensors(ts, src)
 
     def broadcast_object(self, obj, src: int = 0):
-        if not (self.initialized and self.world_size > 1):
+        if not self.multi:
             return obj
         lst = [obj]
         dist.broadcast_object_list(lst, src)

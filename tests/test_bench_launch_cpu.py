@@ -56,3 +56,30 @@ def test_bench_self_launch_two_ranks(tmp_path):
 def test_bench_single_rank_plumbing(tmp_path):
     res = _run(["--gpus", "1"], tmp_path)
     assert res["n_gpus"] == 1 and res["config"]["parallelism"] == "dp1"
+
+
+def test_forced_gradsync_single_rank_gloo(tmp_path):
+    """``PVA_FORCE_GRADSYNC=1`` at world size 1: a real (gloo) process group, every bucket all-reduced through it;
+    the gradient equals the un-synced single-process run bit for bit (average over one rank)."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, OMP_NUM_THREADS="2", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="",
+               PVA_FORCE_GRADSYNC="1")
+    env.pop("WORLD_SIZE", None)
+    d1 = str(tmp_path / "forced.pt")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+                        "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(REPO, "bench.py"),
+                        "--gpus", "1", "--dump", d1] + ARGS, capture_output=True, text=True, timeout=900,
+                       cwd=str(tmp_path), env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    res = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert res["config"]["backend"] == "gloo" and res["config"]["forced_sync"] is True
+    d0 = str(tmp_path / "plain.pt")
+    res0 = _run(["--gpus", "1", "--dump", d0], tmp_path)
+    assert res0["config"]["backend"] == "none"
+    g1 = torch.load(d1, weights_only=True)["grad"]
+    g0 = torch.load(d0, weights_only=True)["grad"]
+    assert torch.equal(g0, g1)
