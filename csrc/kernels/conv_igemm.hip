@@ -891,6 +891,7 @@ void conv_igemm_kernel(const ConvParams p) {
   }
 }
 
+#ifndef PVA_KERNEL_ONLY   // (tools/gemm_lab.hip instantiates the kernel template alone)
 // uniform-tap loader use: 0 never, 1 where it measured faster (default), 2 whenever legal
 static int g_ut_mode = 1;
 
@@ -1009,8 +1010,10 @@ void launch_variant(int v, const ConvParams& p, int ut_force, hipStream_t stream
   }
 }
 
+#endif  // PVA_KERNEL_ONLY
 }  // namespace
 
+#ifndef PVA_KERNEL_ONLY
 static int pick_variant(int M, int N) {
   if (N > 64) return 0;       // 128 x 128
   if (N > 32) return 1;       // 128 x 64
@@ -1091,5 +1094,7 @@ void conv_igemm_launch(const ConvParams& p, int chunk, hipStream_t stream, int c
     if (bk == 64) launch_variant<4, 64>(v, p, ut_force, stream); else launch_variant<4, 32>(v, p, ut_force, stream);
   }
 }
+
+#endif  // PVA_KERNEL_ONLY
 
 PVA_NS_END  // namespace PVA_NS

@@ -153,7 +153,11 @@ class VideoClipDataset(Dataset):
             v.close()
         return d
 
-    def set_epoch(self, epoch: int):
+    def set_epoch(self, epoch: int, force: bool = False):
+        """Plan of ``epoch`` (deterministic in seed and epoch).  Re-planning the current epoch keeps the same
+        ``items`` object (a reader that started on it ahead of time stays valid) unless ``force``."""
+        if not force and getattr(self, "epoch", None) == epoch and getattr(self, "items", None) is not None:
+            return
         self.epoch = epoch
         n = self.videos.num_videos
         if self.distributed:

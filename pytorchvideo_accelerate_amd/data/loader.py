@@ -35,6 +35,7 @@ class NativeRawSource:
         self.C = require()
         self.ds, self.B, self.threads, self.drop_last, self.prefetch = ds, batch_size, threads, drop_last, prefetch
         self._meta: Dict[int, tuple] = {}
+        self._pending = None   # (plan, queue, thread, stop) started ahead of its __iter__ (``start``)
 
     def __len__(self):
         n = len(self.ds)
@@ -77,25 +78,70 @@ class NativeRawSource:
         return {"frames": buf, "desc": torch.tensor(descs, dtype=torch.int32), "num_frames": T,
                 "label": torch.tensor(labels, dtype=torch.long)}
 
-    def __iter__(self):
-        items = self.ds.items
+    def _spawn(self, items):
         chunks = [items[i:i + self.B] for i in range(0, len(items), self.B)]
         if self.drop_last and chunks and len(chunks[-1]) < self.B:
             chunks = chunks[:-1]
         q: "queue.Queue" = queue.Queue(maxsize=self.prefetch)
+        stop = threading.Event()
 
         def producer():
             for c in chunks:
+                if stop.is_set():
+                    break
                 q.put(self._make_batch(c))
             q.put(None)
 
         th = threading.Thread(target=producer, daemon=True)
         th.start()
-        while True:
-            b = q.get()
-            if b is None:
-                break
-            yield b
+        return q, th, stop
+
+    def _cancel(self):
+        if self._pending is None:
+            return
+        _, q, th, stop = self._pending
+        self._pending = None
+        self._stop_producer(q, th, stop)
+
+    @staticmethod
+    def _stop_producer(q, th, stop):
+        stop.set()
+        while th.is_alive():          # unblock a producer waiting on a full queue
+            try:
+                q.get(timeout=0.05)
+            except queue.Empty:
+                pass
+        th.join()
+
+    def start(self):
+        """Start reading the dataset's current plan (``ds.items``) in the background now — e.g. the next epoch's
+        first batches while the validation pass runs — so the next ``__iter__`` over the same plan finds them ready
+        instead of refilling at the epoch boundary (reference ``run.py:233-243``: the DataLoader restarts its
+        workers every epoch)."""
+        if self._pending is not None and self._pending[0] is self.ds.items:
+            return
+        self._cancel()
+        self._pending = (self.ds.items,) + self._spawn(self.ds.items)
+
+    def __iter__(self):
+        items = self.ds.items
+        if self._pending is not None and self._pending[0] is items:
+            _, q, th, _stop = self._pending
+            self._pending = None
+        else:
+            self._cancel()
+            q, th, _stop = self._spawn(items)
+        done = False
+        try:
+            while True:
+                b = q.get()
+                if b is None:
+                    done = True
+                    break
+                yield b
+        finally:
+            if not done:   # abandoned early (limit_*_batches): stop the producer and free its pinned batches
+                self._stop_producer(q, th, _stop)
         th.join()
 
 
@@ -124,6 +170,12 @@ class DeviceLoader:
 
     def __len__(self):
         return len(self.host)
+
+    def start(self):
+        """Begin host reading of the source's current plan ahead of iteration (``NativeRawSource.start``)."""
+        st = getattr(self.host, "start", None)
+        if st is not None:
+            st()
 
     def _h2d(self, b: Dict):
         with torch.cuda.stream(self.copy_stream):

@@ -231,6 +231,10 @@ def training_function(args: Namespace) -> dict:
             # skip without decoding: drop the first `skip` batches of the epoch plan
             train_ds.items = train_ds.items[skip * args.batch_size:]
         it = iter(train_loader)
+        # steps this epoch runs (limit_train_batches breaks at step == limit), for reading the validation set's
+        # first batches ahead of the end of training
+        n_run = min(steps_per_epoch - skip, args.limit_train_batches + 1 - skip) if args.limit_train_batches >= 0 \
+            else steps_per_epoch - skip
         i = -1
         while True:
             timer.begin_step()
@@ -275,14 +279,22 @@ def training_function(args: Namespace) -> dict:
                 acc.save_state(output_dir)
                 acc.print(f"Saving checkpoint to {output_dir}")
             _maybe_inject_fault(global_step, args.output_dir)
+            if i + 3 >= n_run and hasattr(val_loader, "start"):
+                val_loader.start()
             if step == args.limit_train_batches:
                 break
+        if hasattr(it, "close"):   # a loop left at limit_train_batches: stop its reader now, not at collection
+            it.close()
         if acc.device.type == "cuda":
             torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         history["clips_per_sec"].append(clips / max(dt, 1e-9))
         if skip:
-            train_ds.set_epoch(epoch)
+            train_ds.set_epoch(epoch, force=True)
+        if epoch + 1 < args.num_epochs and hasattr(train_loader, "start"):
+            # the next epoch's first batches are read while this epoch's validation runs
+            train_ds.set_epoch(epoch + 1)
+            train_loader.start()
 
         # ---------------- evaluation
         bar.set_description_str("Val Epoch: %s" % epoch)

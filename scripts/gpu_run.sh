@@ -12,6 +12,8 @@
 #   trace    rocprofv3 kernel trace of 3 steps -> steady-state kernel table
 #   pmc      rocprofv3 PMC passes (one run each) over a bench step at B=$BATCH -> per-kernel summary
 #   runpy    the reference CLI (run.py) at the headline shape on a synthetic corpus
+#   lab      tools/gemm_lab.hip: big-tile GEMM main loop at $LAB_SHAPES ("M,N,K ..."), cold and L2-hot A operand,
+#            plus one PMC pass per shape (MFMA busy, waits, L2 hits)
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 out=gpurun_out/${OUT:-run}
@@ -82,6 +84,26 @@ t_runpy() {
     --limit_train_batches 10 --limit_val_batches 0 --num_workers 0 --output_dir /tmp/pva_run --quiet \
     > $out/run_py_${PRECISION:-bf16}.log 2>&1 || fail $out/run_py_${PRECISION:-bf16}.log
   grep -i "clips/s" $out/run_py_${PRECISION:-bf16}.log | tail -4
+}
+
+t_lab() {
+  /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -ffp-contract=fast -I csrc/kernels tools/gemm_lab.hip -o /tmp/gemm_lab > $out/lab_build.log 2>&1 || fail $out/lab_build.log
+  local sh
+  for sh in ${LAB_SHAPES:-"250880,1024,1024 62720,512,3072 250880,256,768"}; do
+    IFS=',' read -r m n k <<< "$sh"
+    timeout -k 10 120 /tmp/gemm_lab $m $n $k 20 0 >> $out/lab.txt 2>&1 || fail $out/lab.txt
+    timeout -k 10 120 /tmp/gemm_lab $m $n $k 20 1 >> $out/lab.txt 2>&1 || fail $out/lab.txt
+  done
+  cat $out/lab.txt
+  if [ -n "$LAB_PMC" ]; then
+    for sh in ${LAB_SHAPES:-"250880,1024,1024"}; do
+      IFS=',' read -r m n k <<< "$sh"
+      for hot in 0 1; do
+        timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_INSTS_MFMA GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d $out/labpmc/${m}_${hot} -o p -- /tmp/gemm_lab $m $n $k 5 $hot $LAB_PMC > $out/labpmc_${m}_${hot}.log 2>&1 || fail $out/labpmc_${m}_${hot}.log
+        timeout -s KILL 90 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-trace --output-format csv -d $out/labpmc2/${m}_${hot} -o p -- /tmp/gemm_lab $m $n $k 5 $hot $LAB_PMC > $out/labpmc2_${m}_${hot}.log 2>&1 || fail $out/labpmc2_${m}_${hot}.log
+      done
+    done
+  fi
 }
 
 for task in "$@"; do
