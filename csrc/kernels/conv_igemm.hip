@@ -248,6 +248,41 @@ void conv_igemm_kernel(const ConvParams p) {
       b_vo[s] = (idx < B_CHUNKS && n < p.Ngemm) ? (n * p.Kfull + bcol * 8) * 2 : 0;  // columns >= N: ignored
       sb[s] = lds_off<BK>(row, col);
     }
+    // UT bit 5 (LDS-DMA loader only): L2 touch-prefetch of the A rows one k-tile ahead of their LDS-DMA — one 4-byte
+    // DMA per 128-B row line into a per-wave dummy LDS slot, so the tile's real DMA finds its lines in L2 (twice the
+    // bytes in flight per CU at one instruction per wave and tile).  Always one touch per issued k-tile step (a touch
+    // past the last tile re-reads a line or reads out of range: zeros, harmless), so its vmcnt share is constant.
+    constexpr bool touch = (UT >> 5) & 1;
+    static_assert(!touch || glds_ut, "touch-prefetch rides on the LDS-DMA loader");
+    constexpr int TRPW = BM / NWAVES;   // A rows touched per wave
+    static_assert(!touch || TRPW <= 64, "one touched row per lane");
+    int t_vo = 0;
+    unsigned t_msk = 0;
+    bool t_on = false;
+    if constexpr (touch) {
+      const int row = wid * TRPW + lane;
+      const int m = m0 + row;
+      t_on = lane < TRPW && m < p.M;
+      int at = 0, ah = 0, aw = 0, off = 0;
+      if (t_on) {
+        const int b = m / RTHW;
+        int r = m - b * RTHW;
+        const int qt = r / RHW; r -= qt * RHW;
+        const int qh = r / p.Rw; const int qw = r - qh * p.Rw;
+        at = qt * p.ast + p.aot; ah = qh * p.ash + p.aoh; aw = qw * p.asw + p.aow;
+        off = (b * GTHW + (at * p.Gh + ah) * p.Gw + aw) * p.ldx;
+        if (check) {
+          int t = 0;
+          for (int jt = 0; jt < p.nt; ++jt)
+            for (int jh = 0; jh < p.nh; ++jh)
+              for (int jw = 0; jw < p.nw; ++jw, ++t)
+                if ((unsigned)(at + p.dir * jt) < (unsigned)p.Gt && (unsigned)(ah + p.dir * jh) < (unsigned)p.Gh &&
+                    (unsigned)(aw + p.dir * jw) < (unsigned)p.Gw)
+                  t_msk |= 1u << t;
+        }
+      }
+      t_vo = check ? off * 2 : (off + tmin) * 2;
+    }
     // uniform k cursor
     int kt_ = 0, kh_ = 0, kw_ = 0, t_ = 0, kb = 0, tapA = 0, tapW = 0;
     auto retap = [&]() {
@@ -350,6 +385,26 @@ void conv_igemm_kernel(const ConvParams p) {
         retap();
       }
     };
+    auto issue_touch = [&]() {   // rows of the tile at the cursor (the one after the tile just issued)
+      if constexpr (touch) {
+        char* dst = smem + MAIN_BYTES + RED_FLOATS * 4 + (EPI >= 1 ? 6 * BN * 4 : 0) + wid * 256;
+        const int ta = tapA + kb;
+        if (t_on) {
+#if defined(__HIP_DEVICE_COMPILE__)
+          if constexpr (check) {
+            const bool v = (t_msk >> t_) & 1u;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void*)dst, 4,
+                                                     v ? t_vo + ta * 2 : (int)OOB, 0, 0, 0);
+          } else {
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void*)dst, 4, t_vo,
+                                                     (ta - tmin) * 2, 0, 0);
+          }
+#endif
+        }
+      }
+    };
+    constexpr int NTOUCH_DMA = touch ? 1 : 0;   // touches younger than the DMA a 2-buffer wait needs
+    constexpr int NTOUCH_RING = touch ? NSTAGE - 1 : 0;   // ... than the DMA a ring wait needs
     // DMA instructions of one tile issued by this wave (A slots always; B slots only for waves whose rows exist)
     int nb_w = 0;
 #pragma unroll
@@ -357,9 +412,12 @@ void conv_igemm_kernel(const ConvParams p) {
     nb_w = __builtin_amdgcn_readfirstlane(nb_w);
     if constexpr (glds_ut) {
       issue_dma(0);
+      issue_touch();
 #pragma unroll
-      for (int i = 1; i + 1 < NSTAGE; ++i)
+      for (int i = 1; i + 1 < NSTAGE; ++i) {
         if (nsteps > i) issue_dma(i);
+        issue_touch();
+      }
     } else {
       // register ring one stage ahead of LDS: tile s+1 is written right after the barrier that frees its
       // buffer, and tile s+2 is re-issued immediately, so each load has a full k-step of MFMA to land
@@ -374,9 +432,10 @@ void conv_igemm_kernel(const ConvParams p) {
       // its first-half fragments are read while the second-half MFMAs of this tile run.  No k-step starts on
       // fragments still in flight; only barrier skew is exposed.
       ev8_t fa0[TM], fb0[TN], fa1[TM], fb1[TN];
-      vm_wait<0>();
+      vm_wait<NTOUCH_DMA>();
       __syncthreads();   // tile 0 landed
       if (nsteps > 1) issue_dma(1);
+      issue_touch();
 #pragma unroll
       for (int i = 0; i < TM; ++i) fa0[i] = *reinterpret_cast<const ev8_t*>(smem + fa[0][i]);
 #pragma unroll
@@ -394,12 +453,13 @@ void conv_igemm_kernel(const ConvParams p) {
           for (int j = 0; j < TN; ++j)
             acc[i][j] = PVA_MFMA16(fb0[j], fa0[i], acc[i][j], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
-        vm_wait<0>();   // this wave's DMA of tile step+1
+        vm_wait<NTOUCH_DMA>();   // this wave's DMA of tile step+1
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's reads of tile step
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         const bool more = step + 1 < nsteps;
         if (step + 2 < nsteps) issue_dma(cur);
+        issue_touch();
         const char* An = smem + (cur ^ 1) * TILE_BYTES;
         if (more) {
 #pragma unroll
@@ -430,16 +490,17 @@ void conv_igemm_kernel(const ConvParams p) {
         // raw s_barrier — __syncthreads would drain the pending LDS-DMA with vmcnt(0)); buffer
         // (step+NSTAGE-1)%NSTAGE held tile step-1, whose readers all passed this barrier
         if (NSTAGE == 4 && step + 2 < nsteps) {
-          vm_wait_dyn<2 * A_SLOTS, 2 * B_SLOTS>(2 * nb_w);   // leave the DMAs of tiles step+1 and step+2
+          vm_wait_dyn<2 * A_SLOTS + NTOUCH_RING, 2 * B_SLOTS>(2 * nb_w);   // leave the DMAs of tiles step+1, step+2
         } else if (step + 1 < nsteps) {
-          vm_wait_dyn<A_SLOTS, B_SLOTS>(nb_w);   // leave this wave's A_SLOTS + nb_w DMAs of tile step+1
+          vm_wait_dyn<A_SLOTS + NTOUCH_RING, B_SLOTS>(nb_w);   // leave this wave's A_SLOTS + nb_w DMAs of tile step+1
         } else {
-          vm_wait<0>();
+          vm_wait<NTOUCH_RING>();
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         if (step + NSTAGE - 1 < nsteps) issue_dma((step + NSTAGE - 1) % NSTAGE);
+        issue_touch();
         A = smem + (step % NSTAGE) * TILE_BYTES;
       } else if constexpr (glds_ut) {
         // 2 buffers (large tiles): tile step landed -> barrier -> DMA of tile step+1 during this step's MFMAs
@@ -621,6 +682,7 @@ void conv_igemm_kernel(const ConvParams p) {
       }
     }
   }
+  if constexpr ((UT >> 5) & 1) vm_wait<0>();   // touch-prefetch DMAs still landing in their dummy LDS slots
   if constexpr (EPI >= 1) __syncthreads();   // the fp32 staging below overwrites the k tiles
 
   // ---- epilogue: D[n][m] fragment: lane holds channels n..n+3 of position m ----
@@ -900,15 +962,19 @@ inline bool conv_ut_legal(const ConvParams& p, int ch, int bk) {
 }
 
 template <int BM, int BN, int WM, int WN, int CH, int BK>
-void launch_cfg(const ConvParams& p, int ut_force, hipStream_t stream, bool dma = false) {
+void launch_cfg(const ConvParams& p, int ut_force, hipStream_t stream, bool dma = false, bool pf = false) {
   constexpr int NT = (BM / WM) * (BN / WN) * 64;
   const int m_tiles = (p.M + BM - 1) / BM, n_tiles = (p.Ngemm + BN - 1) / BN;
   const bool epi = !p.fres && (p.eres || p.emask || p.epart);   // EPI 1 (the fres epilogue is EPI 0)
   constexpr int NW = (BM / WM) * (BN / WN);
   const size_t red_bytes = epi ? (NW * 3 + 6) * BN * 4 : (BM / WM) * 2 * BN * 4;
   const bool use_dma = CH == 8 && dma && !p.affine && conv_ut_legal(p, CH, BK) && ut_force != 0;
+  // touch-prefetch (cfg bit 12, UT bit 5): the 2-buffer BK=64 LDS-DMA loop of the big tiles only; 256 B of dummy LDS
+  // per wave where the input-affine table would be (the DMA loader never has one)
+  constexpr bool PF_OK = BM * BN >= 256 * 128 && BK == 64 && CH == 8;
+  const bool use_pf = PF_OK && pf && use_dma;
   const size_t lds = main_lds_bytes(BM, BN, BK, epi ? 1 : 0, dma_stages(BM, BN, BK, use_dma)) + red_bytes +
-                     (p.affine ? 2 * p.Cg * 4 : 0);
+                     (p.affine ? 2 * p.Cg * 4 : 0) + (use_pf ? NW * 256 : 0);
   const dim3 grid(m_tiles * n_tiles), block(NT);
   // heuristic (ut_force < 0), measured with scripts/conv_bench.py --ut 0/1/2: the uniform-tap loader wins
   // without reachable padding and for spatial (1,k,k) unit-stride gathers (with the consumer-side BN fold
@@ -924,7 +990,12 @@ void launch_cfg(const ConvParams& p, int ut_force, hipStream_t stream, bool dma 
       // lean epilogue (EPI 2): residual / ReLU bits / sum v only
       const bool lean = !p.accum && !p.ey0 && !p.ey1 && !p.emsc && !p.ebias;
       if (lean && ut) {
-        if (dma) {
+        if (dma && use_pf) {
+          if constexpr (PF_OK) {
+            if (p.check) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 2, 51>), grid, block, lds, stream, p);
+            else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 2, 49>), grid, block, lds, stream, p);
+          }
+        } else if (dma) {
           if (p.check) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 2, 19>), grid, block, lds, stream, p);
           else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 2, 17>), grid, block, lds, stream, p);
         } else {
@@ -933,7 +1004,12 @@ void launch_cfg(const ConvParams& p, int ut_force, hipStream_t stream, bool dma 
         }
         return;
       }
-      if (ut && dma) {
+      if (ut && dma && use_pf) {
+        if constexpr (PF_OK) {
+          if (p.check) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 1, 51>), grid, block, lds, stream, p);
+          else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 1, 49>), grid, block, lds, stream, p);
+        }
+      } else if (ut && dma) {
         if (p.check) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 1, 19>), grid, block, lds, stream, p);
         else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 1, 17>), grid, block, lds, stream, p);
       } else if (ut && p.check) {
@@ -945,7 +1021,12 @@ void launch_cfg(const ConvParams& p, int ut_force, hipStream_t stream, bool dma 
       }
       return;
     }
-    if (ut && dma && !p.affine) {
+    if (ut && dma && !p.affine && use_pf) {
+      if constexpr (PF_OK) {
+        if (p.check) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 0, 51>), grid, block, lds, stream, p);
+        else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 0, 49>), grid, block, lds, stream, p);
+      }
+    } else if (ut && dma && !p.affine) {
       if (p.check) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 0, 19>), grid, block, lds, stream, p);
       else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 0, 17>), grid, block, lds, stream, p);
     } else if (ut) {
@@ -995,16 +1076,16 @@ void launch_cfg(const ConvParams& p, int ut_force, hipStream_t stream, bool dma 
 }
 
 template <int CH, int BK>
-void launch_variant(int v, const ConvParams& p, int ut_force, hipStream_t stream, bool dma = false) {
+void launch_variant(int v, const ConvParams& p, int ut_force, hipStream_t stream, bool dma = false, bool pf = false) {
   switch (v) {
     case 0: launch_cfg<128, 128, 64, 64, CH, BK>(p, ut_force, stream, dma); break;
     case 1: launch_cfg<128, 64, 64, 32, CH, BK>(p, ut_force, stream, dma); break;
     case 2: launch_cfg<256, 32, 64, 32, CH, BK>(p, ut_force, stream, dma); break;
     case 4:
-      if constexpr (CH == 8) launch_cfg<256, 256, 128, 64, CH, BK>(p, ut_force, stream, dma);
+      if constexpr (CH == 8) launch_cfg<256, 256, 128, 64, CH, BK>(p, ut_force, stream, dma, pf);
       break;
     case 5:   // 256x128 of 4 waves (128x64 each, as the 256x256 tile's): two independent workgroups per CU
-      if constexpr (CH == 8) launch_cfg<256, 128, 128, 64, CH, BK>(p, ut_force, stream, dma);
+      if constexpr (CH == 8) launch_cfg<256, 128, 128, 64, CH, BK>(p, ut_force, stream, dma, pf);
       break;
     default: launch_cfg<256, 16, 64, 16, CH, BK>(p, ut_force, stream, dma); break;
   }
@@ -1025,7 +1106,8 @@ static int pick_variant(int M, int N) {
 // uniform-tap loader (bit 3), bit 4 set = explicit (else the built-in heuristic), bit 5 = the narrow
 // direct-to-register kernel of conv_direct.hip (bit 6: 2048 rows per workgroup, else 512), bit 7 = LDS-DMA
 // staging of the uniform-tap loader (launches without an input affine), bit 8 = 256x256 tile of 8 waves
-// (bit 0 with it: the 256x128 tile of 4 waves instead; overrides the tile bits).  -1 = heuristic.
+// (bit 0 with it: the 256x128 tile of 4 waves instead; overrides the tile bits; bit 12 with it and BK=64 LDS-DMA: L2
+// touch-prefetch of the A rows one k-tile ahead).  -1 = heuristic.
 int conv_direct_rows(int cfg);
 void conv_direct_launch(const ConvParams& p, int cfg, hipStream_t s);
 // bit 9 = the streaming pointwise kernel of conv_pw.hip (dense 1x1x1 GEMMs; bits 0-1: 1024 << v rows per
@@ -1063,7 +1145,7 @@ int conv_igemm_ut_legal(const ConvParams& p, int chunk, int bk) { return conv_ut
 void conv_igemm_launch(const ConvParams& p, int chunk, hipStream_t stream, int cfg) {
   if ((p.eres || p.emask || p.epart || p.fres) && chunk != 8) return;  // host binding rejects this combination
   int v, bk, ut_force;
-  bool dma = false;
+  bool dma = false, pf = false;
   if (cfg >= 0 && (cfg & 16) && (cfg & 2048)) {  // halo-staged 3x3 kernel (legality checked by the bindings)
     conv_halo_launch(p, cfg, stream);
     return;
@@ -1082,6 +1164,7 @@ void conv_igemm_launch(const ConvParams& p, int chunk, hipStream_t stream, int c
     bk = (cfg & 4) ? 64 : 32;
     ut_force = (cfg >> 3) & 1;
     dma = (cfg & 128) != 0;   // LDS-DMA staging (uniform-tap loader, no input affine)
+    pf = (cfg & 256) && (cfg & 4096);   // big tiles, BK=64 LDS-DMA: L2 touch-prefetch one k-tile ahead
   } else {
     v = pick_variant(p.M, p.Ngemm);
     const int K = p.nt * p.nh * p.nw * p.Cg;
@@ -1089,7 +1172,7 @@ void conv_igemm_launch(const ConvParams& p, int chunk, hipStream_t stream, int c
     ut_force = -1;
   }
   if (chunk == 8) {
-    if (bk == 64) launch_variant<8, 64>(v, p, ut_force, stream, dma); else launch_variant<8, 32>(v, p, ut_force, stream, dma);
+    if (bk == 64) launch_variant<8, 64>(v, p, ut_force, stream, dma, pf); else launch_variant<8, 32>(v, p, ut_force, stream, dma);
   } else {
     if (bk == 64) launch_variant<4, 64>(v, p, ut_force, stream); else launch_variant<4, 32>(v, p, ut_force, stream);
   }

@@ -239,7 +239,7 @@ class _ConvBN:
                 # under fold_slabs) are timed with their fixed-order reduction, whose cost grows with the split count
                 scratch = eng.scratch("wgrad_tune", s.cout * K)
                 cs_scr = eng.scratch("wgrad_tune_cs", 4096 * s.cout) if gram else None
-                cands, times = [], []
+                cands = []
                 for v in range(8):
                     vw = (v & 3) | (8 if v >= 4 else 0)
                     bmw, bnw = C.wgrad_tile(s.cout, K, vw)
@@ -289,22 +289,13 @@ class _ConvBN:
                         C.wgrad_reduce(part, gscr, sp, s.cout, s.taps, s.cin_pad, s.cin, 1.0, 0.0, 1)
                     else:
                         launch(c, scratch, cs_scr)
-                for c in cands:
-                    trial(c)
-                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                    e0.record()
-                    for _ in range(eng.tuner.reps):
-                        trial(c)
-                    e1.record()
-                    e1.synchronize()
-                    times.append(e0.elapsed_time(e1))
-                if eng.tuner.agree is not None:   # same choice on every data-parallel rank
-                    times = eng.tuner.agree(times)
+                # two-phase timing, agreed across data-parallel ranks (ops/tune.ConvTuner.time_candidates)
+                times = eng.tuner.time_candidates(cands, trial) if cands else []
                 cfg = cands[min(range(len(cands)), key=times.__getitem__)] if cands else -1
                 if eng.tuner.log:
                     import sys
                     print("wtune %s%s P=%d Cout=%d K=%d: " % (self.name, ".gram" if gram else "", dy.M, s.cout, K)
-                          + " ".join("%d=%.1fus" % (c, 1e3 * t / eng.tuner.reps) for c, t in zip(cands, times))
+                          + " ".join("%d=%.1fus" % (c, 1e3 * t) for c, t in zip(cands, times))
                           + " -> %d" % cfg, file=sys.stderr, flush=True)
             eng.wtune[tkey] = cfg
         # off the critical path: a weight gradient that lands in the flat buffer runs on the lane's wgrad

@@ -88,15 +88,17 @@ t_runpy() {
 
 t_lab() {
   /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -ffp-contract=fast -I csrc/kernels tools/gemm_lab.hip -o /tmp/gemm_lab > $out/lab_build.log 2>&1 || fail $out/lab_build.log
-  local sh
-  for sh in ${LAB_SHAPES:-"250880,1024,1024 62720,512,3072 250880,256,768"}; do
+  local sh shapes
+  shapes="${LAB_SHAPES:-250880,1024,1024 62720,512,3072 250880,256,768}"
+  for sh in $shapes; do
     IFS=',' read -r m n k <<< "$sh"
+    echo "shape $m $n $k" >> $out/lab.txt
     timeout -k 10 120 /tmp/gemm_lab $m $n $k 20 0 >> $out/lab.txt 2>&1 || fail $out/lab.txt
     timeout -k 10 120 /tmp/gemm_lab $m $n $k 20 1 >> $out/lab.txt 2>&1 || fail $out/lab.txt
   done
   cat $out/lab.txt
   if [ -n "$LAB_PMC" ]; then
-    for sh in ${LAB_SHAPES:-"250880,1024,1024"}; do
+    for sh in $shapes; do
       IFS=',' read -r m n k <<< "$sh"
       for hot in 0 1; do
         timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_INSTS_MFMA GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d $out/labpmc/${m}_${hot} -o p -- /tmp/gemm_lab $m $n $k 5 $hot $LAB_PMC > $out/labpmc_${m}_${hot}.log 2>&1 || fail $out/labpmc_${m}_${hot}.log

@@ -86,43 +86,54 @@ def test_slowfast_r101_32x2x256_step_vs_fp32_oracle():
 
 
 def test_fixed_batch_memorisation_tracks_fp32_oracle():
-    """40 SGD steps on ONE fixed batch of 32x2x224 clips (B=8, lr 0.02, momentum 0.9, no dropout), fused executor
-    and the fp32 PyTorch oracle side by side from the same weights: both memorise the batch (the loss falls well
-    below its start) and the fused plateau (mean of the last ten losses) lies within a stated band of the oracle's,
-    while the first steps track it closely.  (the plateau is judged against the oracle's own
-    trajectory, not a free threshold.)  Measured (profiles/r4_tests): the recipe overshoots at this batch (both rise
-    to ~90 by step 12, the fused run within 1-5 % of the oracle step for step until then), then both settle — fp32
-    oracle at 1.9-2.7, fused at 1.7-1.9 over the last ten steps."""
+    """40 SGD steps on ONE fixed batch of 32x2x224 clips (B=8, lr 0.01, momentum 0.9, no dropout): the fused executor,
+    the fp32 PyTorch oracle and the bf16-autocast oracle side by side from the same weights.  The
+    autocast oracle is the noise floor of 16-bit training: for each of the first 10 steps and for the plateau (mean
+    of the last ten losses) the fused run must stay within ``2 * |autocast - fp32| + 0.05`` of the fp32 oracle, and
+    all three must memorise the batch (loss well below its start)."""
     torch.manual_seed(0)
     model = R.create_slowfast(50, 400, dropout_rate=0.0)
+    lr = 0.01
     oracle = copy.deepcopy(model).to(DEV).train()
-    opt_ref = torch.optim.SGD(oracle.parameters(), lr=0.02, momentum=0.9, weight_decay=1e-4)
+    opt_ref = torch.optim.SGD(oracle.parameters(), lr=lr, momentum=0.9, weight_decay=1e-4)
+    ac = copy.deepcopy(model).to(DEV).train()
+    opt_ac = torch.optim.SGD(ac.parameters(), lr=lr, momentum=0.9, weight_decay=1e-4)
     eng = FusedNet(model, DEV)
-    opt = FusedSGD(eng.flat, lr=0.02, momentum=0.9, weight_decay=1e-4, after_step=eng.pack)
+    opt = FusedSGD(eng.flat, lr=lr, momentum=0.9, weight_decay=1e-4, after_step=eng.pack)
     B = 8
     xs = _clip(B, 32, 224, 4, seed=21)
     labels = torch.randint(0, 400, (B,), generator=torch.Generator().manual_seed(22)).to(DEV)
     xd = [x.to(DEV) for x in xs]
     acts = eng.prepare_inputs(xs)
-    ref, fused = [], []
+    ref, auto, fused = [], [], []
     for _ in range(40):
         opt_ref.zero_grad(set_to_none=True)
         loss_ref = F.cross_entropy(oracle(xd), labels)
         loss_ref.backward()
         opt_ref.step()
         ref.append(float(loss_ref))
+        opt_ac.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out_ac = ac(xd)
+        loss_ac = F.cross_entropy(out_ac.float(), labels)
+        loss_ac.backward()
+        opt_ac.step()
+        auto.append(float(loss_ac))
         opt.zero_grad()
         loss, _ = eng.forward_backward(acts, labels)
         opt.step()
         fused.append(float(loss))
-        print(f"step {len(ref)}: fp32 {ref[-1]:.3f} fused {fused[-1]:.3f}", flush=True)
-    print("fp32 ", " ".join("%.3f" % v for v in ref))
-    print("fused", " ".join("%.3f" % v for v in fused))
+        print(f"step {len(ref)}: fp32 {ref[-1]:.3f} autocast {auto[-1]:.3f} fused {fused[-1]:.3f}", flush=True)
+    print("fp32    ", " ".join("%.3f" % v for v in ref))
+    print("autocast", " ".join("%.3f" % v for v in auto))
+    print("fused   ", " ".join("%.3f" % v for v in fused))
     assert all(torch.isfinite(torch.tensor(fused)))
-    assert all(abs(a - b) < 0.05 * b for a, b in zip(fused[:3], ref[:3])), (fused[:3], ref[:3])
-    assert min(ref[-10:]) < 0.5 * ref[0] and min(fused[-10:]) < 0.5 * fused[0], (ref, fused)
-    pf, pr = sum(fused[-10:]) / 10, sum(ref[-10:]) / 10
-    assert abs(pf - pr) < 0.35 * pr + 0.15, (pf, pr)
+    for i in range(10):
+        assert abs(fused[i] - ref[i]) <= 2 * abs(auto[i] - ref[i]) + 0.05, (i, fused[i], ref[i], auto[i])
+    for tr in (ref, auto, fused):
+        assert min(tr[-10:]) < 0.5 * tr[0], tr
+    pf, pr, pa = sum(fused[-10:]) / 10, sum(ref[-10:]) / 10, sum(auto[-10:]) / 10
+    assert abs(pf - pr) <= 2 * abs(pa - pr) + 0.05, (pf, pr, pa)
 
 
 def test_small_batch_lr01_trajectory_tracks_fp32_oracle():

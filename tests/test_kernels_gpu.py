@@ -508,7 +508,7 @@ def test_conv_big_tile(case):
     + consumer affine for the register path) and plain dgrad phases."""
     from pytorchvideo_accelerate_amd.ops._ext import require
     from pytorchvideo_accelerate_amd.ops.conv import dgrad_phases, fwd_geometry
-    from pytorchvideo_accelerate_amd.ops.tune import BIG, BK64, DMA, EXPLICIT, UT
+    from pytorchvideo_accelerate_amd.ops.tune import BIG, BIG_HALF, BIG_PF, BK64, DMA, EXPLICIT, UT
     C = require()
     x, w, spec = _mk(case, seed=44)
     Ci = spec.cin
@@ -527,7 +527,8 @@ def test_conv_big_tile(case):
         if spec.cout < 256 or not C.conv_ut_legal(g, 8, bk):
             continue
         base = EXPLICIT | BIG | UT | (BK64 if bk == 64 else 0)
-        for cfg, aff in ((base, 0), (base | DMA, 0), (base, 2)):
+        pf = ((base | DMA | BIG_PF, 0), (base | BIG_HALF | DMA | BIG_PF, 0)) if bk == 64 else ()
+        for cfg, aff in ((base, 0), (base | DMA, 0), (base, 2)) + pf:
             y = torch.empty(M, spec.cout, device=DEV, dtype=torch.bfloat16)
             stats = torch.full(((M + 255) // 256, 2, spec.cout), float("nan"), device=DEV)
             C.conv_igemm(xa.t, wf, y, stats, sc if aff else None, sh if aff else None, aff, 0, g, 8, cfg)
@@ -544,7 +545,10 @@ def test_conv_big_tile(case):
     for bk in (32, 64):
         if Ci < 256 or not all(C.conv_ut_legal(list(gg), 8, bk) for gg in geo if gg[28]):
             continue
-        for cfg in (EXPLICIT | BIG | UT | (BK64 if bk == 64 else 0), EXPLICIT | BIG | UT | DMA | (BK64 if bk == 64 else 0)):
+        cfgs = (EXPLICIT | BIG | UT | (BK64 if bk == 64 else 0), EXPLICIT | BIG | UT | DMA | (BK64 if bk == 64 else 0))
+        if bk == 64:   # L2 touch-prefetch of the big tiles (tune.BIG_PF)
+            cfgs += (EXPLICIT | BIG | UT | DMA | BK64 | BIG_PF, EXPLICIT | BIG | BIG_HALF | UT | DMA | BK64 | BIG_PF)
+        for cfg in cfgs:
             out = torch.zeros(N * T * H * W, Ci, device=DEV, dtype=torch.bfloat16)
             for gg in geo:
                 if gg[28]:
@@ -560,7 +564,7 @@ def test_conv_big_tile_bn_epilogue(case):
     partial sums of v, v*xhat0, v*xhat1 (register and LDS-DMA loaders, BK 32/64)."""
     from pytorchvideo_accelerate_amd.ops._ext import require
     from pytorchvideo_accelerate_amd.ops.conv import dgrad_phases
-    from pytorchvideo_accelerate_amd.ops.tune import BIG, BK64, DMA, EXPLICIT, UT
+    from pytorchvideo_accelerate_amd.ops.tune import BIG, BIG_HALF, BIG_PF, BK64, DMA, EXPLICIT, UT
     C = require()
     x, w, spec = _mk(case, seed=45)
     N, Ci, T, H, W = x.shape
@@ -583,7 +587,8 @@ def test_conv_big_tile_bn_epilogue(case):
         if not C.conv_ut_legal(list(geo[0]), 8, bk):
             continue
         base = EXPLICIT | BIG | UT | (BK64 if bk == 64 else 0)
-        for cfg in (base, base | DMA):
+        pf = (base | DMA | BIG_PF, base | BIG_HALF | DMA | BIG_PF) if bk == 64 else ()
+        for cfg in (base, base | DMA) + pf:
             out = old.clone()
             part = torch.full(((M + 255) // 256, 3, Ci), float("nan"), device=DEV)
             C.conv_igemm_epi(dy.t, wd, out, 1, geo[0], 8, res, Ci, _bits(mask), y0, mean0, rstd0, y1, mean1, rstd1,

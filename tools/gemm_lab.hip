@@ -29,7 +29,8 @@ template <int BM, int BN, int WM, int WN, int BK, int UT>
 float run(ConvParams p, int iters) {
   constexpr int NT = (BM / WM) * (BN / WN) * 64;
   const int m_tiles = (p.M + BM - 1) / BM, n_tiles = (p.Ngemm + BN - 1) / BN;
-  const size_t lds = main_lds_bytes(BM, BN, BK, 0, dma_stages(BM, BN, BK, (UT & 17) == 17)) + (BM / WM) * 2 * BN * 4;
+  const size_t lds = main_lds_bytes(BM, BN, BK, 0, dma_stages(BM, BN, BK, (UT & 17) == 17)) + (BM / WM) * 2 * BN * 4 +
+                     ((UT & 32) ? (BM / WM) * (BN / WN) * 256 : 0);
   dim3 grid(m_tiles * n_tiles), block(NT);
   for (int i = 0; i < 2; ++i) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, 8, BK, 0, UT>), grid, block, lds, 0, p);
   hipEvent_t a, b;
@@ -65,6 +66,10 @@ int main(int argc, char** argv) {
       {"256x128/bk64/dma", run<256, 128, 128, 64, 64, 17>},
       {"256x128/bk32/dma", run<256, 128, 128, 64, 32, 17>},
       {"256x256/bk64/ut", run<256, 256, 128, 64, 64, 1>},
+      {"256x256/bk64/dma/pf", run<256, 256, 128, 64, 64, 49>},
+      {"256x256/bk32/dma/pf", run<256, 256, 128, 64, 32, 49>},
+      {"256x128/bk64/dma/pf", run<256, 128, 128, 64, 64, 49>},
+      {"256x128/bk32/dma/pf", run<256, 128, 128, 64, 32, 49>},
   };
   for (auto& v : vs) {
     if (!only.empty() && only != v.name) continue;
