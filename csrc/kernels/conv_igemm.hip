@@ -356,7 +356,9 @@ void conv_igemm_kernel(const ConvParams p) {
     // into LDS (lane-linear: the XOR swizzle moves to the source column), skipping the VGPR round trip and
     // the ds_write_b128 pass (~79 B/clk/CU, the LDS bottleneck of register staging).  Two buffers: the DMA
     // of tile s+1 is issued right after the barrier of step s and lands during its MFMAs.
-    auto issue_dma = [&](int buf) {
+    // live = false (interleaved schedule, UT bit 6): the same instructions with out-of-range offsets (zeros land in a
+    // buffer nobody reads any more), so the loop body stays one basic block the scheduler can interleave
+    auto issue_dma = [&](int buf, bool live = true) {
       char* A = smem + buf * TILE_BYTES;
       char* B = A + BM * BK * 2;
       const int ta = tapA + kb;
@@ -364,43 +366,49 @@ void conv_igemm_kernel(const ConvParams p) {
       for (int s = 0; s < A_SLOTS; ++s) {
         const int rs = __builtin_amdgcn_readfirstlane((s * NT + 64 * wid) / CPR);
         if constexpr (check) {
-          const bool v = (tmask[s] >> t_) & 1u;
+          const bool v = live && ((tmask[s] >> t_) & 1u);
           dma16(xr, A + rs * BK * 2, v ? a_vo[s] + ta * 2 : (int)OOB, 0);
         } else {
-          dma16(xr, A + rs * BK * 2, a_vo[s], (ta - tmin) * 2);
+          dma16(xr, A + rs * BK * 2, live ? a_vo[s] : (int)OOB, live ? (ta - tmin) * 2 : 0);
         }
       }
       const int wso = (tapW + kb) * 2;
 #pragma unroll
       for (int s = 0; s < B_SLOTS; ++s) {
-        if (s * NT + 64 * wid >= B_CHUNKS) break;   // wave-uniform (B_CHUNKS is a multiple of 64)
+        if constexpr (B_CHUNKS % NT != 0)
+          if (s * NT + 64 * wid >= B_CHUNKS) break;   // wave-uniform (B_CHUNKS is a multiple of 64)
         const int rs = __builtin_amdgcn_readfirstlane((s * NT + 64 * wid) / CPR);
-        dma16(wr, B + rs * BK * 2, b_vo[s], wso);
+        dma16(wr, B + rs * BK * 2, live ? b_vo[s] : (int)OOB, live ? wso : 0);
       }
+      // branch-free cursor advance (uniform selects): keeps the loop body one scheduling region
       kb += BK;
-      if (kb == p.Cg) {
-        kb = 0;
-        ++t_;
-        if (++kw_ == p.nw) { kw_ = 0; if (++kh_ == p.nh) { kh_ = 0; ++kt_; } }
-        retap();
-      }
+      const int wrap = kb == p.Cg;
+      kb = wrap ? 0 : kb;
+      t_ += wrap;
+      kw_ += wrap;
+      const int wh = kw_ == p.nw;
+      kw_ = wh ? 0 : kw_;
+      kh_ += wh;
+      const int wt = kh_ == p.nh;
+      kh_ = wt ? 0 : kh_;
+      kt_ += wt;
+      retap();
     };
     auto issue_touch = [&]() {   // rows of the tile at the cursor (the one after the tile just issued)
       if constexpr (touch) {
         char* dst = smem + MAIN_BYTES + RED_FLOATS * 4 + (EPI >= 1 ? 6 * BN * 4 : 0) + wid * 256;
         const int ta = tapA + kb;
-        if (t_on) {
+        // every lane issues (lanes without a row read out of range): no exec branch in the loop body
 #if defined(__HIP_DEVICE_COMPILE__)
-          if constexpr (check) {
-            const bool v = (t_msk >> t_) & 1u;
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void*)dst, 4,
-                                                     v ? t_vo + ta * 2 : (int)OOB, 0, 0, 0);
-          } else {
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void*)dst, 4, t_vo,
-                                                     (ta - tmin) * 2, 0, 0);
-          }
-#endif
+        if constexpr (check) {
+          const bool v = t_on && ((t_msk >> t_) & 1u);
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void*)dst, 4,
+                                                   v ? t_vo + ta * 2 : (int)OOB, 0, 0, 0);
+        } else {
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void*)dst, 4,
+                                                   t_on ? t_vo : (int)OOB, t_on ? (ta - tmin) * 2 : 0, 0, 0);
         }
+#endif
       }
     };
     constexpr int NTOUCH_DMA = touch ? 1 : 0;   // touches younger than the DMA a 2-buffer wait needs
@@ -458,9 +466,39 @@ void conv_igemm_kernel(const ConvParams p) {
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         const bool more = step + 1 < nsteps;
+        const char* An = smem + (cur ^ 1) * TILE_BYTES;
+        if constexpr ((UT >> 6) & 1) {
+          // UT bit 6: the DMA issue (9 VMEM) and the next tile's first-half fragment reads (12 DS) are interleaved
+          // with this tile's second-half MFMAs instead of preceding them: the two waves of a SIMD then cover each
+          // other's issue with MFMA work, where the plain form leaves the matrix pipe idle while both issue DMAs
+          // right after the barrier.  Branch-free (dead DMAs / reads at the tail are harmless) so the body is one
+          // scheduling region.
+          issue_dma(cur, step + 2 < nsteps);
+          issue_touch();
+#pragma unroll
+          for (int i = 0; i < TM; ++i) fa0[i] = *reinterpret_cast<const ev8_t*>(An + fa[0][i]);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) fb0[j] = *reinterpret_cast<const ev8_t*>(An + fb[0][j]);
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              acc[i][j] = PVA_MFMA16(fb1[j], fa1[i], acc[i][j], 0, 0, 0);
+#pragma unroll
+          for (int r = 0; r < (TM * TN) / 4; ++r) {
+            __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);   // one VMEM (LDS-DMA) read
+            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // two DS reads
+            __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);   // four MFMAs
+          }
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int i = 0; i < TM; ++i) fa1[i] = *reinterpret_cast<const ev8_t*>(An + fa[1][i]);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) fb1[j] = *reinterpret_cast<const ev8_t*>(An + fb[1][j]);
+          continue;
+        }
         if (step + 2 < nsteps) issue_dma(cur);
         issue_touch();
-        const char* An = smem + (cur ^ 1) * TILE_BYTES;
         if (more) {
 #pragma unroll
           for (int i = 0; i < TM; ++i) fa0[i] = *reinterpret_cast<const ev8_t*>(An + fa[0][i]);
@@ -682,7 +720,7 @@ void conv_igemm_kernel(const ConvParams p) {
       }
     }
   }
-  if constexpr ((UT >> 5) & 1) vm_wait<0>();   // touch-prefetch DMAs still landing in their dummy LDS slots
+  if constexpr ((UT >> 5) & 3) vm_wait<0>();   // touch-prefetch / dead tail DMAs still landing in LDS
   if constexpr (EPI >= 1) __syncthreads();   // the fp32 staging below overwrites the k tiles
 
   // ---- epilogue: D[n][m] fragment: lane holds channels n..n+3 of position m ----

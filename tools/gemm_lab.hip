@@ -31,6 +31,7 @@ float run(ConvParams p, int iters) {
   const int m_tiles = (p.M + BM - 1) / BM, n_tiles = (p.Ngemm + BN - 1) / BN;
   const size_t lds = main_lds_bytes(BM, BN, BK, 0, dma_stages(BM, BN, BK, (UT & 17) == 17)) + (BM / WM) * 2 * BN * 4 +
                      ((UT & 32) ? (BM / WM) * (BN / WN) * 256 : 0);
+  static_assert(!(UT & 64) || BK == 64, "interleaved schedule: BK=64 2-buffer loop");
   dim3 grid(m_tiles * n_tiles), block(NT);
   for (int i = 0; i < 2; ++i) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, 8, BK, 0, UT>), grid, block, lds, 0, p);
   hipEvent_t a, b;
@@ -70,6 +71,9 @@ int main(int argc, char** argv) {
       {"256x256/bk32/dma/pf", run<256, 256, 128, 64, 32, 49>},
       {"256x128/bk64/dma/pf", run<256, 128, 128, 64, 64, 49>},
       {"256x128/bk32/dma/pf", run<256, 128, 128, 64, 32, 49>},
+      {"256x256/bk64/dma/ilv", run<256, 256, 128, 64, 64, 81>},
+      {"256x256/bk64/dma/pf/ilv", run<256, 256, 128, 64, 64, 113>},
+      {"256x128/bk64/dma/pf/ilv", run<256, 128, 128, 64, 64, 113>},
   };
   for (auto& v : vs) {
     if (!only.empty() && only != v.name) continue;
