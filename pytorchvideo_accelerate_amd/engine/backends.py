@@ -3,7 +3,8 @@
 * :class:`FusedBackend` — the MI355X path: ``models/fused.FusedNet`` (gfx950 kernels, bf16 or fp16) with the
   bucketed RCCL gradient all-reduce of ``parallel/ddp.GradSync`` overlapped with the backward pass.
 * :class:`TorchBackend` — the reference PyTorch modules with autograd: CPU runs (``--cpu``, gloo DDP), fp32
-  (``--mixed_precision no``) or autocast fp16/bf16 on GPU.  Gradients land in the same flat buffer
+  (``--mixed_precision no``) or autocast fp16/bf16 on GPU; its bucketed all-reduce overlaps backward through
+  per-parameter gradient hooks, as DDP's reducer does.  Gradients land in the same flat buffer
   (``FlatParams``), so the optimizer, gradient sync and checkpointing code are shared.
 
 Both expose ``train_step(batch, labels, loss_scale, sync) -> (loss, logits)``, ``eval_step``,
@@ -42,6 +43,33 @@ class TorchBackend:
         self.timer = None
         if mixed_precision == "fp16" and self.device.type == "cuda":
             self.scaler = torch.amp.GradScaler("cuda")
+        self._install_overlap()
+
+    def _install_overlap(self):
+        """DDP-style overlap of the gradient all-reduce with autograd (reference run.py:196-198,257 via DDP's
+        reducer): a post-accumulate hook per parameter marks its gradient final; as soon as every parameter below a
+        flat offset is final (the flat buffer is in reverse execution order), ``GradSync.progress`` launches the
+        buckets that end there while backward continues.  Frozen parameters never get a gradient: they count as
+        final from the start."""
+        ps = self.flat.params
+        self._ends = [self.flat.span(p)[1] for p in ps]
+        self._frozen = [not p.requires_grad for p in ps]
+        self._ready = list(self._frozen)
+        self._front = 0
+        for i, p in enumerate(ps):
+            if p.requires_grad:
+                p.register_post_accumulate_grad_hook(lambda _p, i=i: self._on_grad(i))
+
+    def _on_grad(self, i: int):
+        if not self.sync.active:
+            return
+        self._ready[i] = True
+        f = self._front
+        while f < len(self._ready) and self._ready[f]:
+            f += 1
+        if f != self._front:
+            self._front = f
+            self.sync.progress(self._ends[f - 1])
 
     def _autocast(self):
         if self.amp_dtype is None:
@@ -71,9 +99,12 @@ class TorchBackend:
         scaled = loss * loss_scale
         if self.scaler is not None:
             scaled = self.scaler.scale(scaled)
-        scaled.backward()
-        self.flat.rebind()
+        self.flat.rebind()   # gradients accumulate in place into the flat buffer the buckets are cut from
         self.sync.begin(sync)
+        self._ready = list(self._frozen)
+        self._front = 0
+        scaled.backward()     # buckets are all-reduced from the gradient hooks as backward finalises them
+        self.flat.rebind()
         with (self.timer.phase("comm") if self.timer else contextlib.nullcontext()):
             self.sync.finish()
         return loss.detach(), out.detach().float()

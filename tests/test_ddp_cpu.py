@@ -78,3 +78,47 @@ def test_run_py_two_ranks_cpu(tmp_path):
     assert (d / "model.safetensors").exists() and (d / "random_states_0.pkl").exists()
     assert (d / "random_states_1.pkl").exists()
     assert (tmp_path / "out" / "final" / "optimizer.bin").exists() or (d / "optimizer.bin").exists()
+
+
+def test_torch_backend_overlaps_allreduce_with_backward():
+    """The PyTorch-module path (``--mixed_precision no`` / CPU) launches gradient buckets from autograd hooks while
+    backward runs (DDP-style overlap), front to back over the flat buffer, before ``finish``."""
+    import torch
+    from pytorchvideo_accelerate_amd.engine.backends import TorchBackend
+    from pytorchvideo_accelerate_amd.models import reference as R
+    from pytorchvideo_accelerate_amd.parallel.dist import DistState
+
+    torch.manual_seed(0)
+    model = R.create_slowfast(50, 5, dropout_rate=0.0, head_pool_kernel_sizes=((2, 2, 2), (8, 2, 2)))
+    be = TorchBackend(model, DistState(), "no")
+
+    class Rec:
+        active = False
+
+        def __init__(self):
+            self.calls, self.finished_after = [], None
+
+        def begin(self, sync=True):
+            self.active = sync
+
+        def progress(self, off):
+            self.calls.append(off)
+
+        def finish(self):
+            self.finished_after = len(self.calls)
+            self.active = False
+
+    rec = Rec()
+    be.sync = rec
+    be.train()
+    fast = torch.randn(2, 3, 8, 64, 64)
+    xs = [fast[:, :, ::4].contiguous(), fast]
+    be.train_step(xs, torch.tensor([1, 3]))
+    assert len(rec.calls) > 10, rec.calls
+    assert rec.calls == sorted(rec.calls) and rec.calls[-1] == be.flat.span(be.flat.params[-1])[1]
+    assert rec.finished_after == len(rec.calls)
+    # every bucket end is reached before finish(): nothing left for the end-of-backward flush
+    rec2 = Rec()
+    be.sync = rec2
+    be.train_step(xs, torch.tensor([0, 2]), sync=False)
+    assert rec2.calls == []
