@@ -1007,8 +1007,9 @@ void launch_cfg(const ConvParams& p, int ut_force, hipStream_t stream, bool dma 
   constexpr int NW = (BM / WM) * (BN / WN);
   const size_t red_bytes = epi ? (NW * 3 + 6) * BN * 4 : (BM / WM) * 2 * BN * 4;
   const bool use_dma = CH == 8 && dma && !p.affine && conv_ut_legal(p, CH, BK) && ut_force != 0;
-  // touch-prefetch (cfg bit 12, UT bit 5): the 2-buffer BK=64 LDS-DMA loop of the big tiles only; 256 B of dummy LDS
-  // per wave where the input-affine table would be (the DMA loader never has one)
+  // touch-prefetch (cfg bit 12, UT bit 5) with the interleaved issue schedule (UT bit 6): the 2-buffer BK=64 LDS-DMA
+  // loop of the big tiles only (tools/gemm_lab.hip: +9..33 % over the plain DMA loop at the res4/res5 shapes); 256 B
+  // of dummy LDS per wave where the input-affine table would be (the DMA loader never has one)
   constexpr bool PF_OK = BM * BN >= 256 * 128 && BK == 64 && CH == 8;
   const bool use_pf = PF_OK && pf && use_dma;
   const size_t lds = main_lds_bytes(BM, BN, BK, epi ? 1 : 0, dma_stages(BM, BN, BK, use_dma)) + red_bytes +
@@ -1030,8 +1031,8 @@ void launch_cfg(const ConvParams& p, int ut_force, hipStream_t stream, bool dma 
       if (lean && ut) {
         if (dma && use_pf) {
           if constexpr (PF_OK) {
-            if (p.check) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 2, 51>), grid, block, lds, stream, p);
-            else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 2, 49>), grid, block, lds, stream, p);
+            if (p.check) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 2, 115>), grid, block, lds, stream, p);
+            else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 2, 113>), grid, block, lds, stream, p);
           }
         } else if (dma) {
           if (p.check) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 2, 19>), grid, block, lds, stream, p);
@@ -1044,8 +1045,8 @@ void launch_cfg(const ConvParams& p, int ut_force, hipStream_t stream, bool dma 
       }
       if (ut && dma && use_pf) {
         if constexpr (PF_OK) {
-          if (p.check) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 1, 51>), grid, block, lds, stream, p);
-          else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 1, 49>), grid, block, lds, stream, p);
+          if (p.check) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 1, 115>), grid, block, lds, stream, p);
+          else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 1, 113>), grid, block, lds, stream, p);
         }
       } else if (ut && dma) {
         if (p.check) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 1, 19>), grid, block, lds, stream, p);
@@ -1061,8 +1062,8 @@ void launch_cfg(const ConvParams& p, int ut_force, hipStream_t stream, bool dma 
     }
     if (ut && dma && !p.affine && use_pf) {
       if constexpr (PF_OK) {
-        if (p.check) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 0, 51>), grid, block, lds, stream, p);
-        else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 0, 49>), grid, block, lds, stream, p);
+        if (p.check) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 0, 115>), grid, block, lds, stream, p);
+        else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 0, 113>), grid, block, lds, stream, p);
       }
     } else if (ut && dma && !p.affine) {
       if (p.check) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CH, BK, 0, 19>), grid, block, lds, stream, p);

@@ -17,6 +17,8 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--depth", type=int, default=50)
     ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--frames", type=int, default=32)
+    ap.add_argument("--crop", type=int, default=224)
     a = ap.parse_args()
     from pytorchvideo_accelerate_amd.models import reference as R
     from pytorchvideo_accelerate_amd.models.fused import FusedNet
@@ -24,17 +26,21 @@ def main():
     from pytorchvideo_accelerate_amd.data.transforms import GpuClipBatch, sample_params
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
-    eng = FusedNet(R.create_slowfast(a.depth, 400), dev)
+    T, S = a.frames, a.crop
+    eng = FusedNet(R.create_slowfast(a.depth, 400, head_pool_kernel_sizes=((T // 4, S // 32, S // 32), (T, S // 32, S // 32))), dev)
     opt = FusedSGD(eng.flat, lr=0.1, momentum=0.9, weight_decay=1e-4, after_step=eng.pack)
     B = a.batch
-    frames = torch.empty(B, 64, 256, 340, 3, dtype=torch.uint8, device=dev)
+    src_t = 2 * T
+    frames = torch.empty(B, src_t, 256 if S <= 256 else S, 340 if S <= 256 else S * 4 // 3, 3, dtype=torch.uint8,
+                         device=dev)
     eng.C.synth_frames(frames, 1)
-    prep = GpuClipBatch(dev, 32, 224, 4, s2d=eng.input_s2d)
+    prep = GpuClipBatch(dev, T, S, 4, s2d=eng.input_s2d)
     g = torch.Generator().manual_seed(0)
     labels = torch.randint(0, 400, (B,), generator=g).to(dev)
     rows = None
     for it in range(a.steps + 1):
-        xs = prep(frames, [sample_params(64, 256, 340, 32, 224, True, generator=g) for _ in range(B)])
+        xs = prep(frames, [sample_params(src_t, frames.shape[2], frames.shape[3], T, S, True, generator=g)
+                           for _ in range(B)])
         opt.zero_grad()
         if it == a.steps:
             eng.prof = []

@@ -12,8 +12,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from pytorchvideo_accelerate_amd.models import reference as R  # noqa: E402
 
 
-def conv_shapes(batch, T=32, S=224, alpha=4):
-    net = R.create_slowfast(50, 400)
+def conv_shapes(batch, T=32, S=224, alpha=4, depth=50):
+    net = R.create_slowfast(depth, 400, head_pool_kernel_sizes=((T // alpha, S // 32, S // 32), (T, S // 32, S // 32)))
     shapes = {}
     hooks = []
 
@@ -52,8 +52,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dump")
     ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--frames", type=int, default=32)
+    ap.add_argument("--crop", type=int, default=224)
+    ap.add_argument("--depth", type=int, default=50)
     a = ap.parse_args()
-    sh = conv_shapes(a.batch)
+    sh = conv_shapes(a.batch, a.frames, a.crop, 4, a.depth)
     rows = [l.split() for l in open(a.dump) if l.strip().endswith(" us")]
     print(f"{'op':26s} {'us':>8s} {'TF/s':>7s} {'GB min':>7s} {'TB/s':>6s}")
     agg = collections.defaultdict(lambda: [0.0, 0.0, 0.0])

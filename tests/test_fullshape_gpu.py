@@ -86,14 +86,16 @@ def test_slowfast_r101_32x2x256_step_vs_fp32_oracle():
 
 
 def test_fixed_batch_memorisation_tracks_fp32_oracle():
-    """40 SGD steps on ONE fixed batch of 32x2x224 clips (B=8, lr 0.01, momentum 0.9, no dropout): the fused executor,
+    """40 SGD steps on ONE fixed batch of 32x2x224 clips (B=8, lr 0.003, momentum 0.9, no dropout): the fused executor,
     the fp32 PyTorch oracle and the bf16-autocast oracle side by side from the same weights.  The
     autocast oracle is the noise floor of 16-bit training: for each of the first 10 steps and for the plateau (mean
     of the last ten losses) the fused run must stay within ``2 * |autocast - fp32| + 0.05`` of the fp32 oracle, and
-    all three must memorise the batch (loss well below its start)."""
+    all three must memorise the batch (loss well below its start).  (At lr 0.01 all three trajectories, the fp32
+    oracle's included, leave the memorising regime after ~10 steps and wander chaotically up to loss ~20: the fused run
+    tracked fp32 within 0.01-0.06 for those 10 steps, gpurun_out r5pf; the gate runs in the stable regime.)"""
     torch.manual_seed(0)
     model = R.create_slowfast(50, 400, dropout_rate=0.0)
-    lr = 0.01
+    lr = 0.003
     oracle = copy.deepcopy(model).to(DEV).train()
     opt_ref = torch.optim.SGD(oracle.parameters(), lr=lr, momentum=0.9, weight_decay=1e-4)
     ac = copy.deepcopy(model).to(DEV).train()
