@@ -94,4 +94,9 @@ void head_backward_launch(const float* dlogits, const float* xm, const float* W,
                           float p_drop, uint64_t seed, const uint64_t* seedp, float* dW, float* db, float beta,
                           float* dfeat, float* dlT, float* xmT, float* WT, hipStream_t s);
 void head_dropout_mask_launch(int64_t total, float p_drop, uint64_t seed, uint8_t* out, hipStream_t s);
-
+int narrow_c_bwd_legal(int CO, int CI);
+int narrow_c_bwd_rps(int64_t M, int CO, int splits);
+void narrow_c_bwd_launch(const uint16_t* g, int ldg, int mode, const uint8_t* mask, const uint16_t* yc,
+                         const float* coef, uint16_t* dz, int lddz, int dz_accum, const uint16_t* yb, const float* sb,
+                         const float* hb, const float* mb, const float* rb, const uint16_t* wc, uint16_t* dab,
+                         float* slab, float* part, int64_t M, int CO, int CI, int rps, hipStream_t s);

@@ -1,0 +1,226 @@
+// Fused backward of a narrow 1x1 conv_c whose BatchNorm is not folded (the fast pathway's res2 units: 8 -> 32
+// channels at 16M positions per step at B=160).  One streaming pass replaces three:
+//
+//   BN-backward apply   dyc = A*dz + B*yc + C          dz = g (masked by the unit's ReLU bits)
+//   weight gradient     dWc[c][k] += dyc[c] * act_b[k]     act_b = relu(yb*sb + hb) (BN_b + ReLU recompute)
+//   input gradient      v[k] = sum_c dyc[c] Wc[c][k], masked by act_b > 0; BN_b backward partial sums of v
+//   identity shortcut   dz itself into dx (optional, written or accumulated)
+//
+// so dyc (the widest tensor of the unit's backward) is never written to HBM and read back twice.  The per-element
+// arithmetic follows the unfused kernels: dyc rounded to the 16-bit type (as the apply stored it), act_b rounded
+// after the affine (as the weight-gradient loader staged it), dab rounded before its partial sums (as the dgrad
+// epilogue did).
+//
+// Layout: LPR = CO / 8 lanes per row, each owning 8 output channels c (16-B loads of g / yc / dz); every lane keeps
+// the 8 x CI partial weight gradient of its channels in registers over the workgroup's row range, and the 8 x CI
+// slice of Wc.  The per-row dgrad partials are summed over the row's lanes with xor shuffles; lane q then finishes
+// input channels k = q*CI/LPR .. (q+1)*CI/LPR - 1 (mask, round, store, partial sums).  Workgroup w owns rows
+// [w*rps, (w+1)*rps): its weight-gradient slab and BN partial sums are written once, summed in a fixed order by the
+// slab reduction / BN finalize (bitwise reproducible).
+#include "common.h"
+
+PVA_NS_BEGIN
+
+namespace {
+
+struct NarrowBwdParams {
+  const uint16_t* g;      // [M][ldg] unit-output gradient (already masked when mode == 0)
+  const uint8_t* mask;    // mode 3: ReLU bits [M][CO/8]
+  const uint16_t* yc;     // raw conv_c output [M][CO]
+  const float* coef;      // BN_c backward coefficients [A | B | C] x CO
+  uint16_t* dz;           // optional identity-shortcut gradient out [M][lddz]
+  const uint16_t* yb;     // raw conv_b output [M][CI] (conv_c input before BN_b + ReLU)
+  const float* sb;        // BN_b scale / shift (forward affine)
+  const float* hb;
+  const float* mb;        // BN_b batch mean / rstd (partial-sum rebase)
+  const float* rb;
+  const uint16_t* wc;     // packed conv_c weights [CO][CI]
+  uint16_t* dab;          // [M][CI] input gradient of conv_c, masked (BN_b ReLU)
+  float* slab;            // [splits][CO][CI] weight-gradient partials
+  float* part;            // [splits][3][CI] BN_b partial sums (sum v, sum v*xhat_b, 0)
+  int64_t M;
+  int ldg, lddz, dz_accum, mode, rps;
+};
+
+template <int CO, int CI>
+__global__ __launch_bounds__(256) void narrow_c_bwd_kernel(const NarrowBwdParams p) {
+  constexpr int LPR = CO / 8;            // lanes per row
+  constexpr int RPW = 64 / LPR;          // rows per wave and pass
+  constexpr int KPL = CI / LPR;          // input channels finished per lane
+  static_assert(CO % 8 == 0 && 64 % LPR == 0 && CI % LPR == 0 && CI == 8, "narrow_c_bwd: CO 8..64, CI 8");
+  __shared__ float red[4][LPR][8 * CI + 2 * CI];
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int q = lane % LPR, rr = lane / LPR;
+  const int c0 = 8 * q;
+  float A[8], B[8], Cc[8], W[8][CI], sb[CI], hb[CI];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    A[e] = p.coef[c0 + e];
+    B[e] = p.coef[CO + c0 + e];
+    Cc[e] = p.coef[2 * CO + c0 + e];
+#pragma unroll
+    for (int k = 0; k < CI; ++k) W[e][k] = e2f(p.wc[(c0 + e) * CI + k]);
+  }
+#pragma unroll
+  for (int k = 0; k < CI; ++k) { sb[k] = p.sb[k]; hb[k] = p.hb[k]; }
+  float acc[8][CI];
+#pragma unroll
+  for (int e = 0; e < 8; ++e)
+#pragma unroll
+    for (int k = 0; k < CI; ++k) acc[e][k] = 0.f;
+  float sv[KPL], sy[KPL];
+#pragma unroll
+  for (int j = 0; j < KPL; ++j) { sv[j] = 0.f; sy[j] = 0.f; }
+
+  const int64_t r_begin = (int64_t)blockIdx.x * p.rps;
+  const int64_t r_end = r_begin + p.rps < p.M ? r_begin + p.rps : p.M;
+  for (int64_t r = r_begin + w * RPW + rr; r < r_end; r += 4 * RPW) {
+    float gz[8], yc[8], yb[CI];
+    unpack8(*reinterpret_cast<const uint4*>(p.g + r * p.ldg + c0), gz);
+    unpack8(*reinterpret_cast<const uint4*>(p.yc + r * CO + c0), yc);
+    unpack8(*reinterpret_cast<const uint4*>(p.yb + r * CI), yb);
+    if (p.mode == 3) {
+      const unsigned bits = p.mask[r * (CO / 8) + q];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) gz[e] = (bits >> e) & 1u ? gz[e] : 0.f;
+    }
+    if (p.dz) {
+      uint16_t* d = p.dz + r * p.lddz + c0;
+      float o[8] = {gz[0], gz[1], gz[2], gz[3], gz[4], gz[5], gz[6], gz[7]};
+      if (p.dz_accum) {
+        float x[8];
+        unpack8(*reinterpret_cast<const uint4*>(d), x);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] += x[e];
+      }
+      *reinterpret_cast<uint4*>(d) = pack8(o);
+    }
+    // dyc, rounded to the compute type (the unfused apply stored it so)
+    float dy[8];
+    {
+      float t[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) t[e] = A[e] * gz[e] + B[e] * yc[e] + Cc[e];
+      unpack8(pack8(t), dy);
+    }
+    // act_b = relu(BN_b(yb)) as the weight-gradient loader stages it (affine, round, ReLU)
+    float ab[CI];
+    {
+      float t[CI];
+#pragma unroll
+      for (int k = 0; k < CI; ++k) t[k] = __builtin_fmaf(yb[k], sb[k], hb[k]);
+      uint4 v = relu_e16x8(pack8_fast(t));
+      unpack8(v, ab);
+    }
+    float pd[CI];
+#pragma unroll
+    for (int k = 0; k < CI; ++k) pd[k] = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+#pragma unroll
+      for (int k = 0; k < CI; ++k) {
+        acc[e][k] = __builtin_fmaf(dy[e], ab[k], acc[e][k]);
+        pd[k] = __builtin_fmaf(dy[e], W[e][k], pd[k]);
+      }
+    // sum the row's LPR lanes (adjacent lanes): every lane ends with the row's full dgrad
+#pragma unroll
+    for (int o = 1; o < LPR; o <<= 1)
+#pragma unroll
+      for (int k = 0; k < CI; ++k) pd[k] += __shfl_xor(pd[k], o, 64);
+    // lane q: input channels k = q*KPL + j — BN_b ReLU mask (affine of yb > 0), round, store, partial sums
+    float v[KPL];
+#pragma unroll
+    for (int j = 0; j < KPL; ++j) {
+      const int k = q * KPL + j;
+      float pk = 0.f, yk = 0.f, sk = 0.f, hk = 0.f;
+#pragma unroll
+      for (int kk = 0; kk < CI; ++kk)
+        if (kk == k) { pk = pd[kk]; yk = yb[kk]; sk = sb[kk]; hk = hb[kk]; }
+      v[j] = (yk * sk + hk) > 0.f ? pk : 0.f;
+      v[j] = e2f(f2e(v[j]));
+      sv[j] += v[j];
+      sy[j] += v[j] * yk;
+    }
+    uint16_t* dst = p.dab + r * CI + q * KPL;
+    if constexpr (KPL == 2) {
+      *reinterpret_cast<uint32_t*>(dst) = cvt_pk_e16(v[0], v[1]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < KPL; ++j) dst[j] = f2e(v[j]);
+    }
+  }
+  // weight gradient: lanes of the same channel group q (stride LPR) -> one value per (c, k) per wave
+#pragma unroll
+  for (int e = 0; e < 8; ++e)
+#pragma unroll
+    for (int k = 0; k < CI; ++k) {
+      float t = acc[e][k];
+#pragma unroll
+      for (int o = LPR; o < 64; o <<= 1) t += __shfl_xor(t, o, 64);
+      acc[e][k] = t;
+    }
+#pragma unroll
+  for (int j = 0; j < KPL; ++j)
+#pragma unroll
+    for (int o = LPR; o < 64; o <<= 1) {
+      sv[j] += __shfl_xor(sv[j], o, 64);
+      sy[j] += __shfl_xor(sy[j], o, 64);
+    }
+  if (rr == 0) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+#pragma unroll
+      for (int k = 0; k < CI; ++k) red[w][q][e * CI + k] = acc[e][k];
+#pragma unroll
+    for (int j = 0; j < KPL; ++j) {
+      red[w][q][8 * CI + j] = sv[j];
+      red[w][q][8 * CI + CI + j] = sy[j];
+    }
+  }
+  __syncthreads();
+  float* slab = p.slab + (int64_t)blockIdx.x * CO * CI;
+  for (int i = tid; i < CO * CI; i += 256) {
+    const int c = i / CI, k = i - c * CI;
+    const int qq = c / 8, e = c - qq * 8;
+    slab[i] = ((red[0][qq][e * CI + k] + red[1][qq][e * CI + k]) + red[2][qq][e * CI + k]) + red[3][qq][e * CI + k];
+  }
+  if (tid < CI) {
+    const int k = tid, qq = k / KPL, j = k - qq * KPL;
+    const float s = ((red[0][qq][8 * CI + j] + red[1][qq][8 * CI + j]) + red[2][qq][8 * CI + j]) + red[3][qq][8 * CI + j];
+    const float y = ((red[0][qq][9 * CI + j] + red[1][qq][9 * CI + j]) + red[2][qq][9 * CI + j]) +
+                    red[3][qq][9 * CI + j];
+    float* pt = p.part + (int64_t)blockIdx.x * 3 * CI;
+    pt[k] = s;
+    pt[CI + k] = (y - p.mb[k] * s) * p.rb[k];
+    pt[2 * CI + k] = 0.f;
+  }
+}
+
+}  // namespace
+
+int narrow_c_bwd_legal(int CO, int CI) { return (CO == 32 || CO == 16 || CO == 64) && CI == 8; }
+
+// rows per workgroup (multiple of one pass of 4 waves) for a split count near `splits`
+int narrow_c_bwd_rps(int64_t M, int CO, int splits) {
+  const int pass = 4 * (64 / (CO / 8));
+  int64_t rps = (M + splits - 1) / splits;
+  rps = (rps + pass - 1) / pass * pass;
+  return (int)(rps < pass ? pass : rps);
+}
+
+void narrow_c_bwd_launch(const uint16_t* g, int ldg, int mode, const uint8_t* mask, const uint16_t* yc,
+                         const float* coef, uint16_t* dz, int lddz, int dz_accum, const uint16_t* yb, const float* sb,
+                         const float* hb, const float* mb, const float* rb, const uint16_t* wc, uint16_t* dab,
+                         float* slab, float* part, int64_t M, int CO, int CI, int rps, hipStream_t s) {
+  NarrowBwdParams p{g, mask, yc, coef, dz, yb, sb, hb, mb, rb, wc, dab, slab, part, M, ldg, lddz, dz_accum, mode, rps};
+  const int grid = (int)((M + rps - 1) / rps);
+  if (grid <= 0) return;
+  switch (CO) {
+    case 16: hipLaunchKernelGGL((narrow_c_bwd_kernel<16, 8>), dim3(grid), dim3(256), 0, s, p); break;
+    case 64: hipLaunchKernelGGL((narrow_c_bwd_kernel<64, 8>), dim3(grid), dim3(256), 0, s, p); break;
+    default: hipLaunchKernelGGL((narrow_c_bwd_kernel<32, 8>), dim3(grid), dim3(256), 0, s, p); break;
+  }
+}
+
+PVA_NS_END  // namespace PVA_NS

@@ -578,6 +578,26 @@ void head_dropout_mask(const at::Tensor& out, double p_drop, int64_t seed) {
   pva_bf16::head_dropout_mask_launch(out.numel(), (float)p_drop, (uint64_t)seed, out.data_ptr<uint8_t>(), cur_stream());
 }
 
+// fused BN-backward apply + weight gradient + input gradient of a narrow 1x1 conv_c (narrow_bwd.hip)
+void narrow_c_bwd(const at::Tensor& g, int64_t ldg, int64_t mode, const OptT& mask, const at::Tensor& yc,
+                  const at::Tensor& coef, const OptT& dz, int64_t lddz, int64_t dz_accum, const at::Tensor& yb,
+                  const at::Tensor& sb, const at::Tensor& hb, const at::Tensor& mb, const at::Tensor& rb,
+                  const at::Tensor& wc, const at::Tensor& dab, const at::Tensor& slab, const at::Tensor& part, int64_t M,
+                  int64_t CO, int64_t CI, int64_t rps) {
+  const bool h = kind16(g);
+  TORCH_CHECK(pva_bf16::narrow_c_bwd_legal((int)CO, (int)CI), "narrow_c_bwd: unsupported channels");
+  TORCH_CHECK(mode == 0 || (mode == 3 && mask.has_value()), "narrow_c_bwd: mask mode 0 or 3 (bits)");
+  TORCH_CHECK(yc.numel() >= M * CO && yb.numel() >= M * CI && dab.numel() >= M * CI && wc.numel() >= CO * CI,
+              "narrow_c_bwd: tensor sizes");
+  TORCH_CHECK(ldg % 8 == 0 && (!dz.has_value() || lddz % 8 == 0), "narrow_c_bwd: 16-B aligned rows");
+  const int64_t splits = (M + rps - 1) / rps;
+  TORCH_CHECK(slab.numel() >= splits * CO * CI && part.numel() >= splits * 3 * CI, "narrow_c_bwd: slabs too small");
+  KSEL(h, narrow_c_bwd_launch)(bfp(g), (int)ldg, (int)mode, mask.has_value() ? mask->data_ptr<uint8_t>() : nullptr,
+                               bfp(yc), f32(coef), dz.has_value() ? bfpm(*dz) : nullptr, (int)lddz, (int)dz_accum,
+                               bfp(yb), f32(sb), f32(hb), f32(mb), f32(rb), bfp(wc), bfpm(dab), f32(slab), f32(part), M,
+                               (int)CO, (int)CI, (int)rps, cur_stream());
+}
+
 void synth_frames(const at::Tensor& out, int64_t seed) {
   pva_bf16::synth_frames_launch(out.data_ptr<uint8_t>(), out.numel(), (uint32_t)seed, cur_stream());
 }
@@ -712,6 +732,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("pack_desc_size", &pva_bf16::pack_desc_size);
   m.def("video_preprocess", &video_preprocess);
   m.def("synth_frames", &synth_frames);
+  m.def("narrow_c_bwd", &narrow_c_bwd);
+  m.def("narrow_c_bwd_legal", [](int64_t CO, int64_t CI) { return (bool)pva_bf16::narrow_c_bwd_legal((int)CO, (int)CI); });
+  m.def("narrow_c_bwd_rps", [](int64_t M, int64_t CO, int64_t splits) {
+    return (int64_t)pva_bf16::narrow_c_bwd_rps(M, (int)CO, (int)splits);
+  });
   m.def("stem_tiles", [](int64_t Ho, int64_t Wo, int64_t N) { return pva_bf16::stem_tiles((int)Ho, (int)Wo, (int)N); });
   m.def("stem_supported", [](int64_t Cout, int64_t kt) { return pva_bf16::stem_s2d_supported((int)Cout, (int)kt); });
   m.def("head_forward", &head_forward, py::arg("feat"), py::arg("W"), py::arg("b"), py::arg("p_drop"), py::arg("seed"),

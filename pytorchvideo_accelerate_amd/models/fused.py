@@ -720,6 +720,9 @@ class _ResBlock:
         # BN folding of a stride-1 1x1 branch1 in the BACKWARD (slow res2 unit 0): its BN backward and weight/input
         # gradients come from G1 = dz^T x and the Gram matrix of x (_ConvBN.fold_branch1_*), so neither the
         # branch-1 BN-backward apply pass (dy1) nor the dual y1 read in the next unit's dgrad epilogue happens
+        # narrow unfolded 1x1 conv_c (fast res2: 8 -> 32): fused BN-apply + wgrad + dgrad backward (_bwd_narrow)
+        self.narrow_c = (not self.fold and eng.narrow_bwd and tuple(sc.k) == (1, 1, 1) and tuple(sc.stride) == (1, 1, 1)
+                         and sc.cin == 8 and sc.cin_pad == 8 and bool(eng.C.narrow_c_bwd_legal(sc.cout, sc.cin)))
         s1 = self.one.spec if self.one is not None else None
         self.fold1 = (self.fold and s1 is not None and eng.bn_fold1 and tuple(s1.k) == (1, 1, 1)
                       and tuple(s1.stride) == (1, 1, 1) and s1.cin % 8 == 0 and s1.cin == s1.cin_pad
@@ -775,6 +778,8 @@ class _ResBlock:
         res = None
         if self.fold:
             return self._bwd_fold(dout, dx, dx_accum, pre, prev)
+        if self.narrow_c:
+            return self._bwd_narrow(dout, dx, dx_accum, pre, prev)
         if pre is not None:
             dyc, dy1 = self.c.bn_backward(dout, yc, 0, None, None, other=self.one, other_y=y1, pre=pre)
             if self.one is None:
@@ -801,6 +806,75 @@ class _ResBlock:
             if self._strided_one(prev):
                 return self._dgrad_strided_one(dya, dy1, dx, dx_accum)
             self.one.dgrad(dy1, (x.T, x.H, x.W), dx, dx_accum)
+            acc = True
+        else:
+            acc = dx_accum if pre is not None else True
+        if prev is not None and not self._epi_ok(prev):
+            prev = None
+        if res is None and prev is None:
+            self.a.dgrad(dya, (x.T, x.H, x.W), dx, acc)
+            return None
+        return self.a.dgrad(dya, (x.T, x.H, x.W), dx, acc, res=res, epi=prev)
+
+    def _bwd_narrow(self, dout: Act, dx: torch.Tensor, dx_accum: bool, pre, prev: Optional["_ResBlock"]):
+        """Backward of a unit with a narrow, unfolded 1x1 conv_c (fast res2: 8 -> 32): the BN_c backward apply, the
+        conv_c weight gradient and its input gradient (with BN_b's ReLU mask and BN-backward partial sums) in ONE
+        streaming pass (csrc/kernels/narrow_bwd.hip), so dyc never reaches HBM; branch1's dy1 keeps its own apply."""
+        eng, C = self.eng, self.eng.C
+        x, ya, yb, yc, y1, one, c = self.x, self.ya, self.yb, self.yc, self.y1, self.one, self.c
+        dxa = Act(dx, x.N, x.T, x.H, x.W)
+        M, Cc = yc.M, c.C
+        fg = eng.flat
+        res = None
+        if pre is not None:   # dout is the masked dz, its partial sums came from the next unit's dgrad epilogue
+            part, blocks = pre
+            mode, mask, dz_out = 0, None, None
+            if one is None:
+                res = dout
+        else:
+            mode, mask = 3, self.mask
+            blocks, rpb = eng._bn_blocks(M, Cc)
+            eng.mark(c.name + ".bnred")
+            part = eng.scratch("bnpart", blocks * 3 * Cc)
+            C.bn_bwd_reduce(dout.t, dout.ld, 3, self.mask, Cc // 8, None, None, yc.t, c.mean, c.rstd,
+                            None if one is None else y1.t, None if one is None else one.mean,
+                            None if one is None else one.rstd, M, Cc, blocks, rpb, part)
+            dz_out = dxa if one is None else None
+        C.bn_bwd_finalize(part, blocks, Cc, M, 0, c.bn.weight, c.mean, c.rstd, fg.gview(c.bn.weight),
+                          fg.gview(c.bn.bias), eng.grad_beta, c.coef, c.fin)
+        dy1 = None
+        if one is not None:
+            C.bn_bwd_finalize(part, blocks, Cc, M, 1, one.bn.weight, one.mean, one.rstd, fg.gview(one.bn.weight),
+                              fg.gview(one.bn.bias), eng.grad_beta, one.coef, one.fin)
+            dy1 = eng.ws((one.name, "dy"), (M, Cc), eng.cdt)
+            eng.mark(one.name + ".bnapply")
+            C.bn_bwd_apply(dout.t, dout.ld, mode, mask, Cc // 8 if mask is not None else 0, None, None, None, None,
+                           None, y1.t, one.coef, dy1, None, 0, 0, M, Cc)
+        dab = eng.ws((self.name, "dab"), (yb.M, self.b.C), eng.cdt)
+        rps = int(C.narrow_c_bwd_rps(M, Cc, eng.narrow_splits))
+        splits = (M + rps - 1) // rps
+        slab = eng.scratch("narrow_slab", splits * Cc * yb.C)
+        partb = eng.scratch("narrow_part", splits * 3 * yb.C)
+        eng.mark(c.name + ".fusedbwd")
+        b = self.b
+        C.narrow_c_bwd(dout.t, dout.ld, mode, mask, yc.t, c.coef, None if dz_out is None else dz_out.t,
+                       0 if dz_out is None else dz_out.ld, 1 if (dz_out is not None and dx_accum) else 0, yb.t,
+                       b.scale, b.shift, b.mean, b.rstd, c.wf, dab, slab, partb, M, Cc, yb.C, rps)
+        C.wgrad_reduce(slab, fg.gview(c.conv.weight), splits, Cc, 1, c.spec.cin_pad, c.spec.cin, 1.0,
+                       eng.grad_beta, 1)
+        dyb, _ = b.bn_backward(Act(dab, yb.N, yb.T, yb.H, yb.W), yb, 0, None, None, pre=(partb, splits))
+        b.wgrad(dyb, ya, self.a.xf())
+        daa = eng.ws((self.name, "daa"), (ya.M, self.a.C), eng.cdt)
+        pa = b.dgrad(dyb, (ya.T, ya.H, ya.W), daa, False, bn=(self.a, ya))
+        dya, _ = self.a.bn_backward(Act(daa, ya.N, ya.T, ya.H, ya.W), ya, 0 if pa else 2, None,
+                                    None if pa else self.a.xf(), pre=pa)
+        self.a.wgrad(dya, x, None)
+        if one is not None:
+            d1 = Act(dy1, x.N, yb.T, yb.H, yb.W)
+            one.wgrad(d1, x, None)
+            if self._strided_one(prev):
+                return self._dgrad_strided_one(dya, d1, dx, dx_accum)
+            one.dgrad(d1, (x.T, x.H, x.W), dx, dx_accum)
             acc = True
         else:
             acc = dx_accum if pre is not None else True
@@ -1043,6 +1117,9 @@ class FusedNet:
         self.bn_fold1 = self.bn_fold and os.environ.get("PVA_BN_FOLD1", "1") != '0'
         # folds with fewer input channels than this take exact statistics from a statistics-only conv pass
         self.fold_exact_below = int(os.environ.get("PVA_BN_FOLD_EXACT_BELOW", "32"))
+        # fused narrow conv_c backward (csrc/kernels/narrow_bwd.hip); workgroups (= slab count) per launch
+        self.narrow_bwd = os.environ.get("PVA_NARROW_BWD", "1") != "0"
+        self.narrow_splits = int(os.environ.get("PVA_NARROW_SPLITS", "1024"))
         blocks = list(model.blocks)
         self.slowfast = isinstance(blocks[0], R.MultiPathWayWithFuse)
         self.stages: List[Tuple[List, Optional[_Fuse]]] = []

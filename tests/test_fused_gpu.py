@@ -207,3 +207,26 @@ def test_persistent_tune_cache_reused_and_invalidated(tmp_path, monkeypatch):
     assert len(e3.tuner.cache) == 0
     e3.forward_backward(e3.prepare_inputs(xs), labels)
     assert e3.tuner.tuned > 0
+
+
+def test_narrow_fused_backward_matches_unfused(monkeypatch):
+    """The fused narrow conv_c backward (fast res2: BN apply + weight gradient + input gradient in one pass,
+    csrc/kernels/narrow_bwd.hip) against the three-kernel path it replaces (PVA_NARROW_BWD=0), deterministic mode:
+    same loss, every gradient within bf16 re-association noise."""
+    model = _build(True)
+    xs = _inputs(True, N=2, T=16, S=96, seed=3)
+    labels = torch.tensor([2, 5], device=DEV)
+    grads = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("PVA_NARROW_BWD", flag)
+        m = copy.deepcopy(model)
+        eng = FusedNet(m, DEV, deterministic=True)
+        used = [b for paths, _ in eng.stages for p in paths for b in getattr(p, "blocks", []) if b.narrow_c]
+        assert (len(used) > 0) == (flag == "1")
+        loss, _ = eng.forward_backward(eng.prepare_inputs(xs), labels)
+        torch.cuda.synchronize()
+        grads.append((float(loss), {n: p.grad.detach().clone() for n, p in m.named_parameters()}))
+    (l1, g1), (l0, g0) = grads
+    assert abs(l1 - l0) < 1e-6 * max(1.0, abs(l0))
+    worst = max((_rel(g1[n], g0[n]), n) for n in g0 if g0[n].norm() > 0)
+    assert worst[0] < 2e-2, worst
