@@ -1,5 +1,6 @@
-// Fused backward of a narrow 1x1 conv_c whose BatchNorm is not folded (the fast pathway's res2 units: 8 -> 32
-// channels at 16M positions per step at B=160).  One streaming pass replaces three:
+// Fused backward of a narrow 1x1 conv whose BatchNorm is not folded (the fast pathway's res2 conv_c, 8 -> 32 channels
+// at 16M positions per step at B=160, and the first unit's branch1, whose input is an activation: no affine, no mask,
+// gradient accumulated into dx).  One streaming pass replaces three:
 //
 //   BN-backward apply   dyc = A*dz + B*yc + C          dz = g (masked by the unit's ReLU bits)
 //   weight gradient     dWc[c][k] += dyc[c] * act_b[k]     act_b = relu(yb*sb + hb) (BN_b + ReLU recompute)
@@ -26,20 +27,20 @@ namespace {
 struct NarrowBwdParams {
   const uint16_t* g;      // [M][ldg] unit-output gradient (already masked when mode == 0)
   const uint8_t* mask;    // mode 3: ReLU bits [M][CO/8]
-  const uint16_t* yc;     // raw conv_c output [M][CO]
-  const float* coef;      // BN_c backward coefficients [A | B | C] x CO
+  const uint16_t* yc;     // raw conv output [M][CO] (BN input)
+  const float* coef;      // BN backward coefficients [A | B | C] x CO
   uint16_t* dz;           // optional identity-shortcut gradient out [M][lddz]
-  const uint16_t* yb;     // raw conv_b output [M][CI] (conv_c input before BN_b + ReLU)
-  const float* sb;        // BN_b scale / shift (forward affine)
+  const uint16_t* yb;     // conv input [M][CI]: raw conv_b output (aff: BN_b + ReLU applied here) or an activation
+  const float* sb;        // aff: BN_b scale / shift (forward affine)
   const float* hb;
-  const float* mb;        // BN_b batch mean / rstd (partial-sum rebase)
+  const float* mb;        // aff: BN_b batch mean / rstd (partial-sum rebase)
   const float* rb;
-  const uint16_t* wc;     // packed conv_c weights [CO][CI]
-  uint16_t* dab;          // [M][CI] input gradient of conv_c, masked (BN_b ReLU)
+  const uint16_t* wc;     // packed conv weights [CO][CI]
+  uint16_t* dab;          // [M][ldo] input gradient (aff: masked by the BN_b ReLU); accum: added to it
   float* slab;            // [splits][CO][CI] weight-gradient partials
-  float* part;            // [splits][3][CI] BN_b partial sums (sum v, sum v*xhat_b, 0)
+  float* part;            // aff: [splits][3][CI] BN_b partial sums (sum v, sum v*xhat_b, 0)
   int64_t M;
-  int ldg, lddz, dz_accum, mode, rps;
+  int ldg, lddz, dz_accum, mode, rps, aff, accum, ldo;
 };
 
 template <int CO, int CI>
@@ -48,22 +49,20 @@ __global__ __launch_bounds__(256) void narrow_c_bwd_kernel(const NarrowBwdParams
   constexpr int RPW = 64 / LPR;          // rows per wave and pass
   constexpr int KPL = CI / LPR;          // input channels finished per lane
   static_assert(CO % 8 == 0 && 64 % LPR == 0 && CI % LPR == 0 && CI == 8, "narrow_c_bwd: CO 8..64, CI 8");
+  // loop-invariant operands live in LDS (broadcast reads) rather than in ~100 VGPRs: 3 waves per SIMD
+  __shared__ __attribute__((aligned(16))) float wl[CO * CI];
+  __shared__ __attribute__((aligned(16))) float cl[3 * CO];
+  __shared__ __attribute__((aligned(16))) float al[2 * CI];
   __shared__ float red[4][LPR][8 * CI + 2 * CI];
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int q = lane % LPR, rr = lane / LPR;
   const int c0 = 8 * q;
-  float A[8], B[8], Cc[8], W[8][CI], sb[CI], hb[CI];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    A[e] = p.coef[c0 + e];
-    B[e] = p.coef[CO + c0 + e];
-    Cc[e] = p.coef[2 * CO + c0 + e];
-#pragma unroll
-    for (int k = 0; k < CI; ++k) W[e][k] = e2f(p.wc[(c0 + e) * CI + k]);
-  }
-#pragma unroll
-  for (int k = 0; k < CI; ++k) { sb[k] = p.sb[k]; hb[k] = p.hb[k]; }
+  const bool aff = p.aff != 0;
+  for (int i = tid; i < CO * CI; i += 256) wl[i] = e2f(p.wc[i]);
+  for (int i = tid; i < 3 * CO; i += 256) cl[i] = p.coef[(i / CO) * CO + i % CO];
+  if (tid < CI) { al[tid] = aff ? p.sb[tid] : 1.f; al[CI + tid] = aff ? p.hb[tid] : 0.f; }
+  __syncthreads();
   float acc[8][CI];
 #pragma unroll
   for (int e = 0; e < 8; ++e)
@@ -76,6 +75,7 @@ __global__ __launch_bounds__(256) void narrow_c_bwd_kernel(const NarrowBwdParams
   const int64_t r_begin = (int64_t)blockIdx.x * p.rps;
   const int64_t r_end = r_begin + p.rps < p.M ? r_begin + p.rps : p.M;
   for (int64_t r = r_begin + w * RPW + rr; r < r_end; r += 4 * RPW) {
+    asm volatile("" ::: "memory");   // keep the LDS operand reads inside the loop (no hoisting into registers)
     float gz[8], yc[8], yb[CI];
     unpack8(*reinterpret_cast<const uint4*>(p.g + r * p.ldg + c0), gz);
     unpack8(*reinterpret_cast<const uint4*>(p.yc + r * CO + c0), yc);
@@ -99,30 +99,50 @@ __global__ __launch_bounds__(256) void narrow_c_bwd_kernel(const NarrowBwdParams
     // dyc, rounded to the compute type (the unfused apply stored it so)
     float dy[8];
     {
+      const f32x4_t a0 = *reinterpret_cast<const f32x4_t*>(cl + c0), a1 = *reinterpret_cast<const f32x4_t*>(cl + c0 + 4);
+      const f32x4_t b0 = *reinterpret_cast<const f32x4_t*>(cl + CO + c0);
+      const f32x4_t b1 = *reinterpret_cast<const f32x4_t*>(cl + CO + c0 + 4);
+      const f32x4_t d0 = *reinterpret_cast<const f32x4_t*>(cl + 2 * CO + c0);
+      const f32x4_t d1 = *reinterpret_cast<const f32x4_t*>(cl + 2 * CO + c0 + 4);
+      const float A[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+      const float B[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+      const float D[8] = {d0[0], d0[1], d0[2], d0[3], d1[0], d1[1], d1[2], d1[3]};
       float t[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) t[e] = A[e] * gz[e] + B[e] * yc[e] + Cc[e];
+      for (int e = 0; e < 8; ++e) t[e] = A[e] * gz[e] + B[e] * yc[e] + D[e];
       unpack8(pack8(t), dy);
     }
-    // act_b = relu(BN_b(yb)) as the weight-gradient loader stages it (affine, round, ReLU)
-    float ab[CI];
+    // act_b = relu(BN_b(yb)) as the weight-gradient loader stages it (affine, round, ReLU); or yb itself
+    float ab[CI], sbk[CI], hbk[CI];
     {
-      float t[CI];
+      const f32x4_t s0 = *reinterpret_cast<const f32x4_t*>(al), s1 = *reinterpret_cast<const f32x4_t*>(al + 4);
+      const f32x4_t h0 = *reinterpret_cast<const f32x4_t*>(al + CI), h1 = *reinterpret_cast<const f32x4_t*>(al + CI + 4);
 #pragma unroll
-      for (int k = 0; k < CI; ++k) t[k] = __builtin_fmaf(yb[k], sb[k], hb[k]);
-      uint4 v = relu_e16x8(pack8_fast(t));
-      unpack8(v, ab);
+      for (int k = 0; k < 4; ++k) { sbk[k] = s0[k]; sbk[k + 4] = s1[k]; hbk[k] = h0[k]; hbk[k + 4] = h1[k]; }
+      if (aff) {
+        float t[CI];
+#pragma unroll
+        for (int k = 0; k < CI; ++k) t[k] = __builtin_fmaf(yb[k], sbk[k], hbk[k]);
+        unpack8(relu_e16x8(pack8_fast(t)), ab);
+      } else {
+#pragma unroll
+        for (int k = 0; k < CI; ++k) ab[k] = yb[k];
+      }
     }
     float pd[CI];
 #pragma unroll
     for (int k = 0; k < CI; ++k) pd[k] = 0.f;
 #pragma unroll
-    for (int e = 0; e < 8; ++e)
+    for (int e = 0; e < 8; ++e) {
+      const f32x4_t w0 = *reinterpret_cast<const f32x4_t*>(wl + (c0 + e) * CI);
+      const f32x4_t w1 = *reinterpret_cast<const f32x4_t*>(wl + (c0 + e) * CI + 4);
+      const float W[CI] = {w0[0], w0[1], w0[2], w0[3], w1[0], w1[1], w1[2], w1[3]};
 #pragma unroll
       for (int k = 0; k < CI; ++k) {
         acc[e][k] = __builtin_fmaf(dy[e], ab[k], acc[e][k]);
-        pd[k] = __builtin_fmaf(dy[e], W[e][k], pd[k]);
+        pd[k] = __builtin_fmaf(dy[e], W[k], pd[k]);
       }
+    }
     // sum the row's LPR lanes (adjacent lanes): every lane ends with the row's full dgrad
 #pragma unroll
     for (int o = 1; o < LPR; o <<= 1)
@@ -130,19 +150,27 @@ __global__ __launch_bounds__(256) void narrow_c_bwd_kernel(const NarrowBwdParams
       for (int k = 0; k < CI; ++k) pd[k] += __shfl_xor(pd[k], o, 64);
     // lane q: input channels k = q*KPL + j — BN_b ReLU mask (affine of yb > 0), round, store, partial sums
     float v[KPL];
+    uint16_t* dst = p.dab + r * p.ldo + q * KPL;
+    float old[KPL];
+#pragma unroll
+    for (int j = 0; j < KPL; ++j) old[j] = 0.f;
+    if (p.accum) {
+#pragma unroll
+      for (int j = 0; j < KPL; ++j) old[j] = e2f(dst[j]);
+    }
 #pragma unroll
     for (int j = 0; j < KPL; ++j) {
       const int k = q * KPL + j;
       float pk = 0.f, yk = 0.f, sk = 0.f, hk = 0.f;
 #pragma unroll
       for (int kk = 0; kk < CI; ++kk)
-        if (kk == k) { pk = pd[kk]; yk = yb[kk]; sk = sb[kk]; hk = hb[kk]; }
-      v[j] = (yk * sk + hk) > 0.f ? pk : 0.f;
+        if (kk == k) { pk = pd[kk]; yk = yb[kk]; sk = sbk[kk]; hk = hbk[kk]; }
+      v[j] = pk + old[j];
+      if (aff) v[j] = (yk * sk + hk) > 0.f ? v[j] : 0.f;
       v[j] = e2f(f2e(v[j]));
       sv[j] += v[j];
       sy[j] += v[j] * yk;
     }
-    uint16_t* dst = p.dab + r * CI + q * KPL;
     if constexpr (KPL == 2) {
       *reinterpret_cast<uint32_t*>(dst) = cvt_pk_e16(v[0], v[1]);
     } else {
@@ -185,7 +213,7 @@ __global__ __launch_bounds__(256) void narrow_c_bwd_kernel(const NarrowBwdParams
     const int qq = c / 8, e = c - qq * 8;
     slab[i] = ((red[0][qq][e * CI + k] + red[1][qq][e * CI + k]) + red[2][qq][e * CI + k]) + red[3][qq][e * CI + k];
   }
-  if (tid < CI) {
+  if (aff && tid < CI) {
     const int k = tid, qq = k / KPL, j = k - qq * KPL;
     const float s = ((red[0][qq][8 * CI + j] + red[1][qq][8 * CI + j]) + red[2][qq][8 * CI + j]) + red[3][qq][8 * CI + j];
     const float y = ((red[0][qq][9 * CI + j] + red[1][qq][9 * CI + j]) + red[2][qq][9 * CI + j]) +
@@ -211,9 +239,10 @@ int narrow_c_bwd_rps(int64_t M, int CO, int splits) {
 
 void narrow_c_bwd_launch(const uint16_t* g, int ldg, int mode, const uint8_t* mask, const uint16_t* yc,
                          const float* coef, uint16_t* dz, int lddz, int dz_accum, const uint16_t* yb, const float* sb,
-                         const float* hb, const float* mb, const float* rb, const uint16_t* wc, uint16_t* dab,
-                         float* slab, float* part, int64_t M, int CO, int CI, int rps, hipStream_t s) {
-  NarrowBwdParams p{g, mask, yc, coef, dz, yb, sb, hb, mb, rb, wc, dab, slab, part, M, ldg, lddz, dz_accum, mode, rps};
+                         const float* hb, const float* mb, const float* rb, const uint16_t* wc, uint16_t* dab, int ldo,
+                         int accum, float* slab, float* part, int64_t M, int CO, int CI, int rps, hipStream_t s) {
+  NarrowBwdParams p{g,  mask, yc, coef, dz,   yb,  sb,       hb,   mb,  rb,  wc,  dab, slab, part, M,
+                    ldg, lddz, dz_accum, mode, rps, sb != nullptr ? 1 : 0, accum, ldo};
   const int grid = (int)((M + rps - 1) / rps);
   if (grid <= 0) return;
   switch (CO) {

@@ -579,23 +579,30 @@ void head_dropout_mask(const at::Tensor& out, double p_drop, int64_t seed) {
 }
 
 // fused BN-backward apply + weight gradient + input gradient of a narrow 1x1 conv_c (narrow_bwd.hip)
+// bn = (sb, hb, mb, rb): the input is raw conv_b output under BN_b + ReLU (mask + partial sums into part); without it
+// the input is an activation used as is (branch1 of the unit: no mask, no sums) and dab may be accumulated
 void narrow_c_bwd(const at::Tensor& g, int64_t ldg, int64_t mode, const OptT& mask, const at::Tensor& yc,
                   const at::Tensor& coef, const OptT& dz, int64_t lddz, int64_t dz_accum, const at::Tensor& yb,
-                  const at::Tensor& sb, const at::Tensor& hb, const at::Tensor& mb, const at::Tensor& rb,
-                  const at::Tensor& wc, const at::Tensor& dab, const at::Tensor& slab, const at::Tensor& part, int64_t M,
+                  const OptT& sb, const OptT& hb, const OptT& mb, const OptT& rb, const at::Tensor& wc,
+                  const at::Tensor& dab, int64_t ldo, int64_t accum, const at::Tensor& slab, const OptT& part, int64_t M,
                   int64_t CO, int64_t CI, int64_t rps) {
   const bool h = kind16(g);
   TORCH_CHECK(pva_bf16::narrow_c_bwd_legal((int)CO, (int)CI), "narrow_c_bwd: unsupported channels");
   TORCH_CHECK(mode == 0 || (mode == 3 && mask.has_value()), "narrow_c_bwd: mask mode 0 or 3 (bits)");
-  TORCH_CHECK(yc.numel() >= M * CO && yb.numel() >= M * CI && dab.numel() >= M * CI && wc.numel() >= CO * CI,
-              "narrow_c_bwd: tensor sizes");
-  TORCH_CHECK(ldg % 8 == 0 && (!dz.has_value() || lddz % 8 == 0), "narrow_c_bwd: 16-B aligned rows");
+  TORCH_CHECK(yc.numel() >= M * CO && yb.numel() >= M * CI && dab.numel() >= (M - 1) * ldo + CI &&
+              wc.numel() >= CO * CI, "narrow_c_bwd: tensor sizes");
+  TORCH_CHECK(ldg % 8 == 0 && (!dz.has_value() || lddz % 8 == 0) && ldo % 2 == 0, "narrow_c_bwd: aligned rows");
+  const bool bn = sb.has_value();
+  TORCH_CHECK(bn == (hb.has_value() && mb.has_value() && rb.has_value() && part.has_value()),
+              "narrow_c_bwd: BN_b needs scale, shift, mean, rstd and the partial-sum buffer");
+  TORCH_CHECK(!(bn && accum), "narrow_c_bwd: the BN_b-masked input gradient is written, not accumulated");
   const int64_t splits = (M + rps - 1) / rps;
-  TORCH_CHECK(slab.numel() >= splits * CO * CI && part.numel() >= splits * 3 * CI, "narrow_c_bwd: slabs too small");
+  TORCH_CHECK(slab.numel() >= splits * CO * CI && (!bn || part->numel() >= splits * 3 * CI),
+              "narrow_c_bwd: slabs too small");
   KSEL(h, narrow_c_bwd_launch)(bfp(g), (int)ldg, (int)mode, mask.has_value() ? mask->data_ptr<uint8_t>() : nullptr,
                                bfp(yc), f32(coef), dz.has_value() ? bfpm(*dz) : nullptr, (int)lddz, (int)dz_accum,
-                               bfp(yb), f32(sb), f32(hb), f32(mb), f32(rb), bfp(wc), bfpm(dab), f32(slab), f32(part), M,
-                               (int)CO, (int)CI, (int)rps, cur_stream());
+                               bfp(yb), f32o(sb), f32o(hb), f32o(mb), f32o(rb), bfp(wc), bfpm(dab), (int)ldo,
+                               (int)accum, f32(slab), f32o(part), M, (int)CO, (int)CI, (int)rps, cur_stream());
 }
 
 void synth_frames(const at::Tensor& out, int64_t seed) {

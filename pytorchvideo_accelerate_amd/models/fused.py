@@ -843,13 +843,19 @@ class _ResBlock:
         C.bn_bwd_finalize(part, blocks, Cc, M, 0, c.bn.weight, c.mean, c.rstd, fg.gview(c.bn.weight),
                           fg.gview(c.bn.bias), eng.grad_beta, c.coef, c.fin)
         dy1 = None
+        s1 = one.spec if one is not None else None
+        # branch1 (8 -> 32, stride 1, input = the unit input activation): the same fused pass, without the input
+        # affine / mask, accumulating into dx (after conv_a's weight gradient, before its dgrad)
+        one_fused = (one is not None and tuple(s1.k) == (1, 1, 1) and tuple(s1.stride) == (1, 1, 1) and s1.cin == 8
+                     and s1.cin_pad == 8 and x.ld == 8 and bool(C.narrow_c_bwd_legal(s1.cout, s1.cin)))
         if one is not None:
             C.bn_bwd_finalize(part, blocks, Cc, M, 1, one.bn.weight, one.mean, one.rstd, fg.gview(one.bn.weight),
                               fg.gview(one.bn.bias), eng.grad_beta, one.coef, one.fin)
-            dy1 = eng.ws((one.name, "dy"), (M, Cc), eng.cdt)
-            eng.mark(one.name + ".bnapply")
-            C.bn_bwd_apply(dout.t, dout.ld, mode, mask, Cc // 8 if mask is not None else 0, None, None, None, None,
-                           None, y1.t, one.coef, dy1, None, 0, 0, M, Cc)
+            if not one_fused:
+                dy1 = eng.ws((one.name, "dy"), (M, Cc), eng.cdt)
+                eng.mark(one.name + ".bnapply")
+                C.bn_bwd_apply(dout.t, dout.ld, mode, mask, Cc // 8 if mask is not None else 0, None, None, None,
+                               None, None, y1.t, one.coef, dy1, None, 0, 0, M, Cc)
         dab = eng.ws((self.name, "dab"), (yb.M, self.b.C), eng.cdt)
         rps = int(C.narrow_c_bwd_rps(M, Cc, eng.narrow_splits))
         splits = (M + rps - 1) // rps
@@ -859,7 +865,7 @@ class _ResBlock:
         b = self.b
         C.narrow_c_bwd(dout.t, dout.ld, mode, mask, yc.t, c.coef, None if dz_out is None else dz_out.t,
                        0 if dz_out is None else dz_out.ld, 1 if (dz_out is not None and dx_accum) else 0, yb.t,
-                       b.scale, b.shift, b.mean, b.rstd, c.wf, dab, slab, partb, M, Cc, yb.C, rps)
+                       b.scale, b.shift, b.mean, b.rstd, c.wf, dab, yb.C, 0, slab, partb, M, Cc, yb.C, rps)
         C.wgrad_reduce(slab, fg.gview(c.conv.weight), splits, Cc, 1, c.spec.cin_pad, c.spec.cin, 1.0,
                        eng.grad_beta, 1)
         dyb, _ = b.bn_backward(Act(dab, yb.N, yb.T, yb.H, yb.W), yb, 0, None, None, pre=(partb, splits))
@@ -869,7 +875,15 @@ class _ResBlock:
         dya, _ = self.a.bn_backward(Act(daa, ya.N, ya.T, ya.H, ya.W), ya, 0 if pa else 2, None,
                                     None if pa else self.a.xf(), pre=pa)
         self.a.wgrad(dya, x, None)
-        if one is not None:
+        if one is not None and one_fused:
+            eng.mark(one.name + ".fusedbwd")
+            slab1 = eng.scratch("narrow_slab", splits * Cc * x.C)
+            C.narrow_c_bwd(dout.t, dout.ld, mode, mask, y1.t, one.coef, None, 0, 0, x.t, None, None, None, None,
+                           one.wf, dx, dx.stride(0), 1 if dx_accum else 0, slab1, None, M, Cc, x.C, rps)
+            C.wgrad_reduce(slab1, fg.gview(one.conv.weight), splits, Cc, 1, s1.cin_pad, s1.cin, 1.0,
+                           eng.grad_beta, 1)
+            acc = True
+        elif one is not None:
             d1 = Act(dy1, x.N, yb.T, yb.H, yb.W)
             one.wgrad(d1, x, None)
             if self._strided_one(prev):
