@@ -49,20 +49,25 @@ __global__ __launch_bounds__(256) void narrow_c_bwd_kernel(const NarrowBwdParams
   constexpr int RPW = 64 / LPR;          // rows per wave and pass
   constexpr int KPL = CI / LPR;          // input channels finished per lane
   static_assert(CO % 8 == 0 && 64 % LPR == 0 && CI % LPR == 0 && CI == 8, "narrow_c_bwd: CO 8..64, CI 8");
-  // loop-invariant operands live in LDS (broadcast reads) rather than in ~100 VGPRs: 3 waves per SIMD
-  __shared__ __attribute__((aligned(16))) float wl[CO * CI];
-  __shared__ __attribute__((aligned(16))) float cl[3 * CO];
-  __shared__ __attribute__((aligned(16))) float al[2 * CI];
   __shared__ float red[4][LPR][8 * CI + 2 * CI];
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int q = lane % LPR, rr = lane / LPR;
   const int c0 = 8 * q;
   const bool aff = p.aff != 0;
-  for (int i = tid; i < CO * CI; i += 256) wl[i] = e2f(p.wc[i]);
-  for (int i = tid; i < 3 * CO; i += 256) cl[i] = p.coef[(i / CO) * CO + i % CO];
-  if (tid < CI) { al[tid] = aff ? p.sb[tid] : 1.f; al[CI + tid] = aff ? p.hb[tid] : 0.f; }
-  __syncthreads();
+  // loop-invariant operands in registers (2 waves per SIMD; measured: staging them in LDS for 3 waves per SIMD made
+  // the pass 25 % slower — 26 dependent LDS reads per row)
+  float A[8], B[8], Cc[8], W[8][CI], sb[CI], hb[CI];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    A[e] = p.coef[c0 + e];
+    B[e] = p.coef[CO + c0 + e];
+    Cc[e] = p.coef[2 * CO + c0 + e];
+#pragma unroll
+    for (int k = 0; k < CI; ++k) W[e][k] = e2f(p.wc[(c0 + e) * CI + k]);
+  }
+#pragma unroll
+  for (int k = 0; k < CI; ++k) { sb[k] = aff ? p.sb[k] : 1.f; hb[k] = aff ? p.hb[k] : 0.f; }
   float acc[8][CI];
 #pragma unroll
   for (int e = 0; e < 8; ++e)
@@ -74,14 +79,29 @@ __global__ __launch_bounds__(256) void narrow_c_bwd_kernel(const NarrowBwdParams
 
   const int64_t r_begin = (int64_t)blockIdx.x * p.rps;
   const int64_t r_end = r_begin + p.rps < p.M ? r_begin + p.rps : p.M;
-  for (int64_t r = r_begin + w * RPW + rr; r < r_end; r += 4 * RPW) {
-    asm volatile("" ::: "memory");   // keep the LDS operand reads inside the loop (no hoisting into registers)
+  constexpr int STEP = 4 * RPW;
+  // raw operands of the NEXT row are loaded one iteration ahead (software pipelining: a wave keeps two rows of
+  // loads in flight at 2 waves per SIMD)
+  uint4 ng{}, nc{}, nb{};
+  unsigned nbits = 0xffu;
+  auto fetch = [&](int64_t r) {
+    if (r < r_end) {
+      ng = *reinterpret_cast<const uint4*>(p.g + r * p.ldg + c0);
+      nc = *reinterpret_cast<const uint4*>(p.yc + r * CO + c0);
+      nb = *reinterpret_cast<const uint4*>(p.yb + r * CI);
+      if (p.mode == 3) nbits = p.mask[r * (CO / 8) + q];
+    }
+  };
+  int64_t r = r_begin + w * RPW + rr;
+  fetch(r);
+  for (; r < r_end; r += STEP) {
     float gz[8], yc[8], yb[CI];
-    unpack8(*reinterpret_cast<const uint4*>(p.g + r * p.ldg + c0), gz);
-    unpack8(*reinterpret_cast<const uint4*>(p.yc + r * CO + c0), yc);
-    unpack8(*reinterpret_cast<const uint4*>(p.yb + r * CI), yb);
+    unpack8(ng, gz);
+    unpack8(nc, yc);
+    unpack8(nb, yb);
+    const unsigned bits = nbits;
+    fetch(r + STEP);
     if (p.mode == 3) {
-      const unsigned bits = p.mask[r * (CO / 8) + q];
 #pragma unroll
       for (int e = 0; e < 8; ++e) gz[e] = (bits >> e) & 1u ? gz[e] : 0.f;
     }
@@ -99,57 +119,38 @@ __global__ __launch_bounds__(256) void narrow_c_bwd_kernel(const NarrowBwdParams
     // dyc, rounded to the compute type (the unfused apply stored it so)
     float dy[8];
     {
-      const f32x4_t a0 = *reinterpret_cast<const f32x4_t*>(cl + c0), a1 = *reinterpret_cast<const f32x4_t*>(cl + c0 + 4);
-      const f32x4_t b0 = *reinterpret_cast<const f32x4_t*>(cl + CO + c0);
-      const f32x4_t b1 = *reinterpret_cast<const f32x4_t*>(cl + CO + c0 + 4);
-      const f32x4_t d0 = *reinterpret_cast<const f32x4_t*>(cl + 2 * CO + c0);
-      const f32x4_t d1 = *reinterpret_cast<const f32x4_t*>(cl + 2 * CO + c0 + 4);
-      const float A[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
-      const float B[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
-      const float D[8] = {d0[0], d0[1], d0[2], d0[3], d1[0], d1[1], d1[2], d1[3]};
       float t[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) t[e] = A[e] * gz[e] + B[e] * yc[e] + D[e];
+      for (int e = 0; e < 8; ++e) t[e] = A[e] * gz[e] + B[e] * yc[e] + Cc[e];
       unpack8(pack8(t), dy);
     }
     // act_b = relu(BN_b(yb)) as the weight-gradient loader stages it (affine, round, ReLU); or yb itself
-    float ab[CI], sbk[CI], hbk[CI];
-    {
-      const f32x4_t s0 = *reinterpret_cast<const f32x4_t*>(al), s1 = *reinterpret_cast<const f32x4_t*>(al + 4);
-      const f32x4_t h0 = *reinterpret_cast<const f32x4_t*>(al + CI), h1 = *reinterpret_cast<const f32x4_t*>(al + CI + 4);
+    float ab[CI];
+    if (aff) {
+      float t[CI];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) { sbk[k] = s0[k]; sbk[k + 4] = s1[k]; hbk[k] = h0[k]; hbk[k + 4] = h1[k]; }
-      if (aff) {
-        float t[CI];
+      for (int k = 0; k < CI; ++k) t[k] = __builtin_fmaf(yb[k], sb[k], hb[k]);
+      unpack8(relu_e16x8(pack8_fast(t)), ab);
+    } else {
 #pragma unroll
-        for (int k = 0; k < CI; ++k) t[k] = __builtin_fmaf(yb[k], sbk[k], hbk[k]);
-        unpack8(relu_e16x8(pack8_fast(t)), ab);
-      } else {
-#pragma unroll
-        for (int k = 0; k < CI; ++k) ab[k] = yb[k];
-      }
+      for (int k = 0; k < CI; ++k) ab[k] = yb[k];
     }
     float pd[CI];
 #pragma unroll
     for (int k = 0; k < CI; ++k) pd[k] = 0.f;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const f32x4_t w0 = *reinterpret_cast<const f32x4_t*>(wl + (c0 + e) * CI);
-      const f32x4_t w1 = *reinterpret_cast<const f32x4_t*>(wl + (c0 + e) * CI + 4);
-      const float W[CI] = {w0[0], w0[1], w0[2], w0[3], w1[0], w1[1], w1[2], w1[3]};
+    for (int e = 0; e < 8; ++e)
 #pragma unroll
       for (int k = 0; k < CI; ++k) {
         acc[e][k] = __builtin_fmaf(dy[e], ab[k], acc[e][k]);
-        pd[k] = __builtin_fmaf(dy[e], W[k], pd[k]);
+        pd[k] = __builtin_fmaf(dy[e], W[e][k], pd[k]);
       }
-    }
     // sum the row's LPR lanes (adjacent lanes): every lane ends with the row's full dgrad
 #pragma unroll
     for (int o = 1; o < LPR; o <<= 1)
 #pragma unroll
       for (int k = 0; k < CI; ++k) pd[k] += __shfl_xor(pd[k], o, 64);
     // lane q: input channels k = q*KPL + j — BN_b ReLU mask (affine of yb > 0), round, store, partial sums
-    float v[KPL];
     uint16_t* dst = p.dab + r * p.ldo + q * KPL;
     float old[KPL];
 #pragma unroll
@@ -158,13 +159,14 @@ __global__ __launch_bounds__(256) void narrow_c_bwd_kernel(const NarrowBwdParams
 #pragma unroll
       for (int j = 0; j < KPL; ++j) old[j] = e2f(dst[j]);
     }
+    float v[KPL];
 #pragma unroll
     for (int j = 0; j < KPL; ++j) {
       const int k = q * KPL + j;
       float pk = 0.f, yk = 0.f, sk = 0.f, hk = 0.f;
 #pragma unroll
       for (int kk = 0; kk < CI; ++kk)
-        if (kk == k) { pk = pd[kk]; yk = yb[kk]; sk = sbk[kk]; hk = hbk[kk]; }
+        if (kk == k) { pk = pd[kk]; yk = yb[kk]; sk = sb[kk]; hk = hb[kk]; }
       v[j] = pk + old[j];
       if (aff) v[j] = (yk * sk + hk) > 0.f ? v[j] : 0.f;
       v[j] = e2f(f2e(v[j]));
