@@ -99,4 +99,6 @@ int narrow_c_bwd_rps(int64_t M, int CO, int splits);
 void narrow_c_bwd_launch(const uint16_t* g, int ldg, int mode, const uint8_t* mask, const uint16_t* yc,
                          const float* coef, uint16_t* dz, int lddz, int dz_accum, const uint16_t* yb, const float* sb,
                          const float* hb, const float* mb, const float* rb, const uint16_t* wc, uint16_t* dab, int ldo,
-                         int accum, float* slab, float* part, int64_t M, int CO, int CI, int rps, hipStream_t s);
+                         int accum, float* slab, float* part, const uint16_t* y1, const float* mc, const float* rc,
+                         const float* m1, const float* r1, float* cpart, int form, int64_t M, int CO, int CI, int rps,
+                         hipStream_t s);

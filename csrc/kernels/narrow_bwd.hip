@@ -39,11 +39,21 @@ struct NarrowBwdParams {
   uint16_t* dab;          // [M][ldo] input gradient (aff: masked by the BN_b ReLU); accum: added to it
   float* slab;            // [splits][CO][CI] weight-gradient partials
   float* part;            // aff: [splits][3][CI] BN_b partial sums (sum v, sum v*xhat_b, 0)
+  // reduce pass of a folded unit (no yc in memory): BN_c / BN_1 backward partial sums [splits][3][CO]
+  const uint16_t* y1;     // branch1 raw output (its BN shares dz) or null
+  const float* mc;        // BN_c batch mean / rstd, BN_1 batch mean / rstd
+  const float* rc;
+  const float* m1;
+  const float* r1;
+  float* cpart;
   int64_t M;
   int ldg, lddz, dz_accum, mode, rps, aff, accum, ldo;
 };
 
-template <int CO, int CI>
+// RC: the BN_c input yc is recomputed from act_b (yc[c] = sum_k Wc[c][k] act_b[k], rounded like the stored output)
+// instead of read — the unit's conv_c is BN-folded in the forward (fold_output writes the unit output directly; yc
+// never exists).  RED: the reduce pass of such a unit — only the BN_c (and BN_1) backward partial sums.
+template <int CO, int CI, bool RC, bool RED>
 __global__ __launch_bounds__(256) void narrow_c_bwd_kernel(const NarrowBwdParams p) {
   constexpr int LPR = CO / 8;            // lanes per row
   constexpr int RPW = 64 / LPR;          // rows per wave and pass
@@ -82,28 +92,65 @@ __global__ __launch_bounds__(256) void narrow_c_bwd_kernel(const NarrowBwdParams
   constexpr int STEP = 4 * RPW;
   // raw operands of the NEXT row are loaded one iteration ahead (software pipelining: a wave keeps two rows of
   // loads in flight at 2 waves per SIMD)
-  uint4 ng{}, nc{}, nb{};
+  uint4 ng{}, nc{}, nb{}, n1{};
   unsigned nbits = 0xffu;
+  const bool dual = RED && p.y1 != nullptr;
   auto fetch = [&](int64_t r) {
     if (r < r_end) {
       ng = *reinterpret_cast<const uint4*>(p.g + r * p.ldg + c0);
-      nc = *reinterpret_cast<const uint4*>(p.yc + r * CO + c0);
+      if constexpr (!RC) nc = *reinterpret_cast<const uint4*>(p.yc + r * CO + c0);
       nb = *reinterpret_cast<const uint4*>(p.yb + r * CI);
+      if (dual) n1 = *reinterpret_cast<const uint4*>(p.y1 + r * CO + c0);
       if (p.mode == 3) nbits = p.mask[r * (CO / 8) + q];
     }
   };
+  float rs[8], rsc[8], rs1[8];   // RED: sum dz, sum dz*yc, sum dz*y1 (raw; rebased at the end)
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { rs[e] = 0.f; rsc[e] = 0.f; rs1[e] = 0.f; }
   int64_t r = r_begin + w * RPW + rr;
   fetch(r);
   for (; r < r_end; r += STEP) {
-    float gz[8], yc[8], yb[CI];
+    float gz[8], yc[8], yb[CI], y1v[8];
     unpack8(ng, gz);
-    unpack8(nc, yc);
+    if constexpr (!RC) unpack8(nc, yc);
     unpack8(nb, yb);
+    if (dual) unpack8(n1, y1v);
     const unsigned bits = nbits;
     fetch(r + STEP);
     if (p.mode == 3) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) gz[e] = (bits >> e) & 1u ? gz[e] : 0.f;
+    }
+    // act_b = relu(BN_b(yb)) as the weight-gradient loader stages it (affine, round, ReLU); or yb itself
+    float ab[CI];
+    if (aff) {
+      float t[CI];
+#pragma unroll
+      for (int k = 0; k < CI; ++k) t[k] = __builtin_fmaf(yb[k], sb[k], hb[k]);
+      unpack8(relu_e16x8(pack8_fast(t)), ab);
+    } else {
+#pragma unroll
+      for (int k = 0; k < CI; ++k) ab[k] = yb[k];
+    }
+    if constexpr (RC) {   // the folded forward's conv_c output, rounded as a stored output would be
+      float t[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float a_ = 0.f;
+#pragma unroll
+        for (int k = 0; k < CI; ++k) a_ = __builtin_fmaf(W[e][k], ab[k], a_);
+        t[e] = a_;
+      }
+      unpack8(pack8(t), yc);
+    }
+    if constexpr (RED) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        rs[e] += gz[e];
+        rsc[e] = __builtin_fmaf(gz[e], yc[e], rsc[e]);
+        if (dual) rs1[e] = __builtin_fmaf(gz[e], y1v[e], rs1[e]);
+      }
+      continue;
     }
     if (p.dz) {
       uint16_t* d = p.dz + r * p.lddz + c0;
@@ -123,17 +170,6 @@ __global__ __launch_bounds__(256) void narrow_c_bwd_kernel(const NarrowBwdParams
 #pragma unroll
       for (int e = 0; e < 8; ++e) t[e] = A[e] * gz[e] + B[e] * yc[e] + Cc[e];
       unpack8(pack8(t), dy);
-    }
-    // act_b = relu(BN_b(yb)) as the weight-gradient loader stages it (affine, round, ReLU); or yb itself
-    float ab[CI];
-    if (aff) {
-      float t[CI];
-#pragma unroll
-      for (int k = 0; k < CI; ++k) t[k] = __builtin_fmaf(yb[k], sb[k], hb[k]);
-      unpack8(relu_e16x8(pack8_fast(t)), ab);
-    } else {
-#pragma unroll
-      for (int k = 0; k < CI; ++k) ab[k] = yb[k];
     }
     float pd[CI];
 #pragma unroll
@@ -179,6 +215,40 @@ __global__ __launch_bounds__(256) void narrow_c_bwd_kernel(const NarrowBwdParams
 #pragma unroll
       for (int j = 0; j < KPL; ++j) dst[j] = f2e(v[j]);
     }
+  }
+  if constexpr (RED) {
+    // lanes of the same channel group q (stride LPR), then the 4 waves in a fixed order
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+#pragma unroll
+      for (int o = LPR; o < 64; o <<= 1) {
+        rs[e] += __shfl_xor(rs[e], o, 64);
+        rsc[e] += __shfl_xor(rsc[e], o, 64);
+        rs1[e] += __shfl_xor(rs1[e], o, 64);
+      }
+    float* rr3 = &red[0][0][0];   // [4 waves][3][CO]
+    if (rr == 0) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        rr3[(w * 3 + 0) * CO + c0 + e] = rs[e];
+        rr3[(w * 3 + 1) * CO + c0 + e] = rsc[e];
+        rr3[(w * 3 + 2) * CO + c0 + e] = rs1[e];
+      }
+    }
+    __syncthreads();
+    if (tid < CO) {
+      const int c = tid;
+      float t[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+        t[k] = ((rr3[(0 * 3 + k) * CO + c] + rr3[(1 * 3 + k) * CO + c]) + rr3[(2 * 3 + k) * CO + c]) +
+               rr3[(3 * 3 + k) * CO + c];
+      float* pt = p.cpart + (int64_t)blockIdx.x * 3 * CO;
+      pt[c] = t[0];
+      pt[CO + c] = (t[1] - p.mc[c] * t[0]) * p.rc[c];
+      pt[2 * CO + c] = dual ? (t[2] - p.m1[c] * t[0]) * p.r1[c] : 0.f;
+    }
+    return;
   }
   // weight gradient: lanes of the same channel group q (stride LPR) -> one value per (c, k) per wave
 #pragma unroll
@@ -239,18 +309,28 @@ int narrow_c_bwd_rps(int64_t M, int CO, int splits) {
   return (int)(rps < pass ? pass : rps);
 }
 
+template <int CO>
+static void narrow_launch_co(const NarrowBwdParams& p, int form, int grid, hipStream_t s) {
+  if (form == 2) hipLaunchKernelGGL((narrow_c_bwd_kernel<CO, 8, true, true>), dim3(grid), dim3(256), 0, s, p);
+  else if (form == 1) hipLaunchKernelGGL((narrow_c_bwd_kernel<CO, 8, true, false>), dim3(grid), dim3(256), 0, s, p);
+  else hipLaunchKernelGGL((narrow_c_bwd_kernel<CO, 8, false, false>), dim3(grid), dim3(256), 0, s, p);
+}
+
+// form 0: yc read; 1: yc recomputed (folded unit); 2: reduce pass of a folded unit (cpart only)
 void narrow_c_bwd_launch(const uint16_t* g, int ldg, int mode, const uint8_t* mask, const uint16_t* yc,
                          const float* coef, uint16_t* dz, int lddz, int dz_accum, const uint16_t* yb, const float* sb,
                          const float* hb, const float* mb, const float* rb, const uint16_t* wc, uint16_t* dab, int ldo,
-                         int accum, float* slab, float* part, int64_t M, int CO, int CI, int rps, hipStream_t s) {
-  NarrowBwdParams p{g,  mask, yc, coef, dz,   yb,  sb,       hb,   mb,  rb,  wc,  dab, slab, part, M,
-                    ldg, lddz, dz_accum, mode, rps, sb != nullptr ? 1 : 0, accum, ldo};
+                         int accum, float* slab, float* part, const uint16_t* y1, const float* mc, const float* rc,
+                         const float* m1, const float* r1, float* cpart, int form, int64_t M, int CO, int CI, int rps,
+                         hipStream_t s) {
+  NarrowBwdParams p{g,  mask, yc, coef, dz,   yb,  sb,       hb,   mb,  rb,  wc,  dab, slab, part, y1, mc, rc, m1, r1,
+                    cpart, M, ldg, lddz, dz_accum, mode, rps, sb != nullptr ? 1 : 0, accum, ldo};
   const int grid = (int)((M + rps - 1) / rps);
   if (grid <= 0) return;
   switch (CO) {
-    case 16: hipLaunchKernelGGL((narrow_c_bwd_kernel<16, 8>), dim3(grid), dim3(256), 0, s, p); break;
-    case 64: hipLaunchKernelGGL((narrow_c_bwd_kernel<64, 8>), dim3(grid), dim3(256), 0, s, p); break;
-    default: hipLaunchKernelGGL((narrow_c_bwd_kernel<32, 8>), dim3(grid), dim3(256), 0, s, p); break;
+    case 16: narrow_launch_co<16>(p, form, grid, s); break;
+    case 64: narrow_launch_co<64>(p, form, grid, s); break;
+    default: narrow_launch_co<32>(p, form, grid, s); break;
   }
 }
 

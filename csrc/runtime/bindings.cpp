@@ -580,29 +580,41 @@ void head_dropout_mask(const at::Tensor& out, double p_drop, int64_t seed) {
 
 // fused BN-backward apply + weight gradient + input gradient of a narrow 1x1 conv_c (narrow_bwd.hip)
 // bn = (sb, hb, mb, rb): the input is raw conv_b output under BN_b + ReLU (mask + partial sums into part); without it
-// the input is an activation used as is (branch1 of the unit: no mask, no sums) and dab may be accumulated
-void narrow_c_bwd(const at::Tensor& g, int64_t ldg, int64_t mode, const OptT& mask, const at::Tensor& yc,
+// the input is an activation used as is (branch1 of the unit: no mask, no sums) and dab may be accumulated.
+// form 0: yc read from memory; 1: yc recomputed from act_b (BN-folded unit); 2: the folded unit's reduce pass (BN_c /
+// BN_1 backward partial sums into cpart [splits][3][CO], rebased with mc/rc, m1/r1; nothing else written)
+void narrow_c_bwd(const at::Tensor& g, int64_t ldg, int64_t mode, const OptT& mask, const OptT& yc,
                   const at::Tensor& coef, const OptT& dz, int64_t lddz, int64_t dz_accum, const at::Tensor& yb,
                   const OptT& sb, const OptT& hb, const OptT& mb, const OptT& rb, const at::Tensor& wc,
-                  const at::Tensor& dab, int64_t ldo, int64_t accum, const at::Tensor& slab, const OptT& part, int64_t M,
-                  int64_t CO, int64_t CI, int64_t rps) {
+                  const OptT& dab, int64_t ldo, int64_t accum, const OptT& slab, const OptT& part, int64_t M,
+                  int64_t CO, int64_t CI, int64_t rps, int64_t form, const OptT& y1, const OptT& mc, const OptT& rc,
+                  const OptT& m1, const OptT& r1, const OptT& cpart) {
   const bool h = kind16(g);
   TORCH_CHECK(pva_bf16::narrow_c_bwd_legal((int)CO, (int)CI), "narrow_c_bwd: unsupported channels");
   TORCH_CHECK(mode == 0 || (mode == 3 && mask.has_value()), "narrow_c_bwd: mask mode 0 or 3 (bits)");
-  TORCH_CHECK(yc.numel() >= M * CO && yb.numel() >= M * CI && dab.numel() >= (M - 1) * ldo + CI &&
-              wc.numel() >= CO * CI, "narrow_c_bwd: tensor sizes");
+  TORCH_CHECK(form >= 0 && form <= 2, "narrow_c_bwd: form 0, 1 or 2");
+  TORCH_CHECK(form != 0 || (yc.has_value() && yc->numel() >= M * CO), "narrow_c_bwd: form 0 reads yc");
+  TORCH_CHECK(yb.numel() >= M * CI && wc.numel() >= CO * CI, "narrow_c_bwd: tensor sizes");
   TORCH_CHECK(ldg % 8 == 0 && (!dz.has_value() || lddz % 8 == 0) && ldo % 2 == 0, "narrow_c_bwd: aligned rows");
   const bool bn = sb.has_value();
-  TORCH_CHECK(bn == (hb.has_value() && mb.has_value() && rb.has_value() && part.has_value()),
-              "narrow_c_bwd: BN_b needs scale, shift, mean, rstd and the partial-sum buffer");
-  TORCH_CHECK(!(bn && accum), "narrow_c_bwd: the BN_b-masked input gradient is written, not accumulated");
+  TORCH_CHECK(bn == (hb.has_value() && mb.has_value() && rb.has_value()), "narrow_c_bwd: BN_b scale/shift/mean/rstd");
   const int64_t splits = (M + rps - 1) / rps;
-  TORCH_CHECK(slab.numel() >= splits * CO * CI && (!bn || part->numel() >= splits * 3 * CI),
-              "narrow_c_bwd: slabs too small");
+  if (form == 2) {
+    TORCH_CHECK(bn && mc.has_value() && rc.has_value() && cpart.has_value() && cpart->numel() >= splits * 3 * CO,
+                "narrow_c_bwd reduce: BN_b affine, BN_c mean/rstd and the partial-sum buffer");
+    TORCH_CHECK(!y1.has_value() || (m1.has_value() && r1.has_value() && y1->numel() >= M * CO),
+                "narrow_c_bwd reduce: branch1 needs its mean / rstd");
+  } else {
+    TORCH_CHECK(dab.has_value() && dab->numel() >= (M - 1) * ldo + CI && slab.has_value() &&
+                slab->numel() >= splits * CO * CI, "narrow_c_bwd: dab / slab sizes");
+    TORCH_CHECK(!bn || (part.has_value() && part->numel() >= splits * 3 * CI), "narrow_c_bwd: BN_b partial sums");
+    TORCH_CHECK(!(bn && accum), "narrow_c_bwd: the BN_b-masked input gradient is written, not accumulated");
+  }
   KSEL(h, narrow_c_bwd_launch)(bfp(g), (int)ldg, (int)mode, mask.has_value() ? mask->data_ptr<uint8_t>() : nullptr,
-                               bfp(yc), f32(coef), dz.has_value() ? bfpm(*dz) : nullptr, (int)lddz, (int)dz_accum,
-                               bfp(yb), f32o(sb), f32o(hb), f32o(mb), f32o(rb), bfp(wc), bfpm(dab), (int)ldo,
-                               (int)accum, f32(slab), f32o(part), M, (int)CO, (int)CI, (int)rps, cur_stream());
+                               bfo(yc), f32(coef), bfom(dz), (int)lddz, (int)dz_accum, bfp(yb), f32o(sb), f32o(hb),
+                               f32o(mb), f32o(rb), bfp(wc), bfom(dab), (int)ldo, (int)accum, f32o(slab), f32o(part),
+                               bfo(y1), f32o(mc), f32o(rc), f32o(m1), f32o(r1), f32o(cpart), (int)form, M, (int)CO,
+                               (int)CI, (int)rps, cur_stream());
 }
 
 void synth_frames(const at::Tensor& out, int64_t seed) {
@@ -739,7 +751,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("pack_desc_size", &pva_bf16::pack_desc_size);
   m.def("video_preprocess", &video_preprocess);
   m.def("synth_frames", &synth_frames);
-  m.def("narrow_c_bwd", &narrow_c_bwd);
+  m.def("narrow_c_bwd", &narrow_c_bwd, py::arg("g"), py::arg("ldg"), py::arg("mode"), py::arg("mask"), py::arg("yc"),
+        py::arg("coef"), py::arg("dz"), py::arg("lddz"), py::arg("dz_accum"), py::arg("yb"), py::arg("sb"),
+        py::arg("hb"), py::arg("mb"), py::arg("rb"), py::arg("wc"), py::arg("dab"), py::arg("ldo"), py::arg("accum"),
+        py::arg("slab"), py::arg("part"), py::arg("M"), py::arg("CO"), py::arg("CI"), py::arg("rps"),
+        py::arg("form") = 0, py::arg("y1") = py::none(), py::arg("mc") = py::none(), py::arg("rc") = py::none(),
+        py::arg("m1") = py::none(), py::arg("r1") = py::none(), py::arg("cpart") = py::none());
   m.def("narrow_c_bwd_legal", [](int64_t CO, int64_t CI) { return (bool)pva_bf16::narrow_c_bwd_legal((int)CO, (int)CI); });
   m.def("narrow_c_bwd_rps", [](int64_t M, int64_t CO, int64_t splits) {
     return (int64_t)pva_bf16::narrow_c_bwd_rps(M, (int)CO, (int)splits);

@@ -383,6 +383,35 @@ class _ConvBN:
                           bn.num_batches_tracked, bn.momentum if bn.momentum is not None else 0.1, bn.eps,
                           self.mean, self.rstd, self.scale, self.shift, self.fin)
 
+    def narrow_fold_stats(self, yb: Act, bxf: _Xf, train: bool):
+        """BN statistics of a narrow folded conv_c (``_ResBlock.narrow_fold``) from a statistics-only conv pass over
+        act_b(yb) (the output is computed, never stored); no Gram matrix — its backward recomputes yc
+        (csrc/kernels/narrow_bwd.hip forms 1 and 2) instead of the algebraic fold backward."""
+        eng, C, s = self.eng, self.eng.C, self.spec
+        bn = self.bn
+        if not train:
+            C.bn_eval_affine(bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, self.scale, self.shift)
+            return
+        Co = s.cout
+        eng.mark(self.name + ".foldexact")
+        key = ("fg", yb.N, yb.T, yb.H, yb.W, yb.ld)
+        g = self._geo.get(key)
+        if g is None:
+            g = self._geo[key] = fwd_geometry(s, yb.N, yb.T, yb.H, yb.W, yb.ld, Co)
+        stats = eng.ws((self.name, "stats"), ((yb.M + 127) // 128, 2, Co), torch.float32)
+        dummy = eng.ws(("nostore_y",), (1, 8), eng.cdt)
+        tuner = eng.tuner
+        aff = 2 if bxf.relu else 1
+
+        def run(cfg, scratch):
+            C.conv_igemm(yb.t, self.wf, dummy, tuner.scratch_like(stats) if scratch else stats, bxf.scale,
+                         bxf.shift, aff, 0, g, s.chunk, cfg, None, 1)
+        cfg = tuner.launch(("fst", aff) + tuple(g), g, s.chunk, run, aff=aff, direct=False)
+        tiles = (yb.M + tuner.bm(cfg, Co) - 1) // tuner.bm(cfg, Co)
+        C.bn_finalize(stats, tiles, Co, yb.M, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                      bn.num_batches_tracked, bn.momentum if bn.momentum is not None else 0.1, bn.eps,
+                      self.mean, self.rstd, self.scale, self.shift, self.fin)
+
     def fold_output(self, yb: Act, bxf: _Xf, out: torch.Tensor, res: Act, rxf: Optional[_Xf],
                     mask: torch.Tensor, tag: str) -> Act:
         """out = relu(BN(conv(act_b(yb))) + r), r = res (identity) or BN_1(res) (``rxf``); ReLU bits -> mask."""
@@ -523,7 +552,8 @@ class _ConvBN:
             part, c, one = None, None, None
             if epi is not None:
                 part = self.eng.scratch("bnepi", ((g[0] + 127) // 128) * 3 * g[1])
-                c, one = epi.c, (None if epi.fold1 else epi.one)   # folded branch1: its sums come from G1
+                # folded branch1: its sums come from G; narrow-fold unit: from its own reduce pass
+                c, one = epi.c, (None if (epi.fold1 or epi.narrow_fold) else epi.one)1
 
             yc = None if (epi is None or epi.yc is None) else epi.yc   # folded conv_c: no raw output
 
@@ -723,6 +753,9 @@ class _ResBlock:
         # narrow unfolded 1x1 conv_c (fast res2: 8 -> 32): fused BN-apply + wgrad + dgrad backward (_bwd_narrow)
         self.narrow_c = (not self.fold and eng.narrow_bwd and tuple(sc.k) == (1, 1, 1) and tuple(sc.stride) == (1, 1, 1)
                          and sc.cin == 8 and sc.cin_pad == 8 and bool(eng.C.narrow_c_bwd_legal(sc.cout, sc.cin)))
+        # ... and BN-folded in the forward: the unit output is written by fold_output (no raw yc, no res_out pass);
+        # the backward recomputes yc from act_b (a reduce pass + the fused pass)
+        self.narrow_fold = self.narrow_c and eng.narrow_fold
         s1 = self.one.spec if self.one is not None else None
         self.fold1 = (self.fold and s1 is not None and eng.bn_fold1 and tuple(s1.k) == (1, 1, 1)
                       and tuple(s1.stride) == (1, 1, 1) and s1.cin % 8 == 0 and s1.cin == s1.cin_pad
@@ -745,6 +778,15 @@ class _ResBlock:
             if self.fold1 and train:
                 self.one.fold_branch1_forward(x)
             self.c.fold_forward(yb, self.b.xf(), train)
+            mask = self.eng.ws((self.name, "mask", tag), (yb.M, self.c.C // 8), torch.uint8)
+            res, rxf = (x, None) if y1 is None else (y1, self.one.xf(relu=False))
+            o = self.c.fold_output(yb, self.b.xf(), out, res, rxf, mask, tag)
+            self.mask = mask if train else None
+            self.x, self.ya, self.yb, self.yc, self.y1, self.out = x, ya, yb, None, y1, o
+            return o
+        if self.narrow_fold:
+            y1 = self.one.fwd(x, None, train, tag) if self.one is not None else None
+            self.c.narrow_fold_stats(yb, self.b.xf(), train)
             mask = self.eng.ws((self.name, "mask", tag), (yb.M, self.c.C // 8), torch.uint8)
             res, rxf = (x, None) if y1 is None else (y1, self.one.xf(relu=False))
             o = self.c.fold_output(yb, self.b.xf(), out, res, rxf, mask, tag)
@@ -823,10 +865,29 @@ class _ResBlock:
         eng, C = self.eng, self.eng.C
         x, ya, yb, yc, y1, one, c = self.x, self.ya, self.yb, self.yc, self.y1, self.one, self.c
         dxa = Act(dx, x.N, x.T, x.H, x.W)
-        M, Cc = yc.M, c.C
+        M, Cc = yb.M, c.C
         fg = eng.flat
         res = None
-        if pre is not None:   # dout is the masked dz, its partial sums came from the next unit's dgrad epilogue
+        rps = int(C.narrow_c_bwd_rps(M, Cc, eng.narrow_splits))
+        splits = (M + rps - 1) // rps
+        b = self.b
+        if self.narrow_fold:
+            # no yc: the BN_c (and BN_1) backward sums come from a reduce pass that recomputes yc from act_b
+            if pre is not None:
+                mode, mask, dz_out = 0, None, None
+                if one is None:
+                    res = dout
+            else:
+                mode, mask = 3, self.mask
+                dz_out = dxa if one is None else None
+            part = eng.scratch("narrow_cpart", splits * 3 * Cc)
+            blocks = splits
+            eng.mark(c.name + ".foldred")
+            C.narrow_c_bwd(dout.t, dout.ld, mode, mask, None, c.coef, None, 0, 0, yb.t, b.scale, b.shift, b.mean,
+                           b.rstd, c.wf, None, 8, 0, None, None, M, Cc, yb.C, rps, form=2,
+                           y1=None if one is None else y1.t, mc=c.mean, rc=c.rstd,
+                           m1=None if one is None else one.mean, r1=None if one is None else one.rstd, cpart=part)
+        elif pre is not None:   # dout is the masked dz, its partial sums came from the next unit's dgrad epilogue
             part, blocks = pre
             mode, mask, dz_out = 0, None, None
             if one is None:
@@ -857,15 +918,13 @@ class _ResBlock:
                 C.bn_bwd_apply(dout.t, dout.ld, mode, mask, Cc // 8 if mask is not None else 0, None, None, None,
                                None, None, y1.t, one.coef, dy1, None, 0, 0, M, Cc)
         dab = eng.ws((self.name, "dab"), (yb.M, self.b.C), eng.cdt)
-        rps = int(C.narrow_c_bwd_rps(M, Cc, eng.narrow_splits))
-        splits = (M + rps - 1) // rps
         slab = eng.scratch("narrow_slab", splits * Cc * yb.C)
         partb = eng.scratch("narrow_part", splits * 3 * yb.C)
         eng.mark(c.name + ".fusedbwd")
-        b = self.b
-        C.narrow_c_bwd(dout.t, dout.ld, mode, mask, yc.t, c.coef, None if dz_out is None else dz_out.t,
-                       0 if dz_out is None else dz_out.ld, 1 if (dz_out is not None and dx_accum) else 0, yb.t,
-                       b.scale, b.shift, b.mean, b.rstd, c.wf, dab, yb.C, 0, slab, partb, M, Cc, yb.C, rps)
+        C.narrow_c_bwd(dout.t, dout.ld, mode, mask, None if yc is None else yc.t, c.coef,
+                       None if dz_out is None else dz_out.t, 0 if dz_out is None else dz_out.ld,
+                       1 if (dz_out is not None and dx_accum) else 0, yb.t, b.scale, b.shift, b.mean, b.rstd, c.wf, dab,
+                       yb.C, 0, slab, partb, M, Cc, yb.C, rps, form=1 if self.narrow_fold else 0)
         C.wgrad_reduce(slab, fg.gview(c.conv.weight), splits, Cc, 1, c.spec.cin_pad, c.spec.cin, 1.0,
                        eng.grad_beta, 1)
         dyb, _ = b.bn_backward(Act(dab, yb.N, yb.T, yb.H, yb.W), yb, 0, None, None, pre=(partb, splits))
@@ -879,7 +938,7 @@ class _ResBlock:
             eng.mark(one.name + ".fusedbwd")
             slab1 = eng.scratch("narrow_slab", splits * Cc * x.C)
             C.narrow_c_bwd(dout.t, dout.ld, mode, mask, y1.t, one.coef, None, 0, 0, x.t, None, None, None, None,
-                           one.wf, dx, dx.stride(0), 1 if dx_accum else 0, slab1, None, M, Cc, x.C, rps)
+                           one.wf, dx, dx.stride(0), 1 if dx_accum else 0, slab1, None, M, Cc, x.C, rps, form=0)
             C.wgrad_reduce(slab1, fg.gview(one.conv.weight), splits, Cc, 1, s1.cin_pad, s1.cin, 1.0,
                            eng.grad_beta, 1)
             acc = True
@@ -1134,6 +1193,7 @@ class FusedNet:
         # fused narrow conv_c backward (csrc/kernels/narrow_bwd.hip); workgroups (= slab count) per launch
         self.narrow_bwd = os.environ.get("PVA_NARROW_BWD", "1") != "0"
         self.narrow_splits = int(os.environ.get("PVA_NARROW_SPLITS", "1024"))
+        self.narrow_fold = self.narrow_bwd and os.environ.get("PVA_NARROW_FOLD", "1") != "0"
         blocks = list(model.blocks)
         self.slowfast = isinstance(blocks[0], R.MultiPathWayWithFuse)
         self.stages: List[Tuple[List, Optional[_Fuse]]] = []

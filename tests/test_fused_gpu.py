@@ -211,22 +211,31 @@ def test_persistent_tune_cache_reused_and_invalidated(tmp_path, monkeypatch):
 
 def test_narrow_fused_backward_matches_unfused(monkeypatch):
     """The fused narrow conv_c backward (fast res2: BN apply + weight gradient + input gradient in one pass,
-    csrc/kernels/narrow_bwd.hip) against the three-kernel path it replaces (PVA_NARROW_BWD=0), deterministic mode:
-    same loss, every gradient within bf16 re-association noise."""
+    csrc/kernels/narrow_bwd.hip), with and without the narrow BN fold of the forward (PVA_NARROW_FOLD), against the
+    three-kernel unfolded path it replaces (PVA_NARROW_BWD=0), deterministic mode: loss, every gradient and the BN
+    running statistics within bf16 re-association noise."""
     model = _build(True)
     xs = _inputs(True, N=2, T=16, S=96, seed=3)
     labels = torch.tensor([2, 5], device=DEV)
-    grads = []
-    for flag in ("1", "0"):
+    runs = []
+    for flag, fold in (("1", "1"), ("1", "0"), ("0", "0")):
         monkeypatch.setenv("PVA_NARROW_BWD", flag)
+        monkeypatch.setenv("PVA_NARROW_FOLD", fold)
         m = copy.deepcopy(model)
         eng = FusedNet(m, DEV, deterministic=True)
-        used = [b for paths, _ in eng.stages for p in paths for b in getattr(p, "blocks", []) if b.narrow_c]
-        assert (len(used) > 0) == (flag == "1")
+        blocks = [b for paths, _ in eng.stages for p in paths for b in getattr(p, "blocks", [])]
+        assert any(b.narrow_c for b in blocks) == (flag == "1")
+        assert any(b.narrow_fold for b in blocks) == (fold == "1")
         loss, _ = eng.forward_backward(eng.prepare_inputs(xs), labels)
         torch.cuda.synchronize()
-        grads.append((float(loss), {n: p.grad.detach().clone() for n, p in m.named_parameters()}))
-    (l1, g1), (l0, g0) = grads
-    assert abs(l1 - l0) < 1e-6 * max(1.0, abs(l0))
-    worst = max((_rel(g1[n], g0[n]), n) for n in g0 if g0[n].norm() > 0)
-    assert worst[0] < 2e-2, worst
+        runs.append((float(loss), {n: p.grad.detach().clone() for n, p in m.named_parameters()},
+                     {n: b.detach().clone() for n, b in m.named_buffers()}))
+    l0, g0, b0 = runs[-1]
+    for l1, g1, b1 in runs[:-1]:
+        # the folded forward computes the same math in another order (stats-only pass + recomputing output kernel)
+        assert abs(l1 - l0) < 2e-3 * max(1.0, abs(l0)), (l1, l0)
+        worst = max((_rel(g1[n], g0[n]), n) for n in g0 if g0[n].norm() > 0)
+        assert worst[0] < 3e-2, worst
+        for n in b0:
+            if b0[n].dtype.is_floating_point:
+                assert _rel(b1[n], b0[n]) < 1e-2, n
