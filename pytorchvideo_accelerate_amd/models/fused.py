@@ -552,8 +552,8 @@ class _ConvBN:
             part, c, one = None, None, None
             if epi is not None:
                 part = self.eng.scratch("bnepi", ((g[0] + 127) // 128) * 3 * g[1])
-                # folded branch1: its sums come from G; narrow-fold unit: from its own reduce pass
-                c, one = epi.c, (None if (epi.fold1 or epi.narrow_fold) else epi.one)1
+                # folded branch1: its sums come from G1; narrow-fold unit: from its own reduce pass
+                c, one = epi.c, (None if (epi.fold1 or epi.narrow_fold) else epi.one)
 
             yc = None if (epi is None or epi.yc is None) else epi.yc   # folded conv_c: no raw output
 
