@@ -155,3 +155,25 @@ def test_res_stage_branch1_fold(fold1, monkeypatch):
     blk0 = eng_probe.stages[0][0][0].blocks[0]
     assert blk0.fold1 == (fold1 == "1")
     _run(net, [x], labels, [_act(x)])
+
+
+@pytest.mark.parametrize("narrow,nfold", [("0", "0"), ("1", "0"), ("1", "1")])
+def test_fast_res2_narrow(narrow, nfold, monkeypatch):
+    """The fast pathway's res2 shape (8 -> inner 8 -> 32, temporal conv_a, branch1 8 -> 32 on unit 0): unfolded
+    three-kernel backward, the fused narrow backward (csrc/kernels/narrow_bwd.hip), and the narrow BN fold (statistics
+    pass + fold_output forward, yc recomputed in the backward) — each against the fp32 oracle."""
+    monkeypatch.setenv("PVA_BN_FOLD_MIN_C", "100000")
+    monkeypatch.setenv("PVA_NARROW_BWD", narrow)
+    monkeypatch.setenv("PVA_NARROW_FOLD", nfold)
+    torch.manual_seed(2)
+    N, T, H = 4, 8, 16
+    stage = R.ResStage(3, 8, 8, 32, 3, 1)
+    R.init_net_weights(stage)
+    net = R.Net([stage, R.create_res_basic_head(32, 10, pool="default", pool_kernel_size=(T, H, H),
+                                                 dropout_rate=0.0)])
+    x = _x(N, 8, T, H, H, seed=5)
+    labels = torch.arange(N, device=DEV) % 10
+    probe = FusedNet(copy.deepcopy(net), DEV)
+    blks = probe.stages[0][0][0].blocks
+    assert all(b.narrow_c == (narrow == "1") for b in blks) and all(b.narrow_fold == (nfold == "1") for b in blks)
+    _run(net, [x], labels, [_act(x)])
