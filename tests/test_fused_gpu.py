@@ -243,7 +243,7 @@ def test_narrow_fused_backward_matches_unfused(monkeypatch):
     # (tests/test_blocks_gpu.py::test_fast_res2_narrow) against the fp32 oracle.
     lf, gf, bf = runs[0]
     assert abs(lf - l0) < 1e-2 * max(1.0, abs(l0)), (lf, l0)
-    for b1_ in (b1, bf):
+    for b1_, tol in ((b1, 1e-2), (bf, 3e-2)):
         for n in b0:
             if b0[n].dtype.is_floating_point:
-                assert _rel(b1_[n], b0[n]) < 1e-2, n
+                assert _rel(b1_[n], b0[n]) < tol, n
