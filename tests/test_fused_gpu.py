@@ -243,7 +243,12 @@ def test_narrow_fused_backward_matches_unfused(monkeypatch):
     # (tests/test_blocks_gpu.py::test_fast_res2_narrow) against the fp32 oracle.
     lf, gf, bf = runs[0]
     assert abs(lf - l0) < 1e-2 * max(1.0, abs(l0)), (lf, l0)
-    for b1_, tol in ((b1, 1e-2), (bf, 3e-2)):
+    # a running mean is measured on the scale of its feature's spread (relative to ~0 means it is noise-dominated)
+    def err(b, n):
+        if n.endswith("running_mean"):
+            return float((b[n] - b0[n]).norm() / b0[n[:-4] + "var"].clamp_min(0).sqrt().norm())
+        return _rel(b[n], b0[n])
+    for b1_, tol in ((b1, 1e-2), (bf, 2e-2)):
         for n in b0:
             if b0[n].dtype.is_floating_point:
-                assert _rel(b1_[n], b0[n]) < tol, n
+                assert err(b1_, n) < tol, (n, err(b1_, n))
