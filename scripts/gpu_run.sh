@@ -11,6 +11,8 @@
 #   layers   serialised per-op profile at B=$BATCH (default 160) + roofline table
 #   trace    rocprofv3 kernel trace of 3 steps -> steady-state kernel table
 #   pmc      rocprofv3 PMC passes (one run each) over a bench step at B=$BATCH -> per-kernel summary
+#   cfg      non-headline configs: bench + serialised per-op profile + roofline for R101 32x2x256 (B=160) and
+#            R50 64x2x224 (B=112)
 #   runpy    the reference CLI (run.py) at the headline shape on a synthetic corpus
 #   lab      tools/gemm_lab.hip: big-tile GEMM main loop at $LAB_SHAPES ("M,N,K ..."), cold and L2-hot A operand,
 #            plus one PMC pass per shape (MFMA busy, waits, L2 hits)
@@ -67,6 +69,16 @@ t_pmc() {
   done
   # raw per-dispatch CSVs are large (gpurun copies back at most 64 MiB): keep the summary only
   python3 scripts/pmc_step_summary.py $out/pmc > $out/pmc_summary_b$B.txt && rm -rf $out/pmc && head -30 $out/pmc_summary_b$B.txt
+}
+t_cfg() {
+  local spec tag args
+  for spec in "r101:--depth 101 --crop 256:160" "f64:--frames 64:112"; do
+    IFS=':' read -r tag args b <<< "$spec"
+    timeout -k 10 500 python bench.py --batch $b --steps 10 --warmup 3 $args > $out/cfg_$tag.json 2> $out/cfg_$tag.err || fail $out/cfg_$tag.err
+    cat $out/cfg_$tag.json
+    timeout -k 10 500 python -u scripts/layer_profile.py --batch $b --steps 2 $args > $out/cfg_${tag}_layers.txt 2> $out/cfg_${tag}_layers.err || fail $out/cfg_${tag}_layers.err
+    python scripts/layer_roofline.py $out/cfg_${tag}_layers.txt --batch $b $args > $out/cfg_${tag}_roofline.txt
+  done
 }
 t_runpy() {
   # the reference CLI at the headline shape over the native raw-frame reader (--num_workers 0 selects it): bench.py's
