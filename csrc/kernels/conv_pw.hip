@@ -13,6 +13,10 @@ bool conv_pw_run_ks1(const ConvParams& p, int ep, int ops, int rpb, int gch, siz
 bool conv_pw_run_ks2(const ConvParams& p, int ep, int ops, int rpb, int gch, size_t lds, hipStream_t st);
 bool conv_pw_run_ks4(const ConvParams& p, int ep, int ops, int rpb, int gch, size_t lds, hipStream_t st);
 bool conv_pw_run_ks8(const ConvParams& p, int ep, int ops, int rpb, int gch, size_t lds, hipStream_t st);
+bool conv_pw_run_ks1_w4(const ConvParams& p, int ep, int ops, int rpb, int gch, size_t lds, hipStream_t st);
+bool conv_pw_run_ks2_w4(const ConvParams& p, int ep, int ops, int rpb, int gch, size_t lds, hipStream_t st);
+bool conv_pw_run_ks4_w4(const ConvParams& p, int ep, int ops, int rpb, int gch, size_t lds, hipStream_t st);
+bool conv_pw_run_ks8_w4(const ConvParams& p, int ep, int ops, int rpb, int gch, size_t lds, hipStream_t st);
 
 namespace {
 constexpr int PW_LDS = 156 * 1024;     // LDS budget of a workgroup (weights, statistics, constants)
@@ -49,10 +53,10 @@ int conv_pw_legal(const ConvParams& p, int chunk) {
 
 // 32-channel chunks per output-channel group: the largest group whose weight image, statistics and epilogue
 // constants fit the LDS budget, then balanced over the groups (equal work per workgroup)
-static int pw_group_chunks(int N, int ks, int nslot, int aff_bytes) {
+static int pw_group_chunks(int N, int ks, int nslot, int aff_bytes, int budget) {
   const int nch = N / 32;
   const int per_chunk = 2 * ks * 1024 + (nslot + 4) * 32 * 4;
-  int gmax = std::max(1, (PW_LDS - aff_bytes) / per_chunk);
+  int gmax = std::max(1, (budget - aff_bytes) / per_chunk);
   if (gmax >= 2) gmax &= ~1;   // even groups: chunk pairs stay aligned to 128-B lines
   const int ngrp = (nch + gmax - 1) / gmax;
   const int g = (nch + ngrp - 1) / ngrp;
@@ -63,10 +67,13 @@ void conv_pw_launch(const ConvParams& p, int cfg, hipStream_t st) {
   const bool ep2 = !p.fres && (p.eres || p.emask || p.epart);
   const int ep = p.fres ? 1 : (ep2 ? 2 : 0);
   const int ks = pw_ks(p.Kfull);
-  // per-wave statistic slots [8 waves][statistics] per channel (none for the residual output)
-  const int nslot = ep == 1 ? 0 : (ep == 2 ? 3 : 2) * 8;
+  // cfg bit 3: 4-wave workgroups, their LDS budget halved so that at least two share a CU
+  const bool w4 = (cfg & 8) != 0;
+  const int nw = w4 ? 4 : 8;
+  // per-wave statistic slots [waves][statistics] per channel (none for the residual output)
+  const int nslot = ep == 1 ? 0 : (ep == 2 ? 3 : 2) * nw;
   const int aff_bytes = p.affine ? 2 * p.Cg * 4 : 0;
-  const int gch = pw_group_chunks(p.Ngemm, ks, nslot, aff_bytes);
+  const int gch = pw_group_chunks(p.Ngemm, ks, nslot, aff_bytes, w4 ? PW_LDS / 2 : PW_LDS);
   const int NG = gch * 32;
   size_t lds = (size_t)gch * 2 * ks * 1024 + (size_t)(nslot + 4) * NG * 4 + aff_bytes;
   // cfg bit 2: one workgroup per CU (the LDS request is padded past half the CU's LDS).  Instantiations
@@ -85,11 +92,15 @@ void conv_pw_launch(const ConvParams& p, int cfg, hipStream_t st) {
     if (p.ey1 && stats2) ops |= OP_Y1;
   }
   bool ok;
-  switch (ks) {
+  switch (ks * (w4 ? -1 : 1)) {
     case 1: ok = conv_pw_run_ks1(p, ep, ops, rpb, gch, lds, st); break;
     case 2: ok = conv_pw_run_ks2(p, ep, ops, rpb, gch, lds, st); break;
     case 4: ok = conv_pw_run_ks4(p, ep, ops, rpb, gch, lds, st); break;
-    default: ok = conv_pw_run_ks8(p, ep, ops, rpb, gch, lds, st); break;
+    case 8: ok = conv_pw_run_ks8(p, ep, ops, rpb, gch, lds, st); break;
+    case -1: ok = conv_pw_run_ks1_w4(p, ep, ops, rpb, gch, lds, st); break;
+    case -2: ok = conv_pw_run_ks2_w4(p, ep, ops, rpb, gch, lds, st); break;
+    case -4: ok = conv_pw_run_ks4_w4(p, ep, ops, rpb, gch, lds, st); break;
+    default: ok = conv_pw_run_ks8_w4(p, ep, ops, rpb, gch, lds, st); break;
   }
   if (!ok) {
     char msg[128];

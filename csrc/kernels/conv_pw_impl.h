@@ -37,8 +37,6 @@ PVA_NS_BEGIN
 
 namespace {
 
-constexpr int PW_WAVES = 8;
-constexpr int PW_THREADS = PW_WAVES * 64;
 constexpr int PW_LDS = 156 * 1024;     // LDS budget of a workgroup (weights, statistics, constants)
 
 // Butterfly reduce-scatter over the 16 lanes sharing lane >> 4 (one DPP row): v[L] in; lane rho ends up
@@ -101,11 +99,13 @@ struct Pre {
 // buffer descriptors / branches) only for its own streams, so the ring can be deeper
 constexpr int OP_OLD = 1, OP_RES = 2, OP_Y0 = 4, OP_Y1 = 8, OP_MASK = 16, OP_MSC = 32;
 
-template <int KS, int TM, int EP, int AFF, bool NTS, int OPS, int PD, int CPI, bool TP>
-__global__ __launch_bounds__(PW_THREADS) void conv_pw_kernel(const ConvParams p, int rpb, int gch) {
+// NW: waves per workgroup — 8, or 4 (cfg bit 3: an instantiation between 128 and 168 VGPRs then runs three
+// workgroups = 12 waves per CU instead of one 8-wave workgroup, the register file no longer rounding to 2 per SIMD)
+template <int KS, int TM, int EP, int AFF, bool NTS, int OPS, int PD, int CPI, bool TP, int NW>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) void conv_pw_kernel(const ConvParams p, int rpb, int gch) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NST = EP == 2 ? 3 : 2;
-  constexpr int NSLOT = EP == 1 ? 0 : NST * PW_WAVES;   // per-wave statistic slots (= conv_pw.hip)
+  constexpr int NSLOT = EP == 1 ? 0 : NST * NW;   // per-wave statistic slots (= conv_pw.hip)
   constexpr int MT = 16 * TM;   // PD: prefetch ring depth (chunks)
   const int N = p.Ngemm, K = p.Kfull, Ca = p.Cg;   // K = taps x Ca (1x1: K = Ca)
   // output-channel group of this workgroup (weights of wide convs do not fit LDS at once: the row range
@@ -118,7 +118,7 @@ __global__ __launch_bounds__(PW_THREADS) void conv_pw_kernel(const ConvParams p,
   const int nch = min(gch, (N >> 5) - cbase);               // chunks in this group
   const int NG = nch * 32, nb0 = cbase * 32;                // group channels, first channel
   const int wimg = nch * 2 * KS * 1024;
-  float* st_lds = reinterpret_cast<float*>(smem + wimg);   // [PW_WAVES][NST][NG] per-wave statistics
+  float* st_lds = reinterpret_cast<float*>(smem + wimg);   // [NW][NST][NG] per-wave statistics
   float* cst = st_lds + NSLOT * NG;                         // [4][NG] per-channel epilogue constants
   float* affs = cst + 4 * NG;                               // [2][Ca] input affine (per gathered channel)
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -130,7 +130,7 @@ __global__ __launch_bounds__(PW_THREADS) void conv_pw_kernel(const ConvParams p,
   // ---- weight image: fragment f = (c * 2 + h) * KS + s, lane l's 16 B at f * 1024 + 16 l:
   //      row rho of half h of chunk c = output channel 32c + 8(rho >> 2) + 4h + (rho & 3), k = 32s + 8(l >> 4)
   const int units = nch * 2 * KS * 64;
-  for (int u = tid; u < units; u += PW_THREADS) {
+  for (int u = tid; u < units; u += (NW * 64)) {
     const int l = u & 63, f = u >> 6;
     const int s = f % KS, ch = f / KS;
     const int h = ch & 1, c = ch >> 1;
@@ -144,11 +144,11 @@ __global__ __launch_bounds__(PW_THREADS) void conv_pw_kernel(const ConvParams p,
   const bool do_stats = (EP == 0 && p.stats != nullptr) || (EP == 2 && p.epart != nullptr);
   const bool nostore = EP == 0 && p.nostore != 0;
   if (do_stats)
-    for (int i = tid; i < NSLOT * NG; i += PW_THREADS) st_lds[i] = 0.f;
+    for (int i = tid; i < NSLOT * NG; i += (NW * 64)) st_lds[i] = 0.f;
   if (AFF)
-    for (int i = tid; i < Ca; i += PW_THREADS) { affs[i] = p.in_scale[i]; affs[Ca + i] = p.in_shift[i]; }
+    for (int i = tid; i < Ca; i += (NW * 64)) { affs[i] = p.in_scale[i]; affs[Ca + i] = p.in_shift[i]; }
   // EP 1: fsc fsh rsc rsh ; EP 0 / 2: bias (0 when absent), mask-affine scale and shift
-  for (int i = tid; i < NG; i += PW_THREADS) {
+  for (int i = tid; i < NG; i += (NW * 64)) {
     const int n = nb0 + i;
     if (EP == 1) {
       cst[i] = p.fsc[n]; cst[NG + i] = p.fsh[n];
@@ -207,7 +207,7 @@ __global__ __launch_bounds__(PW_THREADS) void conv_pw_kernel(const ConvParams p,
   //    and spills; so did seemingly equivalent rewrites of the prefetch below — check
   //    -Rpass-analysis=kernel-resource-usage after touching it.)
   const int nit = (nch + CPI - 1) / CPI;
-  const int tstride = PW_WAVES * MT;
+  const int tstride = NW * MT;
   const int mfirst = row0 + wid * MT;
   const int ntw = mfirst < row_end ? (row_end - mfirst + tstride - 1) / tstride : 0;
   // this lane's activation offsets within a row (k past K -> out of bounds -> zero).  Temporal taps (kt,1,1),
@@ -469,18 +469,18 @@ __global__ __launch_bounds__(PW_THREADS) void conv_pw_kernel(const ConvParams p,
   }
   if (!do_stats) return;
   __syncthreads();
-  for (int i = tid; i < NST * NG; i += PW_THREADS) {
+  for (int i = tid; i < NST * NG; i += (NW * 64)) {
     const int k = i / NG, nl = i - k * NG, n = nb0 + nl;
     float v = 0.f;
 #pragma unroll
-    for (int w = 0; w < PW_WAVES; ++w) v += st_lds[w * NST * NG + i];
+    for (int w = 0; w < NW; ++w) v += st_lds[w * NST * NG + i];
     if (EP == 2 && k > 0) {   // sum v * xhat = rstd (sum v y - mean sum v)
       const float* mean = k == 1 ? p.emean0 : p.emean1;
       const float* rstd = k == 1 ? p.erstd0 : p.erstd1;
       const bool have = k == 1 ? p.ey0 != nullptr : p.ey1 != nullptr;
       float s0 = 0.f;   // sum v over the waves (the same fixed order as above)
 #pragma unroll
-      for (int w = 0; w < PW_WAVES; ++w) s0 += st_lds[w * NST * NG + nl];
+      for (int w = 0; w < NW; ++w) s0 += st_lds[w * NST * NG + nl];
       v = have ? (v - mean[n] * s0) * rstd[n] : 0.f;
     }
     if (EP == 2) p.epart[((int64_t)rblk * 3 + k) * N + n] = v;
@@ -488,7 +488,7 @@ __global__ __launch_bounds__(PW_THREADS) void conv_pw_kernel(const ConvParams p,
   }
 }
 
-template <int KS, int TM, int EP, int AFF, int OPS, int PD, bool TP>
+template <int KS, int TM, int EP, int AFF, int OPS, int PD, bool TP, int NW>
 void launch_one(const ConvParams& p, int rpb, int gch, size_t lds, hipStream_t st) {
   // non-temporal (streaming) output stores for the BN-folded residual output, whose 16-B rows are never
   // re-read while L2-resident (measured +8 % on the res2 shape, scripts/pw_probe.py); the other epilogues
@@ -496,35 +496,38 @@ void launch_one(const ConvParams& p, int rpb, int gch, size_t lds, hipStream_t s
   // it, keeping the registers of a ring stage.  One-chunk groups (N = 32) run the single-chunk variant at
   // KS = 1 (the fast pathway's layers) and the pair variant (half a pair idle) otherwise.
   const int ngrp = ((p.Ngemm >> 5) + gch - 1) / gch;
-  const dim3 grid(((p.M + rpb - 1) / rpb) * ngrp), block(PW_THREADS);
+  const dim3 grid(((p.M + rpb - 1) / rpb) * ngrp), block(NW * 64);
+  // 4-wave workgroups: one ring stage less (the third wave per SIMD hides the latency instead), which brings the
+  // residual-output and two-stream epilogues under the 168 VGPRs of three waves per SIMD
+  constexpr int PDW = (NW == 4 && PD > 2) ? PD - 1 : PD;
   if constexpr (KS == 1) {
     if (gch < 2) {
-      hipLaunchKernelGGL((conv_pw_kernel<KS, TM, EP, AFF, EP == 1, OPS, PD, 1, TP>), grid, block, lds, st, p, rpb, gch);
+      hipLaunchKernelGGL((conv_pw_kernel<KS, TM, EP, AFF, EP == 1, OPS, PDW, 1, TP, NW>), grid, block, lds, st, p, rpb, gch);
       return;
     }
   }
-  hipLaunchKernelGGL((conv_pw_kernel<KS, (TM > 1 ? TM / 2 : 1), EP, AFF, EP == 1, OPS, PD, 2, TP>), grid, block, lds,
+  hipLaunchKernelGGL((conv_pw_kernel<KS, (TM > 1 ? TM / 2 : 1), EP, AFF, EP == 1, OPS, PDW, 2, TP, NW>), grid, block, lds,
                      st, p, rpb, gch);
 }
 
-template <int KS, int TM, int EP, int OPS, int PD, bool TP>
+template <int KS, int TM, int EP, int OPS, int PD, bool TP, int NW>
 void launch_aff(const ConvParams& p, int rpb, int gch, size_t lds, hipStream_t st) {
   switch (EP == 2 ? 0 : p.affine) {
-    case 0: launch_one<KS, TM, EP, 0, OPS, PD, TP>(p, rpb, gch, lds, st); break;
-    case 1: launch_one<KS, TM, EP, 1, OPS, PD, TP>(p, rpb, gch, lds, st); break;
-    default: launch_one<KS, TM, EP, 2, OPS, PD, TP>(p, rpb, gch, lds, st); break;
+    case 0: launch_one<KS, TM, EP, 0, OPS, PD, TP, NW>(p, rpb, gch, lds, st); break;
+    case 1: launch_one<KS, TM, EP, 1, OPS, PD, TP, NW>(p, rpb, gch, lds, st); break;
+    default: launch_one<KS, TM, EP, 2, OPS, PD, TP, NW>(p, rpb, gch, lds, st); break;
   }
 }
 
 // backward-BN epilogue: tile rows and ring depth sized by the 16-B operand streams an instantiation
 // carries (a lane holds TM * 16 B per stream per ring stage)
-template <int KS, int OPS, bool TP>
+template <int KS, int OPS, bool TP, int NW>
 void launch_ep2(const ConvParams& p, int rpb, int gch, size_t lds, hipStream_t st) {
   constexpr int nops = ((OPS >> 0) & 1) + ((OPS >> 1) & 1) + ((OPS >> 2) & 1) + ((OPS >> 3) & 1);
   constexpr int TM0 = nops <= 1 ? 4 : 2;
   constexpr int TM = KS <= 2 ? TM0 : KS == 4 ? 2 : TM0 / 2;
   constexpr int PD = nops <= 2 ? 3 : 2;
-  launch_one<KS, TM, 2, 0, OPS, PD, TP>(p, rpb, gch, lds, st);
+  launch_one<KS, TM, 2, 0, OPS, PD, TP, NW>(p, rpb, gch, lds, st);
 }
 
 // the operand-stream combinations the dgrad epilogues produce (models/fused.py): the BN path (ReLU from
@@ -540,14 +543,14 @@ constexpr int EP2_OPS[] = {
     OP_MASK | OP_Y0 | OP_Y1 | OP_RES | OP_OLD};
 constexpr int N_EP2_OPS = sizeof(EP2_OPS) / sizeof(EP2_OPS[0]);
 
-template <int KS, bool TP, int I = 0>
+template <int KS, bool TP, int NW, int I = 0>
 bool launch_ep2_ops(const ConvParams& p, int ops, int rpb, int gch, size_t lds, hipStream_t st) {
   if constexpr (I < N_EP2_OPS) {
     if (ops == EP2_OPS[I]) {
-      launch_ep2<KS, EP2_OPS[I], TP>(p, rpb, gch, lds, st);
+      launch_ep2<KS, EP2_OPS[I], TP, NW>(p, rpb, gch, lds, st);
       return true;
     }
-    return launch_ep2_ops<KS, TP, I + 1>(p, ops, rpb, gch, lds, st);
+    return launch_ep2_ops<KS, TP, NW, I + 1>(p, ops, rpb, gch, lds, st);
   } else {
     return false;
   }
@@ -555,25 +558,25 @@ bool launch_ep2_ops(const ConvParams& p, int ops, int rpb, int gch, size_t lds, 
 
 // forward epilogues: 64-row tiles (32 at K > 128), 3-deep ring; false: no instantiation for `ops`.  TP: the
 // temporal-tap loader (no residual-output epilogue: that one belongs to the 1x1 conv_c)
-template <int KS, bool TP>
+template <int KS, bool TP, int NW>
 bool launch_ks_tp(const ConvParams& p, int ep, int ops, int rpb, int gch, size_t lds, hipStream_t st) {
   constexpr int TMF = KS <= 4 ? 4 : 2;
   if (ep == 1) {
     if constexpr (TP) return false;
-    else { launch_aff<KS, TMF, 1, OP_RES, 3, false>(p, rpb, gch, lds, st); return true; }
+    else { launch_aff<KS, TMF, 1, OP_RES, 3, false, NW>(p, rpb, gch, lds, st); return true; }
   }
   if (ep == 0) {
-    if (ops & OP_OLD) launch_aff<KS, TMF, 0, OP_OLD, 3, TP>(p, rpb, gch, lds, st);
-    else launch_aff<KS, TMF, 0, 0, 3, TP>(p, rpb, gch, lds, st);
+    if (ops & OP_OLD) launch_aff<KS, TMF, 0, OP_OLD, 3, TP, NW>(p, rpb, gch, lds, st);
+    else launch_aff<KS, TMF, 0, 0, 3, TP, NW>(p, rpb, gch, lds, st);
     return true;
   }
-  return launch_ep2_ops<KS, TP>(p, ops, rpb, gch, lds, st);
+  return launch_ep2_ops<KS, TP, NW>(p, ops, rpb, gch, lds, st);
 }
 
-template <int KS>
+template <int KS, int NW>
 bool launch_ks(const ConvParams& p, int ep, int ops, int rpb, int gch, size_t lds, hipStream_t st) {
-  return p.nt > 1 ? launch_ks_tp<KS, true>(p, ep, ops, rpb, gch, lds, st)
-                  : launch_ks_tp<KS, false>(p, ep, ops, rpb, gch, lds, st);
+  return p.nt > 1 ? launch_ks_tp<KS, true, NW>(p, ep, ops, rpb, gch, lds, st)
+                  : launch_ks_tp<KS, false, NW>(p, ep, ops, rpb, gch, lds, st);
 }
 
 }  // namespace

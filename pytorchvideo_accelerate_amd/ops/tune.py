@@ -43,6 +43,7 @@ BIG_PF = 4096         #   with BK64 + DMA: L2 touch-prefetch of the A rows one k
 PW = 512              # streaming pointwise kernel (csrc/kernels/conv_pw.hip): dense 1x1x1 GEMMs, K <= 256,
 PW_ROWS = (1024, 2048, 4096)   # N % 32 == 0, weights in LDS; bits 0-1 select the rows per workgroup,
 PW_SOLO = 4                     # bit 2 one workgroup per CU
+PW_W4 = 8                       # bit 3 4-wave workgroups (three per CU at <= 168 VGPRs)
 HALO = 2048           # halo-staged (1,3,3) stride-1 kernel (csrc/kernels/conv_halo.hip): bit 0 = 64-channel
                       # n-tiles (else 128), bits 12+ = positions per tile; bit 1 = persistent 64-channel variant
 HALO_P = 2            #   (weights resident in LDS; bit 2: 4 workgroups per CU-slot instead of 1)
@@ -60,7 +61,7 @@ def describe(cfg: int) -> str:
             return "halo%d/p%d" % (cfg >> 12, 1024 if cfg & HALO_P4 else 256)
         return "halo%d/n%d" % (cfg >> 12, 64 if cfg & 1 else 128)
     if cfg & PW:
-        return "pw%d%s" % (PW_ROWS[cfg & 3], "s" if cfg & PW_SOLO else "")
+        return "pw%d%s%s" % (PW_ROWS[cfg & 3], "s" if cfg & PW_SOLO else "", "/w4" if cfg & PW_W4 else "")
     if cfg & DIRECT:
         return "direct%d%s" % (2048 if cfg & DIRECT_2K else 512, "/rt2" if cfg & DIRECT_HALF else "")
     if cfg & BIG:
@@ -85,6 +86,7 @@ class ConvTuner:
         self.halo = os.environ.get("PVA_CONV_HALO", "1") != "0"
         self.big_half = os.environ.get("PVA_CONV_BIG_HALF", "1") != "0"
         self.pf = os.environ.get("PVA_CONV_PF", "1") != "0"
+        self.pw_w4 = os.environ.get("PVA_CONV_PW_W4", "1") != "0"
         # debugging aid: PVA_PW_KINDS=f,fres,er,... restricts the pointwise kernel to launches whose key
         # starts with one of these kinds (models/fused.py: f fres fw2 eb er d)
         kinds = os.environ.get("PVA_PW_KINDS")
@@ -146,6 +148,8 @@ class ConvTuner:
             self._pw_seen += 1
             if self.pw_only is None or self.pw_only == self._pw_seen - 1:
                 out += [EXPLICIT | PW | s | v for s in (0, PW_SOLO) for v in range(len(PW_ROWS))]
+                if self.pw_w4:
+                    out += [EXPLICIT | PW | PW_W4 | v for v in range(len(PW_ROWS))]
         return out
 
     def bm(self, cfg: int, N: int) -> int:

@@ -18,8 +18,8 @@ def _C():
 
 
 def _cfgs():
-    from pytorchvideo_accelerate_amd.ops.tune import EXPLICIT, PW, PW_ROWS
-    return [EXPLICIT | PW | v for v in range(len(PW_ROWS))]
+    from pytorchvideo_accelerate_amd.ops.tune import EXPLICIT, PW, PW_ROWS, PW_W4
+    return [EXPLICIT | PW | w | v for w in (0, PW_W4) for v in range(len(PW_ROWS))]
 
 
 def _rel(a, b):
