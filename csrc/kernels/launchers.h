@@ -94,6 +94,10 @@ void head_backward_launch(const float* dlogits, const float* xm, const float* W,
                           float p_drop, uint64_t seed, const uint64_t* seedp, float* dW, float* db, float beta,
                           float* dfeat, float* dlT, float* xmT, float* WT, hipStream_t s);
 void head_dropout_mask_launch(int64_t total, float p_drop, uint64_t seed, uint8_t* out, hipStream_t s);
+int lateral_bwd_legal(int CO, int Cf, int alpha, int To, int Tf, int kt, int pad);
+void lateral_bwd_launch(const uint16_t* g, int ldg, const uint16_t* y, const float* sc, const float* sh,
+                        const float* coef, const uint16_t* wd, uint16_t* dy, uint16_t* dx, int ldx, int N, int To,
+                        int Tf, int HW, int CO, int Cf, int alpha, hipStream_t s);
 int narrow_c_bwd_legal(int CO, int CI);
 int narrow_c_bwd_rps(int64_t M, int CO, int splits);
 void narrow_c_bwd_launch(const uint16_t* g, int ldg, int mode, const uint8_t* mask, const uint16_t* yc,

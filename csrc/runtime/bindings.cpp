@@ -617,6 +617,23 @@ void narrow_c_bwd(const at::Tensor& g, int64_t ldg, int64_t mode, const OptT& ma
                                (int)CI, (int)rps, cur_stream());
 }
 
+// fused lateral-connection backward (csrc/kernels/lateral_bwd.hip): BN-backward apply (ReLU mask from the forward
+// affine) + the strided temporal input gradient accumulated into dx; dy optionally stored for the weight gradient
+void lateral_bwd(const at::Tensor& g, int64_t ldg, const at::Tensor& y, const at::Tensor& sc, const at::Tensor& sh,
+                 const at::Tensor& coef, const at::Tensor& wd, const OptT& dy, const at::Tensor& dx, int64_t ldx,
+                 int64_t N, int64_t To, int64_t Tf, int64_t HW, int64_t CO, int64_t Cf, int64_t alpha) {
+  const bool h = kind16(g);
+  TORCH_CHECK(pva_bf16::lateral_bwd_legal((int)CO, (int)Cf, (int)alpha, (int)To, (int)Tf, 7, 3),
+              "lateral_bwd: unsupported geometry");
+  TORCH_CHECK(ldg % 8 == 0 && ldx % 8 == 0 && ldg >= CO && ldx >= Cf, "lateral_bwd: 16-B aligned rows");
+  TORCH_CHECK(y.numel() >= N * To * HW * CO && g.numel() >= (N * To * HW - 1) * ldg + CO, "lateral_bwd: slow sizes");
+  TORCH_CHECK(dx.numel() >= (N * Tf * HW - 1) * ldx + Cf && wd.numel() >= Cf * 7 * CO, "lateral_bwd: fast sizes");
+  TORCH_CHECK(!dy.has_value() || dy->numel() >= N * To * HW * CO, "lateral_bwd: dy size");
+  TORCH_CHECK(To * HW * ldg < (1LL << 30) && Tf * HW * ldx < (1LL << 30), "lateral_bwd: per-clip 32-bit offsets");
+  KSEL(h, lateral_bwd_launch)(bfp(g), (int)ldg, bfp(y), f32(sc), f32(sh), f32(coef), bfp(wd), bfom(dy), bfpm(dx),
+                              (int)ldx, (int)N, (int)To, (int)Tf, (int)HW, (int)CO, (int)Cf, (int)alpha, cur_stream());
+}
+
 void synth_frames(const at::Tensor& out, int64_t seed) {
   pva_bf16::synth_frames_launch(out.data_ptr<uint8_t>(), out.numel(), (uint32_t)seed, cur_stream());
 }
@@ -757,6 +774,10 @@ PYBIND11_MODULE(_C, m) {
         py::arg("slab"), py::arg("part"), py::arg("M"), py::arg("CO"), py::arg("CI"), py::arg("rps"),
         py::arg("form") = 0, py::arg("y1") = py::none(), py::arg("mc") = py::none(), py::arg("rc") = py::none(),
         py::arg("m1") = py::none(), py::arg("r1") = py::none(), py::arg("cpart") = py::none());
+  m.def("lateral_bwd", &lateral_bwd);
+  m.def("lateral_bwd_legal", [](int64_t CO, int64_t Cf, int64_t alpha, int64_t To, int64_t Tf, int64_t kt, int64_t pad) {
+    return (bool)pva_bf16::lateral_bwd_legal((int)CO, (int)Cf, (int)alpha, (int)To, (int)Tf, (int)kt, (int)pad);
+  });
   m.def("narrow_c_bwd_legal", [](int64_t CO, int64_t CI) { return (bool)pva_bf16::narrow_c_bwd_legal((int)CO, (int)CI); });
   m.def("narrow_c_bwd_rps", [](int64_t M, int64_t CO, int64_t splits) {
     return (int64_t)pva_bf16::narrow_c_bwd_rps(M, (int)CO, (int)splits);

@@ -1105,6 +1105,7 @@ class _Fuse:
         self.u = _ConvBN(eng, f.conv_fast_to_slow, f.norm, name)
         self.eng, self.name = eng, name
         self.units = [self.u]
+        self.lateral_used = False   # the last backward ran the fused lateral kernel
 
     def fwd(self, xf: Act, cat_slice: torch.Tensor, train: bool, tag: str):
         y = self.u.fwd(xf, None, train, tag)
@@ -1112,13 +1113,42 @@ class _Fuse:
         self.eng.C.bn_act(y.t, y.ld, cat_slice, cat_slice.stride(0), self.u.scale, self.u.shift, 1, y.M, self.u.C)
         self.xf_in, self.y = xf, y
 
+    def _lateral_ok(self, x: Act, dcat_slice: Act, dfast: torch.Tensor) -> bool:
+        s, y = self.u.spec, self.y
+        return (self.eng.lateral_bwd and tuple(s.k[1:]) == (1, 1) and tuple(s.stride[1:]) == (1, 1)
+                and tuple(s.pad[1:]) == (0, 0) and s.cin_pad == s.cin and (y.H, y.W) == (x.H, x.W)
+                and dcat_slice.ld % 8 == 0 and dfast.stride(0) % 8 == 0
+                and bool(self.eng.C.lateral_bwd_legal(s.cout, s.cin, s.stride[0], y.T, x.T, s.k[0], s.pad[0])))
+
     def bwd(self, dcat_slice: Act, dfast: torch.Tensor):
-        """dcat_slice: grad wrt the fusion output slice; accumulates into dfast (grad wrt fast input)."""
-        y = self.y
-        dy, _ = self.u.bn_backward(dcat_slice, y, 2, None, self.u.xf())
-        self.u.wgrad(dy, self.xf_in, None)
+        """dcat_slice: grad wrt the fusion output slice; accumulates into dfast (grad wrt fast input).
+
+        Fused path (csrc/kernels/lateral_bwd.hip): after the BN-backward reduce, one kernel applies the BN backward
+        and accumulates the strided temporal input gradient (dy formed in registers, every dx frame read and written
+        once); it also stores dy for the weight gradient.  Otherwise: apply, weight gradient, stride-phase dgrad."""
+        y, u, eng = self.y, self.u, self.eng
         x = self.xf_in
-        self.u.dgrad(dy, (x.T, x.H, x.W), dfast, True)
+        self.lateral_used = self._lateral_ok(x, dcat_slice, dfast)
+        if self.lateral_used:
+            C = eng.C
+            M, Cc = y.M, u.C
+            blocks, rpb = eng._bn_blocks(M, Cc)
+            eng.mark(u.name + ".bnred")
+            part = eng.scratch("bnpart", blocks * 3 * Cc)
+            C.bn_bwd_reduce(dcat_slice.t, dcat_slice.ld, 2, None, 0, u.scale, u.shift, y.t, u.mean, u.rstd,
+                            None, None, None, M, Cc, blocks, rpb, part)
+            fg = eng.flat
+            C.bn_bwd_finalize(part, blocks, Cc, M, 0, u.bn.weight, u.mean, u.rstd, fg.gview(u.bn.weight),
+                              fg.gview(u.bn.bias), eng.grad_beta, u.coef, u.fin)
+            dy = eng.ws((u.name, "dy"), (M, Cc), eng.cdt)
+            eng.mark(self.name + ".latbwd")
+            C.lateral_bwd(dcat_slice.t, dcat_slice.ld, y.t, u.scale, u.shift, u.coef, u.wd, dy, dfast,
+                          dfast.stride(0), x.N, y.T, x.T, y.H * y.W, Cc, u.spec.cin, u.spec.stride[0])
+            u.wgrad(Act(dy, y.N, y.T, y.H, y.W), x, None)
+            return
+        dy, _ = u.bn_backward(dcat_slice, y, 2, None, u.xf())
+        u.wgrad(dy, x, None)
+        u.dgrad(dy, (x.T, x.H, x.W), dfast, True)
 
 
 class FusedNet:
@@ -1146,6 +1176,8 @@ class FusedNet:
         # (cosine ~0.65 at B=4-32: scripts/diag_ms_race.py).  On by default (only the few Gram / G launches pay the
         # slab reduction); PVA_FOLD_SLABS=0 turns it off; implied by ``deterministic``.
         self.fold_slabs = deterministic or os.environ.get("PVA_FOLD_SLABS", "1") == "1"
+        # fused lateral-connection backward (apply + strided dgrad in one pass); PVA_LATERAL_BWD=0: the unfused path
+        self.lateral_bwd = os.environ.get("PVA_LATERAL_BWD", "1") != "0"
         self.stem_s2d = stem_s2d and not deterministic
         self.model = model
         self.device = torch.device(device)
