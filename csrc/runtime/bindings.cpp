@@ -626,8 +626,10 @@ void lateral_bwd(const at::Tensor& g, int64_t ldg, const at::Tensor& y, const at
   TORCH_CHECK(pva_bf16::lateral_bwd_legal((int)CO, (int)Cf, (int)alpha, (int)To, (int)Tf, 7, 3),
               "lateral_bwd: unsupported geometry");
   TORCH_CHECK(ldg % 8 == 0 && ldx % 8 == 0 && ldg >= CO && ldx >= Cf, "lateral_bwd: 16-B aligned rows");
-  TORCH_CHECK(y.numel() >= N * To * HW * CO && g.numel() >= (N * To * HW - 1) * ldg + CO, "lateral_bwd: slow sizes");
-  TORCH_CHECK(dx.numel() >= (N * Tf * HW - 1) * ldx + Cf && wd.numel() >= Cf * 7 * CO, "lateral_bwd: fast sizes");
+  TORCH_CHECK(y.numel() >= N * To * HW * CO && g.dim() == 2 && g.size(0) >= N * To * HW && g.size(1) >= CO &&
+              g.stride(0) == ldg, "lateral_bwd: slow sizes");
+  TORCH_CHECK(dx.dim() == 2 && dx.size(0) >= N * Tf * HW && dx.size(1) >= Cf && dx.stride(0) == ldx &&
+              wd.numel() >= Cf * 7 * CO, "lateral_bwd: fast sizes");
   TORCH_CHECK(!dy.has_value() || dy->numel() >= N * To * HW * CO, "lateral_bwd: dy size");
   TORCH_CHECK(To * HW * ldg < (1LL << 30) && Tf * HW * ldx < (1LL << 30), "lateral_bwd: per-clip 32-bit offsets");
   KSEL(h, lateral_bwd_launch)(bfp(g), (int)ldg, bfp(y), f32(sc), f32(sh), f32(coef), bfp(wd), bfom(dy), bfpm(dx),
