@@ -30,7 +30,7 @@ namespace {
 
 constexpr int LAT_WAVES = 8;
 constexpr int LAT_POS = LAT_WAVES * 16;   // positions of a workgroup (one 16-row MFMA tile per wave)
-constexpr int LAT_CG = 32;                // dx channels of a workgroup
+constexpr int LAT_CG = 32;                // dx channels of a workgroup (8 for the stem lateral's 8 fast channels)
 constexpr int LAT_KT = 7;
 constexpr uint32_t LAT_OOB = 0x80000000u;
 typedef __attribute__((ext_vector_type(4))) unsigned u32x4_t_;
@@ -47,19 +47,22 @@ struct LateralBwdParams {
   int ldg, ldx, N, To, Tf, HW, Cf, alpha;
 };
 
-template <int CO>
+// CO: slow channels (16: the stem lateral — half a k-step, lanes of k-chunks 2-3 carry zeros); CG: dx channels per
+// workgroup, 32 (two 16-row MFMA halves, 8 consecutive channels per lane) or 8 (rows 0-3 of each half: only the
+// lanes of k-chunk 0 hold real outputs)
+template <int CO, int CG>
 __global__ __launch_bounds__(LAT_WAVES * 64) void lateral_bwd_kernel(const LateralBwdParams p) {
-  constexpr int KS = CO / 32;                    // MFMA k-steps over the slow channels
+  constexpr int KS = CO < 32 ? 1 : CO / 32;      // MFMA k-steps over the slow channels
   constexpr int NFRAG = LAT_KT * 2 * KS;         // weight fragments (tap, half, k-step), 1 KB each
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* cst = reinterpret_cast<float*>(smem + NFRAG * 1024);   // [5][CO]: A B C sc sh
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int rho = lane & 15, kc = lane >> 4;
-  const int ngrp = p.Cf / LAT_CG, ntile = (p.HW + LAT_POS - 1) / LAT_POS;
+  const int ngrp = p.Cf / CG, ntile = (p.HW + LAT_POS - 1) / LAT_POS;
   const int L = xcd_remap(blockIdx.x, gridDim.x);   // the channel groups of one tile: adjacent ids, one XCD's L2
   const int grp = L % ngrp, rest = L / ngrp;
   const int tile = rest % ntile, n = rest / ntile;
-  const int cbase = grp * LAT_CG;
+  const int cbase = grp * CG;
 
   // ---- weight image: fragment f = (kt * 2 + h) * KS + s; lane l's 16 B = W[co = 32 s + 8 (l >> 4) .. + 8][kt][ci],
   //      ci = cbase + 8 (r >> 2) + 4 h + (r & 3) for row r = l & 15 — contiguous in the dgrad pack
@@ -69,8 +72,9 @@ __global__ __launch_bounds__(LAT_WAVES * 64) void lateral_bwd_kernel(const Later
     const int r = l & 15;
     const int ci = cbase + 8 * (r >> 2) + 4 * h + (r & 3);
     const int co = 32 * s + 8 * (l >> 4);
+    const bool ok = co < CO && 8 * (r >> 2) < CG;
     *reinterpret_cast<uint4*>(smem + (int64_t)u * 16) =
-        *reinterpret_cast<const uint4*>(p.wd + ((int64_t)ci * LAT_KT + kt) * CO + co);
+        ok ? *reinterpret_cast<const uint4*>(p.wd + ((int64_t)ci * LAT_KT + kt) * CO + co) : uint4{0, 0, 0, 0};
   }
   for (int i = tid; i < CO; i += LAT_WAVES * 64) {
     cst[i] = p.coef[i];
@@ -94,12 +98,19 @@ __global__ __launch_bounds__(LAT_WAVES * 64) void lateral_bwd_kernel(const Later
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(p.dx + fast0 * p.ldx), (short)0, p.Tf * p.HW * p.ldx * 2, 0x00020000);
   const bool store_dy = p.dy != nullptr && grp == 0;
+  const bool kv = 8 * kc < CO;                   // this lane's k-chunk holds slow channels (CO 16: chunks 0-1)
+  const bool ov = CG == 32 || kc == 0;           // this lane holds dx outputs
   // slow-side offsets of frame t (lane: its position, channels 32 s + 8 kc ..)
-  auto goff = [&](int t, int s) { return live ? (uint32_t)(((t * p.HW + pos) * p.ldg + 32 * s + 8 * kc) * 2) : LAT_OOB; };
-  auto yoff = [&](int t, int s) { return live ? (uint32_t)(((t * p.HW + pos) * CO + 32 * s + 8 * kc) * 2) : LAT_OOB; };
+  auto goff = [&](int t, int s) {
+    return live && kv ? (uint32_t)(((t * p.HW + pos) * p.ldg + 32 * s + 8 * kc) * 2) : LAT_OOB;
+  };
+  auto yoff = [&](int t, int s) {
+    return live && kv ? (uint32_t)(((t * p.HW + pos) * CO + 32 * s + 8 * kc) * 2) : LAT_OOB;
+  };
   // fast-side offset of frame t (lane: its position, 8 channels cbase + 8 kc ..); frames outside the clip: OOB
   auto xoff = [&](int t) {
-    return (live && t >= 0 && t < p.Tf) ? (uint32_t)(((t * p.HW + pos) * p.ldx + cbase + 8 * kc) * 2) : LAT_OOB;
+    return (live && ov && t >= 0 && t < p.Tf) ? (uint32_t)(((t * p.HW + pos) * p.ldx + cbase + 8 * kc) * 2)
+                                               : LAT_OOB;
   };
 
   uint4 G[KS], Y[KS];
@@ -132,7 +143,10 @@ __global__ __launch_bounds__(LAT_WAVES * 64) void lateral_bwd_kernel(const Later
   const char* wl = smem + lane * 16;
   // one slow frame: `cur` holds the old dx of its frames, `nxt` receives the next frame's (two named register sets,
   // alternated by the 2x unrolled loop below — no runtime-indexed register array)
+  // CO 256: the next frame's g / y (64 VGPRs) are loaded at the top of its own step instead (one spill otherwise)
+  constexpr bool PF_GY = KS <= 4;
   auto step = [&](int t, const uint4 (&cur)[4], uint4 (&nxt)[4]) {
+    if (!PF_GY) load_gy(t);
     // ---- apply: dy = A * (g masked by relu(y sc + sh)) + B y + C, rounded (bn_bwd_apply's arithmetic)
     ev8_t b[KS];
     // the per-channel constants are re-read from LDS every frame: hoisted out of the loop they pin 5 x 8 x KS VGPRs
@@ -143,7 +157,7 @@ __global__ __launch_bounds__(LAT_WAVES * 64) void lateral_bwd_kernel(const Later
     const float* cs = cst + z;
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
-      const int c0 = 32 * s + 8 * kc;
+      const int c0 = kv ? 32 * s + 8 * kc : 0;   // (lanes past CO: zero operands, constants of channel 0 unused)
       float dz[8], a[8], o[8];
       unpack8(G[s], dz);
       unpack8(Y[s], a);
@@ -152,12 +166,12 @@ __global__ __launch_bounds__(LAT_WAVES * 64) void lateral_bwd_kernel(const Later
         dz[e] = (a[e] * cs[3 * CO + c0 + e] + cs[4 * CO + c0 + e]) > 0.f ? dz[e] : 0.f;
         o[e] = cs[c0 + e] * dz[e] + cs[CO + c0 + e] * a[e] + cs[2 * CO + c0 + e];
       }
-      const uint4 pk = pack8(o);
+      const uint4 pk = kv ? pack8(o) : uint4{0, 0, 0, 0};
       if (store_dy) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t_, pk), dyr, yoff(t, s), 0, 0);
       b[s] = __builtin_bit_cast(ev8_t, pk);
     }
     if (t + 1 < p.To) {
-      load_gy(t + 1);
+      if (PF_GY) load_gy(t + 1);
       load_old(t + 1, nxt);
     }
     // ---- taps: frame alpha t + kt - 3
@@ -185,7 +199,7 @@ __global__ __launch_bounds__(LAT_WAVES * 64) void lateral_bwd_kernel(const Later
     }
   };
   uint4 O0[4], O1[4];
-  load_gy(0);
+  if (PF_GY) load_gy(0);
   load_old(0, O0);
 #pragma unroll 1
   for (int t = 0; t < p.To; t += 2) {
@@ -204,7 +218,7 @@ __global__ __launch_bounds__(LAT_WAVES * 64) void lateral_bwd_kernel(const Later
 }  // namespace
 
 int lateral_bwd_legal(int CO, int Cf, int alpha, int To, int Tf, int kt, int pad) {
-  return (CO == 64 || CO == 128) && Cf % LAT_CG == 0 && alpha == 4 && Tf == alpha * To && kt == LAT_KT && pad == 3 &&
+  return ((CO == 16 && Cf == 8) || ((CO == 64 || CO == 128 || CO == 256) && Cf % LAT_CG == 0)) && alpha == 4 && Tf == alpha * To && kt == LAT_KT && pad == 3 &&
          To >= 1;
 }
 
@@ -213,10 +227,15 @@ void lateral_bwd_launch(const uint16_t* g, int ldg, const uint16_t* y, const flo
                         int Tf, int HW, int CO, int Cf, int alpha, hipStream_t st) {
   LateralBwdParams p{g, y, sc, sh, coef, wd, dy, dx, ldg, ldx, N, To, Tf, HW, Cf, alpha};
   const int ntile = (HW + LAT_POS - 1) / LAT_POS;
-  const dim3 grid(N * ntile * (Cf / LAT_CG)), block(LAT_WAVES * 64);
-  const size_t lds = (size_t)LAT_KT * 2 * (CO / 32) * 1024 + 5 * CO * 4;
-  if (CO == 64) hipLaunchKernelGGL((lateral_bwd_kernel<64>), grid, block, lds, st, p);
-  else hipLaunchKernelGGL((lateral_bwd_kernel<128>), grid, block, lds, st, p);
+  const int cg = Cf < LAT_CG ? Cf : LAT_CG;
+  const dim3 grid(N * ntile * (Cf / cg)), block(LAT_WAVES * 64);
+  const size_t lds = (size_t)LAT_KT * 2 * (CO < 32 ? 1 : CO / 32) * 1024 + 5 * CO * 4;
+  switch (CO) {
+    case 16: hipLaunchKernelGGL((lateral_bwd_kernel<16, 8>), grid, block, lds, st, p); break;
+    case 64: hipLaunchKernelGGL((lateral_bwd_kernel<64, 32>), grid, block, lds, st, p); break;
+    case 128: hipLaunchKernelGGL((lateral_bwd_kernel<128, 32>), grid, block, lds, st, p); break;
+    default: hipLaunchKernelGGL((lateral_bwd_kernel<256, 32>), grid, block, lds, st, p); break;
+  }
 }
 
 PVA_NS_END  // namespace PVA_NS

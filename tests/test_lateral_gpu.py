@@ -21,7 +21,8 @@ def _rel(a, b):
     return ((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-30)).item()
 
 
-@pytest.mark.parametrize("N,To,H,W,CO,Cf", [(2, 3, 5, 7, 64, 32), (1, 8, 10, 20, 128, 64), (3, 2, 16, 16, 64, 32)])
+@pytest.mark.parametrize("N,To,H,W,CO,Cf", [(2, 3, 5, 7, 64, 32), (1, 8, 10, 20, 128, 64), (3, 2, 16, 16, 64, 32),
+                                            (2, 4, 9, 15, 16, 8), (1, 3, 14, 14, 256, 128)])
 def test_lateral_bwd_matches_reference(N, To, H, W, CO, Cf):
     C = _C()
     torch.manual_seed(0)
@@ -80,7 +81,7 @@ def test_lateral_fused_net_matches_unfused(monkeypatch):
         runs.append((float(loss), {n: p.grad.detach().clone() for n, p in m.named_parameters()},
                      sum(f.lateral_used for f in fuses)))
     (l1, g1, n1), (l0, g0, n0) = runs
-    assert n1 == 2 and n0 == 0, (n1, n0)   # the res2 / res3 laterals (stem: 8 fast channels, res4: 256 slow: unfused)
+    assert n1 == 4 and n0 == 0, (n1, n0)   # the stem, res2, res3 and res4 laterals
     assert abs(l1 - l0) < 1e-6 * max(1.0, abs(l0)), (l1, l0)
     worst = max((_rel(g1[n], g0[n]), n) for n in g0 if g0[n].norm() > 0)
     assert worst[0] < 2e-2, worst
