@@ -530,234 +530,6 @@ __global__ void stem_pack_kernel(const float* __restrict__ w, uint16_t* __restri
   }
 }
 
-// ------------------------------------------------------------------------------------------------
-// Cout == 8 temporal stem, forward, four output frames per pass (PVA_STEM_PAIR=2).
-// The pair kernel is LDS-bound: every MFMA reads its own 1-KB B fragment (16 positions x 32 k of one input frame)
-// and at one MFMA per 16 cycles per SIMD four SIMDs want 256 B/clk from a 128 B/clk LDS — it measured 48.7 % MFMA
-// busy (profiles/r5_pmc).  Here row block 0 of the MFMA tile carries output frames t, t+1 and row block 1 frames t+2,
-// t+3, and block 1's A fragment at window frame j is block 0's at j-2 (the pair fragments [W[:, i]; W[:, i-1]]
-// shifted by two frames): each B fragment read from LDS feeds two MFMAs, the weights stay the pair kernel's 6 x 8
-// fragments, and the MFMA count per output frame is unchanged (KT+3 window frames per 4 output frames).
-// 8 waves own the 8 x 16 output tile (one row each, the pair kernel's tile and stem_tiles' grid); the 12-frame LDS
-// ring (8 window + 4 in flight) takes 86 KB: one workgroup of 8 waves per CU.
-// ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ void dma_patch8(__amdgpu_buffer_rsrc_t r, const StemParams& p, int ti, int hs0, int ws0,
-                                           char* slot) {
-  const int tid = threadIdx.x, w = tid >> 6;
-  if (w == 7) return;  // 418 chunks: waves 0-6 (wave-uniform)
-  const int pos = tid >> 1, half = tid & 1;
-  const int r_ = pos / PW, c_ = pos - r_ * PW;
-  const int hs = hs0 + r_ - 2, ws = ws0 + c_ - 2;
-  const bool ok = pos < PH * PW && ti >= 0 && ti < p.T && (unsigned)hs < (unsigned)p.Hs && (unsigned)ws < (unsigned)p.Ws;
-  const uint32_t vo = ok ? (uint32_t)((((ti * p.Hs + hs) * p.Ws + ws) * 16 + half * 8) * 2) : OOB;
-  dma16(r, slot + w * 64 * 16, vo);  // chunks 418..447 land in the slot padding
-}
-
-// the same patch with the wgrad kernels' position swizzle (LDS position k holds patch position pswz(k))
-__device__ __forceinline__ void dma_patch8sw(__amdgpu_buffer_rsrc_t r, const StemParams& p, int ti, int hs0, int ws0,
-                                             char* slot) {
-  const int tid = threadIdx.x, w = tid >> 6;
-  if (w == 7) return;
-  const int pos = pswz(tid >> 1), half = tid & 1;
-  const int r_ = pos / PW, c_ = pos - r_ * PW;
-  const int hs = hs0 + r_ - 2, ws = ws0 + c_ - 2;
-  const bool ok = pos < PH * PW && ti >= 0 && ti < p.T && (unsigned)hs < (unsigned)p.Hs && (unsigned)ws < (unsigned)p.Ws;
-  const uint32_t vo = ok ? (uint32_t)((((ti * p.Hs + hs) * p.Ws + ws) * 16 + half * 8) * 2) : OOB;
-  dma16(r, slot + w * 64 * 16, vo);
-}
-
-template <int KT>
-__global__ __launch_bounds__(512) void stem_fwd_quad_kernel(const StemParams p) {
-  constexpr int J = KT + 3;     // window frames per 4 output frames
-  constexpr int NP = KT + 1;    // pair fragments
-  constexpr int KS = 8;         // k-steps per input frame
-  constexpr int SLOTS = J + 4;
-  constexpr int TAPS = KT * 16;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* red = reinterpret_cast<float*>(smem + SLOTS * SLOT_BYTES);  // [8 waves][16]
-
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int g = lane >> 4, li = lane & 15;
-  int b = blockIdx.x;
-  const int tw = b % p.tiles_w; b /= p.tiles_w;
-  const int th = b % p.tiles_h;
-  const int n = b / p.tiles_h;
-  const int ho0 = th * TH, wo0 = tw * TW;
-  const __amdgpu_buffer_rsrc_t xr =
-      clip_rsrc(p.x + (int64_t)n * p.T * p.Hs * p.Ws * 16, (uint32_t)(p.T * p.Hs * p.Ws * 32));
-
-  for (int f = 0; f < J; ++f) dma_patch8(xr, p, f - p.pt, ho0, wo0, smem + f * SLOT_BYTES);
-
-  ev8_t wa[NP][KS];
-#pragma unroll
-  for (int j = 0; j < NP; ++j) {
-    const int dt = li < 8 ? j : j - 1;
-    const bool ok = dt >= 0 && dt < KT;
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
-      wa[j][ks] = ld_frag(p.w + (int64_t)(li & 7) * (TAPS * 16) + (ok ? dt : 0) * 256 + ks * 32 + 8 * g, ok);
-  }
-  __syncthreads();  // drains this wave's DMAs (vmcnt(0)) and publishes every wave's
-
-  float cs[4] = {0.f, 0.f, 0.f, 0.f}, cq[4] = {0.f, 0.f, 0.f, 0.f};
-  const int half = g & 1;
-  const int co0 = 4 * (g & 1);  // D rows 4g..4g+3 of block k: channels co0.. of output frame t0 + 2k + (g >> 1)
-  for (int t0 = 0; t0 < p.To; t0 += 4) {
-    if (t0 + 4 < p.To) {  // the next pass's four new frames, into the slots outside the current window
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        dma_patch8(xr, p, t0 - p.pt + J + k, ho0, wo0, smem + ((t0 + J + k) % SLOTS) * SLOT_BYTES);
-    }
-    f32x4_t acc[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-      const char* slot = smem + ((t0 + j) % SLOTS) * SLOT_BYTES;
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        const int tap = 2 * ks + (g >> 1);
-        const int bh = tap >> 2, bw = tap & 3;
-        const ev8_t xb = *reinterpret_cast<const ev8_t*>(slot + ((w + bh) * PW + (li + bw)) * POSB + half * 16);
-        if (j < NP) acc[0] = PVA_MFMA16(wa[j][ks], xb, acc[0], 0, 0, 0);
-        if (j >= 2) acc[1] = PVA_MFMA16(wa[j - 2][ks], xb, acc[1], 0, 0, 0);
-      }
-    }
-    __syncthreads();  // next frames landed; window frames 0-3 free.  Stores after the barrier
-    const int ho = ho0 + w, wo = wo0 + li;
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int to = t0 + 2 * k + (g >> 1);
-      if (ho < p.Ho && wo < p.Wo && to < p.To) {
-        const int64_t pos = (((int64_t)n * p.To + to) * p.Ho + ho) * p.Wo + wo;
-        float v[4] = {acc[k][0], acc[k][1], acc[k][2], acc[k][3]};
-        const uint2 pk = pack4(v);
-        *reinterpret_cast<uint2*>(p.y + pos * 8 + co0) = pk;
-        float f[4];
-        unpack4(pk, f);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) { cs[r] += f[r]; cq[r] += f[r] * f[r]; }
-      }
-    }
-  }
-  // BN partial sums: lanes g and g^2 hold the same channels; one slot per wave, summed in wave order
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    float s = sum16(cs[r]), q = sum16(cq[r]);
-    s += __shfl_xor(s, 32, 64);
-    q += __shfl_xor(q, 32, 64);
-    if (li == 0 && g < 2) {
-      red[w * 16 + 4 * g + r] = s;
-      red[w * 16 + 8 + 4 * g + r] = q;
-    }
-  }
-  __syncthreads();
-  if (tid < 16) {
-    float v = 0.f;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) v += red[k * 16 + tid];
-    p.stats[(int64_t)blockIdx.x * 16 + tid] = v;
-  }
-}
-
-// Cout == 8 temporal stem, weight gradient, four output frames per pass (PVA_STEM_PAIR=2): the pair wgrad's dY
-// fragments of frames (t, t+1) and (t+2, t+3) are two A fragments, and the B fragment of input window frame j
-// (the LDS-bound operand, 1 KB per MFMA in the pair kernel) feeds acc[j] with the first and acc[j-2] with the second
-// — the same accumulators (row block semantics shift by two frames with the A fragment), so the accumulator count
-// stays J_pair per tap.  8 waves: wave w owns spatial taps (bh = w & 3, bw = 2 (w >> 2) + 0..1) over the whole tile.  dY tile in LDS: [128 pos][4 frames][8 co], the two 32-B frame pairs of a position
-// swapped when position bit 3 is set (the two 16-lane groups of a transpose read then hit disjoint banks).
-template <int KT>
-__global__ __launch_bounds__(512) void stem_wgrad_quad_kernel(const StemParams p) {
-  constexpr int TAPS = KT * 16;
-  constexpr int NP = KT + 1;           // accumulator frames (pair-window indexing)
-  constexpr int J = KT + 3;            // window frames per 4 output frames
-  constexpr int SLOTS = J + 4;
-  constexpr int DYB = TH * TW * 32 * 2;  // [128 pos][32]: frames t0..t0+3 x 8 co
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* dyt = smem + SLOTS * SLOT_BYTES;  // two dY tile buffers (pass parity)
-
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int g = lane >> 4, li = lane & 15;
-  int b = blockIdx.x;
-  const int tw = b % p.tiles_w; b /= p.tiles_w;
-  const int th = b % p.tiles_h;
-  const int n = b / p.tiles_h;
-  const int ho0 = th * TH, wo0 = tw * TW;
-  const __amdgpu_buffer_rsrc_t xr =
-      clip_rsrc(p.x + (int64_t)n * p.T * p.Hs * p.Ws * 16, (uint32_t)(p.T * p.Hs * p.Ws * 32));
-  const __amdgpu_buffer_rsrc_t yr =
-      clip_rsrc(p.dy + (int64_t)n * p.To * p.Ho * p.Wo * 8, (uint32_t)(p.To * p.Ho * p.Wo * 16));
-  // dY chunk of this lane: LDS chunk tid = position P (tid >> 2), 16-B slot tid & 3 = (pair half ^ P bit 3, frame bit 0)
-  const int dP = tid >> 2, ds4 = tid & 3;
-  const int dfr = 2 * ((ds4 >> 1) ^ ((dP >> 3) & 1)) + (ds4 & 1);   // frame offset 0..3 stored in this chunk
-  const int dho = ho0 + dP / TW, dwo = wo0 + dP % TW;
-  const bool dok = dho < p.Ho && dwo < p.Wo;
-  auto dma_dy = [&](int t0, char* buf) {
-    const int to = t0 + dfr;
-    const uint32_t vo = dok && to < p.To ? (uint32_t)((((to * p.Ho + dho) * p.Wo + dwo) * 8) * 2) : OOB;
-    dma16(yr, buf + w * 64 * 16, vo);
-  };
-
-  f32x4_t acc[NP][2];
-#pragma unroll
-  for (int j = 0; j < NP; ++j)
-#pragma unroll
-    for (int s = 0; s < 2; ++s) acc[j][s] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-  for (int f = 0; f < J; ++f) dma_patch8sw(xr, p, f - p.pt, ho0, wo0, smem + f * SLOT_BYTES);
-  dma_dy(0, dyt);
-  __syncthreads();
-  const int bh = w & 3, s0 = 2 * (w >> 2);   // this wave's taps: row bh, columns s0, s0 + 1
-  const int rq = li >> 2, cb = (li & 3) * 8;
-  for (int t0 = 0; t0 < p.To; t0 += 4) {
-    const char* dcur = dyt + ((t0 >> 2) & 1) * DYB;
-    if (t0 + 4 < p.To) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        dma_patch8sw(xr, p, t0 - p.pt + J + k, ho0, wo0, smem + ((t0 + J + k) % SLOTS) * SLOT_BYTES);
-      dma_dy(t0 + 4, dyt + (((t0 >> 2) + 1) & 1) * DYB);
-    }
-#pragma unroll
-    for (int kstep = 0; kstep < TH * TW / 32; ++kstep) {
-      const int hh = 2 * kstep + (g >> 1);
-      const int wq = 8 * (g & 1) + rq;
-      ev8_t a[2];
-#pragma unroll
-      for (int blk = 0; blk < 2; ++blk) {
-        const int dp = hh * TW + wq;
-        const int o0 = dp * 64 + 32 * (blk ^ ((dp >> 3) & 1)) + cb;
-        const int o1 = (dp + 4) * 64 + 32 * (blk ^ (((dp + 4) >> 3) & 1)) + cb;
-        s16x4_t lo = trr(dcur + o0), hi = trr(dcur + o1);
-        s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        a[blk] = __builtin_bit_cast(ev8_t, v);
-      }
-#pragma unroll
-      for (int j = 0; j < J; ++j) {
-        const char* slot = smem + ((t0 + j) % SLOTS) * SLOT_BYTES;
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          const int ip = (hh + bh) * PW + (wq + s0 + s);
-          s16x4_t lo = trr(slot + pswz(ip) * POSB + cb), hi = trr(slot + pswz(ip + 4) * POSB + cb);
-          s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-          const ev8_t xb = __builtin_bit_cast(ev8_t, v);
-          if (j < NP) acc[j][s] = PVA_MFMA16(a[0], xb, acc[j][s], 0, 0, 0);
-          if (j >= 2) acc[j - 2][s] = PVA_MFMA16(a[1], xb, acc[j - 2][s], 0, 0, 0);
-        }
-      }
-    }
-    __syncthreads();  // next frames / dY tile landed; current window frames 0-3 and dY buffer are free
-  }
-  // dW[co][dt][tap] = rows 0-7 of acc[dt] (lanes g < 2) + rows 8-15 of acc[dt + 1] (lanes g >= 2)
-#pragma unroll
-  for (int dt = 0; dt < KT; ++dt)
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float v = g < 2 ? acc[dt][s][r] : acc[dt + 1][s][r];
-        v += __shfl_xor(v, 32, 64);
-        if (g < 2) atomicAdd(p.dw + (int64_t)(4 * g + r) * TAPS * 16 + (dt * 16 + 4 * bh + s0 + s) * 16 + li, v);
-      }
-}
-
 template <int KT, int COT>
 void launch_fwd(const StemParams& p, hipStream_t s) {
   const size_t lds = (KT + 1) * SLOT_BYTES + 4 * 2 * COT * 16 * 4;
@@ -777,18 +549,6 @@ void launch_fwd_pair(const StemParams& p, hipStream_t s) {
 }
 
 template <int KT>
-void launch_fwd_quad(const StemParams& p, hipStream_t s) {
-  const size_t lds = (KT + 7) * SLOT_BYTES + 8 * 16 * 4;
-  hipLaunchKernelGGL((stem_fwd_quad_kernel<KT>), dim3(p.N * p.tiles_h * p.tiles_w), dim3(512), lds, s, p);
-}
-
-template <int KT>
-void launch_wgrad_quad(const StemParams& p, hipStream_t s) {
-  const size_t lds = (KT + 7) * SLOT_BYTES + 2 * TH * TW * 32 * 2;
-  hipLaunchKernelGGL((stem_wgrad_quad_kernel<KT>), dim3(p.N * p.tiles_h * p.tiles_w), dim3(512), lds, s, p);
-}
-
-template <int KT>
 void launch_wgrad_pair(const StemParams& p, hipStream_t s) {
   const size_t lds = (KT + 3) * SLOT_BYTES + 2 * TH * TW * 16 * 2;
   hipLaunchKernelGGL((stem_wgrad_pair_kernel<KT>), dim3(p.N * p.tiles_h * p.tiles_w), dim3(256), lds, s, p);
@@ -798,11 +558,11 @@ void launch_wgrad_pair(const StemParams& p, hipStream_t s) {
 
 int stem_tiles(int Ho, int Wo, int N) { return N * ((Ho + TH - 1) / TH) * ((Wo + TW - 1) / TW); }
 
-// Cout == 8 temporal stems: PVA_STEM_PAIR=1 frame-pair kernels (default), 2 the four-frame kernels,
-// 0 the one-frame kernels (A/B, tests); read per launch — two launches per step — so tests can switch in-process
-static int stem_pair_mode() {
+// frame-pair kernels for Cout == 8 temporal stems; PVA_STEM_PAIR=0 selects the one-frame kernels (A/B, tests)
+// (read per launch — two launches per step — so tests can switch kernels within one process)
+static bool stem_pair_enabled() {
   const char* e = getenv("PVA_STEM_PAIR");
-  return e && e[0] == '0' ? 0 : e && e[0] == '2' ? 2 : 1;
+  return !(e && e[0] == '0');
 }
 
 // mode 0: forward, 1: wgrad.  Shapes outside stem_s2d_supported() are rejected by the bindings (TORCH_CHECK)
@@ -814,16 +574,13 @@ void stem_s2d_launch(int mode, const uint16_t* x, const uint16_t* w, uint16_t* y
   p.N = N; p.T = T; p.Hs = Hs; p.Ws = Ws; p.Cout = Cout;
   p.To = T; p.Ho = Hs; p.Wo = Ws; p.pt = kt / 2;
   p.tiles_h = (Hs + TH - 1) / TH; p.tiles_w = (Ws + TW - 1) / TW;
-  const int pm = stem_pair_mode();
-  const bool pair = pm != 0 && kt == 5 && Cout == 8;
+  const bool pair = stem_pair_enabled() && kt == 5 && Cout == 8;
   if (mode == 0) {
-    if (pair && pm == 2) launch_fwd_quad<5>(p, s);
-    else if (pair) launch_fwd_pair<5>(p, s);
+    if (pair) launch_fwd_pair<5>(p, s);
     else if (kt == 5 && Cout <= 16) launch_fwd<5, 1>(p, s);
     else if (kt == 1 && Cout <= 64) launch_fwd<1, 4>(p, s);
   } else {
-    if (pair && pm == 2) launch_wgrad_quad<5>(p, s);
-    else if (pair) launch_wgrad_pair<5>(p, s);
+    if (pair) launch_wgrad_pair<5>(p, s);
     else if (kt == 5 && Cout <= 16) launch_wgrad<5, 1>(p, s);
     else if (kt == 1 && Cout <= 64) launch_wgrad<1, 4>(p, s);
   }
