@@ -85,7 +85,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t clip_rsrc(const uint16_t* base
 // ------------------------------------------------------------------------------------------------
 // forward
 // ------------------------------------------------------------------------------------------------
-template <int KT, int COT>
+// PERM (Cout == 16 COT, COT even): the A fragment rows of block pair (2m, 2m+1) are permuted so that a lane ends with
+// 8 consecutive channels of its position (row r of block 2m+h = channel 32m + 8(r>>2) + 4h + (r&3)): one 16-B store
+// per block pair instead of two 8-B stores, a position's 128-B row written by 2 instructions of 64-B pieces (the
+// slow stem writes 2 GB per step)
+template <int KT, int COT, bool PERM = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void stem_fwd_kernel(const StemParams p) {
   constexpr int TAPS = KT * 16;
   constexpr int KSTEPS = TAPS * 16 / 32;  // 2 taps per MFMA k-step
@@ -105,11 +109,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void s
       clip_rsrc(p.x + (int64_t)n * p.T * p.Hs * p.Ws * 16, (uint32_t)(p.T * p.Hs * p.Ws * 32));
   // weight fragments (A operand: lane holds W[co = 16*c + li][k = 32*ks + 8*g .. +8])
   ev8_t wa[COT][KSTEPS];
+  auto chan = [&](int c, int r) { return PERM ? 32 * (c >> 1) + 8 * (r >> 2) + 4 * (c & 1) + (r & 3) : 16 * c + r; };
 #pragma unroll
   for (int c = 0; c < COT; ++c)
 #pragma unroll
     for (int ks = 0; ks < KSTEPS; ++ks)
-      wa[c][ks] = *reinterpret_cast<const ev8_t*>(p.w + (int64_t)(16 * c + li) * (TAPS * 16) + ks * 32 + 8 * g);
+      wa[c][ks] = *reinterpret_cast<const ev8_t*>(p.w + (int64_t)chan(c, li) * (TAPS * 16) + ks * 32 + 8 * g);
 
   // prologue: frames -pt .. -pt+KT-1 into slots 0..KT-1 (frame ti lives in slot (ti + pt) % SLOTS)
   for (int f = 0; f < KT; ++f) dma_patch(xr, p, f - p.pt, ho0, wo0, smem + f * SLOT_BYTES);
@@ -147,12 +152,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void s
       }
     }
     __syncthreads();  // next frame landed; window frame 0's slot is free.  Stores after the barrier.
-    // epilogue: D[co][pos]: lane holds co = 16c + 4g + r for position (row 2w+q, col li)
+    // epilogue: D[co][pos]: lane holds co = chan(c, 4g + r) for position (row 2w+q, col li)
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int ho = ho0 + 2 * w + q, wo = wo0 + li;
       const bool valid = ho < p.Ho && wo < p.Wo;
       const int64_t pos = (((int64_t)n * p.To + to) * p.Ho + ho) * p.Wo + wo;
+      if constexpr (PERM) {
+#pragma unroll
+        for (int m = 0; m < COT / 2; ++m) {
+          if (valid) {
+            float v[8] = {acc[q][2 * m][0], acc[q][2 * m][1], acc[q][2 * m][2], acc[q][2 * m][3],
+                          acc[q][2 * m + 1][0], acc[q][2 * m + 1][1], acc[q][2 * m + 1][2], acc[q][2 * m + 1][3]};
+            const uint4 pk = pack8(v);
+            *reinterpret_cast<uint4*>(p.y + pos * p.Cout + 32 * m + 8 * g) = pk;
+            float f[8];
+            unpack8(pk, f);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              cs[2 * m][r] += f[r]; cq[2 * m][r] += f[r] * f[r];
+              cs[2 * m + 1][r] += f[4 + r]; cq[2 * m + 1][r] += f[4 + r] * f[4 + r];
+            }
+          }
+        }
+        continue;
+      }
 #pragma unroll
       for (int c = 0; c < COT; ++c) {
         const int co = 16 * c + 4 * g;
@@ -176,8 +200,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void s
     for (int r = 0; r < 4; ++r) {
       const float s = sum16(cs[c][r]), q = sum16(cq[c][r]);
       if (li == 0) {
-        red[w * 2 * CT + 16 * c + 4 * g + r] = s;
-        red[w * 2 * CT + CT + 16 * c + 4 * g + r] = q;
+        red[w * 2 * CT + chan(c, 4 * g + r)] = s;
+        red[w * 2 * CT + CT + chan(c, 4 * g + r)] = q;
       }
     }
   __syncthreads();
@@ -530,10 +554,10 @@ __global__ void stem_pack_kernel(const float* __restrict__ w, uint16_t* __restri
   }
 }
 
-template <int KT, int COT>
+template <int KT, int COT, bool PERM = false>
 void launch_fwd(const StemParams& p, hipStream_t s) {
   const size_t lds = (KT + 1) * SLOT_BYTES + 4 * 2 * COT * 16 * 4;
-  hipLaunchKernelGGL((stem_fwd_kernel<KT, COT>), dim3(p.N * p.tiles_h * p.tiles_w), dim3(256), lds, s, p);
+  hipLaunchKernelGGL((stem_fwd_kernel<KT, COT, PERM>), dim3(p.N * p.tiles_h * p.tiles_w), dim3(256), lds, s, p);
 }
 
 template <int KT, int COT>
@@ -565,6 +589,12 @@ static bool stem_pair_enabled() {
   return !(e && e[0] == '0');
 }
 
+// PVA_STEM_PERM=0: the 8-B-store epilogue of the Cout-64 stem forward (A/B, tests)
+static bool stem_perm_enabled() {
+  const char* e = getenv("PVA_STEM_PERM");
+  return !(e && e[0] == '0');
+}
+
 // mode 0: forward, 1: wgrad.  Shapes outside stem_s2d_supported() are rejected by the bindings (TORCH_CHECK)
 // before this is reached, so every call launches exactly one kernel.
 void stem_s2d_launch(int mode, const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, const uint16_t* dy,
@@ -578,6 +608,7 @@ void stem_s2d_launch(int mode, const uint16_t* x, const uint16_t* w, uint16_t* y
   if (mode == 0) {
     if (pair) launch_fwd_pair<5>(p, s);
     else if (kt == 5 && Cout <= 16) launch_fwd<5, 1>(p, s);
+    else if (kt == 1 && Cout == 64 && stem_perm_enabled()) launch_fwd<1, 4, true>(p, s);
     else if (kt == 1 && Cout <= 64) launch_fwd<1, 4>(p, s);
   } else {
     if (pair) launch_wgrad_pair<5>(p, s);
