@@ -11,6 +11,7 @@
 //   False, PyTorch source-index rule), crop, horizontal flip, (x/255 - mean)/std, all in one pass
 //   (normalisation commutes with the bilinear resize since the weights sum to 1).
 #include "common.h"
+#include <cstdlib>
 
 PVA_NS_BEGIN
 
@@ -121,7 +122,7 @@ __global__ void pack_weights_kernel(const float* __restrict__ master, uint16_t* 
 // read the same pixels straight from global memory.
 // Measured (profiles/r4_pmc): the per-pixel form took 2.7 ms/step at B=160 — 12 byte loads and an 8-B store per pixel
 // with half-filled 32-B sectors in the s2d layout.
-constexpr int PRE_ROWS = 4, PRE_LDS = 16384;
+constexpr int PRE_ROWS = 4;
 
 __device__ __forceinline__ void pre_pixel(const uint8_t* f, int Ws, int x0, int x1, float lx, int y0r, int y1r, float ly,
                                           float m0, float m1, float m2, float is0, float is1, float is2, float* v) {
@@ -141,6 +142,8 @@ __device__ __forceinline__ void pre_pixel(const uint8_t* f, int Ws, int x0, int 
   v[3] = 0.f;
 }
 
+// PRE_LDS: row-staging bytes per workgroup; it bounds the workgroups per CU (16 KB: 10, 6 KB: 16 = the wave limit)
+template <int PRE_LDS>
 __global__ __launch_bounds__(128) void video_preprocess_kernel(const uint8_t* __restrict__ frames,
                                                                const int* __restrict__ desc, const int* __restrict__ tidx,
                                                                int T, int S, float m0, float m1, float m2, float is0,
@@ -255,8 +258,14 @@ void video_preprocess_launch(const uint8_t* frames, const int* desc, const int* 
   const int64_t units = (int64_t)B * T * ((S + 1) / 2);
   const int blocks = (int)(units < 65536 ? units : 65536);
   if (blocks <= 0) return;
-  hipLaunchKernelGGL(video_preprocess_kernel, dim3(blocks), dim3(128), 0, s, frames, desc, tidx, T, S, mean[0],
-                     mean[1], mean[2], 1.f / std_[0], 1.f / std_[1], 1.f / std_[2], out, B, s2d);
+  const char* e = getenv("PVA_PRE_LDS");
+  const int lds = e ? atoi(e) : 6144;
+  if (lds >= 16384)
+    hipLaunchKernelGGL(video_preprocess_kernel<16384>, dim3(blocks), dim3(128), 0, s, frames, desc, tidx, T, S, mean[0],
+                       mean[1], mean[2], 1.f / std_[0], 1.f / std_[1], 1.f / std_[2], out, B, s2d);
+  else
+    hipLaunchKernelGGL(video_preprocess_kernel<6144>, dim3(blocks), dim3(128), 0, s, frames, desc, tidx, T, S, mean[0],
+                       mean[1], mean[2], 1.f / std_[0], 1.f / std_[1], 1.f / std_[2], out, B, s2d);
 }
 
 void synth_frames_launch(uint8_t* out, int64_t n, uint32_t seed, hipStream_t s) {
