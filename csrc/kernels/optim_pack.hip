@@ -178,8 +178,22 @@ __global__ __launch_bounds__(128) void video_preprocess_kernel(const uint8_t* __
     const bool staged = yhi - ylo + 1 <= PRE_ROWS && span <= PRE_LDS && (((uintptr_t)src | (uintptr_t)span) & 3) == 0;
     __syncthreads();   // the previous unit's readers are done with `rows`
     if (staged) {
+      // every load of the span is issued before the first LDS store (a load-store loop waited out one memory
+      // latency per 512 B: the kernel ran at ~1 TB/s)
+      constexpr int PER = PRE_LDS / 4 / 128;
       const uint32_t* s4 = reinterpret_cast<const uint32_t*>(src);
-      for (int i = threadIdx.x; i < (span >> 2); i += blockDim.x) reinterpret_cast<uint32_t*>(rows)[i] = s4[i];
+      const int n4 = span >> 2;
+      uint32_t tmp[PER];
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const int i = threadIdx.x + k * 128;
+        tmp[k] = i < n4 ? s4[i] : 0u;
+      }
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const int i = threadIdx.x + k * 128;
+        if (i < n4) reinterpret_cast<uint32_t*>(rows)[i] = tmp[k];
+      }
     }
     __syncthreads();
     const uint8_t* base = staged ? rows : src;   // both indexed relative to row ylo
