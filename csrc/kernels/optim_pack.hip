@@ -196,7 +196,9 @@ __global__ __launch_bounds__(128) void video_preprocess_kernel(const uint8_t* __
       }
     }
     __syncthreads();
-    const uint8_t* base = staged ? rows : src;   // both indexed relative to row ylo
+    // both sources are indexed relative to row ylo; two inlined copies of the cell loop, so the staged one keeps
+    // the LDS address space (a merged pointer made every pixel read a FLAT load)
+    auto cells = [&](const uint8_t* base) {
     for (int c = threadIdx.x; c < RP; c += blockDim.x) {
       float v[2][2][4];
 #pragma unroll
@@ -229,6 +231,9 @@ __global__ __launch_bounds__(128) void video_preprocess_kernel(const uint8_t* __
         }
       }
     }
+    };
+    if (staged) cells(rows);
+    else cells(src);
   }
 }
 
