@@ -237,6 +237,102 @@ __global__ __launch_bounds__(128) void video_preprocess_kernel(const uint8_t* __
   }
 }
 
+// Chunked form (default; PVA_PRE_CHUNK=0 selects the row-pair form above): a workgroup owns PRE2_RP output row pairs
+// of one frame.  The row-pair form paid a dependent chain per 2 output rows — descriptor, frame index, then the rows
+// (three memory latencies, ~13 us per unit measured: 1.1 TB/s, scripts/preprocess_bench.py); here the descriptor
+// and frame index are read once, the whole source-row span of the chunk is copied to LDS by LDS-DMA in one phase
+// (4-B lanes, no VGPR staging), and 256 threads then produce the chunk's cells.  Same per-pixel arithmetic.
+constexpr int PRE2_RP = 8, PRE2_LDS = 24 * 1024;
+
+__device__ __forceinline__ void dma4(__amdgpu_buffer_rsrc_t r, uint8_t* lds, int voff) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 4, voff, 0, 0, 0);
+#endif
+}
+
+__global__ __launch_bounds__(256) void video_preprocess2_kernel(const uint8_t* __restrict__ frames,
+                                                                const int* __restrict__ desc,
+                                                                const int* __restrict__ tidx, int T, int S, float m0,
+                                                                float m1, float m2, float is0, float is1, float is2,
+                                                                uint16_t* __restrict__ out, int s2d) {
+  __shared__ __attribute__((aligned(16))) uint8_t rows[PRE2_LDS];
+  const int RP = (S + 1) >> 1;
+  const int nch = (RP + PRE2_RP - 1) / PRE2_RP;
+  const int u = blockIdx.x;
+  const int b = u / (T * nch);
+  const int rem = u - b * T * nch;
+  const int t = rem / nch, ch = rem - t * nch;
+  const int* d = desc + b * 10;
+  const int64_t off = (int64_t)(uint32_t)d[0] | ((int64_t)d[1] << 31);
+  const int Hs = d[3], Ws = d[4], rh = d[5], rw = d[6], top = d[7], left = d[8], flip = d[9];
+  const uint8_t* f = frames + off + (int64_t)tidx[b * T + t] * Hs * Ws * 3;
+  const int r0 = ch * PRE2_RP, r1 = min(RP, r0 + PRE2_RP);
+  auto src_rows = [&](int y, int& y0, int& y1, float& ly) {   // the row-pair form's expressions
+    const float sy = fmaxf(((float)(y + top) + 0.5f) * ((float)Hs / (float)rh) - 0.5f, 0.f);
+    y0 = min((int)sy, Hs - 1);
+    y1 = min(y0 + 1, Hs - 1);
+    ly = sy - (float)y0;
+  };
+  int ylo, yhi, dummy;
+  float fd;
+  src_rows(2 * r0, ylo, dummy, fd);
+  src_rows(min(2 * r1 - 1, S - 1), dummy, yhi, fd);
+  const int rowb = Ws * 3;
+  const int span = (yhi - ylo + 1) * rowb;
+  const uint8_t* src = f + (int64_t)ylo * rowb;
+  const bool staged = span <= PRE2_LDS && (((uintptr_t)src | (uintptr_t)span) & 3) == 0;
+  if (staged) {
+    const __amdgpu_buffer_rsrc_t sr = __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, span, 0x00020000);
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int nchunk = (span + 255) >> 8;   // 256-B wave chunks (lanes past the span read zeros)
+    for (int k = w; k < nchunk; k += 4) dma4(sr, rows + k * 256, k * 256 + lane * 4);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  auto cells = [&](const uint8_t* base) {
+    const int ncell = (r1 - r0) * RP;
+    for (int q = threadIdx.x; q < ncell; q += 256) {
+      const int r = r0 + q / RP, c = q - (q / RP) * RP;
+      int y0s[2], y1s[2];
+      float lys[2];
+#pragma unroll
+      for (int k = 0; k < 2; ++k) src_rows(min(2 * r + k, S - 1), y0s[k], y1s[k], lys[k]);
+      float v[2][2][4];
+#pragma unroll
+      for (int dx = 0; dx < 2; ++dx) {
+        const int x = min(2 * c + dx, S - 1);
+        const int xr = (flip ? (S - 1 - x) : x) + left;
+        const float sx = fmaxf(((float)xr + 0.5f) * ((float)Ws / (float)rw) - 0.5f, 0.f);
+        const int x0 = min((int)sx, Ws - 1);
+        const int x1 = min(x0 + 1, Ws - 1);
+        const float lx = sx - (float)x0;
+#pragma unroll
+        for (int dy = 0; dy < 2; ++dy)
+          pre_pixel(base, Ws, x0, x1, lx, y0s[dy] - ylo, y1s[dy] - ylo, lys[dy], m0, m1, m2, is0, is1, is2, v[dy][dx]);
+      }
+      const uint2 q00 = pack4(v[0][0]), q01 = pack4(v[0][1]), q10 = pack4(v[1][0]), q11 = pack4(v[1][1]);
+      const int64_t fr = (int64_t)b * T + t;
+      if (s2d) {
+        uint16_t* o = out + ((fr * RP + r) * RP + c) * 16;
+        *reinterpret_cast<uint4*>(o) = make_uint4(q00.x, q00.y, q01.x, q01.y);
+        *reinterpret_cast<uint4*>(o + 8) = make_uint4(q10.x, q10.y, q11.x, q11.y);
+      } else {
+        const int y = 2 * r, x = 2 * c;
+        uint16_t* o0 = out + ((fr * S + y) * S + x) * 4;
+        if (x + 1 < S) *reinterpret_cast<uint4*>(o0) = make_uint4(q00.x, q00.y, q01.x, q01.y);
+        else *reinterpret_cast<uint2*>(o0) = q00;
+        if (y + 1 < S) {
+          uint16_t* o1 = o0 + (int64_t)S * 4;
+          if (x + 1 < S) *reinterpret_cast<uint4*>(o1) = make_uint4(q10.x, q10.y, q11.x, q11.y);
+          else *reinterpret_cast<uint2*>(o1) = q10;
+        }
+      }
+    }
+  };
+  if (staged) cells(rows);
+  else cells(src);
+}
+
 // synthetic decoded frames on device: deterministic hash -> uint8 (no zeros: DVFS, BASELINE.md protocol)
 __global__ void synth_frames_kernel(uint8_t* __restrict__ out, int64_t n, uint32_t seed) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
@@ -277,6 +373,14 @@ void video_preprocess_launch(const uint8_t* frames, const int* desc, const int* 
   const int64_t units = (int64_t)B * T * ((S + 1) / 2);
   const int blocks = (int)(units < 65536 ? units : 65536);
   if (blocks <= 0) return;
+  const char* ec = getenv("PVA_PRE_CHUNK");
+  if (!(ec && ec[0] == '0')) {
+    const int RP = (S + 1) / 2;
+    const int64_t wgs = (int64_t)B * T * ((RP + PRE2_RP - 1) / PRE2_RP);
+    hipLaunchKernelGGL(video_preprocess2_kernel, dim3((unsigned)wgs), dim3(256), 0, s, frames, desc, tidx, T, S,
+                       mean[0], mean[1], mean[2], 1.f / std_[0], 1.f / std_[1], 1.f / std_[2], out, s2d);
+    return;
+  }
   const char* e = getenv("PVA_PRE_LDS");
   const int lds = e ? atoi(e) : 6144;
   if (lds >= 16384)
