@@ -99,7 +99,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void s
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
-  int b = blockIdx.x;
+  // XCD-aware tile order: consecutive tiles (horizontal neighbours, then rows) on one XCD, so the halo rows/columns a
+  // tile shares with its neighbours come from that XCD's L2 (blockIdx order spread them over all 8: 1.75x the input
+  // bytes from HBM, profiles/r5_pmc)
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  int b = L;
   const int tw = b % p.tiles_w; b /= p.tiles_w;
   const int th = b % p.tiles_h;
   const int n = b / p.tiles_h;
@@ -209,8 +213,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void s
     float s = 0.f, q = 0.f;
 #pragma unroll
     for (int k = 0; k < 4; ++k) { s += red[k * 2 * CT + i]; q += red[k * 2 * CT + CT + i]; }
-    p.stats[(int64_t)blockIdx.x * 2 * p.Cout + i] = s;
-    p.stats[(int64_t)blockIdx.x * 2 * p.Cout + p.Cout + i] = q;
+    p.stats[(int64_t)L * 2 * p.Cout + i] = s;
+    p.stats[(int64_t)L * 2 * p.Cout + p.Cout + i] = q;
   }
 }
 
@@ -234,7 +238,11 @@ __global__ __launch_bounds__(256) void stem_wgrad_kernel(const StemParams p) {
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
-  int b = blockIdx.x;
+  // XCD-aware tile order: consecutive tiles (horizontal neighbours, then rows) on one XCD, so the halo rows/columns a
+  // tile shares with its neighbours come from that XCD's L2 (blockIdx order spread them over all 8: 1.75x the input
+  // bytes from HBM, profiles/r5_pmc)
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  int b = L;
   const int tw = b % p.tiles_w; b /= p.tiles_w;
   const int th = b % p.tiles_h;
   const int n = b / p.tiles_h;
@@ -341,7 +349,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void s
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
-  int b = blockIdx.x;
+  // XCD-aware tile order: consecutive tiles (horizontal neighbours, then rows) on one XCD, so the halo rows/columns a
+  // tile shares with its neighbours come from that XCD's L2 (blockIdx order spread them over all 8: 1.75x the input
+  // bytes from HBM, profiles/r5_pmc)
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  int b = L;
   const int tw = b % p.tiles_w; b /= p.tiles_w;
   const int th = b % p.tiles_h;
   const int n = b / p.tiles_h;
@@ -422,8 +434,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void s
     float s = 0.f, q = 0.f;
 #pragma unroll
     for (int k = 0; k < 4; ++k) { s += red[k * 16 + tid]; q += red[k * 16 + 8 + tid]; }
-    p.stats[(int64_t)blockIdx.x * 16 + tid] = s;
-    p.stats[(int64_t)blockIdx.x * 16 + 8 + tid] = q;
+    p.stats[(int64_t)L * 16 + tid] = s;
+    p.stats[(int64_t)L * 16 + 8 + tid] = q;
   }
 }
 
@@ -438,7 +450,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void s
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
-  int b = blockIdx.x;
+  // XCD-aware tile order: consecutive tiles (horizontal neighbours, then rows) on one XCD, so the halo rows/columns a
+  // tile shares with its neighbours come from that XCD's L2 (blockIdx order spread them over all 8: 1.75x the input
+  // bytes from HBM, profiles/r5_pmc)
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  int b = L;
   const int tw = b % p.tiles_w; b /= p.tiles_w;
   const int th = b % p.tiles_h;
   const int n = b / p.tiles_h;
