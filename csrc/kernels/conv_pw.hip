@@ -84,6 +84,7 @@ void conv_pw_launch(const ConvParams& p, int cfg, hipStream_t st) {
   // operand streams of the epilogue (the kernel is instantiated per combination)
   const bool stats2 = ep == 2 && p.epart != nullptr;
   int ops = p.accum && ep != 1 ? OP_OLD : 0;
+  if (ep == 1 && p.rsc) ops |= 64;   // OP_RAFF: BN_1 affine on the residual
   if (ep == 2) {
     if (p.eres) ops |= OP_RES;
     if (p.emask) ops |= OP_MASK;

@@ -98,6 +98,20 @@ struct Pre {
 // OP_Y1 BN inputs, OP_MASK ReLU bits, OP_MSC ReLU from affine(y0)); an instantiation carries registers (and
 // buffer descriptors / branches) only for its own streams, so the ring can be deeper
 constexpr int OP_OLD = 1, OP_RES = 2, OP_Y0 = 4, OP_Y1 = 8, OP_MASK = 16, OP_MSC = 32;
+constexpr int OP_RAFF = 64;   // EP 1: the residual goes through BN_1's affine (unit 0's branch1); else identity
+
+// ReLU bits of 8 packed non-negative 16-bit values (bit e: element e > 0, i.e. a non-zero magnitude — the sign bit of
+// a ReLU output is set only for -0): (w & 0x7fff7fff) + 0x7fff7fff carries each non-zero half into its top bit
+// (bit 15 / 31) without crossing halves, then one bitfield extract per element (the compare/select chains the
+// compiler made of the per-half test cost ~4.5 VALU per element in the residual-output epilogue)
+__device__ __forceinline__ unsigned relu_bits8(const uint4& pk) {
+  const uint32_t t0 = (pk.x & 0x7fff7fffu) + 0x7fff7fffu, t1 = (pk.y & 0x7fff7fffu) + 0x7fff7fffu;
+  const uint32_t t2 = (pk.z & 0x7fff7fffu) + 0x7fff7fffu, t3 = (pk.w & 0x7fff7fffu) + 0x7fff7fffu;
+  return __builtin_amdgcn_ubfe(t0, 15, 1) | (__builtin_amdgcn_ubfe(t0, 31, 1) << 1) |
+         (__builtin_amdgcn_ubfe(t1, 15, 1) << 2) | (__builtin_amdgcn_ubfe(t1, 31, 1) << 3) |
+         (__builtin_amdgcn_ubfe(t2, 15, 1) << 4) | (__builtin_amdgcn_ubfe(t2, 31, 1) << 5) |
+         (__builtin_amdgcn_ubfe(t3, 15, 1) << 6) | (__builtin_amdgcn_ubfe(t3, 31, 1) << 7);
+}
 
 // NW: waves per workgroup — 8, or 4 (cfg bit 3: an instantiation between 128 and 168 VGPRs then runs three
 // workgroups = 12 waves per CU instead of one 8-wave workgroup, the register file no longer rounding to 2 per SIMD)
@@ -361,8 +375,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
         for (int e = 0; e < 8; ++e) {
           cb[e] = cst[nl + e];
           c2[e] = EP == 1 ? cst[NG + nl + e] : 0.f;
-          c3[e] = EP == 1 ? cst[2 * NG + nl + e] : (masky ? cst[NG + nl + e] : 0.f);
-          c4[e] = EP == 1 ? cst[3 * NG + nl + e] : (masky ? cst[2 * NG + nl + e] : 0.f);
+          c3[e] = EP == 1 ? ((OPS & OP_RAFF) ? cst[2 * NG + nl + e] : 1.f) : (masky ? cst[NG + nl + e] : 0.f);
+          c4[e] = EP == 1 ? ((OPS & OP_RAFF) ? cst[3 * NG + nl + e] : 0.f) : (masky ? cst[2 * NG + nl + e] : 0.f);
         }
         float s_a[8], s_b[8], s_c[8];
 #pragma unroll
@@ -376,21 +390,17 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
           if (EP == 1) {
             float rr[8];
             unpack8(E.res[i], rr);
+            if constexpr ((OPS & OP_RAFF) != 0) {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) rr[e] = __builtin_fmaf(rr[e], c3[e], c4[e]);   // identity: 1, 0
+              for (int e = 0; e < 8; ++e) rr[e] = __builtin_fmaf(rr[e], c3[e], c4[e]);
+            }
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] = fmaxf(__builtin_fmaf(v[e], cb[e], c2[e]) + rr[e], 0.f);
             const uint4 pk = pack8_fast(v);
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, pk), yr, r * yb + 16 * g + nc * 2, 0,
                                                    ST_AUX);
-            const uint32_t w4[4] = {pk.x, pk.y, pk.z, pk.w};
-            unsigned bits = 0;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {   // bit = stored bf16 > 0 (res_out's convention)
-              bits |= ((w4[e] & 0x7fffu) != 0 && !(w4[e] & 0x8000u)) ? 1u << (2 * e) : 0u;
-              bits |= ((w4[e] & 0x7fff0000u) != 0 && !(w4[e] & 0x80000000u)) ? 1u << (2 * e + 1) : 0u;
-            }
-            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)bits, mor, r * mrow + g + (nc >> 3), 0, 0);
+            // bit = stored 16-bit value > 0 (res_out's convention)
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)relu_bits8(pk), mor, r * mrow + g + (nc >> 3), 0, 0);
           } else if (EP == 0) {
             float o[8];
             unpack8(E.old[i], o);
@@ -563,7 +573,11 @@ bool launch_ks_tp(const ConvParams& p, int ep, int ops, int rpb, int gch, size_t
   constexpr int TMF = KS <= 4 ? 4 : 2;
   if (ep == 1) {
     if constexpr (TP) return false;
-    else { launch_aff<KS, TMF, 1, OP_RES, 3, false, NW>(p, rpb, gch, lds, st); return true; }
+    else {
+      if (ops & OP_RAFF) launch_aff<KS, TMF, 1, OP_RES | OP_RAFF, 3, false, NW>(p, rpb, gch, lds, st);
+      else launch_aff<KS, TMF, 1, OP_RES, 3, false, NW>(p, rpb, gch, lds, st);
+      return true;
+    }
   }
   if (ep == 0) {
     if (ops & OP_OLD) launch_aff<KS, TMF, 0, OP_OLD, 3, TP, NW>(p, rpb, gch, lds, st);
