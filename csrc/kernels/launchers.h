@@ -68,7 +68,8 @@ void pack_weights_launch(const float* master, uint16_t* fwd, uint16_t* dgr, cons
                          hipStream_t s);
 int pack_desc_size();
 void video_preprocess_launch(const uint8_t* frames, const int* desc, const int* tidx, int B, int T, int S,
-                             const float* mean, const float* std_, uint16_t* out, int s2d, hipStream_t s);
+                             const float* mean, const float* std_, uint16_t* out, int s2d, hipStream_t s,
+                             const int* slow_of = nullptr, uint16_t* slow_out = nullptr, int Ts = 0);
 int stem_tiles(int Ho, int Wo, int N);
 void stem_s2d_launch(int mode, const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, const uint16_t* dy,
                      float* dw, int N, int T, int Hs, int Ws, int Cout, int kt, hipStream_t s);

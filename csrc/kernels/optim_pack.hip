@@ -11,7 +11,6 @@
 //   False, PyTorch source-index rule), crop, horizontal flip, (x/255 - mean)/std, all in one pass
 //   (normalisation commutes with the bilinear resize since the weights sum to 1).
 #include "common.h"
-#include <cstdlib>
 
 PVA_NS_BEGIN
 
@@ -112,17 +111,12 @@ __global__ void pack_weights_kernel(const float* __restrict__ master, uint16_t* 
 
 // frames: packed uint8 clips, clip b = [Ts][Hs][Ws][3] at byte offset desc[b].off ;
 // desc: [B][10] int32 = (off_lo, off_hi, Ts, Hs, Ws, rh, rw, top, left, flip) ; tidx: [B][T] frame index
-// inside the clip ; out: [B][T][S][S][4] bf16 (channel 3 = 0).  One thread per output pixel; per-clip
-// geometry lets one launch serve a batch of differently sized source videos.
-// One workgroup per (clip, frame, output row pair): the (at most 4) source rows the two output rows interpolate from
-// are one contiguous span of the frame, staged into LDS with dword loads; each thread then produces a 2x2 output
-// cell (s2d: one 32-B, 16-channel position — two 16-B stores, consecutive threads consecutive cells; NDHWC RGB0: 16 B
-// per output row).  The per-pixel arithmetic is the per-pixel kernel's, expression for expression, so the values are
-// bitwise those of the per-pixel form it replaced; spans that do not fit the staging window (or are not 4-B aligned)
-// read the same pixels straight from global memory.
+// inside the clip ; out: [B][T][S][S][4] bf16 (channel 3 = 0), or s2d [B][T][S/2][S/2][16].  Per-clip geometry lets
+// one launch serve a batch of differently sized source videos.  Each thread produces a 2x2 output cell (s2d: one 32-B,
+// 16-channel position — two 16-B stores, consecutive threads consecutive cells; NDHWC RGB0: 16 B per output row); the
+// per-pixel arithmetic is the original per-pixel kernel's, expression for expression (bitwise the same values).
 // Measured (profiles/r4_pmc): the per-pixel form took 2.7 ms/step at B=160 — 12 byte loads and an 8-B store per pixel
 // with half-filled 32-B sectors in the s2d layout.
-constexpr int PRE_ROWS = 4;
 
 __device__ __forceinline__ void pre_pixel(const uint8_t* f, int Ws, int x0, int x1, float lx, int y0r, int y1r, float ly,
                                           float m0, float m1, float m2, float is0, float is1, float is2, float* v) {
@@ -142,103 +136,8 @@ __device__ __forceinline__ void pre_pixel(const uint8_t* f, int Ws, int x0, int 
   v[3] = 0.f;
 }
 
-// PRE_LDS: row-staging bytes per workgroup; it bounds the workgroups per CU (16 KB: 10, 6 KB: 16 = the wave limit)
-template <int PRE_LDS>
-__global__ __launch_bounds__(128) void video_preprocess_kernel(const uint8_t* __restrict__ frames,
-                                                               const int* __restrict__ desc, const int* __restrict__ tidx,
-                                                               int T, int S, float m0, float m1, float m2, float is0,
-                                                               float is1, float is2, uint16_t* __restrict__ out, int B,
-                                                               int s2d) {
-  __shared__ __attribute__((aligned(16))) uint8_t rows[PRE_LDS];
-  const int RP = (S + 1) >> 1;   // output row pairs (= cells per row)
-  const int64_t units = (int64_t)B * T * RP;
-  for (int64_t u = blockIdx.x; u < units; u += gridDim.x) {
-    const int b = (int)(u / ((int64_t)T * RP));
-    const int rem = (int)(u - (int64_t)b * T * RP);
-    const int t = rem / RP, r = rem - t * RP;
-    const int* d = desc + b * 10;
-    const int64_t off = (int64_t)(uint32_t)d[0] | ((int64_t)d[1] << 31);
-    const int Hs = d[3], Ws = d[4], rh = d[5], rw = d[6], top = d[7], left = d[8], flip = d[9];
-    const uint8_t* f = frames + off + (int64_t)tidx[b * T + t] * Hs * Ws * 3;
-    // the two output rows' source rows (identical expressions to the per-pixel form)
-    int y0s[2], y1s[2];
-    float lys[2];
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int y = min(2 * r + k, S - 1);
-      const float sy = fmaxf(((float)(y + top) + 0.5f) * ((float)Hs / (float)rh) - 0.5f, 0.f);
-      y0s[k] = min((int)sy, Hs - 1);
-      y1s[k] = min(y0s[k] + 1, Hs - 1);
-      lys[k] = sy - (float)y0s[k];
-    }
-    const int ylo = min(y0s[0], y0s[1]), yhi = max(y1s[0], y1s[1]);
-    const int rowb = Ws * 3;
-    const int span = (yhi - ylo + 1) * rowb;
-    const uint8_t* src = f + (int64_t)ylo * rowb;
-    const bool staged = yhi - ylo + 1 <= PRE_ROWS && span <= PRE_LDS && (((uintptr_t)src | (uintptr_t)span) & 3) == 0;
-    __syncthreads();   // the previous unit's readers are done with `rows`
-    if (staged) {
-      // every load of the span is issued before the first LDS store (a load-store loop waited out one memory
-      // latency per 512 B: the kernel ran at ~1 TB/s)
-      constexpr int PER = PRE_LDS / 4 / 128;
-      const uint32_t* s4 = reinterpret_cast<const uint32_t*>(src);
-      const int n4 = span >> 2;
-      uint32_t tmp[PER];
-#pragma unroll
-      for (int k = 0; k < PER; ++k) {
-        const int i = threadIdx.x + k * 128;
-        tmp[k] = i < n4 ? s4[i] : 0u;
-      }
-#pragma unroll
-      for (int k = 0; k < PER; ++k) {
-        const int i = threadIdx.x + k * 128;
-        if (i < n4) reinterpret_cast<uint32_t*>(rows)[i] = tmp[k];
-      }
-    }
-    __syncthreads();
-    // both sources are indexed relative to row ylo; two inlined copies of the cell loop, so the staged one keeps
-    // the LDS address space (a merged pointer made every pixel read a FLAT load)
-    auto cells = [&](const uint8_t* base) {
-    for (int c = threadIdx.x; c < RP; c += blockDim.x) {
-      float v[2][2][4];
-#pragma unroll
-      for (int dx = 0; dx < 2; ++dx) {
-        const int x = min(2 * c + dx, S - 1);
-        const int xr = (flip ? (S - 1 - x) : x) + left;
-        const float sx = fmaxf(((float)xr + 0.5f) * ((float)Ws / (float)rw) - 0.5f, 0.f);
-        const int x0 = min((int)sx, Ws - 1);
-        const int x1 = min(x0 + 1, Ws - 1);
-        const float lx = sx - (float)x0;
-#pragma unroll
-        for (int dy = 0; dy < 2; ++dy)
-          pre_pixel(base, Ws, x0, x1, lx, y0s[dy] - ylo, y1s[dy] - ylo, lys[dy], m0, m1, m2, is0, is1, is2, v[dy][dx]);
-      }
-      const uint2 q00 = pack4(v[0][0]), q01 = pack4(v[0][1]), q10 = pack4(v[1][0]), q11 = pack4(v[1][1]);
-      const int64_t fr = (int64_t)b * T + t;
-      if (s2d) {   // S even: position (r, c) of the S/2 x S/2 grid, channels (dy*2 + dx)*4 + rgb0
-        uint16_t* o = out + ((fr * RP + r) * RP + c) * 16;
-        *reinterpret_cast<uint4*>(o) = make_uint4(q00.x, q00.y, q01.x, q01.y);
-        *reinterpret_cast<uint4*>(o + 8) = make_uint4(q10.x, q10.y, q11.x, q11.y);
-      } else {     // NDHWC RGB0 rows 2r, 2r+1; odd S: the last column / row are not stored twice
-        const int y = 2 * r, x = 2 * c;
-        uint16_t* o0 = out + ((fr * S + y) * S + x) * 4;
-        if (x + 1 < S) *reinterpret_cast<uint4*>(o0) = make_uint4(q00.x, q00.y, q01.x, q01.y);
-        else *reinterpret_cast<uint2*>(o0) = q00;
-        if (y + 1 < S) {
-          uint16_t* o1 = o0 + (int64_t)S * 4;
-          if (x + 1 < S) *reinterpret_cast<uint4*>(o1) = make_uint4(q10.x, q10.y, q11.x, q11.y);
-          else *reinterpret_cast<uint2*>(o1) = q10;
-        }
-      }
-    }
-    };
-    if (staged) cells(rows);
-    else cells(src);
-  }
-}
-
-// Chunked form (default; PVA_PRE_CHUNK=0 selects the row-pair form above): a workgroup owns PRE2_RP output row pairs
-// of one frame.  The row-pair form paid a dependent chain per 2 output rows — descriptor, frame index, then the rows
+// A workgroup owns PRE2_RP output row pairs of one frame.  The previous row-pair form (one workgroup per 2 output
+// rows, profiles/r5_preprocess) paid a dependent chain per 2 output rows — descriptor, frame index, then the rows
 // (three memory latencies, ~13 us per unit measured: 1.1 TB/s, scripts/preprocess_bench.py); here the descriptor
 // and frame index are read once, the whole source-row span of the chunk is copied to LDS by LDS-DMA in one phase
 // (4-B lanes, no VGPR staging), and 256 threads then produce the chunk's cells.  Same per-pixel arithmetic.
@@ -254,7 +153,9 @@ __global__ __launch_bounds__(256) void video_preprocess2_kernel(const uint8_t* _
                                                                 const int* __restrict__ desc,
                                                                 const int* __restrict__ tidx, int T, int S, float m0,
                                                                 float m1, float m2, float is0, float is1, float is2,
-                                                                uint16_t* __restrict__ out, int s2d) {
+                                                                uint16_t* __restrict__ out, int s2d,
+                                                                const int* __restrict__ slow_of,
+                                                                uint16_t* __restrict__ slow_out, int Ts) {
   __shared__ __attribute__((aligned(16))) uint8_t rows[PRE2_LDS];
   const int RP = (S + 1) >> 1;
   const int nch = (RP + PRE2_RP - 1) / PRE2_RP;
@@ -267,6 +168,9 @@ __global__ __launch_bounds__(256) void video_preprocess2_kernel(const uint8_t* _
   const int Hs = d[3], Ws = d[4], rh = d[5], rw = d[6], top = d[7], left = d[8], flip = d[9];
   const uint8_t* f = frames + off + (int64_t)tidx[b * T + t] * Hs * Ws * 3;
   const int r0 = ch * PRE2_RP, r1 = min(RP, r0 + PRE2_RP);
+  // slow pathway: its frames are a subset of this clip's (pack_pathway_indices); frame t's cells also go to slow frame
+  // slow_of[t] (-1: not a slow frame) — one pass over the source instead of a second launch
+  const int ts = slow_out ? slow_of[t] : -1;
   auto src_rows = [&](int y, int& y0, int& y1, float& ly) {   // the row-pair form's expressions
     const float sy = fmaxf(((float)(y + top) + 0.5f) * ((float)Hs / (float)rh) - 0.5f, 0.f);
     y0 = min((int)sy, Hs - 1);
@@ -311,22 +215,25 @@ __global__ __launch_bounds__(256) void video_preprocess2_kernel(const uint8_t* _
           pre_pixel(base, Ws, x0, x1, lx, y0s[dy] - ylo, y1s[dy] - ylo, lys[dy], m0, m1, m2, is0, is1, is2, v[dy][dx]);
       }
       const uint2 q00 = pack4(v[0][0]), q01 = pack4(v[0][1]), q10 = pack4(v[1][0]), q11 = pack4(v[1][1]);
-      const int64_t fr = (int64_t)b * T + t;
-      if (s2d) {
-        uint16_t* o = out + ((fr * RP + r) * RP + c) * 16;
-        *reinterpret_cast<uint4*>(o) = make_uint4(q00.x, q00.y, q01.x, q01.y);
-        *reinterpret_cast<uint4*>(o + 8) = make_uint4(q10.x, q10.y, q11.x, q11.y);
-      } else {
-        const int y = 2 * r, x = 2 * c;
-        uint16_t* o0 = out + ((fr * S + y) * S + x) * 4;
-        if (x + 1 < S) *reinterpret_cast<uint4*>(o0) = make_uint4(q00.x, q00.y, q01.x, q01.y);
-        else *reinterpret_cast<uint2*>(o0) = q00;
-        if (y + 1 < S) {
-          uint16_t* o1 = o0 + (int64_t)S * 4;
-          if (x + 1 < S) *reinterpret_cast<uint4*>(o1) = make_uint4(q10.x, q10.y, q11.x, q11.y);
-          else *reinterpret_cast<uint2*>(o1) = q10;
+      auto store = [&](uint16_t* dst, int64_t fr) {
+        if (s2d) {
+          uint16_t* o = dst + ((fr * RP + r) * RP + c) * 16;
+          *reinterpret_cast<uint4*>(o) = make_uint4(q00.x, q00.y, q01.x, q01.y);
+          *reinterpret_cast<uint4*>(o + 8) = make_uint4(q10.x, q10.y, q11.x, q11.y);
+        } else {
+          const int y = 2 * r, x = 2 * c;
+          uint16_t* o0 = dst + ((fr * S + y) * S + x) * 4;
+          if (x + 1 < S) *reinterpret_cast<uint4*>(o0) = make_uint4(q00.x, q00.y, q01.x, q01.y);
+          else *reinterpret_cast<uint2*>(o0) = q00;
+          if (y + 1 < S) {
+            uint16_t* o1 = o0 + (int64_t)S * 4;
+            if (x + 1 < S) *reinterpret_cast<uint4*>(o1) = make_uint4(q10.x, q10.y, q11.x, q11.y);
+            else *reinterpret_cast<uint2*>(o1) = q10;
+          }
         }
-      }
+      };
+      store(out, (int64_t)b * T + t);
+      if (ts >= 0) store(slow_out, (int64_t)b * Ts + ts);
     }
   };
   if (staged) cells(rows);
@@ -369,26 +276,13 @@ void pack_weights_launch(const float* master, uint16_t* fwd, uint16_t* dgr, cons
 int pack_desc_size() { return (int)sizeof(PackDesc); }
 
 void video_preprocess_launch(const uint8_t* frames, const int* desc, const int* tidx, int B, int T, int S,
-                             const float* mean, const float* std_, uint16_t* out, int s2d, hipStream_t s) {
-  const int64_t units = (int64_t)B * T * ((S + 1) / 2);
-  const int blocks = (int)(units < 65536 ? units : 65536);
-  if (blocks <= 0) return;
-  const char* ec = getenv("PVA_PRE_CHUNK");
-  if (!(ec && ec[0] == '0')) {
-    const int RP = (S + 1) / 2;
-    const int64_t wgs = (int64_t)B * T * ((RP + PRE2_RP - 1) / PRE2_RP);
-    hipLaunchKernelGGL(video_preprocess2_kernel, dim3((unsigned)wgs), dim3(256), 0, s, frames, desc, tidx, T, S,
-                       mean[0], mean[1], mean[2], 1.f / std_[0], 1.f / std_[1], 1.f / std_[2], out, s2d);
-    return;
-  }
-  const char* e = getenv("PVA_PRE_LDS");
-  const int lds = e ? atoi(e) : 6144;
-  if (lds >= 16384)
-    hipLaunchKernelGGL(video_preprocess_kernel<16384>, dim3(blocks), dim3(128), 0, s, frames, desc, tidx, T, S, mean[0],
-                       mean[1], mean[2], 1.f / std_[0], 1.f / std_[1], 1.f / std_[2], out, B, s2d);
-  else
-    hipLaunchKernelGGL(video_preprocess_kernel<6144>, dim3(blocks), dim3(128), 0, s, frames, desc, tidx, T, S, mean[0],
-                       mean[1], mean[2], 1.f / std_[0], 1.f / std_[1], 1.f / std_[2], out, B, s2d);
+                             const float* mean, const float* std_, uint16_t* out, int s2d, hipStream_t s,
+                             const int* slow_of, uint16_t* slow_out, int Ts) {
+  const int RP = (S + 1) / 2;
+  const int64_t wgs = (int64_t)B * T * ((RP + PRE2_RP - 1) / PRE2_RP);
+  if (wgs <= 0) return;
+  hipLaunchKernelGGL(video_preprocess2_kernel, dim3((unsigned)wgs), dim3(256), 0, s, frames, desc, tidx, T, S, mean[0],
+                     mean[1], mean[2], 1.f / std_[0], 1.f / std_[1], 1.f / std_[2], out, s2d, slow_of, slow_out, Ts);
 }
 
 void synth_frames_launch(uint8_t* out, int64_t n, uint32_t seed, hipStream_t s) {

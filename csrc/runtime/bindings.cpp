@@ -452,8 +452,11 @@ void pack_weights(const at::Tensor& master, const at::Tensor& fwd, const at::Ten
 }
 
 // frames: packed uint8 ; desc [B,10] int32 ; tidx [B,T] int32 ; out [B*T*S*S, 4] bf16
+// slow_of [T] int32 (slow frame of each frame, -1 if none) + slow_out: the slow pathway's frames, written in the same
+// pass (pack_pathway_indices selects a subset of the clip's frames)
 void video_preprocess(const at::Tensor& frames, const at::Tensor& desc, const at::Tensor& tidx, int64_t T, int64_t S,
-                      std::vector<double> mean, std::vector<double> std_, const at::Tensor& out, bool s2d) {
+                      std::vector<double> mean, std::vector<double> std_, const at::Tensor& out, bool s2d,
+                      const OptT& slow_of, const OptT& slow_out, int64_t Ts) {
   const bool h = kind16(out);
   TORCH_CHECK(!s2d || S % 2 == 0, "space-to-depth output needs an even crop");
   TORCH_CHECK(frames.scalar_type() == at::kByte, "frames must be uint8");
@@ -462,8 +465,14 @@ void video_preprocess(const at::Tensor& frames, const at::Tensor& desc, const at
   TORCH_CHECK(out.numel() >= desc.size(0) * T * S * S * 4, "output too small");
   const float m[3] = {(float)mean[0], (float)mean[1], (float)mean[2]};
   const float s[3] = {(float)std_[0], (float)std_[1], (float)std_[2]};
+  TORCH_CHECK(slow_of.has_value() == slow_out.has_value(), "slow_of and slow_out go together");
+  if (slow_of.has_value()) {
+    TORCH_CHECK(slow_of->scalar_type() == at::kInt && slow_of->numel() == T, "slow_of [T] int32");
+    TORCH_CHECK(slow_out->numel() >= desc.size(0) * Ts * S * S * 4 && kind16(*slow_out) == h, "slow output size / type");
+  }
   KSEL(h, video_preprocess_launch)(frames.data_ptr<uint8_t>(), desc.data_ptr<int>(), tidx.data_ptr<int>(), (int)desc.size(0),
-                          (int)T, (int)S, m, s, bfpm(out), s2d ? 1 : 0, cur_stream());
+                          (int)T, (int)S, m, s, bfpm(out), s2d ? 1 : 0, cur_stream(),
+                          slow_of.has_value() ? slow_of->data_ptr<int>() : nullptr, bfom(slow_out), (int)Ts);
 }
 
 // space-to-depth stems: x [N*T*Hs*Ws, 16] bf16 ; wpack [Cout_pad16, kt*256] bf16
@@ -768,7 +777,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("nonfinite_check", &nonfinite_check);
   m.def("pack_weights", &pack_weights);
   m.def("pack_desc_size", &pva_bf16::pack_desc_size);
-  m.def("video_preprocess", &video_preprocess);
+  m.def("video_preprocess", &video_preprocess, py::arg("frames"), py::arg("desc"), py::arg("tidx"), py::arg("T"),
+        py::arg("S"), py::arg("mean"), py::arg("std"), py::arg("out"), py::arg("s2d"), py::arg("slow_of") = py::none(),
+        py::arg("slow_out") = py::none(), py::arg("Ts") = 0);
   m.def("synth_frames", &synth_frames);
   m.def("narrow_c_bwd", &narrow_c_bwd, py::arg("g"), py::arg("ldg"), py::arg("mode"), py::arg("mask"), py::arg("yc"),
         py::arg("coef"), py::arg("dz"), py::arg("lddz"), py::arg("dz_accum"), py::arg("yb"), py::arg("sb"),

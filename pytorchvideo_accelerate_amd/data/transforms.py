@@ -125,22 +125,41 @@ class GpuClipBatch:
             return Act(buf.view(-1, 16), B, T, self.S // 2, self.S // 2)
         return Act(buf, B, T, self.S, self.S)
 
+    def _slow_of(self, device):
+        """[T] int32: the slow frame each frame also feeds (-1: none); None if the selection repeats a frame."""
+        key = ("slow_of", device)
+        if key not in self._out:
+            sel = self.slow_sel.tolist()
+            m = None
+            if len(set(sel)) == len(sel):
+                m = torch.full((self.T,), -1, dtype=torch.int32)
+                for s, t in enumerate(sel):
+                    m[t] = s
+                m = m.to(device)
+            self._out[key] = m
+        return self._out[key]
+
     def _run(self, frames: torch.Tensor, desc: torch.Tensor, tidx: torch.Tensor):
         B = desc.shape[0]
-        outs = []
-        if self.alpha:
+        fast = self._buf("fast", (B * self.T * self.S * self.S, 4))
+        if not self.alpha:
+            self.C.video_preprocess(frames, desc, tidx, self.T, self.S, self.mean, self.std, fast, self.s2d)
+            return [self._act(fast, B, self.T)]
+        Ts = len(self.slow_sel)
+        slow = self._buf("slow", (B * Ts * self.S * self.S, 4))
+        slow_of = self._slow_of(tidx.device)
+        if slow_of is not None:
+            # one pass: the slow frames are a subset of the fast ones, written from the same cells
+            self.C.video_preprocess(frames, desc, tidx, self.T, self.S, self.mean, self.std, fast, self.s2d,
+                                    slow_of, slow, Ts)
+        else:
             sel = self._out.get(("sel", tidx.device))
             if sel is None:
                 sel = self._out[("sel", tidx.device)] = self.slow_sel.to(tidx.device)
             stidx = tidx.index_select(1, sel).contiguous()
-            Ts = stidx.shape[1]
-            slow = self._buf("slow", (B * Ts * self.S * self.S, 4))
             self.C.video_preprocess(frames, desc, stidx, Ts, self.S, self.mean, self.std, slow, self.s2d)
-            outs.append(self._act(slow, B, Ts))
-        fast = self._buf("fast", (B * self.T * self.S * self.S, 4))
-        self.C.video_preprocess(frames, desc, tidx, self.T, self.S, self.mean, self.std, fast, self.s2d)
-        outs.append(self._act(fast, B, self.T))
-        return outs
+            self.C.video_preprocess(frames, desc, tidx, self.T, self.S, self.mean, self.std, fast, self.s2d)
+        return [self._act(slow, B, Ts), self._act(fast, B, self.T)]
 
     def __call__(self, frames: torch.Tensor, params: Sequence[ClipParams]):
         """frames: [B, T_src, H, W, 3] uint8 on device (same source shape) -> [slow, fast] or [clip] Acts."""

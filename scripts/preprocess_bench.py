@@ -30,9 +30,10 @@ def main():
     desc = torch.tensor([[(b * per) & 0x7FFFFFFF, (b * per) >> 31, SF, H, W, p.rh, p.rw, p.top, p.left, int(p.flip)]
                          for b, p in enumerate(params)], dtype=torch.int32, device=dev)
     tidx = torch.tensor([p.tidx for p in params], dtype=torch.int32, device=dev)
-    for knob in os.environ.get("PRE_VARIANTS", "PVA_PRE_LDS=16384,PVA_PRE_LDS=6144").split(","):
-        k, v = knob.split("=")
-        os.environ[k] = v
+    for knob in os.environ.get("PRE_VARIANTS", "default").split(","):
+        if "=" in knob:
+            k, v = knob.split("=")
+            os.environ[k] = v
         for _ in range(3):
             xs = prep._run(frames, desc, tidx)   # kernels only (the per-batch descriptor upload is host work)
         torch.cuda.synchronize()
