@@ -86,6 +86,7 @@ __device__ __forceinline__ void rs16(float (&v)[L], int lane) {
 }
 
 typedef __attribute__((ext_vector_type(4))) unsigned u32x4_t;
+typedef __attribute__((ext_vector_type(2))) unsigned u32x2_t_;
 
 // epilogue operands of one 32-channel chunk (members an epilogue does not use are optimised away)
 template <int TM>
@@ -347,6 +348,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
 #pragma unroll 1
     for (int it = 0; it < nit; ++it) {
       if (it + PD - 1 < nit) prefetch(P[PD - 1]);
+      unsigned mbits[TM][CPI];   // EP 1: ReLU bytes of this iteration's chunks, stored together below
 #pragma unroll
       for (int cc = 0; cc < CPI; ++cc) {
         const int c = it * CPI + cc;
@@ -400,7 +402,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, pk), yr, r * yb + 16 * g + nc * 2, 0,
                                                    ST_AUX);
             // bit = stored 16-bit value > 0 (res_out's convention)
-            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)relu_bits8(pk), mor, r * mrow + g + (nc >> 3), 0, 0);
+            mbits[i][cc] = relu_bits8(pk);
           } else if (EP == 0) {
             float o[8];
             unpack8(E.old[i], o);
@@ -469,6 +471,29 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
             rs16<8>(s_c, lane);
             if (!(rho & 1)) sw[2 * NG + nl + (rho >> 1)] += s_c[0];
           }
+        }
+      }
+      if constexpr (EP == 1) {
+        // a row's ReLU bytes of the iteration's chunks are contiguous (chunk c, lane group g -> byte 4c + g): gathered
+        // from the row's 4 lanes (lane rho + 16 g) and written by lane g = 0 as one 4-B / 8-B store, instead of one
+        // byte store per lane and chunk (measured ~8 % of the residual-output pass, tools/probe/fres_probe.py)
+        const int c0 = it * CPI;
+        const bool pair = CPI == 2 && c0 + 1 < nch;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          unsigned lo = mbits[i][0] << (8 * g), hi = CPI == 2 ? mbits[i][CPI - 1] << (8 * g) : 0u;
+          lo |= __shfl_xor(lo, 16, 64);
+          lo |= __shfl_xor(lo, 32, 64);
+          if (CPI == 2) {
+            hi |= __shfl_xor(hi, 16, 64);
+            hi |= __shfl_xor(hi, 32, 64);
+          }
+          const uint32_t r = (uint32_t)(m0 - row0 + 16 * i + rho);
+          const uint32_t mo = g == 0 ? r * mrow + ((nb0 + 32 * c0) >> 3) : 0x80000000u;   // other lanes: dropped
+          if (pair)
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t_, (uint2){lo, hi}), mor, mo, 0, 0);
+          else
+            __builtin_amdgcn_raw_buffer_store_b32(lo, mor, mo, 0, 0);
         }
       }
 #pragma unroll
