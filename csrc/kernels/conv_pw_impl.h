@@ -279,6 +279,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
     }
   };
   Pre<TM> P[PD][CPI];
+  bool pairbits = false;   // the current prefetch loads a chunk pair's ReLU bits with one 8-B load
   // row r's offsets (rows relative to row0; this lane's 8 channels 8g.. folded in)
   auto prefetch1 = [&](int m0, int c, Pre<TM>& Q) {
     const int nc = nb0 + 32 * c;   // chunk's first channel (uniform)
@@ -292,7 +293,10 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
       if constexpr (EP != 0 && (OPS & OP_RES))
         Q.res[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(resr, r * rb + 16 * g, nc * 2, 0));
       if constexpr (EP == 2) {
-        if constexpr ((OPS & OP_MASK) != 0) Q.bits[i] = __builtin_amdgcn_raw_buffer_load_b8(mr, r * mrow + g, nc >> 3, 0);
+        // ReLU bits: the chunk's 4 bytes of the row as one dword (the row's 4 lanes read the same word; byte g is this
+        // lane's, extracted at use) — chunk pairs take both dwords with one 8-B load in prefetch() below
+        if constexpr ((OPS & OP_MASK) != 0)
+          if (!pairbits) Q.bits[i] = __builtin_amdgcn_raw_buffer_load_b32(mr, r * mrow, nc >> 3, 0);
         if constexpr (need_y0)
           Q.y0[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(y0r, r * nb + 16 * g, nc * 2, 0));
         if constexpr (dual)
@@ -304,9 +308,22 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
   int tp = 0, ip = 0;
   auto prefetch = [&](Pre<TM> (&Q)[CPI]) {
     const int m0 = mfirst + tp * tstride;
+    pairbits = EP == 2 && (OPS & OP_MASK) != 0 && CPI == 2 && ip * CPI + 1 < nch;
 #pragma unroll
     for (int cc = 0; cc < CPI; ++cc)
       if (ip * CPI + cc < nch) prefetch1(m0, ip * CPI + cc, Q[cc]);
+    if constexpr (EP == 2 && (OPS & OP_MASK) != 0 && CPI == 2) {
+      if (pairbits) {
+        const int nc = nb0 + 32 * ip * CPI;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const uint32_t r = (uint32_t)(m0 - row0 + 16 * i + rho);
+          const u32x2_t_ v = __builtin_bit_cast(u32x2_t_, __builtin_amdgcn_raw_buffer_load_b64(mr, r * mrow, nc >> 3, 0));
+          Q[0].bits[i] = v[0];
+          Q[CPI - 1].bits[i] = v[1];
+        }
+      }
+    }
     if (++ip == nit) { ip = 0; ++tp; }
   };
   if (ntw > 0) load_a(mfirst);
@@ -426,7 +443,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
             unpack8(E.old[i], o);
             unpack8(E.res[i], rr);
             unpack8(E.y0[i], y0);
-            unsigned bits = E.bits[i];
+            unsigned bits = (OPS & OP_MASK) ? (E.bits[i] >> (8 * g)) & 0xffu : E.bits[i];
             if (masky) {
 #pragma unroll
               for (int e = 0; e < 8; ++e)
