@@ -77,6 +77,30 @@ def timeline(sel, steps):
     for lv in sorted(at):
         if lv:
             print(f"  {lv} kernel(s) running: {at[lv] / 1e6 / steps:8.2f} ms/step")
+    alone(sel, steps)
+
+
+def alone(sel, steps, top=25):
+    """Per kernel instantiation: time it ran with no other kernel beside it (the step's single-stream stretches —
+    where the other streams had nothing to overlap)."""
+    ev = []
+    for i, r in enumerate(sel):
+        ev.append((int(r["Start_Timestamp"]), 1, i))
+        ev.append((int(r["End_Timestamp"]), -1, i))
+    ev.sort()
+    running, last = set(), ev[0][0]
+    solo = collections.defaultdict(float)
+    for t, d, i in ev:
+        if t > last and len(running) == 1:
+            solo[family(sel[next(iter(running))]["Kernel_Name"])[1]] += t - last
+        if d > 0:
+            running.add(i)
+        else:
+            running.discard(i)
+        last = t
+    print(f"\n# running alone (ms/step; top {top})")
+    for k, v in sorted(solo.items(), key=lambda kv: -kv[1])[:top]:
+        print(f"{v / 1e6 / steps:9.3f}  {k[:120]}")
 
 
 if __name__ == "__main__":
