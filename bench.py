@@ -410,6 +410,7 @@ def run(a):
                        "global_batch": B * a.grad_accum * st.world_size,
                        "per_gpu_batch": B, "grad_accum": a.grad_accum, "seq_len": a.frames,
                        "parallelism": f"dp{st.world_size}", "backend": st.backend or "none",
+                       "comm": "framework-rccl" if st.comm is not None else ("process-group" if st.multi else "none"),
                        "forced_sync": st.forced,
                        "grad_dtype": a.grad_dtype, "classes": a.classes, "hip_graph": bool(gstep is not None),
                        "deterministic": a.deterministic, "source": a.source,

@@ -22,6 +22,7 @@ namespace pva_f16 {
 #include "../kernels/launchers.h"
 }
 void register_clip_reader(pybind11::module& m);
+void register_rccl(pybind11::module& m);
 
 namespace {
 
@@ -815,4 +816,5 @@ PYBIND11_MODULE(_C, m) {
     KSEL(h, stem_pack_launch)(f32(w), bfpm(out), (int)Cout, (int)kt, cur_stream());
   });
   register_clip_reader(m);
+  register_rccl(m);
 }

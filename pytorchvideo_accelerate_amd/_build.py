@@ -144,7 +144,8 @@ def build(jobs: int = 0, force: bool = False, verbose: bool = False, csrc: str =
         futs.append(ex.submit(_compile, id_src, common, "", force, "", build_dir))
         objs = [f.result() for f in futs]
     libs = ["-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
-            f"-L{ROCM_LIB}", f"-Wl,-rpath,{ROCM_LIB}", "-lrocprofiler-sdk-roctx"]   # ROCTx ranges
+            f"-L{ROCM_LIB}", f"-Wl,-rpath,{ROCM_LIB}", "-lrocprofiler-sdk-roctx",   # ROCTx ranges
+            "-ldl"]   # RCCL: bound at run time to torch's copy (csrc/runtime/rccl_comm.cpp)
     cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}"] + objs + [f"-L{tlib}", f"-Wl,-rpath,{tlib}"] + libs + [
         "-o", out + ".tmp"]
     r = subprocess.run(cmd, capture_output=True, text=True)

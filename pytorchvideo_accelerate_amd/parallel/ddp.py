@@ -27,6 +27,9 @@ before the collective is issued from it, so no compute stream ever waits for ano
 ``finish()`` — buckets can be reported per residual block even while both pathways and their weight-gradient streams
 are in flight.  Without ``producers`` (or for CPU gradients) the collective follows the current stream.
 
+``PVA_COMM=rccl`` (``dist.DistState.comm``): the collective is the framework's own RCCL communicator's
+``ncclAllReduce(avg)`` enqueued on that comm stream (``parallel/rccl.py``) instead of ProcessGroupNCCL's.
+
 Options beyond DDP's defaults: ``grad_dtype=torch.bfloat16`` all-reduces a bf16 copy of each bucket
 (half the xGMI bytes; the analogue of DDP's ``bf16_compress_hook``) and ``timing=True`` records, per
 step, every bucket's ready→reduced latency and the *exposed* communication time (how long the compute
@@ -126,7 +129,10 @@ class GradSync:
             else:
                 comm = t
             with trace_range(f"allreduce/bucket{b}"):
-                if self.state.backend == "nccl":
+                if self.state.comm is not None:   # framework-owned communicator: ncclAllReduce on this stream
+                    w = self.state.comm.all_reduce_(comm, "avg")
+                    post = None
+                elif self.state.backend == "nccl":
                     w = dist.all_reduce(comm, op=dist.ReduceOp.AVG, async_op=True)
                     post = None
                 else:

@@ -32,6 +32,7 @@ class DistState:
     device: torch.device = torch.device("cpu")
     distributed_type: str = "NO"
     forced: bool = False      # PVA_FORCE_GRADSYNC=1: a process group (and every collective) even at world size 1
+    comm: Optional[object] = None   # PVA_COMM=rccl: the framework-owned RCCL communicator (parallel/rccl.py)
 
     @property
     def is_main_process(self) -> bool:
@@ -85,6 +86,11 @@ class DistState:
                     attempt = os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")
                     kw["store"] = dist.PrefixStore(f"pva/attempt_{attempt}/", base)
                 dist.init_process_group(st.backend, rank=rank, world_size=ws, timeout=timeout, **kw)
+            if use_gpu and st.backend == "nccl" and os.environ.get("PVA_COMM", "pg") == "rccl":
+                import atexit
+                from .rccl import RcclCommunicator
+                st.comm = RcclCommunicator(rank, ws, st.broadcast_object)
+                atexit.register(st.comm.close)   # destroyed while the HIP runtime is still up
         return st
 
     # -------------------------------------------------------------- collectives

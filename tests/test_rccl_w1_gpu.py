@@ -59,11 +59,15 @@ def test_rccl_collectives_world_size_one(tmp_path):
         assert math.isfinite(st[k]) and st[k] >= 0, st
 
 
-def test_rccl_forced_gradsync_bench_matches_unsynced(tmp_path):
+@pytest.mark.parametrize("comm", ["pg", "rccl"])
+def test_rccl_forced_gradsync_bench_matches_unsynced(tmp_path, comm):
+    """``comm``: the bucket all-reduce through ProcessGroupNCCL, or through the framework-owned communicator
+    (``PVA_COMM=rccl``, parallel/rccl.py)."""
     d1 = str(tmp_path / "rccl.pt")
-    res = _torchrun([os.path.join(REPO, "bench.py")] + BENCH + ["--dump", d1], tmp_path)
+    res = _torchrun([os.path.join(REPO, "bench.py")] + BENCH + ["--dump", d1], tmp_path, PVA_COMM=comm)
     cfg = res["config"]
     assert cfg["backend"] == "nccl" and cfg["forced_sync"] is True and res["n_gpus"] == 1
+    assert cfg["comm"] == ("framework-rccl" if comm == "rccl" else "process-group"), cfg["comm"]
     for k in ("comm_exposed_ms", "comm_bucket_ms", "comm_last_bucket_ms"):
         assert k in cfg and math.isfinite(cfg[k]), cfg
     assert cfg["buckets"] > 1
