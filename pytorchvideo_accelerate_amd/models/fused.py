@@ -1619,20 +1619,32 @@ class FusedNet:
         main = torch.cuda.current_stream(self.device) if ms else None
         side = self._side_stream() if ms else None
         self._ms_bwd = ms   # per-block progress reports are deferred to stage ends (grads come from two streams)
+        # Per stage: the lateral fusion's backward (its input is the slow stage above's dcat, its output the fast
+        # pathway's dfast) runs on the fast-pathway stream — the slow pathway depends on neither, so the main stream goes
+        # straight on with the slow stage instead of waiting for it (it ran alone: ~1 ms/step in the steady-state
+        # trace, profiles/r5_final).  Without a gradient hook (or with the multi-stream GradSync, whose comm stream
+        # waits on every producer) the streams are not joined per stage at all: the main stream runs ahead and each
+        # stage's fusion waits only for the dcat it reads.
+        free = ms and (self.grad_hook is None or self.grad_multi_stream)
         for si in range(len(self.stages) - 1, -1, -1):
             with trace_range(f"bwd/b{si}"):
                 paths, fuse = self.stages[si]
-                if ms:
+                if ms and not free:
                     self._join(main, side)   # the fast pathway's dx of the stage above is final
                 # grads for this stage's pathway outputs: douts (slow may be the full concat grad)
                 if fuse is not None:
                     dcat = douts[0]
                     co = paths[0].out_channels()
-                    fuse.bwd(dcat.narrow(co, fuse.u.C), douts[1].t)
+                    if ms:
+                        self._join(side, main)   # dcat: written by the slow stage above (main stream)
+                        self.lane = 1
+                        with torch.cuda.stream(side):
+                            fuse.bwd(dcat.narrow(co, fuse.u.C), douts[1].t)
+                        self.lane = 0
+                    else:
+                        fuse.bwd(dcat.narrow(co, fuse.u.C), douts[1].t)
                     self._progress(fuse.flat_hi, force=True)
                     douts[0] = dcat.narrow(0, co)
-                if ms:
-                    self._join(side, main)   # the fused dfast accumulation is complete
                 new = [None] * len(paths)
                 # pathways in reverse order: matches the flat (reverse-execution) gradient layout
                 for p in range(len(paths) - 1, -1, -1):
@@ -1657,11 +1669,13 @@ class FusedNet:
                             ctx.__exit__(None, None, None)
                             self.lane = 0
                 if ms:
-                    self._join(main, side)
+                    if not free:
+                        self._join(main, side)
                     self._progress(max(m.flat_hi if isinstance(m, _Stem) else m.blocks[0].flat_hi for m in paths),
                                    force=True)
                 douts = new
         if ms:
+            self._join(main, side)
             self._join_wgrads()
         self._ms_bwd = False
 
