@@ -1178,6 +1178,9 @@ class FusedNet:
         self.fold_slabs = deterministic or os.environ.get("PVA_FOLD_SLABS", "1") == "1"
         # fused lateral-connection backward (apply + strided dgrad in one pass); PVA_LATERAL_BWD=0: the unfused path
         self.lateral_bwd = os.environ.get("PVA_LATERAL_BWD", "1") != "0"
+        # two-stream backward: the lateral fusion's backward on the fast-pathway stream (PVA_SIDE_FUSE=0: on the main
+        # stream, both streams joined around it and at every stage end)
+        self.side_fuse = os.environ.get("PVA_SIDE_FUSE", "1") != "0"
         self.stem_s2d = stem_s2d and not deterministic
         self.model = model
         self.device = torch.device(device)
@@ -1625,7 +1628,8 @@ class FusedNet:
         # trace, profiles/r5_final).  Without a gradient hook (or with the multi-stream GradSync, whose comm stream
         # waits on every producer) the streams are not joined per stage at all: the main stream runs ahead and each
         # stage's fusion waits only for the dcat it reads.
-        free = ms and (self.grad_hook is None or self.grad_multi_stream)
+        side_fuse = ms and self.side_fuse
+        free = side_fuse and (self.grad_hook is None or self.grad_multi_stream)
         for si in range(len(self.stages) - 1, -1, -1):
             with trace_range(f"bwd/b{si}"):
                 paths, fuse = self.stages[si]
@@ -1635,16 +1639,22 @@ class FusedNet:
                 if fuse is not None:
                     dcat = douts[0]
                     co = paths[0].out_channels()
-                    if ms:
+                    if side_fuse:
                         self._join(side, main)   # dcat: written by the slow stage above (main stream)
                         self.lane = 1
                         with torch.cuda.stream(side):
                             fuse.bwd(dcat.narrow(co, fuse.u.C), douts[1].t)
                         self.lane = 0
+                        if not free:
+                            self._join(main, side)   # the per-stage report below follows the current stream
                     else:
                         fuse.bwd(dcat.narrow(co, fuse.u.C), douts[1].t)
+                        if ms:
+                            self._join(side, main)   # the fast pathway's dx now includes the lateral term
                     self._progress(fuse.flat_hi, force=True)
                     douts[0] = dcat.narrow(0, co)
+                elif ms:
+                    self._join(side, main)   # the head's pooled-gradient scatter (main stream) feeds the fast stage
                 new = [None] * len(paths)
                 # pathways in reverse order: matches the flat (reverse-execution) gradient layout
                 for p in range(len(paths) - 1, -1, -1):
