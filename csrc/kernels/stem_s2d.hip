@@ -439,7 +439,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void s
   }
 }
 
-template <int KT>
+// ROLL (default): wave w owns spatial tap column bw = w and walks the four tap rows bh in registers.  The B fragment of
+// (kstep k, bh + 2) is the one of (k + 1, bh) (two output rows per kstep), so each kstep reads two new input fragments
+// instead of four and a window frame's 16 MFMAs cost 5 fragment reads instead of 16; the dY fragments of the four
+// ksteps are read once per frame pair.  Without it (PVA_STEM_ROLL=0) wave w owns tap row bh = w and reads every
+// fragment per MFMA: 2 transpose reads per MFMA make the kernel LDS-bound (35.7 % MFMA busy, profiles/r5_final).
+template <int KT, bool ROLL>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void stem_wgrad_pair_kernel(const StemParams p) {
   constexpr int TAPS = KT * 16;
   constexpr int J = KT + 1;
@@ -493,6 +498,42 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void s
       dma_patch<true>(xr, p, tn + 1, ho0, wo0, smem + ((t0 + J + 1) % SLOTS) * SLOT_BYTES);
       dma_dy(t0 + 2, dyt + (((t0 >> 1) + 1) & 1) * DYB);
     }
+    if constexpr (ROLL) {
+      constexpr int KS = TH * TW / 32;
+      const int h0 = g >> 1, wq = 8 * (g & 1) + rq;
+      ev8_t af[KS];
+#pragma unroll
+      for (int kstep = 0; kstep < KS; ++kstep) {
+        const int dp = (2 * kstep + h0) * TW + wq;
+        s16x4_t lo = trr(dcur + pswz(dp) * 32 + cb), hi = trr(dcur + pswz(dp + 4) * 32 + cb);
+        s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        af[kstep] = __builtin_bit_cast(ev8_t, v);
+      }
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        const char* slot = smem + ((t0 + j) % SLOTS) * SLOT_BYTES;
+        auto frag = [&](int row) {   // patch row `row` (per lane), tap column w
+          const int ip = row * PW + wq + w;
+          s16x4_t lo = trr(slot + pswz(ip) * POSB + cb), hi = trr(slot + pswz(ip + 4) * POSB + cb);
+          s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          return __builtin_bit_cast(ev8_t, v);
+        };
+        ev8_t fe = frag(h0), fo = frag(h0 + 1);
+#pragma unroll
+        for (int kstep = 0; kstep < KS; ++kstep) {
+          const int hh = 2 * kstep + h0;
+          const ev8_t fe2 = frag(hh + 2), fo2 = frag(hh + 3);
+          acc[j][0] = PVA_MFMA16(af[kstep], fe, acc[j][0], 0, 0, 0);
+          acc[j][1] = PVA_MFMA16(af[kstep], fo, acc[j][1], 0, 0, 0);
+          acc[j][2] = PVA_MFMA16(af[kstep], fe2, acc[j][2], 0, 0, 0);
+          acc[j][3] = PVA_MFMA16(af[kstep], fo2, acc[j][3], 0, 0, 0);
+          fe = fe2;
+          fo = fo2;
+        }
+      }
+      __syncthreads();  // next frames / dY tile landed; current window frames 0, 1 and dY buffer are free
+      continue;
+    }
 #pragma unroll
     for (int kstep = 0; kstep < TH * TW / 32; ++kstep) {
       const int hh = 2 * kstep + (g >> 1);
@@ -527,7 +568,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void s
       for (int r = 0; r < 4; ++r) {
         float v = g < 2 ? acc[dt][s][r] : acc[dt + 1][s][r];
         v += __shfl_xor(v, 32, 64);
-        if (g < 2) atomicAdd(p.dw + (int64_t)(4 * g + r) * TAPS * 16 + (dt * 16 + 4 * w + s) * 16 + li, v);
+        // acc[.][s]: tap (bh = w, bw = s), or with ROLL (bh = s, bw = w)
+        const int tap = ROLL ? 4 * s + w : 4 * w + s;
+        if (g < 2) atomicAdd(p.dw + (int64_t)(4 * g + r) * TAPS * 16 + (dt * 16 + tap) * 16 + li, v);
       }
 }
 
@@ -588,10 +631,10 @@ void launch_fwd_pair(const StemParams& p, hipStream_t s) {
   hipLaunchKernelGGL((stem_fwd_pair_kernel<KT>), dim3(p.N * p.tiles_h * p.tiles_w), dim3(256), lds, s, p);
 }
 
-template <int KT>
+template <int KT, bool ROLL>
 void launch_wgrad_pair(const StemParams& p, hipStream_t s) {
   const size_t lds = (KT + 3) * SLOT_BYTES + 2 * TH * TW * 16 * 2;
-  hipLaunchKernelGGL((stem_wgrad_pair_kernel<KT>), dim3(p.N * p.tiles_h * p.tiles_w), dim3(256), lds, s, p);
+  hipLaunchKernelGGL((stem_wgrad_pair_kernel<KT, ROLL>), dim3(p.N * p.tiles_h * p.tiles_w), dim3(256), lds, s, p);
 }
 
 }  // namespace
@@ -611,6 +654,12 @@ static bool stem_perm_enabled() {
   return !(e && e[0] == '0');
 }
 
+// PVA_STEM_ROLL=0: the frame-pair wgrad with one tap row per wave (every B fragment read per MFMA; A/B, tests)
+static bool stem_roll_enabled() {
+  const char* e = getenv("PVA_STEM_ROLL");
+  return !(e && e[0] == '0');
+}
+
 // mode 0: forward, 1: wgrad.  Shapes outside stem_s2d_supported() are rejected by the bindings (TORCH_CHECK)
 // before this is reached, so every call launches exactly one kernel.
 void stem_s2d_launch(int mode, const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, const uint16_t* dy,
@@ -627,7 +676,8 @@ void stem_s2d_launch(int mode, const uint16_t* x, const uint16_t* w, uint16_t* y
     else if (kt == 1 && Cout == 64 && stem_perm_enabled()) launch_fwd<1, 4, true>(p, s);
     else if (kt == 1 && Cout <= 64) launch_fwd<1, 4>(p, s);
   } else {
-    if (pair) launch_wgrad_pair<5>(p, s);
+    if (pair && stem_roll_enabled()) launch_wgrad_pair<5, true>(p, s);
+    else if (pair) launch_wgrad_pair<5, false>(p, s);
     else if (kt == 5 && Cout <= 16) launch_wgrad<5, 1>(p, s);
     else if (kt == 1 && Cout <= 64) launch_wgrad<1, 4>(p, s);
   }
