@@ -225,7 +225,32 @@ __device__ __forceinline__ s16x4_t trr(const char* a) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(a));
 }
 
-template <int KT, int COT>
+// The same transpose read as inline asm: the compiler's wait-count pass treats the intrinsic as possibly reading the
+// LDS an in-flight LDS-DMA writes and puts an s_waitcnt vmcnt(0) in front of it — right after the next frame pair's
+// DMAs are issued, so no DMA overlapped the MFMAs (the barrier at the end of the pair already waits for them).  The
+// asm form is invisible to that pass: its results are made ready by explicit lgkmcnt waits (lgkm_tie) that also carry
+// the registers, so nothing consumes them earlier.
+__device__ __forceinline__ s16x4_t trr_nw(const char* a) {
+  s16x4_t r;
+  const uint32_t off = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) const char*)a);
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(off));
+  return r;
+}
+
+// s_waitcnt lgkmcnt(N) that the four registers depend on.  LDS reads retire in order, so after the wait every LDS
+// read older than the N newest is complete, whatever other lgkm operations are in flight.
+template <int N>
+__device__ __forceinline__ void lgkm_tie(s16x4_t& a, s16x4_t& b, s16x4_t& c, s16x4_t& d) {
+  asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : "n"(N));
+}
+
+__device__ __forceinline__ ev8_t frag8(s16x4_t lo, s16x4_t hi) {
+  s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(ev8_t, v);
+}
+
+// AR: transpose reads through trr_nw, the reads of k-step k + 1 requested before the MFMAs of k-step k (see trr_nw)
+template <int KT, int COT, bool AR = false>
 __global__ __launch_bounds__(256) void stem_wgrad_kernel(const StemParams p) {
   constexpr int TAPS = KT * 16;
   constexpr int TPW = TAPS / 4;              // taps per wave
@@ -281,6 +306,50 @@ __global__ __launch_bounds__(256) void stem_wgrad_kernel(const StemParams p) {
     if (to + 1 < p.To) {  // next frame's input (slot outside the window) and dY tile (other buffer)
       dma_patch(xr, p, to - p.pt + KT, ho0, wo0, smem + ((to + KT) % SLOTS) * SLOT_BYTES);
       dma_dy(to + 1, dyt + ((to + 1) & 1) * DYB);
+    }
+    if constexpr (AR) {
+      constexpr int KS = TH * TW / 32, NR = COT + TPW;   // fragments per k-step: COT dY + TPW taps, 2 reads each
+      static_assert(NR % 2 == 0, "ties go by 4 halves");
+      s16x4_t R[2][NR][2];
+      auto issue = [&](int kstep, s16x4_t (&Rk)[NR][2]) {
+        const int hh = 2 * kstep + (g >> 1), wq = 8 * (g & 1) + rq;
+#pragma unroll
+        for (int c = 0; c < COT; ++c) {
+          const char* base = dcur + (hh * TW + wq) * COP * 2 + c * 32 + cb;
+          Rk[c][0] = trr_nw(base);
+          Rk[c][1] = trr_nw(base + 4 * COP * 2);
+        }
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) {
+          const int tap = w * TPW + t;
+          const int dt = tap >> 4, bh = (tap >> 2) & 3, bw = tap & 3;
+          const char* base = smem + ((to + dt) % SLOTS) * SLOT_BYTES + ((hh + bh) * PW + (wq + bw)) * POSB + cb;
+          Rk[COT + t][0] = trr_nw(base);
+          Rk[COT + t][1] = trr_nw(base + 4 * POSB);
+        }
+      };
+      issue(0, R[0]);
+#pragma unroll
+      for (int kstep = 0; kstep < KS; ++kstep) {
+        s16x4_t(&Rk)[NR][2] = R[kstep & 1];
+        if (kstep + 1 < KS) {
+          issue(kstep + 1, R[(kstep + 1) & 1]);
+          // at most 15 reads (the counter's limit) in flight: all of this k-step's reads are older than those
+#pragma unroll
+          for (int i = 0; i < NR; i += 2) lgkm_tie<(2 * NR < 15 ? 2 * NR : 15)>(Rk[i][0], Rk[i][1], Rk[i + 1][0], Rk[i + 1][1]);
+        } else {
+#pragma unroll
+          for (int i = 0; i < NR; i += 2) lgkm_tie<0>(Rk[i][0], Rk[i][1], Rk[i + 1][0], Rk[i + 1][1]);
+        }
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) {
+          const ev8_t xb = frag8(Rk[COT + t][0], Rk[COT + t][1]);
+#pragma unroll
+          for (int c = 0; c < COT; ++c) acc[c][t] = PVA_MFMA16(frag8(Rk[c][0], Rk[c][1]), xb, acc[c][t], 0, 0, 0);
+        }
+      }
+      __syncthreads();  // next frame + dY tile landed; the window's first slot and this dY buffer are free
+      continue;
     }
 #pragma unroll
     for (int kstep = 0; kstep < TH * TW / 32; ++kstep) {
@@ -444,7 +513,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void s
 // instead of four and a window frame's 16 MFMAs cost 5 fragment reads instead of 16; the dY fragments of the four
 // ksteps are read once per frame pair.  Without it (PVA_STEM_ROLL=0) wave w owns tap row bh = w and reads every
 // fragment per MFMA: 2 transpose reads per MFMA make the kernel LDS-bound (35.7 % MFMA busy, profiles/r5_final).
-template <int KT, bool ROLL>
+// AR (with ROLL, default): every transpose read through trr_nw, software-pipelined — the fragments of k-step k + 1 are
+// requested before the MFMAs of k-step k — so the next pair's DMAs overlap this pair's MFMAs (PVA_STEM_ASYNC=0: the
+// intrinsic reads and the vmcnt(0) the compiler puts in front of them).
+template <int KT, bool ROLL, bool AR = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void stem_wgrad_pair_kernel(const StemParams p) {
   constexpr int TAPS = KT * 16;
   constexpr int J = KT + 1;
@@ -497,6 +569,57 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void s
       dma_patch<true>(xr, p, tn, ho0, wo0, smem + ((t0 + J) % SLOTS) * SLOT_BYTES);
       dma_patch<true>(xr, p, tn + 1, ho0, wo0, smem + ((t0 + J + 1) % SLOTS) * SLOT_BYTES);
       dma_dy(t0 + 2, dyt + (((t0 >> 1) + 1) & 1) * DYB);
+    }
+    if constexpr (ROLL && AR) {
+      constexpr int KS = TH * TW / 32;
+      const int h0 = g >> 1, wq = 8 * (g & 1) + rq;
+      ev8_t af[KS];
+      {
+        s16x4_t al[KS], ah[KS];
+#pragma unroll
+        for (int kstep = 0; kstep < KS; ++kstep) {
+          const int dp = (2 * kstep + h0) * TW + wq;
+          al[kstep] = trr_nw(dcur + pswz(dp) * 32 + cb);
+          ah[kstep] = trr_nw(dcur + pswz(dp + 4) * 32 + cb);
+        }
+        lgkm_tie<0>(al[0], ah[0], al[1], ah[1]);
+        lgkm_tie<0>(al[2], ah[2], al[3], ah[3]);
+#pragma unroll
+        for (int kstep = 0; kstep < KS; ++kstep) af[kstep] = frag8(al[kstep], ah[kstep]);
+      }
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        const char* slot = smem + ((t0 + j) % SLOTS) * SLOT_BYTES;
+        // F[m]: patch rows 2m + h0 (even fragment: halves 0, 1) and 2m + h0 + 1 (odd: halves 2, 3), tap column w;
+        // k-step k uses F[k] (tap rows 0, 1) and F[k + 1] (tap rows 2, 3)
+        s16x4_t F[KS + 1][4];
+        auto issue = [&](int m) {
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const int ip = (2 * m + h0 + e) * PW + wq + w;
+            F[m][2 * e] = trr_nw(slot + pswz(ip) * POSB + cb);
+            F[m][2 * e + 1] = trr_nw(slot + pswz(ip + 4) * POSB + cb);
+          }
+        };
+        issue(0);
+        issue(1);
+#pragma unroll
+        for (int kstep = 0; kstep < KS; ++kstep) {
+          if (kstep + 2 <= KS) {
+            issue(kstep + 2);   // in flight during this k-step's MFMAs
+            if (kstep == 0) lgkm_tie<4>(F[0][0], F[0][1], F[0][2], F[0][3]);
+            lgkm_tie<4>(F[kstep + 1][0], F[kstep + 1][1], F[kstep + 1][2], F[kstep + 1][3]);
+          } else {
+            lgkm_tie<0>(F[kstep + 1][0], F[kstep + 1][1], F[kstep + 1][2], F[kstep + 1][3]);
+          }
+          acc[j][0] = PVA_MFMA16(af[kstep], frag8(F[kstep][0], F[kstep][1]), acc[j][0], 0, 0, 0);
+          acc[j][1] = PVA_MFMA16(af[kstep], frag8(F[kstep][2], F[kstep][3]), acc[j][1], 0, 0, 0);
+          acc[j][2] = PVA_MFMA16(af[kstep], frag8(F[kstep + 1][0], F[kstep + 1][1]), acc[j][2], 0, 0, 0);
+          acc[j][3] = PVA_MFMA16(af[kstep], frag8(F[kstep + 1][2], F[kstep + 1][3]), acc[j][3], 0, 0, 0);
+        }
+      }
+      __syncthreads();  // next frames / dY tile landed; current window frames 0, 1 and dY buffer are free
+      continue;
     }
     if constexpr (ROLL) {
       constexpr int KS = TH * TW / 32;
@@ -619,10 +742,10 @@ void launch_fwd(const StemParams& p, hipStream_t s) {
   hipLaunchKernelGGL((stem_fwd_kernel<KT, COT, PERM>), dim3(p.N * p.tiles_h * p.tiles_w), dim3(256), lds, s, p);
 }
 
-template <int KT, int COT>
+template <int KT, int COT, bool AR = false>
 void launch_wgrad(const StemParams& p, hipStream_t s) {
   const size_t lds = (KT + 1) * SLOT_BYTES + 2 * TH * TW * COT * 16 * 2;
-  hipLaunchKernelGGL((stem_wgrad_kernel<KT, COT>), dim3(p.N * p.tiles_h * p.tiles_w), dim3(256), lds, s, p);
+  hipLaunchKernelGGL((stem_wgrad_kernel<KT, COT, AR>), dim3(p.N * p.tiles_h * p.tiles_w), dim3(256), lds, s, p);
 }
 
 template <int KT>
@@ -631,10 +754,10 @@ void launch_fwd_pair(const StemParams& p, hipStream_t s) {
   hipLaunchKernelGGL((stem_fwd_pair_kernel<KT>), dim3(p.N * p.tiles_h * p.tiles_w), dim3(256), lds, s, p);
 }
 
-template <int KT, bool ROLL>
+template <int KT, bool ROLL, bool AR = false>
 void launch_wgrad_pair(const StemParams& p, hipStream_t s) {
   const size_t lds = (KT + 3) * SLOT_BYTES + 2 * TH * TW * 16 * 2;
-  hipLaunchKernelGGL((stem_wgrad_pair_kernel<KT, ROLL>), dim3(p.N * p.tiles_h * p.tiles_w), dim3(256), lds, s, p);
+  hipLaunchKernelGGL((stem_wgrad_pair_kernel<KT, ROLL, AR>), dim3(p.N * p.tiles_h * p.tiles_w), dim3(256), lds, s, p);
 }
 
 }  // namespace
@@ -660,6 +783,12 @@ static bool stem_roll_enabled() {
   return !(e && e[0] == '0');
 }
 
+// PVA_STEM_ASYNC=0: the rolling frame-pair wgrad with intrinsic transpose reads (A/B, tests)
+static bool stem_async_enabled() {
+  const char* e = getenv("PVA_STEM_ASYNC");
+  return !(e && e[0] == '0');
+}
+
 // mode 0: forward, 1: wgrad.  Shapes outside stem_s2d_supported() are rejected by the bindings (TORCH_CHECK)
 // before this is reached, so every call launches exactly one kernel.
 void stem_s2d_launch(int mode, const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, const uint16_t* dy,
@@ -676,9 +805,11 @@ void stem_s2d_launch(int mode, const uint16_t* x, const uint16_t* w, uint16_t* y
     else if (kt == 1 && Cout == 64 && stem_perm_enabled()) launch_fwd<1, 4, true>(p, s);
     else if (kt == 1 && Cout <= 64) launch_fwd<1, 4>(p, s);
   } else {
-    if (pair && stem_roll_enabled()) launch_wgrad_pair<5, true>(p, s);
+    if (pair && stem_roll_enabled() && stem_async_enabled()) launch_wgrad_pair<5, true, true>(p, s);
+    else if (pair && stem_roll_enabled()) launch_wgrad_pair<5, true>(p, s);
     else if (pair) launch_wgrad_pair<5, false>(p, s);
     else if (kt == 5 && Cout <= 16) launch_wgrad<5, 1>(p, s);
+    else if (kt == 1 && Cout <= 64 && stem_async_enabled()) launch_wgrad<1, 4, true>(p, s);
     else if (kt == 1 && Cout <= 64) launch_wgrad<1, 4>(p, s);
   }
 }

@@ -1,6 +1,7 @@
 """Fast-stem weight gradient at the headline shape (SlowFast-R50 32x2x224, B=160: s2d input [160, 32, 112, 112, 16],
 dY [.., 8]), the rolling-fragment frame-pair kernel (default) against the one-tap-row-per-wave form
-(PVA_STEM_ROLL=0, read per launch).  Prints the mean kernel time of each and their results' relative difference."""
+(PVA_STEM_ROLL=0) and the rolling form with intrinsic transpose reads (PVA_STEM_ASYNC=0); both read per launch.
+Prints the mean kernel time of each and the results' relative differences."""
 import os
 import sys
 
@@ -17,8 +18,9 @@ def main():
     x = torch.randn(N * T * H * H, 16, device=dev).to(torch.bfloat16)
     dy = torch.randn(N * T * H * H, cout, device=dev).to(torch.bfloat16)
     res = {}
-    for roll in ("0", "1", "0", "1"):
-        os.environ["PVA_STEM_ROLL"] = roll
+    arms = {"0": ("0", "0"), "1": ("1", "0"), "2": ("1", "1")}   # (PVA_STEM_ROLL, PVA_STEM_ASYNC)
+    for roll in ("0", "1", "2", "0", "1", "2"):
+        os.environ["PVA_STEM_ROLL"], os.environ["PVA_STEM_ASYNC"] = arms[roll]
         acc = torch.zeros(cout * kt * 256, device=dev)
         C.stem_wgrad(x, dy, acc, [N, T, H, H], cout, kt)   # warm-up (and the result)
         torch.cuda.synchronize()
@@ -32,9 +34,30 @@ def main():
         ms = e0.elapsed_time(e1) / 10
         res.setdefault(roll, []).append(ms)
         res["out" + roll] = out
-        print(f"PVA_STEM_ROLL={roll}: {ms * 1000:.0f} us", flush=True)
-    a, b = res["out0"], res["out1"]
-    print(f"rel diff roll vs no-roll: {float((a - b).norm() / b.norm()):.2e}")
+        print(f"PVA_STEM_ROLL={arms[roll][0]} PVA_STEM_ASYNC={arms[roll][1]}: {ms * 1000:.0f} us", flush=True)
+    for k in ("1", "2"):
+        a, b = res["out" + k], res["out0"]
+        print(f"rel diff {arms[k]} vs {arms['0']}: {float((a - b).norm() / b.norm()):.2e}")
+    # slow stem (k(1,7,7), Cout 64, 8 frames): intrinsic vs asm transpose reads
+    del x, dy
+    Ts, cs = 8, 64
+    x = torch.randn(N * Ts * H * H, 16, device=dev).to(torch.bfloat16)
+    dy = torch.randn(N * Ts * H * H, cs, device=dev).to(torch.bfloat16)
+    outs = {}
+    for asy in ("0", "1", "0", "1"):
+        os.environ["PVA_STEM_ASYNC"] = asy
+        acc = torch.zeros(cs * 256, device=dev)
+        C.stem_wgrad(x, dy, acc, [N, Ts, H, H], cs, 1)
+        torch.cuda.synchronize()
+        outs[asy] = acc.clone()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(10):
+            C.stem_wgrad(x, dy, acc, [N, Ts, H, H], cs, 1)
+        e1.record()
+        torch.cuda.synchronize()
+        print(f"slow stem PVA_STEM_ASYNC={asy}: {e0.elapsed_time(e1) / 10 * 1000:.0f} us", flush=True)
+    print(f"slow stem rel diff: {float((outs['1'] - outs['0']).norm() / outs['0'].norm()):.2e}")
 
 
 if __name__ == "__main__":
