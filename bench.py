@@ -45,8 +45,11 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=int(os.environ.get("PVA_BENCH_BATCH", 160)),
-                    help="per-GPU clips per step")
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("PVA_BENCH_BATCH", 0)),
+                    help="per-GPU clips per step (default 160; 32 for --precision fp32)")
+    ap.add_argument("--model", choices=("slowfast", "slow_r50"), default="slowfast",
+                    help="slowfast: SlowFast-R{--depth} (headline); slow_r50: Slow-only R50 (the reference run.py default "
+                         "model, is_slowfast=False, run.py:338-351), e.g. --model slow_r50 --frames 8")
     ap.add_argument("--frames", type=int, default=32)
     ap.add_argument("--alpha", type=int, default=4)
     ap.add_argument("--crop", type=int, default=224)
@@ -59,9 +62,10 @@ def parse(argv=None):
     ap.add_argument("--first-bucket-mb", type=float, default=4.0)
     ap.add_argument("--grad-dtype", choices=("fp32", "bf16"), default="fp32",
                     help="all-reduce payload dtype (bf16 = DDP bf16_compress_hook analogue)")
-    ap.add_argument("--precision", choices=("bf16", "fp16"), default="bf16",
-                    help="16-bit compute type of the fused kernels; fp16 adds dynamic loss scaling (the reference "
-                         "recipe's --mixed_precision fp16, run_slowfast_r50.sh:9)")
+    ap.add_argument("--precision", choices=("bf16", "fp16", "fp32"), default="bf16",
+                    help="bf16/fp16: compute type of the fused kernels (fp16 adds dynamic loss scaling, the reference "
+                         "recipe's --mixed_precision fp16, run_slowfast_r50.sh:9); fp32: the native fp32 kernels (the "
+                         "reference default --mixed_precision no, run.py:330; models/native32.py)")
     ap.add_argument("--lr", type=float, default=0.1)
     ap.add_argument("--grad-accum", type=int, default=1,
                     help="micro-batches of --batch clips per optimizer step (gradients all-reduced once, on the last)")
@@ -85,7 +89,10 @@ def parse(argv=None):
     ap.add_argument("--data-rank", type=int, default=-1,
                     help="draw the synthetic data of this rank instead of the own one (single-process oracle runs "
                          "of a multi-rank job's shards)")
-    return ap.parse_args(argv)
+    a = ap.parse_args(argv)
+    if not a.batch:
+        a.batch = 32 if a.precision == "fp32" else 160
+    return a
 
 
 def _free_port() -> int:
@@ -172,10 +179,11 @@ def host_loader(a, st, eng, dev):
     need = (a.warmup + a.steps + 3) * a.batch * a.grad_accum * st.world_size
     reps = -(-need // max(len(vids), 1))
     paths = LabeledVideoPaths([vids[i] for i in range(len(vids))] * reps, vids.classes)
-    ds = VideoClipDataset(paths, a.src_frames / 30.0, True, a.frames, a.crop, a.alpha, rank=st.rank,
+    alpha = None if a.model == "slow_r50" else a.alpha
+    ds = VideoClipDataset(paths, a.src_frames / 30.0, True, a.frames, a.crop, alpha, rank=st.rank,
                           world=st.world_size, distributed=st.world_size > 1, seed=0, mode="gpu")
     src = NativeRawSource(ds, a.batch, threads=a.reader_threads, drop_last=True, prefetch=3)
-    prep = GpuClipBatch(dev, a.frames, a.crop, a.alpha, s2d=eng.input_s2d, dtype=eng.cdt)
+    prep = GpuClipBatch(dev, a.frames, a.crop, alpha, s2d=eng.input_s2d, dtype=eng.cdt)
     while True:
         for b in DeviceLoader(src, prep, dev):
             yield b["video"], b["label"]
@@ -220,7 +228,46 @@ def run(a):
         from pytorchvideo_accelerate_amd.data.transforms import GpuClipBatch, sample_params
         assert dev.type == "cuda", "bench.py needs a GPU (or --plumbing)"
         torch.manual_seed(1234)
-        model = R.create_slowfast(a.depth, a.classes)
+        slow_only = a.model == "slow_r50"
+        model = (R.create_resnet(50, a.classes, head_pool_kernel_size=(a.frames, a.crop // 32, a.crop // 32))
+                 if slow_only else R.create_slowfast(a.depth, a.classes))
+        alpha = None if slow_only else a.alpha
+    if not a.plumbing and a.precision == "fp32":
+        from pytorchvideo_accelerate_amd.models.native32 import NativeF32Net
+        assert a.source == "synthetic" and not a.graph, "--precision fp32 runs synthetic device clips, eagerly"
+        eng = NativeF32Net(model, dev)
+        st.broadcast_tensors([eng.flat.data] + [b for b in model.buffers()])
+        opt = FusedSGD(eng.flat, lr=a.lr, momentum=0.9, weight_decay=1e-4)
+        bounds = sorted(set(eng.flat.span(p)[1] for p in eng.flat.params))
+        sync = GradSync(eng.flat.grad, st, a.bucket_mb, boundaries=bounds, first_mb=a.first_bucket_mb,
+                        grad_dtype=gdt, timing=st.multi)
+        eng.grad_hook = sync.progress if st.multi else None
+        sync.producers = lambda: [torch.cuda.current_stream(dev)]
+        drank = st.rank if a.data_rank < 0 else a.data_rank
+        gen = torch.Generator().manual_seed(1000 + drank)
+        labels_all = torch.randint(0, a.classes, (64, B), generator=gen).to(dev)
+        # synthetic normalised clips already on the device (what the host transform + H2D deliver), two batches
+        # alternated; the NCTHW -> NDHWC layout pass runs inside every step
+        clips = []
+        for _ in range(2):
+            fast = torch.randn(B, 3, a.frames, a.crop, a.crop, generator=gen).to(dev)
+            clips.append(fast if slow_only else
+                         [fast[:, :, torch.linspace(0, a.frames - 1, a.frames // a.alpha).long()].contiguous(), fast])
+
+        def step(i, tune=False):
+            opt.zero_grad()
+            for j in range(a.grad_accum):
+                k = i * a.grad_accum + j
+                last = j == a.grad_accum - 1
+                sync.begin(last and not tune)
+                loss, _ = eng.forward_backward(clips[k % 2], labels_all[k % 64], loss_scale=1.0 / a.grad_accum)
+                sync.finish()
+            if tune:
+                return None
+            with trace_range("sgd"):
+                opt.step()
+            return loss
+    elif not a.plumbing:
         from pytorchvideo_accelerate_amd.ops.optim import FusedGradScaler
         assert not (a.graph and a.precision == "fp16"), "--graph replays no loss-scale check"
         eng = FusedNet(model, dev, deterministic=a.deterministic, load_tuning=st.world_size == 1,
@@ -259,7 +306,7 @@ def run(a):
             eng.C.synth_frames(frames, 7 + drank)
             # double-buffered on-device preprocessing: micro-batch k+1 is decoded/resized/cropped on its own
             # stream while micro-batch k trains (a prefetching data loader; every step still pays its batch)
-            preps = [GpuClipBatch(dev, a.frames, a.crop, a.alpha, s2d=eng.input_s2d, dtype=eng.cdt) for _ in range(2)]
+            preps = [GpuClipBatch(dev, a.frames, a.crop, alpha, s2d=eng.input_s2d, dtype=eng.cdt) for _ in range(2)]
             pstream = torch.cuda.Stream(dev)
             pending = {}
 
@@ -382,11 +429,13 @@ def run(a):
             torch.save({"grad": dump["grad"].cpu(), "params": [g.cpu() for g in gathered],
                         "world_size": st.world_size}, a.dump)
     if st.is_main_process:
-        headline = (a.depth, a.frames, a.crop, a.alpha) == (50, 32, 224, 4) and not a.plumbing
+        headline = ((a.model, a.depth, a.frames, a.crop, a.alpha) == ("slowfast", 50, 32, 224, 4)
+                    and not a.plumbing)
+        mname = (f"Slow-R50 {a.frames}x{64 // a.frames}x{a.crop}" if a.model == "slow_r50" else
+                 f"SlowFast-R{a.depth} {a.frames}x2x{a.crop}")
         fp16 = {"loss_scale": scaler.get_scale(), "skipped_steps": skipped[0]} if scaler is not None else {}
         print(json.dumps({
-            "metric": METRIC if headline else
-                      f"clips/sec (whole node) SlowFast-R{a.depth} {a.frames}x2x{a.crop}; step-time p50",
+            "metric": METRIC if headline else f"clips/sec (whole node) {mname}; step-time p50",
             "value": round(clips, 2),
             "unit": "clips/s",
             "n_gpus": st.world_size,
@@ -401,12 +450,14 @@ def run(a):
                             if headline and a.precision == "bf16" else None),
             "dtype": "fp32" if a.plumbing else a.precision,
             "data": ("synthetic normal clips, CPU plumbing run" if a.plumbing else
+                     "synthetic normalised fp32 clips resident on the device (two batches alternated; NCTHW->NDHWC "
+                     "layout pass inside the step); random-init weights" if a.precision == "fp32" else
                      "synthetic uint8 raw-frame .npy corpus (64x256x340 per video) read by the native C++ reader into "
                      "pinned memory, H2D on a copy stream, on-device preprocessing; random-init weights"
                      if a.source == "host" else
                      "synthetic uint8 decoded clips (64x256x340), on-device preprocessing (next batch prefetched "
                      "on a side stream); random-init weights"),
-            "config": {"model": f"SlowFast-R{a.depth} {a.frames}x2x{a.crop}",
+            "config": {"model": mname,
                        "global_batch": B * a.grad_accum * st.world_size,
                        "per_gpu_batch": B, "grad_accum": a.grad_accum, "seq_len": a.frames,
                        "parallelism": f"dp{st.world_size}", "backend": st.backend or "none",

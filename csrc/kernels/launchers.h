@@ -72,7 +72,7 @@ void video_preprocess_launch(const uint8_t* frames, const int* desc, const int* 
                              const int* slow_of = nullptr, uint16_t* slow_out = nullptr, int Ts = 0);
 int stem_tiles(int Ho, int Wo, int N);
 void stem_s2d_launch(int mode, const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, const uint16_t* dy,
-                     float* dw, int N, int T, int Hs, int Ws, int Cout, int kt, hipStream_t s);
+                     float* dw, int N, int T, int Hs, int Ws, int Cout, int kt, hipStream_t s, float* slab = nullptr);
 bool stem_s2d_supported(int Cout, int kt);
 void stem_wgrad_convert_launch(float* acc, float* grad, int Cout, int kt, float beta, hipStream_t s);
 void stem_pack_launch(const float* w, uint16_t* out, int Cout, int kt, hipStream_t s);

@@ -38,7 +38,8 @@ struct StemParams {
   int To, Ho, Wo;
   int pt;               // temporal padding (kt/2)
   int tiles_h, tiles_w;
-};
+  int slab;             // wgrad: 0 = fp32 atomics into dw; else each workgroup stores its partial dW to dw + block * slab
+};                      //        (reproducible mode: fixed-order reduction by stem_slab_reduce)
 
 constexpr uint32_t OOB = 0x7ffffff0u;         // buffer offset past num_records: the load returns zeros
 constexpr int SLOT_BYTES = 448 * 16;           // frame slot: 418 chunks padded to 7 x 64 lanes
@@ -389,7 +390,11 @@ __global__ __launch_bounds__(256) void stem_wgrad_kernel(const StemParams p) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int co = 16 * c + 4 * g + r;
-        if (co < p.Cout) atomicAdd(p.dw + (int64_t)co * TAPS * 16 + tap * 16 + li, acc[c][t][r]);
+        if (co < p.Cout) {
+          const int64_t o = (int64_t)co * TAPS * 16 + tap * 16 + li;
+          if (p.slab) p.dw[(int64_t)blockIdx.x * p.slab + o] = acc[c][t][r];
+          else atomicAdd(p.dw + o, acc[c][t][r]);
+        }
       }
     }
 }
@@ -693,8 +698,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void s
         v += __shfl_xor(v, 32, 64);
         // acc[.][s]: tap (bh = w, bw = s), or with ROLL (bh = s, bw = w)
         const int tap = ROLL ? 4 * s + w : 4 * w + s;
-        if (g < 2) atomicAdd(p.dw + (int64_t)(4 * g + r) * TAPS * 16 + (dt * 16 + tap) * 16 + li, v);
+        if (g < 2) {
+          const int64_t o = (int64_t)(4 * g + r) * TAPS * 16 + (dt * 16 + tap) * 16 + li;
+          if (p.slab) p.dw[(int64_t)blockIdx.x * p.slab + o] = v;
+          else atomicAdd(p.dw + o, v);
+        }
       }
+}
+
+// acc[i] += sum over slabs s = 0, 1, ... of slab[s * n + i], in that order (bitwise reproducible)
+__global__ __launch_bounds__(256) void stem_slab_reduce_kernel(const float* slab, int nslab, int n, float* acc) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float v = acc[i];
+  for (int k = 0; k < nslab; ++k) v += slab[(int64_t)k * n + i];
+  acc[i] = v;
 }
 
 // dW (s2d accumulator [Cout][kt][4][4][sy][sx][c4]) -> grad [Cout][3][kt][7][7] ; re-zeroes the accumulator
@@ -792,9 +810,10 @@ static bool stem_async_enabled() {
 // mode 0: forward, 1: wgrad.  Shapes outside stem_s2d_supported() are rejected by the bindings (TORCH_CHECK)
 // before this is reached, so every call launches exactly one kernel.
 void stem_s2d_launch(int mode, const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, const uint16_t* dy,
-                     float* dw, int N, int T, int Hs, int Ws, int Cout, int kt, hipStream_t s) {
+                     float* dw, int N, int T, int Hs, int Ws, int Cout, int kt, hipStream_t s, float* slab) {
   StemParams p{};
-  p.x = x; p.w = w; p.y = y; p.stats = stats; p.dy = dy; p.dw = dw;
+  p.x = x; p.w = w; p.y = y; p.stats = stats; p.dy = dy; p.dw = slab != nullptr ? slab : dw;
+  p.slab = slab != nullptr ? Cout * kt * 256 : 0;
   p.N = N; p.T = T; p.Hs = Hs; p.Ws = Ws; p.Cout = Cout;
   p.To = T; p.Ho = Hs; p.Wo = Ws; p.pt = kt / 2;
   p.tiles_h = (Hs + TH - 1) / TH; p.tiles_w = (Ws + TW - 1) / TW;
@@ -811,6 +830,10 @@ void stem_s2d_launch(int mode, const uint16_t* x, const uint16_t* w, uint16_t* y
     else if (kt == 5 && Cout <= 16) launch_wgrad<5, 1>(p, s);
     else if (kt == 1 && Cout <= 64 && stem_async_enabled()) launch_wgrad<1, 4, true>(p, s);
     else if (kt == 1 && Cout <= 64) launch_wgrad<1, 4>(p, s);
+    if (slab != nullptr) {   // fixed-order sum of the per-workgroup partials into the accumulator
+      const int n = Cout * kt * 256, nslab = p.N * p.tiles_h * p.tiles_w;
+      hipLaunchKernelGGL(stem_slab_reduce_kernel, dim3((n + 255) / 256), dim3(256), 0, s, slab, nslab, n, dw);
+    }
   }
 }
 

@@ -23,6 +23,7 @@ namespace pva_f16 {
 }
 void register_clip_reader(pybind11::module& m);
 void register_rccl(pybind11::module& m);
+void register_fp32(pybind11::module& m);
 
 namespace {
 
@@ -485,17 +486,20 @@ void stem_fwd(const at::Tensor& x, const at::Tensor& wpack, const at::Tensor& y,
   const int N = dims[0], T = dims[1], Hs = dims[2], Ws = dims[3];
   TORCH_CHECK(stats.numel() >= (int64_t)KSEL(h, stem_tiles)(Hs, Ws, N) * 2 * Cout, "stats too small");
   KSEL(h, stem_s2d_launch)(0, bfp(x), bfp(wpack), bfpm(y), f32(stats), nullptr, nullptr, N, T, Hs, Ws, (int)Cout, (int)kt,
-                  cur_stream());
+                  cur_stream(), nullptr);
 }
 
 void stem_wgrad(const at::Tensor& x, const at::Tensor& dy, const at::Tensor& acc, std::vector<int64_t> dims,
-                int64_t Cout, int64_t kt) {
+                int64_t Cout, int64_t kt, const OptT& slab) {
   const bool h = kind16(x);
   TORCH_CHECK(KSEL(h, stem_s2d_supported)((int)Cout, (int)kt), "unsupported stem");
   TORCH_CHECK(acc.numel() >= Cout * kt * 256, "accumulator too small");
   const int N = dims[0], T = dims[1], Hs = dims[2], Ws = dims[3];
+  // slab (reproducible mode): one partial dW per workgroup, summed in a fixed order into acc
+  TORCH_CHECK(!slab.has_value() || slab->numel() >= (int64_t)KSEL(h, stem_tiles)(Hs, Ws, N) * Cout * kt * 256,
+              "stem slab too small");
   KSEL(h, stem_s2d_launch)(1, bfp(x), nullptr, nullptr, nullptr, bfp(dy), f32(acc), N, T, Hs, Ws, (int)Cout, (int)kt,
-                  cur_stream());
+                  cur_stream(), f32o(slab));
 }
 
 // ---- classification head (csrc/kernels/head.hip) ----
@@ -807,7 +811,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("scratch"), py::arg("seed_dev") = py::none());
   m.def("head_dropout_mask", &head_dropout_mask);
   m.def("stem_fwd", &stem_fwd);
-  m.def("stem_wgrad", &stem_wgrad);
+  m.def("stem_wgrad", &stem_wgrad, py::arg("x"), py::arg("dy"), py::arg("acc"), py::arg("dims"), py::arg("Cout"),
+        py::arg("kt"), py::arg("slab") = py::none());
   m.def("stem_wgrad_convert", [](const at::Tensor& acc, const at::Tensor& grad, int64_t Cout, int64_t kt, double beta) {
     pva_bf16::stem_wgrad_convert_launch(f32(acc), f32(grad), (int)Cout, (int)kt, (float)beta, cur_stream());
   });
@@ -817,4 +822,5 @@ PYBIND11_MODULE(_C, m) {
   });
   register_clip_reader(m);
   register_rccl(m);
+  register_fp32(m);
 }

@@ -54,16 +54,36 @@ def _headers_digest(csrc: str = CSRC) -> str:
     return h.hexdigest()
 
 
-# compile flags that change the generated code (include paths excluded: they do not)
-FLAGS_SIG = "-O3 -std=c++17 -ffp-contract=fast PVA_F16=0,1 arch=" + ARCH
 ID_MARK = b"PVA_BUILD_ID:"
 _ID_RE = re.compile(re.escape(ID_MARK) + rb"([0-9a-f]{40})")
+
+
+def _flags():
+    """(common, kernel, binding) compile flags — the one source of truth for ``build()`` and ``tree_id()``."""
+    _, tinc, _, abi = _torch_paths()
+    pyinc = sysconfig.get_paths()["include"]
+    common = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
+              "-Wno-unused-result", "-Wno-unused-variable"]
+    kern = common + ["-ffp-contract=fast"]
+    bind = common + ["-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H", "-DUSE_ROCM=1",
+                     "-D__HIP_PLATFORM_AMD__=1", f"-I{pyinc}"] + [f"-I{p}" for p in tinc]
+    return common, kern, bind
+
+
+def flags_signature() -> str:
+    """Everything that changes the generated code: the real flag lists (include paths dropped — they only say where
+    the same headers live), the per-type builds, the torch version (its headers are compiled into the bindings)."""
+    import torch
+    common, kern, bind = _flags()
+    keep = lambda fl: [f for f in fl if not f.startswith("-I")]   # noqa: E731
+    return "|".join([" ".join(keep(common)), " ".join(keep(kern)), " ".join(keep(bind)), "PVA_F16=0,1;fp32:0",
+                     "torch=" + torch.__version__])
 
 
 def tree_id(csrc: str = CSRC) -> str:
     """Build id of a source tree: sha1 over every csrc source/header (relative path + bytes) and the flags.
     Compiled into the extension (``_C.build_id()``), so a binary can be checked against the tree it ships with."""
-    h = hashlib.sha1(FLAGS_SIG.encode())
+    h = hashlib.sha1(flags_signature().encode())
     files = []
     for ext in ("*.hip", "*.h", "*.cpp"):
         files += glob.glob(os.path.join(csrc, "**", ext), recursive=True)
@@ -75,14 +95,28 @@ def tree_id(csrc: str = CSRC) -> str:
     return h.hexdigest()
 
 
+_EMB_CACHE = {}
+
+
 def embedded_id(so_path: str) -> Optional[str]:
-    """The build id compiled into a built ``_C*.so`` (read from the file, without importing it), or None."""
+    """The build id compiled into a built ``_C*.so`` (read from the file, without importing it), or None.
+    The file is scanned through ``mmap`` (no 40 MB read) and the answer cached per (path, size, mtime)."""
+    import mmap
     try:
-        with open(so_path, "rb") as fh:
-            m = _ID_RE.search(fh.read())
+        st = os.stat(so_path)
     except OSError:
         return None
-    return m.group(1).decode() if m else None
+    key = (os.path.abspath(so_path), st.st_size, st.st_mtime_ns)
+    if key in _EMB_CACHE:
+        return _EMB_CACHE[key]
+    try:
+        with open(so_path, "rb") as fh, mmap.mmap(fh.fileno(), 0, access=mmap.ACCESS_READ) as mm:
+            m = _ID_RE.search(mm)
+            val = m.group(1).decode() if m else None
+    except (OSError, ValueError):
+        return None
+    _EMB_CACHE[key] = val
+    return val
 
 
 def check(so_path: Optional[str] = None, csrc: Optional[str] = None) -> Tuple[bool, Optional[str], Optional[str]]:
@@ -104,54 +138,65 @@ def _compile(src: str, flags: list, hdr: str, force: bool, tag: str = "", build_
     obj = os.path.join(build_dir, os.path.basename(src) + tag + "." + key + ".o")
     if os.path.exists(obj) and not force:
         return obj
-    cmd = [HIPCC] + flags + ["-c", src, "-o", obj + ".tmp"]
+    tmp = f"{obj}.{os.getpid()}.tmp"
+    cmd = [HIPCC] + flags + ["-c", src, "-o", tmp]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
-    os.replace(obj + ".tmp", obj)
+    os.replace(tmp, obj)
     return obj
 
 
 def build(jobs: int = 0, force: bool = False, verbose: bool = False, csrc: str = CSRC, build_dir: str = BUILD,
           out: Optional[str] = None) -> str:
     """Compile (object cache keyed by content) and relink whenever the binary's embedded build id differs from
-    the tree's — never trusts a side file.  ``csrc`` / ``build_dir`` / ``out`` let a test build a copy of the tree."""
+    the tree's — never trusts a side file.  ``csrc`` / ``build_dir`` / ``out`` let a test build a copy of the tree.
+    Serialised across processes by a lock file in ``build_dir`` (every torchrun rank may find a stale binary at
+    once under ``PVA_AUTOBUILD=1``): the first builds, the others then see an up-to-date binary and return."""
+    import fcntl
     os.makedirs(build_dir, exist_ok=True)
-    _, tinc, tlib, abi = _torch_paths()
-    pyinc = sysconfig.get_paths()["include"]
-    common = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
-              "-Wno-unused-result", "-Wno-unused-variable"]
-    kern_flags = common + ["-ffp-contract=fast"]
-    bind_flags = common + ["-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H", "-DUSE_ROCM=1",
-                           "-D__HIP_PLATFORM_AMD__=1", f"-I{pyinc}"] + [f"-I{p}" for p in tinc]
+    with open(os.path.join(build_dir, ".build.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        try:
+            return _build_locked(jobs, force, verbose, csrc, build_dir, out)
+        finally:
+            fcntl.flock(lk, fcntl.LOCK_UN)
+
+
+def _build_locked(jobs, force, verbose, csrc, build_dir, out) -> str:
+    _, _, tlib, _ = _torch_paths()
+    common, kern_flags, bind_flags = _flags()
     out = out or ext_path()
     bid = tree_id(csrc)
     if os.path.exists(out) and not force and embedded_id(out) == bid:
         return out
     hdr = _headers_digest(csrc)
     kernels = sorted(glob.glob(os.path.join(csrc, "kernels", "*.hip")))
+    kernels32 = sorted(glob.glob(os.path.join(csrc, "fp32", "*.hip")))   # fp32 path: one build (bf16x3 MFMA)
     runtime = sorted(glob.glob(os.path.join(csrc, "runtime", "*.cpp")))
     id_src = os.path.join(build_dir, f"build_id.{bid}.cpp")
     if not os.path.exists(id_src):
-        with open(id_src + ".tmp", "w") as fh:
+        with open(f"{id_src}.{os.getpid()}.tmp", "w") as fh:
             fh.write('extern "C" const char pva_build_id_str[] = "%s%s";\n' % (ID_MARK.decode(), bid))
-        os.replace(id_src + ".tmp", id_src)
+        os.replace(f"{id_src}.{os.getpid()}.tmp", id_src)
     jobs = jobs or min(16, os.cpu_count() or 4)
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         futs = [ex.submit(_compile, s, kern_flags + [f"-DPVA_F16={h}"], hdr, force, (".f16" if h else ".bf16"), build_dir)
                 for s in kernels for h in (0, 1)]
+        futs += [ex.submit(_compile, s, kern_flags + ["-DPVA_F16=0"], hdr, force, ".f32", build_dir) for s in kernels32]
         futs += [ex.submit(_compile, s, bind_flags, hdr, force, "", build_dir) for s in runtime]
         futs.append(ex.submit(_compile, id_src, common, "", force, "", build_dir))
         objs = [f.result() for f in futs]
     libs = ["-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
             f"-L{ROCM_LIB}", f"-Wl,-rpath,{ROCM_LIB}", "-lrocprofiler-sdk-roctx",   # ROCTx ranges
             "-ldl"]   # RCCL: bound at run time to torch's copy (csrc/runtime/rccl_comm.cpp)
+    tmp = f"{out}.{os.getpid()}.tmp"
     cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}"] + objs + [f"-L{tlib}", f"-Wl,-rpath,{tlib}"] + libs + [
-        "-o", out + ".tmp"]
+        "-o", tmp]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
-    os.replace(out + ".tmp", out)
+    os.replace(tmp, out)
     if embedded_id(out) != bid:
         raise RuntimeError(f"linked {out} but its embedded build id is not {bid}")
     if verbose:

@@ -1,7 +1,8 @@
 """Clip samplers with pytorchvideo semantics (reference ``run.py:154,163`` → SURVEY.md D16).
 
-* ``RandomClipSampler(d)``: one clip per video per epoch, ``start ~ U(0, max(dur - d, 0))`` drawn with
-  Python ``random`` (as pytorchvideo), ``is_last_clip = True``.
+* ``RandomClipSampler(d, rng=None)``: one clip per video per epoch, ``start ~ U(0, max(dur - d, 0))`` drawn with
+  Python ``random`` (as pytorchvideo) — or with the given ``random.Random`` (the datasets pass a per-item generator,
+  ``kinetics.VideoClipDataset.item_rng``), ``is_last_clip = True``.
 * ``UniformClipSampler(d, stride=d)``: consecutive clips ``[k*stride, k*stride + d)``; a clip is the last
   one when the *next* clip would end past the video (``next_end - dur > eps``), so a 10 s video at
   d = 2.133 s yields 4 clips.
@@ -37,9 +38,13 @@ class ClipSampler:
 
 
 class RandomClipSampler(ClipSampler):
+    def __init__(self, clip_duration, rng: Optional[random.Random] = None):
+        super().__init__(clip_duration)
+        self._rng = rng
+
     def __call__(self, last_clip_end_time, video_duration, annotation=None) -> ClipInfo:
         max_start = max(Fraction(video_duration) - self._clip_duration, 0)
-        start = Fraction(random.uniform(0, float(max_start)))
+        start = Fraction((self._rng or random).uniform(0, float(max_start)))
         return ClipInfo(start, start + self._clip_duration, 0, 0, True)
 
 

@@ -116,6 +116,7 @@ class ClipItem:
     clip_index: int
     clip_start: Optional[Fraction] = None
     clip_end: Optional[Fraction] = None
+    order: int = 0      # position in the epoch plan (keys the item's random draws)
 
 
 class VideoClipDataset(Dataset):
@@ -171,7 +172,7 @@ class VideoClipDataset(Dataset):
             order = list(range(n))
         items: List[ClipItem] = []
         if self.training:
-            items = [ClipItem(v, 0) for v in order]
+            items = [ClipItem(v, 0, order=k) for k, v in enumerate(order)]
         else:
             for v in order:
                 k = UniformClipSampler(self.clip_duration).num_clips(self.duration(v)) if self.full_val else 1
@@ -183,17 +184,29 @@ class VideoClipDataset(Dataset):
         return len(self.items)
 
     # ------------------------------------------------------------------ items
-    def _clip_times(self, it: ClipItem, video: Video):
+    def item_rng(self, it: ClipItem):
+        """(random.Random, torch.Generator) of one training item, seeded by (seed, epoch, rank, plan position, video):
+        the clip start and the scale/crop/flip draws do not depend on global RNG state, so a reader that runs ahead
+        of the training loop (next epoch prefetched before the epoch checkpoint, trainer.py) cannot shift them, and a
+        run resumed from a checkpoint draws exactly what the uninterrupted run drew.  Same distributions as the
+        reference's global-RNG draws (pytorchvideo RandomClipSampler, RandomShortSideScale / RandomCrop / flip)."""
+        key = hash((int(self.seed), int(self.epoch), int(self.rank), int(it.order), int(it.video_index))) & (2 ** 62 - 1)
+        g = torch.Generator()
+        g.manual_seed(key)
+        return random.Random(key), g
+
+    def _clip_times(self, it: ClipItem, video: Video, rng=None):
         if it.clip_start is not None:
             return it.clip_start, it.clip_end
-        info = RandomClipSampler(self.clip_duration)(None, video.duration)
+        info = RandomClipSampler(self.clip_duration, rng)(None, video.duration)
         return info.clip_start_sec, info.clip_end_sec
 
     def __getitem__(self, i: int):
         it = self.items[i]
         path, info = self.videos[it.video_index]
         video = self._open(it.video_index)
-        start, end = self._clip_times(it, video)
+        rng, gen = self.item_rng(it) if self.training else (None, None)
+        start, end = self._clip_times(it, video, rng)
         frame_idx = video.frame_indices(start, end)
         if not frame_idx:
             frame_idx = [max(video.num_frames - 1, 0)]
@@ -205,13 +218,13 @@ class VideoClipDataset(Dataset):
             # only the frames UniformTemporalSubsample keeps are read; tidx is the identity on them
             frames = video.read_frames(src)
             p = sample_params(self.num_frames, video.height, video.width, self.num_frames, self.crop,
-                              self.training, self.min_scale, self.max_scale)
+                              self.training, self.min_scale, self.max_scale, generator=gen)
             sample["frames"] = torch.from_numpy(frames)
             sample["params"] = (p.rh, p.rw, p.top, p.left, int(p.flip))
         else:
             frames = torch.from_numpy(video.read_frames(src))
             p = sample_params(self.num_frames, video.height, video.width, self.num_frames, self.crop,
-                              self.training, self.min_scale, self.max_scale)
+                              self.training, self.min_scale, self.max_scale, generator=gen)
             clip = reference_transform(frames, p, self.crop, self.mean, self.std)  # [3, T, S, S]
             if self.alpha:
                 slow = clip.index_select(1, pack_pathway_indices(self.num_frames, self.alpha))

@@ -61,14 +61,15 @@ class NativeRawSource:
             path, doff, fb, H, W, fps, nf, dur = self._video_meta(it.video_index)
             from .video import frame_range
             from .clip_sampling import RandomClipSampler
+            rng, gen = ds.item_rng(it) if ds.training else (None, None)
             if it.clip_start is None:
-                info = RandomClipSampler(ds.clip_duration)(None, dur)
+                info = RandomClipSampler(ds.clip_duration, rng)(None, dur)
                 a, b = frame_range(info.clip_start_sec, info.clip_end_sec, fps, nf)
             else:
                 a, b = frame_range(it.clip_start, it.clip_end, fps, nf)
             fr = list(range(a, b)) or [max(nf - 1, 0)]
             src = [fr[j] for j in uniform_temporal_indices(len(fr), T).tolist()]
-            p = sample_params(T, H, W, T, ds.crop, ds.training, ds.min_scale, ds.max_scale)
+            p = sample_params(T, H, W, T, ds.crop, ds.training, ds.min_scale, ds.max_scale, generator=gen)
             jobs.append((path, doff, fb, src, off))
             descs.append([off & 0x7FFFFFFF, off >> 31, T, H, W, p.rh, p.rw, p.top, p.left, int(p.flip)])
             labels.append(ds.videos[it.video_index][1]["label"])

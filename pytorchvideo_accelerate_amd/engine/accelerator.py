@@ -64,19 +64,22 @@ class Accelerator:
         #  * bf16 / fp16 on a GPU -> the fused gfx950 kernels in that dtype (bf16 or fp16 MFMA operands and
         #    activations, fp32 accumulation, statistics, master weights and optimizer); fp16 also runs the dynamic
         #    loss-scale state machine of the reference recipe (run_slowfast_r50.sh, GradScaler semantics);
-        #  * "no" (the reference default, fp32 math) on a GPU -> the PyTorch fp32 module path, unless the fused
-        #    kernels are requested explicitly with kernels="fused" (then bf16 compute, said so in compute_dtype);
-        #  * CPU -> the PyTorch path.
+        #  * "no" (the reference default, fp32 math) on a GPU -> the native fp32 kernels (kernels="fp32":
+        #    fp32 activations, bf16x3-MFMA convolutions with fp32 accumulation, fp32 BatchNorm / pooling / head);
+        #  * CPU, or kernels="torch" -> the PyTorch module path (fp32, or autocast for bf16 / fp16).
         if kernels == "auto":
-            if self.device.type == "cuda" and mixed_precision in ("bf16", "fp16"):
-                kernels = "fused"
+            if self.device.type == "cuda":
+                kernels = "fused" if mixed_precision in ("bf16", "fp16") else "fp32"
             else:
                 kernels = "torch"
-                if self.device.type == "cuda" and self.state.is_main_process:
-                    print("note: --mixed_precision no requests fp32 math: running the PyTorch fp32 path; "
-                          "--mixed_precision bf16 (or --kernels fused) selects the fused MI355X kernels", flush=True)
+        if kernels == "fp32" and self.device.type != "cuda":
+            raise ValueError("--kernels fp32 runs the gfx950 fp32 kernels: it needs a GPU")
         if kernels == "fused":
             self.compute_dtype = "fp16" if mixed_precision == "fp16" else "bf16"
+        elif kernels == "fp32":
+            if mixed_precision not in ("no", None):
+                raise ValueError(f"--kernels fp32 is the --mixed_precision no path (got {mixed_precision})")
+            self.compute_dtype = "fp32"
         else:
             self.compute_dtype = {"bf16": "bf16-autocast", "fp16": "fp16-autocast"}.get(mixed_precision, "fp32")
         self.kernels = kernels
@@ -112,9 +115,11 @@ class Accelerator:
 
     # ------------------------------------------------------------------ prepare
     def prepare_model(self, model: torch.nn.Module):
-        from .backends import FusedBackend, TorchBackend
+        from .backends import FusedBackend, NativeF32Backend, TorchBackend
         if self.kernels == "fused":
             be = FusedBackend(model, self.state, self.bucket_mb, mixed_precision=self.mixed_precision)
+        elif self.kernels == "fp32":
+            be = NativeF32Backend(model, self.state, self.bucket_mb)
         else:
             be = TorchBackend(model, self.state, self.mixed_precision, self.bucket_mb)
         # rank-0 parameters + BN buffers everywhere (DDP construction broadcast)

@@ -2,8 +2,10 @@
 
 * :class:`FusedBackend` — the MI355X path: ``models/fused.FusedNet`` (gfx950 kernels, bf16 or fp16) with the
   bucketed RCCL gradient all-reduce of ``parallel/ddp.GradSync`` overlapped with the backward pass.
-* :class:`TorchBackend` — the reference PyTorch modules with autograd: CPU runs (``--cpu``, gloo DDP), fp32
-  (``--mixed_precision no``) or autocast fp16/bf16 on GPU; its bucketed all-reduce overlaps backward through
+* :class:`NativeF32Backend` — the reference default precision (``--mixed_precision no``) on the gfx950 fp32 kernels
+  (``models/native32.NativeF32Net``: bf16x3-MFMA convolutions, fp32 BatchNorm/pool/head), same bucketed all-reduce.
+* :class:`TorchBackend` — the reference PyTorch modules with autograd: CPU runs (``--cpu``, gloo DDP), or
+  autocast fp16/bf16 / fp32 modules on GPU when asked for (``--kernels torch``); its bucketed all-reduce overlaps backward through
   per-parameter gradient hooks, as DDP's reducer does.  Gradients land in the same flat buffer
   (``FlatParams``), so the optimizer, gradient sync and checkpointing code are shared.
 
@@ -116,6 +118,54 @@ class TorchBackend:
 
     def after_optimizer_step(self):
         pass
+
+
+class NativeF32Backend:
+    """fp32 training on the native fp32 kernels (reference run.py:330 default ``mixed_precision="no"``)."""
+    name = "native32"
+
+    def __init__(self, model: torch.nn.Module, state: DistState, bucket_mb: float = 32.0):
+        from ..models.native32 import NativeF32Net
+        self.state = state
+        self.device = state.device
+        self.net = NativeF32Net(model, self.device)
+        self.model = model
+        self.flat = self.net.flat
+        bounds = sorted(set(self.flat.span(p)[1] for p in self.flat.params))
+        self.sync = GradSync(self.flat.grad, state, bucket_mb, boundaries=bounds)
+        self.net.grad_hook = self.sync.progress if state.multi else None
+        # one producing stream: buckets leave from the sync's comm stream after an event on it
+        self.sync.producers = lambda: [torch.cuda.current_stream(self.device)]
+        self.scaler = None
+        self.timer = None
+
+    def train(self):
+        self.model.train()
+
+    def eval(self):
+        self.model.eval()
+
+    def train_step(self, video, labels, loss_scale: float = 1.0, sync: bool = True):
+        t = self.timer
+        with (t.phase("fwd_bwd") if t else contextlib.nullcontext()):
+            self.sync.begin(sync)
+            loss, logits = self.net.forward_backward(video, labels, loss_scale)
+        with (t.phase("comm") if t else contextlib.nullcontext()):
+            self.sync.finish()
+        return loss, logits
+
+    @torch.no_grad()
+    def eval_step(self, video):
+        return self.net.forward_eval(video)
+
+    def eval_counts(self, logits, labels):
+        return self.net.eval_counts(logits, labels)
+
+    def after_optimizer_step(self):
+        pass
+
+    def reload_weights(self):
+        self.flat.rebind()
 
 
 class FusedBackend:

@@ -180,7 +180,7 @@ class _ConvBN:
         from ..ops.conv import RT, box_wgrad_plan, box_wgrad_slabs, wgrad_splits
         aff = 0 if xf is None else (2 if xf.relu else 1)
         sc_, sh_ = (None, None) if xf is None else (xf.scale, xf.shift)
-        slab = 1 if (eng.deterministic or (eng.fold_slabs and dest is not None)) else 0
+        slab = 1 if (eng.deterministic or eng.reproducible or (eng.fold_slabs and dest is not None)) else 0
         dya = 1 if gram else 0
 
         def geometry(cfg):
@@ -301,7 +301,8 @@ class _ConvBN:
         # off the critical path: a weight gradient that lands in the flat buffer runs on the lane's wgrad
         # stream, concurrently with the dgrad chain (its inputs are per-unit buffers nothing rewrites before
         # the end-of-backward join)
-        wst = eng._wgrad_stream() if (dest is None and not gram and not slab and eng._ms_active()) else None
+        wst = eng._wgrad_stream() if (dest is None and not gram and (not slab or eng.reproducible)
+                                      and eng._ms_active()) else None
         if wst is not None:
             src = torch.cuda.current_stream(eng.device)
             ev = torch.cuda.Event()
@@ -314,10 +315,11 @@ class _ConvBN:
                     if cfg >= 0 and cfg & 1024:
                         splits = box_run(cfg, eng.flat.gview(self.conv.weight), eng.grad_beta)
                     else:
-                        part = eng.scratch("wgrad_acc", s.cout * K, zero=True)
+                        part = (eng.scratch("wgrad_slab", geometry(cfg)[0] * s.cout * K) if slab else
+                                eng.scratch("wgrad_acc", s.cout * K, zero=True))
                         splits = launch(cfg, part, colsum)
                         C.wgrad_reduce(part, eng.flat.gview(self.conv.weight), splits, s.cout, s.taps, s.cin_pad,
-                                       s.cin, 1.0, eng.grad_beta, 0)
+                                       s.cin, 1.0, eng.grad_beta, slab)
             finally:
                 eng.lane = lane0
             return splits
@@ -728,7 +730,11 @@ class _Stem:
             x = self.x
             acc = eng.scratch("stem_acc_" + self.name, self.u.C * self.kt * 256, zero=True)
             eng.mark(self.u.name + ".wgrad")
-            C.stem_wgrad(x.t, dy.t, acc, [x.N, x.T, x.H, x.W], self.u.C, self.kt)
+            slab = None
+            if eng.reproducible:   # per-workgroup partials summed in a fixed order instead of fp32 atomics
+                slab = eng.scratch("stem_slab_" + self.name,
+                                   C.stem_tiles(x.H, x.W, x.N) * self.u.C * self.kt * 256)
+            C.stem_wgrad(x.t, dy.t, acc, [x.N, x.T, x.H, x.W], self.u.C, self.kt, slab)
             C.stem_wgrad_convert(acc, eng.flat.gview(self.u.conv.weight), self.u.C, self.kt, eng.grad_beta)
         else:
             self.u.wgrad(dy, self.x, None)
@@ -1155,9 +1161,13 @@ class FusedNet:
     """Executor bound to a reference ``Net`` (SlowFast or Slow ResNet3D) whose parameters it shares."""
 
     def __init__(self, model: R.Net, device: torch.device, stem_s2d: bool = True, deterministic: bool = False,
-                 load_tuning: bool = True, compute_dtype: torch.dtype = torch.bfloat16):
+                 load_tuning: bool = True, compute_dtype: torch.dtype = torch.bfloat16, reproducible: bool = False):
         """``deterministic``: bitwise-reproducible gradients (slab wgrad reduction, generic stems; BN
-        statistics are always reduced in a fixed order).  Costs a little speed.  ``load_tuning``: restore the
+        statistics are always reduced in a fixed order) on one stream with heuristic kernel choices.  Costs a little
+        speed.  ``reproducible``: the production schedule (both pathway streams, the weight-gradient streams, s2d
+        stems, autotuned kernels) with every fp32 atomic replaced by a fixed-order (slab) reduction — once the kernel
+        choices are fixed (tuned on the first step, or loaded from the persistent table) every step is bitwise
+        reproducible, so a race in the stream schedule shows up as a bitwise difference (tests/test_race_gpu.py).  ``load_tuning``: restore the
         persistent autotuner table now (data parallelism restores rank 0's copy instead: ``FusedBackend``).
         ``compute_dtype``: the 16-bit MFMA operand / activation type, bf16 or fp16 (``--mixed_precision fp16``: the
         fp16 build of every kernel, csrc/kernels/common.h; fp32 accumulation, statistics and master weights)."""
@@ -1165,6 +1175,7 @@ class FusedNet:
         self.cdt = compute_dtype
         self.C = require()
         self.deterministic = deterministic
+        self.reproducible = reproducible
         # fixed-order (slab) reduction for the weight-gradient launches whose results feed back into the step —
         # the BN-fold Gram matrices (forward statistics) and G = dz^T act (backward coefficients) — while the
         # leaf weight gradients keep their fp32 atomics: the loss and the dgrad chain are then reproducible
@@ -1175,7 +1186,7 @@ class FusedNet:
         # flips ReLU masks and the random-init network's chaotic backward decorrelates two runs' gradients
         # (cosine ~0.65 at B=4-32: scripts/diag_ms_race.py).  On by default (only the few Gram / G launches pay the
         # slab reduction); PVA_FOLD_SLABS=0 turns it off; implied by ``deterministic``.
-        self.fold_slabs = deterministic or os.environ.get("PVA_FOLD_SLABS", "1") == "1"
+        self.fold_slabs = deterministic or reproducible or os.environ.get("PVA_FOLD_SLABS", "1") == "1"
         # fused lateral-connection backward (apply + strided dgrad in one pass); PVA_LATERAL_BWD=0: the unfused path
         self.lateral_bwd = os.environ.get("PVA_LATERAL_BWD", "1") != "0"
         # two-stream backward: the lateral fusion's backward on the fast-pathway stream (PVA_SIDE_FUSE=0: on the main
@@ -1213,6 +1224,7 @@ class FusedNet:
         self._ms_bwd = False
         self._wst = [None, None]          # weight-gradient streams of the two lanes
         self._wst_used = [False, False]
+        self.debug_skip_joins = set()      # race-detection tests only (see _join)
         self._ms_ok = (not deterministic and torch.device(device).type == "cuda"
                        and os.environ.get("PVA_STREAMS", "1") != "0")
         # BN folding of the 1x1 conv_c (never materialise its output); units whose conv_c input has at least
@@ -1386,7 +1398,11 @@ class FusedNet:
                 self._join(main, st)
                 self._wst_used[i] = False
 
-    def _join(self, waiter, signaller):
+    def _join(self, waiter, signaller, tag: Optional[str] = None):
+        """``waiter`` waits for everything issued so far on ``signaller`` (one event).  ``tag`` names joins that a
+        race-detection test may drop on purpose (``debug_skip_joins``, tests/test_race_gpu.py)."""
+        if tag is not None and tag in self.debug_skip_joins:
+            return
         ev = torch.cuda.Event()
         ev.record(signaller)
         waiter.wait_event(ev)
@@ -1654,7 +1670,8 @@ class FusedNet:
                     self._progress(fuse.flat_hi, force=True)
                     douts[0] = dcat.narrow(0, co)
                 elif ms:
-                    self._join(side, main)   # the head's pooled-gradient scatter (main stream) feeds the fast stage
+                    # the head's pooled-gradient scatter (main stream) feeds the fast stage
+                    self._join(side, main, tag="head_scatter")
                 new = [None] * len(paths)
                 # pathways in reverse order: matches the flat (reverse-execution) gradient layout
                 for p in range(len(paths) - 1, -1, -1):

@@ -96,7 +96,7 @@ class ConvTuner:
         self._pw_seen = 0
         self.log = os.environ.get("PVA_TUNE_LOG", "0") != "0"
         self.reps = int(os.environ.get("PVA_TUNE_REPS", reps))   # timed launches per re-timed contender
-        self.top = int(os.environ.get("PVA_TUNE_TOP", 3))        # contenders re-timed after the single-shot pass
+        self.top = max(1, int(os.environ.get("PVA_TUNE_TOP", 3)))   # contenders re-timed after the single-shot pass
         self.tuned = 0          # geometries timed by this process (conv + weight-gradient tunings)
         self.cache: Dict[Tuple, int] = {}
         self._scratch: Dict[Tuple, torch.Tensor] = {}

@@ -62,7 +62,8 @@ def main(
       synthetic          use a synthetic Kinetics-like corpus instead of --data_dir
       synthetic_videos / synthetic_classes   its size
       synthetic_min_frames  vary synthetic video lengths in [this, 300] frames (default: all 300)
-      kernels            auto | fused | torch  (fused = gfx950 HIP kernels, bf16)
+      kernels            auto | fused | fp32 | torch  (fused = gfx950 HIP kernels in bf16/fp16; fp32 = gfx950 fp32
+                         kernels, the --mixed_precision no default on a GPU; torch = PyTorch modules)
       reference_val      evaluate only one clip per video (reference LimitDataset behaviour)
       pretrained_path    local weights for --pretrained (no network)
     As in the reference, the script flag decides mixed precision (default "no"): the launcher's

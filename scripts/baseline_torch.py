@@ -44,13 +44,12 @@ def main():
     if a.channels_last:
         fast = fast.contiguous(memory_format=torch.channels_last_3d)
         slow = slow.contiguous(memory_format=torch.channels_last_3d)
-    x = [slow] if a.slow else [slow, fast]
-    x = x[0] if a.slow else x
+    x = fast if a.slow else [slow, fast]  # Slow-R50 takes the T-frame clip itself
     y = torch.randint(0, a.classes, (B,), device=dev)
-    dt = torch.bfloat16 if a.dtype == "bf16" else torch.float16
+    dt = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": None}[a.dtype]
 
     def step():
-        with torch.autocast("cuda", dtype=dt):
+        with torch.autocast("cuda", dtype=dt or torch.bfloat16, enabled=dt is not None):
             out = model(x)
         loss = F.cross_entropy(out.float(), y)
         loss.backward()
@@ -73,7 +72,7 @@ def main():
     times.sort()
     p50 = times[len(times) // 2]
     mean = sum(times) / len(times)
-    print(json.dumps({"impl": "stock_torch", "channels_last": a.channels_last, "batch": B, "frames": T, "crop": S,
+    print(json.dumps({"impl": "stock_torch", "dtype": a.dtype, "slow": a.slow, "channels_last": a.channels_last, "batch": B, "frames": T, "crop": S,
                       "p50_ms": p50, "mean_ms": mean, "p90_ms": times[int(len(times) * 0.9) - 1],
                       "clips_per_s": B * 1000.0 / mean, "loss": float(l)}))
 

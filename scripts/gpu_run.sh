@@ -14,6 +14,8 @@
 #   cfg      non-headline configs: bench + serialised per-op profile + roofline for R101 32x2x256 (B=160) and
 #            R50 64x2x224 (B=112)
 #   runpy    the reference CLI (run.py) at the headline shape on a synthetic corpus
+#   benches  bench.py once per ";"-separated $BENCHES argument set
+#   stock    stock PyTorch eager baselines (scripts/baseline_torch.py) for each ";"-separated $STOCK argument set
 #   lab      tools/gemm_lab.hip: big-tile GEMM main loop at $LAB_SHAPES ("M,N,K ..."), cold and L2-hot A operand,
 #            plus one PMC pass per shape (MFMA busy, waits, L2 hits)
 set -o pipefail
@@ -98,6 +100,26 @@ t_runpy() {
   grep -i "clips/s" $out/run_py_${PRECISION:-bf16}.log | tail -4
 }
 
+t_benches() {
+  # bench.py once per ";"-separated argument set in $BENCHES (non-headline models / precisions)
+  local i=0
+  IFS=';' read -ra arms <<< "$BENCHES"
+  for arm in "${arms[@]}"; do
+    i=$((i+1))
+    PVA_TUNE_LOG=1 timeout -k 10 500 python bench.py $arm > $out/benches$i.json 2> $out/benches$i.err || fail $out/benches$i.err
+    echo "$arm: $(cat $out/benches$i.json)"
+  done
+}
+t_stock() {
+  # stock PyTorch-ROCm eager baselines (scripts/baseline_torch.py), one run per ";"-separated argument set
+  local i=0
+  IFS=';' read -ra arms <<< "${STOCK:---dtype bf16 --batch 32}"
+  for arm in "${arms[@]}"; do
+    i=$((i+1))
+    timeout -k 10 300 python -u scripts/baseline_torch.py --steps ${STEPS:-8} --warmup 3 $arm >> $out/stock.jsonl 2> $out/stock$i.err || fail $out/stock$i.err
+  done
+  cat $out/stock.jsonl
+}
 t_lab() {
   /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -ffp-contract=fast -I csrc/kernels tools/gemm_lab.hip -o /tmp/gemm_lab > $out/lab_build.log 2>&1 || fail $out/lab_build.log
   local sh shapes

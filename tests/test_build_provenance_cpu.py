@@ -76,3 +76,33 @@ def test_build_relinks_after_kernel_edit(tmp_path):
     _build.build(csrc=csrc, build_dir=str(bdir), out=out)
     assert _build.embedded_id(out) == _build.tree_id(csrc)
     assert os.stat(out).st_mtime_ns != m0
+
+
+def test_tree_id_covers_real_flags_and_torch_version(monkeypatch):
+    """Advisor r5: the build id hashes the flag lists build() actually uses and the torch version, so a changed
+    compile flag or a torch upgrade makes the shipped binary stale (no hand-written flags string)."""
+    from pytorchvideo_accelerate_amd import _build
+    import torch
+    base = _build.tree_id()
+    orig = _build._flags
+
+    def more_flags():
+        c, k, b = orig()
+        return c, k + ["-mcumode"], b
+    monkeypatch.setattr(_build, "_flags", more_flags)
+    assert _build.tree_id() != base
+    monkeypatch.setattr(_build, "_flags", orig)
+    monkeypatch.setattr(torch, "__version__", torch.__version__ + "+other")
+    assert _build.tree_id() != base
+    monkeypatch.undo()
+    assert _build.tree_id() == base
+
+
+def test_embedded_id_is_cached_and_mmap_scanned(tmp_path):
+    from pytorchvideo_accelerate_amd import _build
+    p = tmp_path / "x.so"
+    p.write_bytes(b"\0" * 1000 + _build.ID_MARK + b"a" * 40 + b"\0" * 10)
+    assert _build.embedded_id(str(p)) == "a" * 40
+    assert any(k[0] == str(p) for k in _build._EMB_CACHE)
+    p.write_bytes(b"\0" * 5000)   # new size -> new cache key -> rescanned
+    assert _build.embedded_id(str(p)) is None

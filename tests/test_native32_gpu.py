@@ -1,0 +1,290 @@
+"""fp32 path (csrc/fp32, models/native32.py) against plain PyTorch fp32/fp64 references.
+
+* every convolution geometry family of SlowFast / Slow-R50 (stems with RGB padded to 4 channels, temporal conv_a,
+  strided and stride-1 conv_b, strided 1x1 branch1, lateral (7,1,1)/(4,1,1), fast stem (5,7,7)): forward, stride-phase
+  input gradient (plain and accumulating) and weight gradient vs an fp64 CPU oracle — bf16x3 must give ~1e-5;
+* BatchNorm train forward (statistics, running-stat update) + backward, max pool and stride-1 average pool;
+* whole networks (SlowFast-R50 and Slow-R50 at small shapes): one training step (loss, logits, every parameter
+  gradient, BN running statistics) and an eval forward vs the PyTorch fp32 module path — median per-parameter
+  relative L2 <= 1e-3 (verdict round 5, item 3) and every parameter <= 1e-2.
+"""
+import pytest
+import torch
+import torch.nn.functional as Fnn
+
+from pytorchvideo_accelerate_amd.ops._ext import require
+from pytorchvideo_accelerate_amd.ops.f32 import ConvGeom, conv_dgrad, conv_fwd, conv_wgrad
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+# (cin, cout, k, s, p, N, T, H, W)
+CONVS = [
+    (3, 64, (1, 7, 7), (1, 2, 2), (0, 3, 3), 2, 2, 32, 32),     # slow stem (RGB padded to 4)
+    (3, 8, (5, 7, 7), (1, 2, 2), (2, 3, 3), 1, 6, 24, 24),      # fast stem
+    (64, 64, (1, 1, 1), (1, 1, 1), (0, 0, 0), 2, 2, 14, 14),    # 1x1
+    (80, 64, (3, 1, 1), (1, 1, 1), (1, 0, 0), 2, 4, 14, 14),    # temporal conv_a on a lateral concat (80 ch)
+    (64, 64, (1, 3, 3), (1, 1, 1), (0, 1, 1), 2, 2, 14, 14),    # conv_b
+    (128, 128, (1, 3, 3), (1, 2, 2), (0, 1, 1), 1, 2, 14, 14),  # strided conv_b (4 phases)
+    (256, 512, (1, 1, 1), (1, 2, 2), (0, 0, 0), 1, 2, 14, 14),  # strided branch1 (3 empty phases)
+    (8, 16, (7, 1, 1), (4, 1, 1), (3, 0, 0), 2, 16, 8, 8),      # lateral fast->slow
+    (8, 8, (3, 1, 1), (1, 1, 1), (1, 0, 0), 2, 8, 12, 12),      # narrow fast conv_a
+    (2048, 256, (1, 1, 1), (1, 1, 1), (0, 0, 0), 1, 1, 7, 7),   # wide K, partial M tile
+    (32, 2048, (1, 1, 1), (1, 1, 1), (0, 0, 0), 1, 2, 7, 7),    # wide N
+]
+
+
+def _rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def _ndhwc(x, cp=None):
+    x = x.permute(0, 2, 3, 4, 1)
+    if cp and cp > x.shape[-1]:
+        x = torch.cat([x, torch.zeros(*x.shape[:-1], cp - x.shape[-1], dtype=x.dtype)], -1)
+    return x.contiguous()
+
+
+@pytest.mark.parametrize("case", CONVS)
+def test_conv32_fwd_dgrad_wgrad(case):
+    cin, cout, k, s, p, N, T, H, W = case
+    F = require().f32
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(N, cin, T, H, W, generator=g, dtype=torch.float64)
+    w = torch.randn(cout, cin, *k, generator=g, dtype=torch.float64) / (cin * k[0] * k[1] * k[2]) ** 0.5
+    x.requires_grad_(True)
+    w.requires_grad_(True)
+    y = Fnn.conv3d(x, w, None, s, p)
+    dy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    y.backward(dy)
+    geo = ConvGeom(cin, cout, k, s, p, cip=(cin + 3) // 4 * 4)
+    xd = _ndhwc(x.detach(), geo.cip).float().to(DEV)
+    wd = w.detach().float().to(DEV).contiguous()
+    wf = torch.empty(cout, geo.ntap * geo.cip, device=DEV)
+    F.wpack32(0, wd, wf, cout, cin, geo.ntap, geo.cip, 0.0)
+    yd = torch.empty(N, *y.shape[2:], cout, device=DEV)
+    conv_fwd(F, geo, xd, wf, yd, geo.taps_fwd(DEV))
+    assert _rel(yd, _ndhwc(y.detach())) < 3e-5
+    dyd = _ndhwc(dy).float().to(DEV)
+    # weight gradient
+    dwf = torch.empty(cout, geo.ntap * geo.cip, device=DEV)
+    F.zero32(dwf)
+    conv_wgrad(F, geo, dyd, xd, dwf, geo.taps_fwd(DEV))
+    dw = torch.full_like(wd, 7.0)
+    F.wpack32(2, dwf, dw, cout, cin, geo.ntap, geo.cip, 0.0)
+    assert _rel(dw, w.grad) < 3e-5
+    # accumulate form (beta = 1)
+    dw2 = dw.clone()
+    F.wpack32(2, dwf, dw2, cout, cin, geo.ntap, geo.cip, 1.0)
+    assert _rel(dw2, 2 * w.grad) < 3e-5
+    if cin % 4:
+        return
+    wt = torch.empty(cin, geo.ntap, cout, device=DEV)
+    F.wpack32(1, wd, wt, cout, cin, geo.ntap, geo.cip, 0.0)
+    dx = torch.full((N, T, H, W, cin), float("nan"), device=DEV)   # every position must be written
+    conv_dgrad(F, geo, dyd, wt, dx, geo.phases(DEV))
+    assert torch.isfinite(dx).all()
+    assert _rel(dx, _ndhwc(x.grad)) < 3e-5
+
+
+def test_dgrad_accumulate_phases():
+    """The executor's accumulating input gradient (residual / lateral sums) on a strided conv."""
+    from pytorchvideo_accelerate_amd.models.native32 import _ConvBN
+    F = require().f32
+    torch.manual_seed(0)
+    conv = torch.nn.Conv3d(64, 128, (1, 3, 3), (1, 2, 2), (0, 1, 1), bias=False).to(DEV)
+    bn = torch.nn.BatchNorm3d(128).to(DEV)
+
+    class _N:
+        device = torch.device(DEV)
+    n = _N()
+    n.F = F
+    cb = _ConvBN(n, conv, bn, True)
+    dy = torch.randn(2, 2, 7, 7, 128, device=DEV)
+    wt = torch.empty(64, 9, 128, device=DEV)
+    F.wpack32(1, conv.weight.detach(), wt, 128, 64, 9, 64, 0.0)
+    base = torch.randn(2, 2, 14, 14, 64, device=DEV)
+    acc = base.clone()
+    cb._dgrad(dy, wt, acc, True)
+    ref = torch.nn.grad.conv3d_input((2, 64, 2, 14, 14), conv.weight.detach().double(),
+                                     dy.permute(0, 4, 1, 2, 3).double(), (1, 2, 2), (0, 1, 1))
+    assert _rel(acc - base, _ndhwc(ref)) < 3e-5
+
+
+@pytest.mark.parametrize("C,M,relu,add", [(64, 3000, True, False), (8, 50000, True, True), (2048, 98, False, True),
+                                          (80, 1000, True, False)])
+def test_bn32_train_forward_backward(C, M, relu, add):
+    F = require().f32
+    torch.manual_seed(1)
+    y = (torch.randn(M, C, dtype=torch.float64) * 3 + 1.5)
+    gamma = torch.rand(C, dtype=torch.float64) + 0.5
+    beta = torch.randn(C, dtype=torch.float64)
+    a = torch.randn(M, C, dtype=torch.float64) if add else None
+    yr = y.clone().requires_grad_(True)
+    gr = gamma.clone().requires_grad_(True)
+    br = beta.clone().requires_grad_(True)
+    ar = a.clone().requires_grad_(True) if add else None
+    mean = yr.mean(0)
+    var = yr.var(0, unbiased=False)
+    o = (yr - mean) / torch.sqrt(var + 1e-5) * gr + br
+    if add:
+        o = o + ar
+    if relu:
+        o = torch.relu(o)
+    dout = torch.randn(M, C, dtype=torch.float64)
+    o.backward(dout)
+    yd, gd, bd = y.float().to(DEV), gamma.float().to(DEV), beta.float().to(DEV)
+    rm = torch.zeros(C, device=DEV)
+    rv = torch.ones(C, device=DEV)
+    nbt = torch.zeros((), dtype=torch.long, device=DEV)
+    part = torch.empty(F.chan_reduce32_blocks(M, C), 2, C, device=DEV)
+    F.chan_reduce32(yd, C, None, C, None, C, None, 0, 0, M, C, part)
+    stat = torch.empty(4, C, device=DEV)
+    F.bn32_finalize(part, C, M, 0, gd, bd, rm, rv, nbt, 0.1, 1e-5, stat, None, None, None, None, 0.0)
+    out = torch.empty(M, C, device=DEV)
+    ad = a.float().to(DEV) if add else None
+    F.bn32_apply(yd, C, stat, ad, C, int(relu), out, C, M, C)
+    assert _rel(out, o.detach()) < 1e-5
+    assert _rel(rm, 0.1 * y.mean(0)) < 1e-5
+    assert _rel(rv, 0.9 + 0.1 * y.var(0, unbiased=True)) < 1e-5
+    assert int(nbt) == 1
+    dd = dout.float().to(DEV)
+    part2 = torch.empty_like(part)
+    F.chan_reduce32(yd, C, dd, C, out if relu else None, C, stat[0], 1, int(relu), M, C, part2)
+    coef = torch.empty(3, C, device=DEV)
+    dg = torch.full((C,), 100.0, device=DEV)
+    db = torch.full((C,), 100.0, device=DEV)
+    F.bn32_finalize(part2, C, M, 1, gd, bd, None, None, None, 0.0, 1e-5, None, stat, dg, db, coef, 1.0)
+    dyd = torch.empty(M, C, device=DEV)
+    gout = torch.empty(M, C, device=DEV)
+    F.bn32_bwd_apply(dd, C, out if relu else None, C, int(relu), yd, C, stat, coef, dyd, C, gout, C, M, C)
+    assert _rel(dyd, yr.grad) < 1e-4
+    assert _rel(dg - 100.0, gr.grad) < 1e-4
+    assert _rel(db - 100.0, br.grad) < 1e-4
+    if add:
+        assert _rel(gout, ar.grad) < 1e-6
+
+
+def test_maxpool32_and_avgpool32():
+    F = require().f32
+    torch.manual_seed(2)
+    N, C, T, H, W = 2, 8, 3, 17, 16
+    x = torch.randn(N, C, T, H, W, dtype=torch.float64, requires_grad=True)
+    y = Fnn.max_pool3d(x, (1, 3, 3), (1, 2, 2), (0, 1, 1))
+    dy = torch.randn(y.shape, dtype=torch.float64)
+    y.backward(dy)
+    To, Ho, Wo = y.shape[2:]
+    xd = _ndhwc(x.detach()).float().to(DEV)
+    out = torch.empty(N, To, Ho, Wo, C, device=DEV)
+    arg = torch.empty(N, To, Ho, Wo, C, device=DEV, dtype=torch.uint8)
+    F.maxpool32(0, xd, out, arg, [N, T, H, W, To, Ho, Wo, C], [1, 3, 3], [1, 2, 2], [0, 1, 1])
+    assert _rel(out, _ndhwc(y.detach())) < 1e-7
+    dx = torch.empty_like(xd)
+    F.maxpool32(1, _ndhwc(dy).float().to(DEV), dx, arg, [N, T, H, W, To, Ho, Wo, C], [1, 3, 3], [1, 2, 2], [0, 1, 1])
+    assert _rel(dx, _ndhwc(x.grad)) < 1e-6
+    # stride-1 average pool into a channel slice of the head features, and its backward
+    x2 = torch.randn(N, C, 4, 8, 8, dtype=torch.float64, requires_grad=True)
+    k = (4, 7, 7)
+    p2 = Fnn.avg_pool3d(x2, k, 1)                     # [N, C, 1, 2, 2]
+    P = p2.shape[2] * p2.shape[3] * p2.shape[4]
+    dp = torch.randn(p2.shape, dtype=torch.float64)
+    p2.backward(dp)
+    Ct, coff = C + 4, 4
+    feat = torch.zeros(N, P, Ct, device=DEV)
+    F.avgpool32(0, _ndhwc(x2.detach()).float().to(DEV), feat, [N, 4, 8, 8, C], list(k), Ct, coff)
+    ref = p2.detach().reshape(N, C, P).transpose(1, 2)
+    assert _rel(feat[..., coff:], ref) < 1e-6
+    dfeat = torch.zeros(N, P, Ct, device=DEV)
+    dfeat[..., coff:] = dp.reshape(N, C, P).transpose(1, 2).float().to(DEV)
+    dx2 = torch.empty(N, 4, 8, 8, C, device=DEV)
+    F.avgpool32(1, dfeat, dx2, [N, 4, 8, 8, C], list(k), Ct, coff)
+    assert _rel(dx2, _ndhwc(x2.grad)) < 1e-6
+
+
+def _prel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def _net_case(slowfast: bool):
+    from pytorchvideo_accelerate_amd.models import reference as R
+    torch.manual_seed(5)
+    if slowfast:
+        T, S = 16, 64
+        model = R.create_slowfast(50, 11, head_pool_kernel_sizes=((T // 4, 2, 2), (T, 2, 2)), dropout_rate=0.0)
+        fast = torch.randn(2, 3, T, S, S)
+        xs = [fast[:, :, ::4].contiguous(), fast]
+    else:
+        T, S = 8, 64
+        model = R.create_resnet(50, 11, head_pool_kernel_size=(T, 2, 2), dropout_rate=0.0)
+        xs = torch.randn(2, 3, T, S, S)
+    labels = torch.tensor([3, 7])
+    return model, xs, labels
+
+
+@pytest.mark.parametrize("slowfast", [True, False], ids=["slowfast_r50", "slow_r50"])
+def test_native32_net_matches_torch_fp32(slowfast):
+    """One training step against an fp64 oracle (the same module tree in float64 on the CPU).  The stock PyTorch fp32
+    GPU step (MIOpen) is measured against the same oracle as the fp32 noise floor: a 50-layer train-mode BN network at
+    B=2 amplifies per-op rounding, so agreement is judged relative to that floor."""
+    import copy
+    from pytorchvideo_accelerate_amd.models.native32 import NativeF32Net
+    model, xs, labels = _net_case(slowfast)
+    ref64 = copy.deepcopy(model).double().train()
+    x64 = [x.double() for x in xs] if isinstance(xs, list) else xs.double()
+    out64 = ref64(x64)
+    loss64 = Fnn.cross_entropy(out64, labels)
+    loss64.backward()
+    ref32 = copy.deepcopy(model).to(DEV).train()
+    xin = [x.to(DEV) for x in xs] if isinstance(xs, list) else xs.to(DEV)
+    out32 = ref32(xin)
+    Fnn.cross_entropy(out32, labels.to(DEV)).backward()
+    net = NativeF32Net(model, DEV)
+    net.model.train()
+    loss, logits = net.forward_backward(xs, labels, 1.0)
+    torch.cuda.synchronize()
+    g64 = dict(ref64.named_parameters())
+    g32 = dict(ref32.named_parameters())
+    ours, stock = {}, {}
+    for n, p in model.named_parameters():
+        ours[n] = _prel(net.flat.gview(p), g64[n].grad)
+        stock[n] = _prel(g32[n].grad, g64[n].grad)
+    med = lambda d: sorted(d.values())[len(d) // 2]   # noqa: E731
+    worst = max(ours, key=ours.get)
+    for n in list(ours)[:6] + [worst]:
+        print(f"  {n}: ours {ours[n]:.2e} stock {stock[n]:.2e}")
+    print(f"\nlogits rel: ours {_prel(logits, out64):.2e} stock-fp32 {_prel(out32, out64):.2e}; loss {loss.item():.6f} "
+          f"vs {loss64.item():.6f}; grad rel-L2 median ours {med(ours):.2e} stock {med(stock):.2e}; worst ours "
+          f"{ours[worst]:.2e} ({worst}) stock {max(stock.values()):.2e}")
+    assert abs(loss.item() - loss64.item()) < 1e-4 * max(1.0, abs(loss64.item()))
+    assert _prel(logits, out64) < max(1e-4, 4 * _prel(out32, out64))
+    assert med(ours) < 1e-3
+    assert ours[worst] < max(1e-2, 4 * max(stock.values())), (worst, ours[worst])
+    for (n, b), (_, b64) in zip(model.named_buffers(), ref64.named_buffers()):
+        if b.dtype.is_floating_point:
+            assert _prel(b, b64) < 1e-4, n
+        else:
+            assert int(b) == int(b64), n
+    # eval forward (running statistics) matches the module path too
+    ref64.eval()
+    net.model.eval()
+    with torch.no_grad():
+        e64 = ref64(x64)
+    e = net.forward_eval(xs)
+    assert _prel(e, e64) < 1e-4
+
+
+def test_native32_grad_accumulates_and_progress_hook():
+    """Second micro-step adds into the flat gradient; the progress hook sees monotone offsets ending at the end."""
+    from pytorchvideo_accelerate_amd.models.native32 import NativeF32Net
+    model, xs, labels = _net_case(False)
+    net = NativeF32Net(model, DEV)
+    seen = []
+    net.grad_hook = seen.append
+    net.forward_backward(xs, labels, 1.0, accumulate=False)
+    g1 = net.flat.grad.clone()
+    assert seen == sorted(seen) and seen[-1] == net.flat.span(net.flat.params[-1])[1]
+    # BN running statistics moved: undo by re-running at the same weights gives the same gradients (batch stats)
+    net.forward_backward(xs, labels, 1.0, accumulate=True)
+    assert _prel(net.flat.grad, 2 * g1) < 1e-5

@@ -83,11 +83,11 @@ def test_run_py_fused_gpu(tmp_path):
     assert h2["global_step"] == 6
 
 
-@pytest.mark.parametrize("mp,kernels", [("fp16", "auto"), ("no", "fused"), ("no", "auto")])
+@pytest.mark.parametrize("mp,kernels", [("fp16", "auto"), ("no", "fused"), ("no", "auto"), ("no", "torch")])
 def test_run_py_precision_policy(tmp_path, mp, kernels):
     """fp16 = the fp16 fused kernels + dynamic loss scaling (scaler.pt saved/restored); "no" (the reference default, fp32
-    math) runs the PyTorch fp32 path unless the fused kernels are asked for explicitly — and the precision that
-    ran is recorded (history / tracker config ``compute_dtype``)."""
+    math) runs the native fp32 kernels (models/native32.py) unless the fused bf16 kernels or the PyTorch modules are
+    asked for explicitly — and the precision that ran is recorded (history / tracker config ``compute_dtype``)."""
     import run
     kw = dict(synthetic=True, synthetic_videos=8, synthetic_classes=4, is_slowfast=True, num_frames=8, crop_size=64,
               batch_size=4, num_workers=0, limit_val_batches=0, mixed_precision=mp, checkpointing_steps="epoch",
@@ -95,7 +95,8 @@ def test_run_py_precision_policy(tmp_path, mp, kernels):
               logging_dir=str(tmp_path / "l"), kernels=kernels)
     h = run.main(num_epochs=1, **kw)
     fused = mp == "fp16" or kernels == "fused"
-    assert h["global_step"] == 2 and h["backend"] == ("fused" if fused else "torch")
+    assert h["global_step"] == 2
+    assert h["backend"] == ("fused" if fused else "torch" if kernels == "torch" else "native32")
     assert h["compute_dtype"] == {"fp16": "fp16", "no": "bf16" if fused else "fp32"}[mp]
     assert (tmp_path / "o" / "epoch_0" / "scaler.pt").exists() == (mp == "fp16")
     if mp == "fp16":
