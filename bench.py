@@ -45,7 +45,7 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=int(os.environ.get("PVA_BENCH_BATCH", 0)),
+    ap.add_argument("--batch", type=int, default=0,
                     help="per-GPU clips per step (default 160; 32 for --precision fp32)")
     ap.add_argument("--model", choices=("slowfast", "slow_r50"), default="slowfast",
                     help="slowfast: SlowFast-R{--depth} (headline); slow_r50: Slow-only R50 (the reference run.py default "
@@ -69,7 +69,7 @@ def parse(argv=None):
     ap.add_argument("--lr", type=float, default=0.1)
     ap.add_argument("--grad-accum", type=int, default=1,
                     help="micro-batches of --batch clips per optimizer step (gradients all-reduced once, on the last)")
-    ap.add_argument("--graph", type=int, default=int(os.environ.get("PVA_BENCH_GRAPH", "0")),
+    ap.add_argument("--graph", type=int, default=0,
                     help="1: replay each micro-step (+ SGD) as a captured HIP graph (single process; engine/graph.py)")
     ap.add_argument("--plumbing", action="store_true", help="CPU/gloo rehearsal on the PyTorch modules")
     ap.add_argument("--dump", default=None,
@@ -82,7 +82,7 @@ def parse(argv=None):
                     help="synthetic: decoded uint8 clips resident on the device (preprocessing only); host: a raw-frame "
                          ".npy corpus read by the native C++ reader into pinned memory, H2D on a copy stream, then "
                          "the same on-device preprocessing (the reference's DataLoader + H2D path, run.py:170-183,243)")
-    ap.add_argument("--corpus", default=os.environ.get("PVA_BENCH_CORPUS", "/tmp/pva_bench_corpus"),
+    ap.add_argument("--corpus", default="/tmp/pva_bench_corpus",
                     help="--source host: corpus directory (generated on first use)")
     ap.add_argument("--corpus-videos", type=int, default=96)
     ap.add_argument("--reader-threads", type=int, default=16)

@@ -17,6 +17,8 @@
 //     transpose read ds_read_b64_tr_b16 (positions are the reduction axis), each wave keeps a slice of
 //     the taps in accumulators across all frames, and adds it to the fp32 dW accumulator once.
 #include "common.h"
+#include <stdlib.h>
+#include <string.h>
 #include <cstdlib>
 
 PVA_NS_BEGIN
@@ -516,10 +518,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void s
 // ROLL (default): wave w owns spatial tap column bw = w and walks the four tap rows bh in registers.  The B fragment of
 // (kstep k, bh + 2) is the one of (k + 1, bh) (two output rows per kstep), so each kstep reads two new input fragments
 // instead of four and a window frame's 16 MFMAs cost 5 fragment reads instead of 16; the dY fragments of the four
-// ksteps are read once per frame pair.  Without it (PVA_STEM_ROLL=0) wave w owns tap row bh = w and reads every
+// ksteps are read once per frame pair.  Without it (arm stem_roll=0) wave w owns tap row bh = w and reads every
 // fragment per MFMA: 2 transpose reads per MFMA make the kernel LDS-bound (35.7 % MFMA busy, profiles/r5_final).
 // AR (with ROLL, default): every transpose read through trr_nw, software-pipelined — the fragments of k-step k + 1 are
-// requested before the MFMAs of k-step k — so the next pair's DMAs overlap this pair's MFMAs (PVA_STEM_ASYNC=0: the
+// requested before the MFMAs of k-step k — so the next pair's DMAs overlap this pair's MFMAs (arm stem_async=0: the
 // intrinsic reads and the vmcnt(0) the compiler puts in front of them).
 template <int KT, bool ROLL, bool AR = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void stem_wgrad_pair_kernel(const StemParams p) {
@@ -782,30 +784,26 @@ void launch_wgrad_pair(const StemParams& p, hipStream_t s) {
 
 int stem_tiles(int Ho, int Wo, int N) { return N * ((Ho + TH - 1) / TH) * ((Wo + TW - 1) / TW); }
 
-// frame-pair kernels for Cout == 8 temporal stems; PVA_STEM_PAIR=0 selects the one-frame kernels (A/B, tests)
-// (read per launch — two launches per step — so tests can switch kernels within one process)
-static bool stem_pair_enabled() {
-  const char* e = getenv("PVA_STEM_PAIR");
-  return !(e && e[0] == '0');
+// Alternate arms of the stem A/Bs (pytorchvideo_accelerate_amd/utils/arms.py, one knob: PVA_ARMS="stem_pair=0,...").
+// Read per launch (two launches per step) so tests can switch kernels within one process.
+//   stem_pair  frame-pair kernels for Cout == 8 temporal stems (0: the one-frame kernels)
+//   stem_perm  channel-permuted 16-B stores of the Cout-64 stem forward (0: the 8-B-store epilogue)
+//   stem_roll  frame-pair wgrad with B fragments rolled across k-steps (0: one tap row per wave)
+//   stem_async rolling wgrad with asm transpose reads + explicit lgkmcnt (0: the intrinsic reads)
+static int stem_arm(const char* name) {
+  const char* e = getenv("PVA_ARMS");
+  if (e == nullptr) return 1;
+  const size_t n = strlen(name);
+  for (const char* p = strstr(e, name); p != nullptr; p = strstr(p + 1, name)) {
+    const bool start = p == e || p[-1] == ',' || p[-1] == ' ';
+    if (start && p[n] == '=') return atoi(p + n + 1);
+  }
+  return 1;
 }
-
-// PVA_STEM_PERM=0: the 8-B-store epilogue of the Cout-64 stem forward (A/B, tests)
-static bool stem_perm_enabled() {
-  const char* e = getenv("PVA_STEM_PERM");
-  return !(e && e[0] == '0');
-}
-
-// PVA_STEM_ROLL=0: the frame-pair wgrad with one tap row per wave (every B fragment read per MFMA; A/B, tests)
-static bool stem_roll_enabled() {
-  const char* e = getenv("PVA_STEM_ROLL");
-  return !(e && e[0] == '0');
-}
-
-// PVA_STEM_ASYNC=0: the rolling frame-pair wgrad with intrinsic transpose reads (A/B, tests)
-static bool stem_async_enabled() {
-  const char* e = getenv("PVA_STEM_ASYNC");
-  return !(e && e[0] == '0');
-}
+static bool stem_pair_enabled() { return stem_arm("stem_pair") != 0; }
+static bool stem_perm_enabled() { return stem_arm("stem_perm") != 0; }
+static bool stem_roll_enabled() { return stem_arm("stem_roll") != 0; }
+static bool stem_async_enabled() { return stem_arm("stem_async") != 0; }
 
 // mode 0: forward, 1: wgrad.  Shapes outside stem_s2d_supported() are rejected by the bindings (TORCH_CHECK)
 // before this is reached, so every call launches exactly one kernel.

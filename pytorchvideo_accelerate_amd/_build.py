@@ -28,7 +28,7 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(PKG_DIR)
 CSRC = os.path.join(REPO, "csrc")
 BUILD = os.path.join(REPO, "build", "obj")
-ARCH = os.environ.get("PVA_OFFLOAD_ARCH", "gfx950")
+ARCH = "gfx950"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ROCM_LIB = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "lib")
 

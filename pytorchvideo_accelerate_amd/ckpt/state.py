@@ -19,7 +19,7 @@ Saves are atomic: the main process writes the shared files into ``<dir>.tmp``, f
 directory into place (``os.replace``); after a barrier every rank writes its RNG file (temp file + rename), and
 after a second barrier the main process writes the completion marker.  ``latest_checkpoint`` (auto-resume after an
 elastic restart) only considers directories with that marker, so a crash in the middle of a save resumes from the
-previous complete checkpoint instead of failing on a half-written one (``PVA_FAULT_IN_SAVE=N`` injects such a crash
+previous complete checkpoint instead of failing on a half-written one (``PVA_FAULT=save=N`` injects such a crash
 into the save of global step N: ``tests/test_checkpoint.py``).
 
 Only the main process writes shared files; everything it reads back goes through ``weights_only=True``
@@ -46,7 +46,7 @@ COMPLETE_FILE = ".pva_complete"
 
 
 class InjectedSaveFault(RuntimeError):
-    """Raised by ``PVA_FAULT_IN_SAVE`` (crash in the middle of a checkpoint save; test hook)."""
+    """Raised by ``PVA_FAULT=save=N`` (crash in the middle of a checkpoint save; test hook)."""
 
 
 def _fsync_path(path: str):
@@ -65,8 +65,9 @@ def _atomic_torch_save(obj, path: str):
 
 
 def _maybe_fault_in_save(step: int, output_dir: str):
-    at = os.environ.get("PVA_FAULT_IN_SAVE")
-    if not at or step != int(at):
+    from ..utils.misc import fault_at
+    at = fault_at("save")
+    if at is None or step != at:
         return
     marker = os.path.join(os.path.dirname(output_dir) or ".", f".save_fault_injected_{os.environ.get('RANK', '0')}")
     if os.path.exists(marker):

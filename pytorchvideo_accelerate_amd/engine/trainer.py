@@ -40,14 +40,15 @@ from .accelerator import Accelerator
 
 
 class InjectedFault(RuntimeError):
-    """Raised by ``PVA_FAULT_AT_STEP`` (fault-injection test hook for elastic restarts)."""
+    """Raised by ``PVA_FAULT=step=N`` (fault-injection test hook for elastic restarts)."""
 
 
 def _maybe_inject_fault(global_step: int, output_dir: str):
-    """``PVA_FAULT_AT_STEP=N``: fail once when global step N completes (a marker file in ``output_dir``
+    """``PVA_FAULT=step=N``: fail once when global step N completes (a marker file in ``output_dir``
     makes the restarted run pass through)."""
-    at = os.environ.get("PVA_FAULT_AT_STEP")
-    if not at or global_step != int(at):
+    from ..utils.misc import fault_at
+    at = fault_at("step")
+    if at is None or global_step != at:
         return
     marker = os.path.join(output_dir or ".", f".fault_injected_{os.environ.get('RANK', '0')}")
     if os.path.exists(marker):

@@ -36,6 +36,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..utils.arms import arm, on
 from ..ops._ext import require
 from ..ops.conv import Act, ConvSpec, dgrad_phases, fwd_geometry
 from . import reference as R
@@ -1184,14 +1185,14 @@ class FusedNet:
         # persisted tune table, ops/tune.py TuneStore, or run deterministic=True, which fixes the split heuristic)
         # and only the weight gradients carry atomic-order noise (~1e-6).  Without it that noise
         # flips ReLU masks and the random-init network's chaotic backward decorrelates two runs' gradients
-        # (cosine ~0.65 at B=4-32: scripts/diag_ms_race.py).  On by default (only the few Gram / G launches pay the
-        # slab reduction); PVA_FOLD_SLABS=0 turns it off; implied by ``deterministic``.
-        self.fold_slabs = deterministic or reproducible or os.environ.get("PVA_FOLD_SLABS", "1") == "1"
-        # fused lateral-connection backward (apply + strided dgrad in one pass); PVA_LATERAL_BWD=0: the unfused path
-        self.lateral_bwd = os.environ.get("PVA_LATERAL_BWD", "1") != "0"
-        # two-stream backward: the lateral fusion's backward on the fast-pathway stream (PVA_SIDE_FUSE=0: on the main
+        # (cosine ~0.65 at B=4-32: scripts/diag_ms_race.py @ a59cdac).  On by default (only the few Gram / G launches pay the
+        # slab reduction); arm fold_slabs=0 (PVA_ARMS) turns it off; implied by ``deterministic``.
+        self.fold_slabs = deterministic or reproducible or on("fold_slabs")
+        # fused lateral-connection backward (apply + strided dgrad in one pass); arm lateral_bwd=0: the unfused path
+        self.lateral_bwd = on("lateral_bwd")
+        # two-stream backward: the lateral fusion's backward on the fast-pathway stream (arm side_fuse=0: on the main
         # stream, both streams joined around it and at every stage end)
-        self.side_fuse = os.environ.get("PVA_SIDE_FUSE", "1") != "0"
+        self.side_fuse = on("side_fuse")
         self.stem_s2d = stem_s2d and not deterministic
         self.model = model
         self.device = torch.device(device)
@@ -1226,21 +1227,21 @@ class FusedNet:
         self._wst_used = [False, False]
         self.debug_skip_joins = set()      # race-detection tests only (see _join)
         self._ms_ok = (not deterministic and torch.device(device).type == "cuda"
-                       and os.environ.get("PVA_STREAMS", "1") != "0")
+                       and on("streams"))
         # BN folding of the 1x1 conv_c (never materialise its output); units whose conv_c input has at least
         # fold_min_c channels.  Narrow (fast-pathway) folds take exact statistics from a statistics-only conv pass
         # (Gram-derived variances E[y^2] - E[y]^2 over fp32-atomic sums were not reproducible there:
-        # scripts/diag_ms_fold.py).  Measured (profiles/r4_fold): min C 32 / 16 / 8 -> 1182.4 / 1192.5 / 1190.6
+        # scripts/diag_ms_fold.py @ a59cdac).  Measured (profiles/r4_fold): min C 32 / 16 / 8 -> 1182.4 / 1192.5 / 1190.6
         # clips/s once the fold's slab reductions were parallel, so the fast res3+ units fold too (default 16).
-        self.bn_fold = os.environ.get("PVA_BN_FOLD", "1") != "0"
-        self.fold_min_c = int(os.environ.get("PVA_BN_FOLD_MIN_C", "16"))
-        self.bn_fold1 = self.bn_fold and os.environ.get("PVA_BN_FOLD1", "1") != '0'
+        self.bn_fold = on("bn_fold")
+        self.fold_min_c = int(arm("bn_fold_min_c"))
+        self.bn_fold1 = self.bn_fold and on("bn_fold1")
         # folds with fewer input channels than this take exact statistics from a statistics-only conv pass
-        self.fold_exact_below = int(os.environ.get("PVA_BN_FOLD_EXACT_BELOW", "32"))
+        self.fold_exact_below = int(arm("bn_fold_exact_below"))
         # fused narrow conv_c backward (csrc/kernels/narrow_bwd.hip); workgroups (= slab count) per launch
-        self.narrow_bwd = os.environ.get("PVA_NARROW_BWD", "1") != "0"
-        self.narrow_splits = int(os.environ.get("PVA_NARROW_SPLITS", "1024"))
-        self.narrow_fold = self.narrow_bwd and os.environ.get("PVA_NARROW_FOLD", "1") != "0"
+        self.narrow_bwd = on("narrow_bwd")
+        self.narrow_splits = int(arm("narrow_splits"))
+        self.narrow_fold = self.narrow_bwd and on("narrow_fold")
         blocks = list(model.blocks)
         self.slowfast = isinstance(blocks[0], R.MultiPathWayWithFuse)
         self.stages: List[Tuple[List, Optional[_Fuse]]] = []
@@ -1373,14 +1374,14 @@ class FusedNet:
         """The fast pathway runs on its own HIP stream, concurrently with the slow pathway (both are
         independent between lateral fusions; the narrow fast-path kernels are latency-bound and fill the CUs
         the slow path's MFMA kernels leave idle).  Off for the first (autotuning) step, in deterministic
-        mode, for single-pathway nets, under the per-op profiler and with ``PVA_STREAMS=0``."""
+        mode, for single-pathway nets, under the per-op profiler and with the arm ``streams=0``."""
         return (self._ms_ok and self._ms_warm and self.npath == 2 and self.prof is None)
 
     def _side_stream(self):
         if self._side is None:
-            # PVA_SIDE_PRIORITY: HIP stream priority of the fast-pathway stream (lower = higher priority)
+            # arm side_priority: HIP stream priority of the fast-pathway stream (lower = higher priority)
             self._side = torch.cuda.Stream(device=self.device,
-                                           priority=int(os.environ.get("PVA_SIDE_PRIORITY", "0")))
+                                           priority=int(arm("side_priority")))
         return self._side
 
     def _wgrad_stream(self):

@@ -3,15 +3,15 @@
 The gfx950 conv kernel (csrc/kernels/conv_igemm.hip) has several launch configurations per conv: output
 tile (128x128, 128x64, 256x32, 256x16), K depth per LDS stage (BK 32 / 64) and the uniform-tap loader
 on or off; convs with <= 64 output channels can also run the direct-to-register kernel
-(csrc/kernels/conv_direct.hip, 512 or 2048 rows per workgroup; ``PVA_CONV_DIRECT=0`` excludes it), and dense
-1x1x1 convs the streaming pointwise kernel (csrc/kernels/conv_pw.hip; ``PVA_CONV_PW=0`` excludes it).  Which one wins depends on the layer (measured: the uniform-tap loader is 20-25 % faster on
+(csrc/kernels/conv_direct.hip, 512 or 2048 rows per workgroup; arm ``conv_direct=0`` (``PVA_ARMS``, utils/arms.py) excludes it), and dense
+1x1x1 convs the streaming pointwise kernel (csrc/kernels/conv_pw.hip; ``conv_pw=0`` excludes it).  Which one wins depends on the layer (measured: the uniform-tap loader is 20-25 % faster on
 3x3 convs with the consumer-side BN fold and 15-30 % slower on padded temporal convs; BK=64 wins only for
 deep K).  The first time a geometry is launched, :class:`ConvTuner` times every legal configuration on
 scratch outputs (same shapes and strides, so inputs and real outputs are untouched — including
 accumulating dgrads), caches the fastest and launches it for real.  Every configuration accumulates K in
 the same order, so the result does not depend on the choice.
 
-Disabled by ``PVA_AUTOTUNE=0`` and in deterministic mode (the built-in heuristic is used instead).
+Disabled by the arm ``autotune=0`` and in deterministic mode (the built-in heuristic is used instead).
 
 Tuned choices persist across processes (:class:`TuneStore`): a JSON table under ``~/.cache/pva/`` (or
 ``$PVA_TUNE_CACHE``; ``PVA_TUNE_CACHE=0`` disables it) whose file name hashes the extension's embedded build id, the planner sources, the
@@ -79,24 +79,26 @@ def cfg_word(variant: int, bk: int, ut: bool) -> int:
 class ConvTuner:
     def __init__(self, C, enabled: bool = True, reps: int = 3):
         self.C = C
-        self.enabled = enabled and os.environ.get("PVA_AUTOTUNE", "1") != "0"
-        self.direct = os.environ.get("PVA_CONV_DIRECT", "1") != "0"
-        self.dma = os.environ.get("PVA_CONV_DMA", "1") != "0"
-        self.pw = os.environ.get("PVA_CONV_PW", "1") != "0"
-        self.halo = os.environ.get("PVA_CONV_HALO", "1") != "0"
-        self.big_half = os.environ.get("PVA_CONV_BIG_HALF", "1") != "0"
-        self.pf = os.environ.get("PVA_CONV_PF", "1") != "0"
-        self.pw_w4 = os.environ.get("PVA_CONV_PW_W4", "1") != "0"
-        # debugging aid: PVA_PW_KINDS=f,fres,er,... restricts the pointwise kernel to launches whose key
-        # starts with one of these kinds (models/fused.py: f fres fw2 eb er d)
-        kinds = os.environ.get("PVA_PW_KINDS")
-        self.pw_kinds = None if kinds is None else set(k for k in kinds.split(",") if k)
+        from ..utils.arms import arm, on
+        # candidate families: PVA_ARMS (utils/arms.py) selects the arms of the finished A/Bs
+        self.enabled = enabled and on("autotune")
+        self.direct = on("conv_direct")
+        self.dma = on("conv_dma")
+        self.pw = on("conv_pw")
+        self.halo = on("conv_halo")
+        self.big_half = on("conv_big_half")
+        self.pf = on("conv_pf")
+        self.pw_w4 = on("conv_pw_w4")
+        # debugging aid: pw_kinds=f:fres:er restricts the pointwise kernel to launches whose key starts with one of
+        # these kinds (models/fused.py: f fres fw2 eb er d)
+        kinds = arm("pw_kinds")
+        self.pw_kinds = None if kinds is None else set(k for k in kinds.split(":") if k)
         self._pw_now = True
         self.pw_only: Optional[int] = None   # debugging aid: allow the pointwise kernel on the n-th PW-legal tuning only
         self._pw_seen = 0
         self.log = os.environ.get("PVA_TUNE_LOG", "0") != "0"
-        self.reps = int(os.environ.get("PVA_TUNE_REPS", reps))   # timed launches per re-timed contender
-        self.top = max(1, int(os.environ.get("PVA_TUNE_TOP", 3)))   # contenders re-timed after the single-shot pass
+        self.reps = int(arm("tune_reps"))   # timed launches per re-timed contender
+        self.top = max(1, int(arm("tune_top")))   # contenders re-timed after the single-shot pass
         self.tuned = 0          # geometries timed by this process (conv + weight-gradient tunings)
         self.cache: Dict[Tuple, int] = {}
         self._scratch: Dict[Tuple, torch.Tensor] = {}
@@ -238,15 +240,14 @@ class TuneStore:
     """Persistent autotuner table (module docstring).  ``tables``: name -> dict (the live caches, updated in place
     by :meth:`load` / :meth:`restore`); :meth:`save` writes them when they grew since the last save."""
 
-    KNOBS = ("PVA_CONV_", "PVA_PW_", "PVA_WGRAD_", "PVA_AUTOTUNE")
-
     def __init__(self, tables: Dict[str, Dict], ident: Dict[str, str], root: Optional[str] = None):
         self.tables = tables
         env = os.environ.get("PVA_TUNE_CACHE", "")
         self.enabled = env != "0"
         root = root or env or os.path.join(os.path.expanduser("~"), ".cache", "pva")
         ident = dict(ident)
-        ident.update({k: v for k, v in os.environ.items() if k.startswith(self.KNOBS)})
+        from ..utils.arms import selected   # the selected A/B arms (PVA_ARMS) change kernel selection
+        ident["arms"] = ",".join(f"{k}={v}" for k, v in sorted(selected().items()))
         self.ident = ident
         h = hashlib.sha1(json.dumps(ident, sort_keys=True).encode()).hexdigest()[:16]
         self.path = os.path.join(root, f"tune-{h}.json")

@@ -57,3 +57,15 @@ def safe_torch_load(path, map_location="cpu"):
             allow.append(t)
     with ser.safe_globals(allow):
         return torch.load(path, map_location=map_location, weights_only=True)
+
+
+def fault_at(kind: str):
+    """Fault-injection test hook ``PVA_FAULT="<kind>=N"`` (kinds: ``step`` — fail once when global step N completes,
+    engine/trainer.py; ``save`` — crash inside the save of step N, ckpt/state.py).  Returns N or None."""
+    import os
+    spec = os.environ.get("PVA_FAULT", "")
+    for item in spec.split(","):
+        k, _, v = item.partition("=")
+        if k.strip() == kind and v.strip():
+            return int(v)
+    return None

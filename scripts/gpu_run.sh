@@ -14,6 +14,7 @@
 #   cfg      non-headline configs: bench + serialised per-op profile + roofline for R101 32x2x256 (B=160) and
 #            R50 64x2x224 (B=112)
 #   runpy    the reference CLI (run.py) at the headline shape on a synthetic corpus
+#   kstats   rocprofv3 --stats of bench.py $KSTATS_ARGS: per-kernel totals (kernel_stats.csv + top-25 table)
 #   benches  bench.py once per ";"-separated $BENCHES argument set
 #   stock    stock PyTorch eager baselines (scripts/baseline_torch.py) for each ";"-separated $STOCK argument set
 #   lab      tools/gemm_lab.hip: big-tile GEMM main loop at $LAB_SHAPES ("M,N,K ..."), cold and L2-hot A operand,
@@ -109,6 +110,22 @@ t_benches() {
     PVA_TUNE_LOG=1 timeout -k 10 500 python bench.py $arm > $out/benches$i.json 2> $out/benches$i.err || fail $out/benches$i.err
     echo "$arm: $(cat $out/benches$i.json)"
   done
+}
+t_kstats() {
+  # rocprofv3 per-kernel statistics of bench.py $KSTATS_ARGS (3 timed steps): top kernels by total time
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $out/kstats -o k -- python3 bench.py --steps 3 --warmup 1 $KSTATS_ARGS > $out/kstats.log 2>&1 || fail $out/kstats.log
+  local f
+  f=$(ls $out/kstats/*/k_kernel_stats.csv $out/kstats/k_kernel_stats.csv 2>/dev/null | head -1)
+  cp "$f" $out/kernel_stats.csv
+  rm -rf $out/kstats
+  python3 - "$out/kernel_stats.csv" <<'PY'
+import csv, sys
+rows = list(csv.DictReader(open(sys.argv[1])))
+tot = sum(float(r["TotalDurationNs"]) for r in rows)
+print(f"total kernel time {tot/1e6:.1f} ms over {sum(int(r['Calls']) for r in rows)} launches")
+for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:25]:
+    print(f"{float(r['TotalDurationNs'])/1e6:9.2f} ms {int(r['Calls']):6d}  {r['Name'][:110]}")
+PY
 }
 t_stock() {
   # stock PyTorch-ROCm eager baselines (scripts/baseline_torch.py), one run per ";"-separated argument set

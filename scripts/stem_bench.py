@@ -1,5 +1,5 @@
 """Fast-stem (k(5,7,7), Cout 8) s2d kernels at the B=160 SlowFast-R50 shape: forward and weight gradient, per kernel
-variant (PVA_STEM_PAIR is read per launch).  Round 4 also timed a two-pair weight-gradient kernel here (8 waves,
+variant (stem_pair is read per launch).  Round 4 also timed a two-pair weight-gradient kernel here (8 waves,
 12-frame ring, each LDS fragment feeding both pairs): 2412 vs 1956 us for the pair kernel — removed.
     python scripts/stem_bench.py [--batch 160] [--iters 10]
 """
@@ -44,7 +44,7 @@ def main():
     flop = 2.0 * M * cout * 3 * kt * 49
     ref = None
     for pair in ("0", "1", "0", "1"):   # twice each: the first launches of a process run at lower clocks
-        os.environ["PVA_STEM_PAIR"] = pair
+        os.environ["PVA_ARMS"] = f"stem_pair={pair}"
         tf = timeit(lambda: C.stem_fwd(xs, wp, y, stats, [N, T, Hs, Hs], cout, kt), a.iters)
         acc.zero_()
         tw = timeit(lambda: C.stem_wgrad(xs, dy, acc, [N, T, Hs, Hs], cout, kt), a.iters)

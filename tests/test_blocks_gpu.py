@@ -75,7 +75,7 @@ def _act(x):
 @pytest.mark.parametrize("kt,stride,depth", [(1, 1, 2), (3, 2, 2), (1, 1, 3)])
 def test_res_stage(kt, stride, depth, fold, monkeypatch):
     """fold: conv_c BatchNorm folded (Gram statistics, fused residual-output epilogue, yc-free backward)."""
-    monkeypatch.setenv("PVA_BN_FOLD_MIN_C", "8" if fold else "100000")
+    monkeypatch.setenv("PVA_ARMS", "bn_fold_min_c=" + ("8" if fold else "100000"))
     torch.manual_seed(0)
     N, C, T, H = 4, 32, 4, 16
     stage = R.ResStage(depth, C, 16, 64, kt, stride)
@@ -102,7 +102,7 @@ def test_stem():
 
 @pytest.mark.parametrize("fold", [False, True])
 def test_fusion_pathways(fold, monkeypatch):
-    monkeypatch.setenv("PVA_BN_FOLD_MIN_C", "8" if fold else "100000")
+    monkeypatch.setenv("PVA_ARMS", "bn_fold_min_c=" + ("8" if fold else "100000"))
     torch.manual_seed(0)
     N, T, H = 2, 8, 8
     blk = R.MultiPathWayWithFuse([R.ResStage(1, 16, 8, 32, 1, 1), R.ResStage(1, 8, 8, 16, 3, 1)],
@@ -124,18 +124,18 @@ def test_fusion_pathways(fold, monkeypatch):
     if fold:
         # This N=2, 8x8 geometry is noise-dominated: every path (autocast, unfolded and folded fused) is 5-20 %
         # off the fp32 oracle on the BN weights, and any rounding change moves single gradients by that much
-        # (scripts/diag_fold_fusion.py).  The fold is held to the unfolded fused path as well as to autocast.
-        monkeypatch.setenv("PVA_BN_FOLD_MIN_C", "100000")
+        # (scripts/diag_fold_fusion.py @ a59cdac).  The fold is held to the unfolded fused path as well as to autocast.
+        monkeypatch.setenv("PVA_ARMS", "bn_fold_min_c=100000")
         net0 = copy.deepcopy(net)
         FusedNet(net0, DEV).forward_backward([_act(x) for x in xs], labels)
         floor = {n: _rel(p.grad, ref[n].grad) for n, p in net0.named_parameters()}
-        monkeypatch.setenv("PVA_BN_FOLD_MIN_C", "8")
+        monkeypatch.setenv("PVA_ARMS", "bn_fold_min_c=8")
     eng = FusedNet(net, DEV)
     loss, _ = eng.forward_backward([_act(x) for x in xs], labels)
     torch.cuda.synchronize()
     assert abs(loss.item() - loss_ref.item()) < 1e-2 * max(1.0, abs(loss_ref.item()))
     # 2.5x autocast: at this N=2, 8x8 geometry the fast unit's BN_a weight gradient sits at 0.131 from the oracle under
-    # every kernel selection (scripts/diag_fusion_noise.py: pointwise 8/4-wave, no pointwise, heuristic), while stock
+    # every kernel selection (scripts/diag_fusion_noise.py @ a59cdac: pointwise 8/4-wave, no pointwise, heuristic), while stock
     # autocast's own distance moves 0.063-0.070 run to run (MIOpen algorithm choice) — 2x of it is a coin flip
     _check_grads(net, oracle, xs, labels, floor, ac_factor=2.5)
 
@@ -144,8 +144,7 @@ def test_fusion_pathways(fold, monkeypatch):
 def test_res_stage_branch1_fold(fold1, monkeypatch):
     """Unit 0's stride-1 1x1 branch1 with its BatchNorm folded in the backward (G1 = dz^T x, Gram of x; no dy1 pass,
     no y1 read in unit 1's dgrad epilogue) vs the unfolded branch1, both against the fp32 oracle."""
-    monkeypatch.setenv("PVA_BN_FOLD_MIN_C", "8")
-    monkeypatch.setenv("PVA_BN_FOLD1", fold1)
+    monkeypatch.setenv("PVA_ARMS", f"bn_fold_min_c=8,bn_fold1={fold1}")
     torch.manual_seed(1)
     N, C, T, H = 4, 40, 4, 16
     stage = R.ResStage(3, C, 16, 64, 1, 1)
@@ -165,9 +164,7 @@ def test_fast_res2_narrow(narrow, nfold, monkeypatch):
     """The fast pathway's res2 shape (8 -> inner 8 -> 32, temporal conv_a, branch1 8 -> 32 on unit 0): unfolded
     three-kernel backward, the fused narrow backward (csrc/kernels/narrow_bwd.hip), and the narrow BN fold (statistics
     pass + fold_output forward, yc recomputed in the backward) — each against the fp32 oracle."""
-    monkeypatch.setenv("PVA_BN_FOLD_MIN_C", "100000")
-    monkeypatch.setenv("PVA_NARROW_BWD", narrow)
-    monkeypatch.setenv("PVA_NARROW_FOLD", nfold)
+    monkeypatch.setenv("PVA_ARMS", f"bn_fold_min_c=100000,narrow_bwd={narrow},narrow_fold={nfold}")
     torch.manual_seed(2)
     N, T, H = 4, 8, 16
     stage = R.ResStage(3, 8, 8, 32, 3, 1)

@@ -118,7 +118,7 @@ def test_crash_mid_save_resumes_from_previous_complete(tmp_path, monkeypatch):
     from pytorchvideo_accelerate_amd.ckpt.state import InjectedSaveFault, is_complete
     m, opt, sch = _ours()
     save_state(str(tmp_path / "step_2"), m, [opt], [sch], [sch], step=2)
-    monkeypatch.setenv("PVA_FAULT_IN_SAVE", "4")
+    monkeypatch.setenv("PVA_FAULT", "save=4")
     with pytest.raises(InjectedSaveFault):
         save_state(str(tmp_path / "step_4"), m, [opt], [sch], [sch], step=4)
     assert not (tmp_path / "step_4").exists() and (tmp_path / "step_4.tmp" / "model.safetensors").exists()

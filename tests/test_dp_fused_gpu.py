@@ -9,9 +9,9 @@ on each rank's shard (``bench.py --data-rank r``):
 * production schedule (fast pathway on its own HIP stream, weight gradients on side streams joined per stage,
   stage-granular bucket progress, heuristic kernels, and the shipped default with the autotuner on) with the
   default fixed-order BN-fold reductions: the same equality within the fp32-atomic noise of the leaf weight
-  gradients.  (Without the fold slabs, ``PVA_FOLD_SLABS=0``, two runs
+  gradients.  (Without the fold slabs, arm ``fold_slabs=0``, two runs
   of the same rank already differ at cosine ~0.65: atomic-order noise in the fold statistics flips ReLU masks
-  and the random-init network's backward is chaotic — ``scripts/diag_ms_race.py``, ``scripts/diag_chaos.py``.)
+  and the random-init network's backward is chaotic — ``scripts/diag_ms_race.py @ a59cdac``, ``scripts/diag_chaos.py @ a59cdac``.)
 * default production path (autotuner agreed across ranks): parameters bitwise identical on both ranks;
 * ``run.py`` over a corpus whose videos give the two ranks different numbers of uniform validation clips (so
   different eval batch counts and last-batch shapes) completes a full evaluation — eval-time kernel tuning is
@@ -74,7 +74,7 @@ def test_fused_two_rank_deterministic_exact(tmp_path):
 
 
 def test_fused_two_rank_streams_and_buckets(tmp_path):
-    err, spread = _dp_vs_singles(tmp_path, [], "ms", PVA_AUTOTUNE="0")
+    err, spread = _dp_vs_singles(tmp_path, [], "ms", PVA_ARMS="autotune=0")
     assert spread > 0.1, spread
     assert err < 2e-3, (err, spread)   # leaf weight gradients: fp32 split-K atomics in any order
 
@@ -85,7 +85,7 @@ def test_fused_two_rank_shipped_default_config(tmp_path):
     noise of the leaf weight gradients (the production DP path checked on gradients, not only params)."""
     # The single-rank oracle runs restore the autotuner table the two-rank run agreed on and wrote (the persistent
     # cache, as a re-run of the job would): kernel choices change fp32 summation orders, and this random-init network
-    # amplifies such differences chaotically (scripts/diag_chaos.py), so the comparison needs the same kernels.
+    # amplifies such differences chaotically (scripts/diag_chaos.py @ a59cdac), so the comparison needs the same kernels.
     err, spread = _dp_vs_singles(tmp_path, [], "dflt", PVA_TUNE_CACHE=str(tmp_path / "tune"))
     assert spread > 0.1, spread
     assert err < 2e-3, (err, spread)

@@ -142,7 +142,7 @@ def test_small_batch_lr01_trajectory_tracks_fp32_oracle():
     """B=16 bench runs at lr 0.1 end at loss ~21.  The fp32 PyTorch oracle on the same
     weights, clips and labels blows up the same way (6.2 -> 17 -> 23 -> 36 over four steps: SGD momentum 0.9 at
     lr 0.1 on 16 random-label clips diverges), and the fused executor tracks it step for step until the
-    trajectories decorrelate chaotically.  The blow-up is the recipe, not the kernels (scripts/diag_small_batch.py
+    trajectories decorrelate chaotically.  The blow-up is the recipe, not the kernels (scripts/diag_small_batch.py @ a59cdac
     prints the fp32 / autocast / fused trajectories over 10 steps)."""
     torch.manual_seed(0)
     model = R.create_slowfast(50, 400, dropout_rate=0.0)

@@ -64,7 +64,7 @@ def test_fused_step_matches_oracle(slowfast):
     loss_ac.backward()
     # One autocast run is a single sample of that noise: equally valid bf16 executions that differ only in
     # launch configuration (i.e. fp32 summation order of the BN partial sums) land up to ~4 % apart at this
-    # size (scripts/debug_direct.py: 2.246 / 2.258 / 2.320 / 2.338 for four configuration mixes; random-init
+    # size (scripts/debug_direct.py @ a59cdac: 2.246 / 2.258 / 2.320 / 2.338 for four configuration mixes; random-init
     # BN nets amplify bf16 rounding with depth), so the loss floor is 8 %.
     tol = max(8e-2, 2 * abs(loss_ac.item() - loss_ref.item()))
     assert abs(loss.item() - loss_ref.item()) < tol * max(1.0, abs(loss_ref.item()))
@@ -211,16 +211,15 @@ def test_persistent_tune_cache_reused_and_invalidated(tmp_path, monkeypatch):
 
 def test_narrow_fused_backward_matches_unfused(monkeypatch):
     """The fused narrow conv_c backward (fast res2: BN apply + weight gradient + input gradient in one pass,
-    csrc/kernels/narrow_bwd.hip), with and without the narrow BN fold of the forward (PVA_NARROW_FOLD), against the
-    three-kernel unfolded path it replaces (PVA_NARROW_BWD=0), deterministic mode: loss, every gradient and the BN
+    csrc/kernels/narrow_bwd.hip), with and without the narrow BN fold of the forward (arm narrow_fold), against the
+    three-kernel unfolded path it replaces (narrow_bwd=0), deterministic mode: loss, every gradient and the BN
     running statistics within bf16 re-association noise."""
     model = _build(True)
     xs = _inputs(True, N=2, T=16, S=96, seed=3)
     labels = torch.tensor([2, 5], device=DEV)
     runs = []
     for flag, fold in (("1", "1"), ("1", "0"), ("0", "0")):
-        monkeypatch.setenv("PVA_NARROW_BWD", flag)
-        monkeypatch.setenv("PVA_NARROW_FOLD", fold)
+        monkeypatch.setenv("PVA_ARMS", f"narrow_bwd={flag},narrow_fold={fold}")
         m = copy.deepcopy(model)
         eng = FusedNet(m, DEV, deterministic=True)
         blocks = [b for paths, _ in eng.stages for p in paths for b in getattr(p, "blocks", [])]
@@ -238,7 +237,7 @@ def test_narrow_fused_backward_matches_unfused(monkeypatch):
     assert worst[0] < 2e-2, worst
     # folded: the unit output comes from a recomputing kernel and the BN statistics from a statistics-only pass —
     # other bf16 roundings of the same forward.  At this random-init whole-net shape the backward is chaotic (every
-    # fused variant, unfolded included, sits at median rel-L2 ~1.2 from the fp32 oracle: scripts/diag_narrow.py), so
+    # fused variant, unfolded included, sits at median rel-L2 ~1.2 from the fp32 oracle: scripts/diag_narrow.py @ a59cdac), so
     # only the loss and the running statistics are compared here; the folded backward is gated block-level
     # (tests/test_blocks_gpu.py::test_fast_res2_narrow) against the fp32 oracle.
     lf, gf, bf = runs[0]

@@ -377,10 +377,10 @@ def test_pack_weights_kernel_matches_host_pack():
             assert torch.equal(u.wd.view_as(wd), wd), u.name
 
 
-# (5, 8): frame-pair kernels (PVA_STEM_PAIR default) for T = 4k .. 4k+3, and the one-frame kernels
-# (1, 64): the slow stem with the channel-permuted 16-B-store epilogue (default) and without (PVA_STEM_PERM=0);
-# roll "0": the frame-pair wgrad with one tap row per wave instead of the rolling-fragment default (PVA_STEM_ROLL=0);
-# roll "s": the rolling form with intrinsic (synchronous) transpose reads instead of the asm ones (PVA_STEM_ASYNC=0)
+# (5, 8): frame-pair kernels (arm stem_pair, PVA_ARMS, default) for T = 4k .. 4k+3, and the one-frame kernels
+# (1, 64): the slow stem with the channel-permuted 16-B-store epilogue (default) and without (stem_perm=0);
+# roll "0": the frame-pair wgrad with one tap row per wave instead of the rolling-fragment default (stem_roll=0);
+# roll "s": the rolling form with intrinsic (synchronous) transpose reads instead of the asm ones (stem_async=0)
 @pytest.mark.parametrize("kt,cout,T,pair,perm,roll", [(5, 8, 6, "1", "1", "1"), (5, 8, 5, "1", "1", "1"),
                                                       (5, 8, 8, "1", "1", "1"), (5, 8, 7, "1", "1", "1"),
                                                       (5, 8, 7, "1", "1", "0"), (5, 8, 7, "1", "1", "s"),
@@ -391,10 +391,8 @@ def test_pack_weights_kernel_matches_host_pack():
 def test_stem_s2d_fwd_wgrad(kt, cout, T, pair, perm, roll, monkeypatch):
     from pytorchvideo_accelerate_amd.models.fused import to_s2d
     from pytorchvideo_accelerate_amd.ops._ext import require
-    monkeypatch.setenv("PVA_STEM_PAIR", pair)
-    monkeypatch.setenv("PVA_STEM_PERM", perm)
-    monkeypatch.setenv("PVA_STEM_ROLL", "0" if roll == "0" else "1")
-    monkeypatch.setenv("PVA_STEM_ASYNC", "0" if roll == "s" else "1")
+    monkeypatch.setenv("PVA_ARMS", f"stem_pair={pair},stem_perm={perm},stem_roll={0 if roll == '0' else 1},"
+                                   f"stem_async={0 if roll == 's' else 1}")
     C = require()
     g = torch.Generator(device="cpu").manual_seed(7)
     N, H = 2, 40

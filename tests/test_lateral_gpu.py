@@ -72,7 +72,7 @@ def test_lateral_fused_net_matches_unfused(monkeypatch):
     labels = torch.tensor([1, 7], device=DEV)
     runs = []
     for flag in ("1", "0"):
-        monkeypatch.setenv("PVA_LATERAL_BWD", flag)
+        monkeypatch.setenv("PVA_ARMS", f"lateral_bwd={flag}")
         m = copy.deepcopy(model)
         eng = FusedNet(m, DEV, deterministic=True)
         loss, _ = eng.forward_backward(eng.prepare_inputs(xs), labels)

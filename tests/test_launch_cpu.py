@@ -70,7 +70,7 @@ def test_fault_injection_elastic_restart_auto_resume(tmp_path):
            "--num_frames", "8", "--crop_size", "64", "--batch_size", "2", "--num_workers", "0", "--num_epochs", "2",
            "--limit_val_batches", "0", "--checkpointing_steps", "2", "--output_dir", str(out),
            "--gradient_accumulation_steps", "1", "--quiet", "--logging_dir", str(tmp_path / "logs")]
-    env = dict(os.environ, PVA_FAULT_AT_STEP="3", OMP_NUM_THREADS="2", CUDA_VISIBLE_DEVICES="",
+    env = dict(os.environ, PVA_FAULT="step=3", OMP_NUM_THREADS="2", CUDA_VISIBLE_DEVICES="",
                HIP_VISIBLE_DEVICES="", PYTHONPATH=REPO)
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, cwd=str(tmp_path), env=env)
     log = r.stdout[-4000:] + r.stderr[-4000:]
@@ -93,7 +93,7 @@ def test_crash_inside_checkpoint_save_restarts_from_previous(tmp_path, nproc):
            "--num_frames", "8", "--crop_size", "64", "--batch_size", "2", "--num_workers", "0", "--num_epochs", "2",
            "--limit_val_batches", "0", "--checkpointing_steps", "2", "--output_dir", str(out),
            "--gradient_accumulation_steps", "1", "--quiet", "--logging_dir", str(tmp_path / "logs")]
-    env = dict(os.environ, PVA_FAULT_IN_SAVE="4", OMP_NUM_THREADS="2", CUDA_VISIBLE_DEVICES="",
+    env = dict(os.environ, PVA_FAULT="save=4", OMP_NUM_THREADS="2", CUDA_VISIBLE_DEVICES="",
                HIP_VISIBLE_DEVICES="", PYTHONPATH=REPO)
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, cwd=str(tmp_path), env=env)
     log = r.stdout[-4000:] + r.stderr[-4000:]

@@ -34,9 +34,9 @@ def test_stale_identity_or_knob_invalidates(tmp_path, monkeypatch):
     t["conv"][("d", 1)] = 17
     st.save()
     assert TuneStore(_tables(), dict(IDENT, so="rebuilt")).load() == 0         # other .so build: other file
-    monkeypatch.setenv("PVA_CONV_DIRECT", "0")
-    assert TuneStore(_tables(), IDENT).load() == 0                              # kernel-selection knob changed
-    monkeypatch.delenv("PVA_CONV_DIRECT")
+    monkeypatch.setenv("PVA_ARMS", "conv_direct=0")
+    assert TuneStore(_tables(), IDENT).load() == 0                              # kernel-selection arm changed
+    monkeypatch.delenv("PVA_ARMS")
     # a file whose recorded identity does not match (hash collision, hand edit) is ignored
     doc = json.load(open(st.path))
     doc["ident"]["so"] = "other"

@@ -45,3 +45,25 @@ def test_accuracy_metric():
     assert m.compute().item() == pytest.approx(3 / 5)
     m.reset()
     assert m.compute().item() == 0.0
+
+
+def test_arms_single_knob(monkeypatch):
+    """Decided A/B arms live behind one knob (PVA_ARMS); defaults are the shipped arms; typos raise."""
+    from pytorchvideo_accelerate_amd.utils import arms
+    monkeypatch.delenv("PVA_ARMS", raising=False)
+    assert arms.arm("stem_pair") == 1 and arms.arm("bn_fold_min_c") == 16 and arms.selected() == {}
+    monkeypatch.setenv("PVA_ARMS", "stem_pair=0, bn_fold_min_c=8")
+    assert arms.arm("stem_pair") == 0 and arms.arm("bn_fold_min_c") == 8
+    assert arms.selected() == {"stem_pair": 0, "bn_fold_min_c": 8}
+    assert arms.arms_spec(side_fuse=False) == "stem_pair=0,bn_fold_min_c=8,side_fuse=0"
+    monkeypatch.setenv("PVA_ARMS", "stem_pari=0")
+    with pytest.raises(ValueError):
+        arms.arm("stem_pair")
+
+
+def test_fault_spec(monkeypatch):
+    from pytorchvideo_accelerate_amd.utils.misc import fault_at
+    monkeypatch.setenv("PVA_FAULT", "step=3,save=4")
+    assert fault_at("step") == 3 and fault_at("save") == 4
+    monkeypatch.delenv("PVA_FAULT")
+    assert fault_at("step") is None
