@@ -1,42 +1,62 @@
-// fp32 convolutions for gfx950 on bf16x3 MFMA (the "--mixed_precision no" path; reference run.py:330 default).
+// fp32 convolutions for gfx950 on split-bf16 MFMA (the "--mixed_precision no" path; reference run.py:330 default).
 //
-// Every fp32 operand is split while it is staged into LDS: hi = bf16(x) (RNE), lo = bf16(x - hi).  Each MFMA
-// 16x16x32 fragment pair then issues three products into one fp32 accumulator: hi*hi + hi*lo + lo*hi (the lo*lo term,
-// 2^-16 relative, is dropped).  That is ~fp32 accuracy at a third of the bf16 MFMA rate (~830 TF/s peak), against
-// 157 TF/s for gfx950's f32-input MFMA (MI355X_MICROARCH.md, matrix cores).
+// Every fp32 operand is split while it is staged into LDS into NP bf16 pieces, x = p0 + p1 [+ p2] (p0 = bf16(x) RNE,
+// p1 = bf16(x - p0), p2 = bf16(x - p0 - p1)), and each MFMA 16x16x32 fragment pair issues the products whose order is
+// above the target precision, into one fp32 accumulator:
+//   NP = 3 ("bf16x6", default): p0p0 + p0p1 + p1p0 + p0p2 + p2p0 + p1p1 — operands carry 24 bits, dropped terms are
+//          <= 2^-24 relative: fp32 accuracy at a sixth of the bf16 MFMA rate (~415 TF/s peak);
+//   NP = 2 ("bf16x3"): p0p0 + p0p1 + p1p0 — ~16-bit operands (2^-16 relative per product) at a third of the rate.
+// Both beat gfx950's f32-input MFMA (157 TF/s, MI355X_MICROARCH.md "matrix cores") on throughput.
 //
-// LDS image of a tile: one 128-B row per GEMM row holding 32 k values as eight 16-B chunks (chunks 0-3: hi of k
-// 8c..8c+7, chunks 4-7: lo), chunk c stored at chunk c ^ (row & 7) — conflict-free for the ds_read_b128 fragment
-// reads (lane l reads row l&15, chunk l>>4) under gfx950's 4 x 16-lane grouping.
+// LDS image of a tile: NP planes, plane p = [rows][64 B] holding piece p of 32 k values as four 16-B chunks, chunk c
+// stored at chunk c ^ ((row >> 1) & 3) — conflict-free for the ds_read_b128 fragment reads (lane l reads row l & 15,
+// chunk l >> 4) under gfx950's 4 x 16-lane grouping.
 //
 // igemm32: implicit GEMM over positions (forward, and each stride phase of the input gradient: csrc/fp32/f32_params.h),
-//   register-staged double-buffered LDS, one barrier per 32-k step, swapped MFMA operands so each lane owns 4
-//   consecutive output channels (16-B stores).
+//   register-staged LDS (double-buffered at NP = 2: one barrier per 32-k step), swapped MFMA operands so each lane
+//   owns 4 consecutive output channels (16-B stores).
 // wgrad32: weight gradient, positions on the reduction axis (split across workgroups, fp32 atomics): both operands
-//   are staged transposed (each thread loads 8 positions x 4 channels and writes one 16-B chunk per channel).
+//   are staged transposed (each loading thread holds 8 positions x 4 channels and writes one 16-B chunk per channel
+//   and piece); half the threads load the gathered input, half the output gradient.
 #include "../kernels/common.h"
 #include "f32_params.h"
 
 namespace pva_f32 {
 
-__device__ __forceinline__ void split4(const float4& v, uint2& hi, uint2& lo) {
-  const uint32_t h0 = cvt_pk_e16(v.x, v.y), h1 = cvt_pk_e16(v.z, v.w);
-  hi = make_uint2(h0, h1);
-  lo = make_uint2(cvt_pk_e16(v.x - lo2f(h0), v.y - hi2f(h0)), cvt_pk_e16(v.z - lo2f(h1), v.w - hi2f(h1)));
-}
-
-__device__ __forceinline__ void split8(const float* f, uint4& hi, uint4& lo) {
-  uint32_t h[4], l[4];
+template <int NP>
+__device__ __forceinline__ void split4(const float4& v, uint2 (&o)[NP]) {
+  float r0 = v.x, r1 = v.y, r2 = v.z, r3 = v.w;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    h[i] = cvt_pk_e16(f[2 * i], f[2 * i + 1]);
-    l[i] = cvt_pk_e16(f[2 * i] - lo2f(h[i]), f[2 * i + 1] - hi2f(h[i]));
+  for (int p = 0; p < NP; ++p) {
+    const uint32_t a = cvt_pk_e16(r0, r1), b = cvt_pk_e16(r2, r3);
+    o[p] = make_uint2(a, b);
+    if (p + 1 < NP) {
+      r0 -= lo2f(a);
+      r1 -= hi2f(a);
+      r2 -= lo2f(b);
+      r3 -= hi2f(b);
+    }
   }
-  hi = make_uint4(h[0], h[1], h[2], h[3]);
-  lo = make_uint4(l[0], l[1], l[2], l[3]);
 }
 
-__device__ __forceinline__ int chunk_off(int r, int c) { return r * 128 + ((c ^ (r & 7)) << 4); }
+template <int NP>
+__device__ __forceinline__ void split8(float (&f)[8], uint4 (&o)[NP]) {
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      w[i] = cvt_pk_e16(f[2 * i], f[2 * i + 1]);
+      if (p + 1 < NP) {
+        f[2 * i] -= lo2f(w[i]);
+        f[2 * i + 1] -= hi2f(w[i]);
+      }
+    }
+    o[p] = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
+__device__ __forceinline__ int chunk_off(int r, int c) { return r * 64 + ((c ^ ((r >> 1) & 3)) << 4); }
 
 __device__ __forceinline__ float4 affine4(float4 v, const float4& s, const float4& h, int relu) {
   v.x = fmaf(v.x, s.x, h.x);
@@ -52,43 +72,52 @@ __device__ __forceinline__ float4 affine4(float4 v, const float4& s, const float
   return v;
 }
 
-// One 32-k step of a wave's (16 FM) x (16 FN) sub-tile: D[n][m] += B[n][:] . A[m][:] in bf16x3.
-template <int FM, int FN>
-__device__ __forceinline__ void mma3(const uint8_t* sA, const uint8_t* sB, int ra, int rb, int lane,
-                                     f32x4_t (&acc)[FM][FN]) {
+#define PVA_MF(x, y, c) __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(ev8_t, x), __builtin_bit_cast(ev8_t, y), c, 0, 0, 0)
+
+// One 32-k step of a wave's (16 FM) x (16 FN) sub-tile: D[n][m] += B[n][:] . A[m][:] over the split pieces.
+// sA / sB: plane 0 of the A (rowsA rows) / B (rowsB rows) images; plane p is p * rows * 64 bytes further.
+template <int NP, int FM, int FN>
+__device__ __forceinline__ void mma_split(const uint8_t* sA, int rowsA, const uint8_t* sB, int rowsB, int ra, int rb,
+                                          int lane, f32x4_t (&acc)[FM][FN]) {
   const int g = lane >> 4, l15 = lane & 15;
-  uint4 ah[FM], al[FM], bh[FN], bl[FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i) {
-    const int r = ra + 16 * i + l15;
-    ah[i] = *reinterpret_cast<const uint4*>(sA + chunk_off(r, g));
-    al[i] = *reinterpret_cast<const uint4*>(sA + chunk_off(r, 4 + g));
-  }
+  uint4 b[NP][FN];
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
-    const int r = rb + 16 * j + l15;
-    bh[j] = *reinterpret_cast<const uint4*>(sB + chunk_off(r, g));
-    bl[j] = *reinterpret_cast<const uint4*>(sB + chunk_off(r, 4 + g));
+    const int o = chunk_off(rb + 16 * j + l15, g);
+#pragma unroll
+    for (int p = 0; p < NP; ++p) b[p][j] = *reinterpret_cast<const uint4*>(sB + p * rowsB * 64 + o);
   }
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
+    uint4 a[NP];
+    const int o = chunk_off(ra + 16 * i + l15, g);
+#pragma unroll
+    for (int p = 0; p < NP; ++p) a[p] = *reinterpret_cast<const uint4*>(sA + p * rowsA * 64 + o);
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
-      const ev8_t bhv = __builtin_bit_cast(ev8_t, bh[j]), blv = __builtin_bit_cast(ev8_t, bl[j]);
-      const ev8_t ahv = __builtin_bit_cast(ev8_t, ah[i]), alv = __builtin_bit_cast(ev8_t, al[i]);
-      acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(blv, ahv, acc[i][j], 0, 0, 0);
-      acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bhv, alv, acc[i][j], 0, 0, 0);
-      acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bhv, ahv, acc[i][j], 0, 0, 0);
+      f32x4_t c = acc[i][j];
+      // smallest terms first
+      if constexpr (NP == 3) {
+        c = PVA_MF(b[1][j], a[1], c);
+        c = PVA_MF(b[2][j], a[0], c);
+        c = PVA_MF(b[0][j], a[2], c);
+      }
+      c = PVA_MF(b[1][j], a[0], c);
+      c = PVA_MF(b[0][j], a[1], c);
+      c = PVA_MF(b[0][j], a[0], c);
+      acc[i][j] = c;
     }
   }
 }
 
-template <int BM, int BN, int WGM>
+template <int NP, int BM, int BN, int WGM>
 __global__ __launch_bounds__(256) void igemm32_kernel(const Conv32 p) {
   constexpr int WGN = 4 / WGM, TM = BM / WGM, TN = BN / WGN, FM = TM / 16, FN = TN / 16;
   constexpr int LA = (BM + 31) / 32, LB = (BN + 31) / 32;
+  constexpr int NBUF = NP == 2 ? 2 : 1;   // NP = 3 images are 1.5x larger: one buffer, two barriers per step
+  constexpr int IMG = NP * (BM + BN) * 64;
   static_assert(FM >= 1 && FN >= 1 && TM % 16 == 0 && TN % 16 == 0, "wave tile");
-  __shared__ __attribute__((aligned(16))) uint8_t smem[2][(BM + BN) * 128];
+  __shared__ __attribute__((aligned(16))) uint8_t smem[NBUF][IMG];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave % WGM, wn = wave / WGM;
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
@@ -151,28 +180,29 @@ __global__ __launch_bounds__(256) void igemm32_kernel(const Conv32 p) {
         rb[i] = *reinterpret_cast<const float4*>(p.w + (int64_t)n * p.ldw + tp.w * p.Cr + c);
     }
   };
-  auto store = [&](int buf) {
-    uint8_t* sA = smem[buf];
-    uint8_t* sB = smem[buf] + BM * 128;
+  auto store = [&](uint8_t* img) {
     const int hc = kq >> 1, ho = (kq & 1) << 3;
 #pragma unroll
     for (int i = 0; i < LA; ++i) {
       const int r = r0 + 32 * i;
       if (r < BM) {
-        uint2 h, l;
-        split4(ra[i], h, l);
-        *reinterpret_cast<uint2*>(sA + chunk_off(r, hc) + ho) = h;
-        *reinterpret_cast<uint2*>(sA + chunk_off(r, 4 + hc) + ho) = l;
+        uint2 o[NP];
+        split4<NP>(ra[i], o);
+        const int off = chunk_off(r, hc) + ho;
+#pragma unroll
+        for (int q = 0; q < NP; ++q) *reinterpret_cast<uint2*>(img + q * BM * 64 + off) = o[q];
       }
     }
+    uint8_t* imgB = img + NP * BM * 64;
 #pragma unroll
     for (int i = 0; i < LB; ++i) {
       const int r = r0 + 32 * i;
       if (r < BN) {
-        uint2 h, l;
-        split4(rb[i], h, l);
-        *reinterpret_cast<uint2*>(sB + chunk_off(r, hc) + ho) = h;
-        *reinterpret_cast<uint2*>(sB + chunk_off(r, 4 + hc) + ho) = l;
+        uint2 o[NP];
+        split4<NP>(rb[i], o);
+        const int off = chunk_off(r, hc) + ho;
+#pragma unroll
+        for (int q = 0; q < NP; ++q) *reinterpret_cast<uint2*>(imgB + q * BN * 64 + off) = o[q];
       }
     }
   };
@@ -185,13 +215,50 @@ __global__ __launch_bounds__(256) void igemm32_kernel(const Conv32 p) {
 
   load(0);
   for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    store(buf);
+    uint8_t* img = smem[NBUF == 2 ? (kt & 1) : 0];
+    if (NBUF == 1 && kt > 0) __syncthreads();   // every wave is done reading the previous step
+    store(img);
     __syncthreads();
     if (kt + 1 < nk) load(kt + 1);
-    mma3<FM, FN>(smem[buf], smem[buf] + BM * 128, wm * TM, wn * TN, lane, acc);
+    mma_split<NP, FM, FN>(img, BM, img + NP * BM * 64, BN, wm * TM, wn * TN, lane, acc);
   }
 
+  if (p.stats != nullptr) {   // per-tile channel sums of y and y^2 (BatchNorm statistics, no re-read of y)
+    float* red = reinterpret_cast<float*>(&smem[0][0]);   // [WGM][2][BN]
+    __syncthreads();                                      // every wave is done with the last step's image
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+          if (m0 + wm * TM + 16 * i + (lane & 15) < p.M) {
+            const float v = acc[i][j][r];
+            s1 += v;
+            s2 = fmaf(v, v, s2);
+          }
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          s1 += __shfl_xor(s1, o, 64);
+          s2 += __shfl_xor(s2, o, 64);
+        }
+        if ((lane & 15) == 0) {
+          const int nl = wn * TN + 16 * j + 4 * (lane >> 4) + r;
+          red[(wm * 2) * BN + nl] = s1;
+          red[(wm * 2 + 1) * BN + nl] = s2;
+        }
+      }
+    __syncthreads();
+    for (int t = tid; t < 2 * BN; t += 256) {
+      const int q = t / BN, nl = t - q * BN;
+      if (n0 + nl >= p.N) continue;
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < WGM; ++w) v += red[(w * 2 + q) * BN + nl];
+      p.stats[((int64_t)blockIdx.x * 2 + q) * p.N + n0 + nl] = v;
+    }
+  }
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
     const int m = m0 + wm * TM + 16 * i + (lane & 15);
@@ -223,55 +290,70 @@ __global__ __launch_bounds__(256) void igemm32_kernel(const Conv32 p) {
   }
 }
 
-// Weight gradient.  sA rows = k = (tap, cin) (BM per tile), sB rows = cout (BN per tile); D[cout][k] so the 16 lanes
-// of a fragment column hold consecutive k (coalesced atomics).
-template <int BM, int BN, int WGM>
+// channel E of 8 staged positions -> NP split pieces, one 16-B chunk each, into row r of a transposed image
+template <int NP, int E>
+__device__ __forceinline__ void store_comp(const f32x4_t (&rv)[8], uint8_t* base, int rows, int r, int po) {
+  float f[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) f[u] = rv[u][E];
+  uint4 o[NP];
+  split8<NP>(f, o);
+  const int off = chunk_off(r, po);
+#pragma unroll
+  for (int k = 0; k < NP; ++k) *reinterpret_cast<uint4*>(base + k * rows * 64 + off) = o[k];
+}
+
+// Weight gradient.  A rows = k = (tap, cin) (BM per tile), B rows = cout (BN per tile); D[cout][k] so the 16 lanes of
+// a fragment column hold consecutive k (coalesced atomics).  Stages of 32 positions; threads [0, BM) load the
+// gathered input (BM/4 channel quads x 4 position octets), threads [BM, BM + BN) the output gradient.
+template <int NP, int BM, int BN, int WGM>
 __global__ __launch_bounds__(256) void wgrad32_kernel(const Wgrad32 p) {
   constexpr int WGN = 4 / WGM, TM = BM / WGM, TN = BN / WGN, FM = TM / 16, FN = TN / 16;
   constexpr int QA = BM / 4, QB = BN / 4;
-  static_assert(FM >= 1 && FN >= 1 && 8 * QA <= 256 && 8 * QB <= 256, "tile");
-  __shared__ __attribute__((aligned(16))) uint8_t smem[2][(BM + BN) * 128];  // two 32-position sub-steps
+  static_assert(FM >= 1 && FN >= 1 && BM + BN <= 256, "tile");
+  __shared__ __attribute__((aligned(16))) uint8_t smem[NP * (BM + BN) * 64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave % WGM, wn = wave / WGM;
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
   const int p_begin = blockIdx.z * p.chunk;
   const int p_end = min(p.P, p_begin + p.chunk);
   if (p_begin >= p_end) return;
-  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-  // X (gathered) role: rows k = m0 + 4*xq .. +3, positions 8*xpo .. +7 of each 64-position stage
-  const bool xr = tid < 8 * QA;
-  const int xq = tid % QA, xpo = tid / QA;
-  const int kk = m0 + 4 * xq;
+  const f32x4_t z4 = {0.f, 0.f, 0.f, 0.f};   // native vectors: a select of HIP's float4 struct goes through scratch
+  const bool xr = tid < BM;                          // gathered-input role
+  const bool dr = tid >= BM && tid < BM + BN;        // output-gradient role
+  const int lt = xr ? tid : tid - BM;
+  const int q = xr ? lt % QA : lt % QB, po = xr ? lt / QA : lt / QB;   // channel quad, position octet (0..3)
+  const int kk = m0 + 4 * q;
   const bool kkv = xr && kk < p.K;
-  int xc = 0;
-  int4 tp = make_int4(0, 0, 0, 0);
+  int xc = 0, tdt = 0, tdh = 0, tdw = 0;
   if (kkv) {
     const int j = kk / p.Cin;
     xc = kk - j * p.Cin;
-    tp = reinterpret_cast<const int4*>(p.taps)[j];
+    tdt = p.taps[4 * j];
+    tdh = p.taps[4 * j + 1];
+    tdw = p.taps[4 * j + 2];
   }
-  float4 isc = z4, ish = z4;
-  if (kkv && p.isc != nullptr) {
-    isc = *reinterpret_cast<const float4*>(p.isc + xc);
-    ish = *reinterpret_cast<const float4*>(p.ish + xc);
-  }
-  // dY role: rows cout = n0 + 4*dq .. +3
-  const bool dr = tid < 8 * QB;
-  const int dq = tid % QB, dpo = tid / QB;
-  const int dn = n0 + 4 * dq;
+  const int dn = n0 + 4 * q;
   const bool dnv = dr && dn < p.Cout;
   const int HWi = p.Hi * p.Wi;
 
-  float4 rx[8], rd[8];
+  f32x4_t rv[8];
   auto load = [&](int s0) {
-    {
-      const int pos = s0 + 8 * dpo;
+    const int pos = s0 + 8 * po;
+    // loads are unconditional from a valid address (a predicated "cond ? *ptr : 0" becomes a flat load through a
+    // pointer select with a zero in scratch); out-of-range values are zeroed afterwards
+    if (dr) {
 #pragma unroll
-      for (int u = 0; u < 8; ++u)
-        rd[u] = (dnv && pos + u < p_end) ? *reinterpret_cast<const float4*>(p.dy + (int64_t)(pos + u) * p.ldd + dn)
-                                         : z4;
+      for (int u = 0; u < 8; ++u) {
+        const bool ok = dnv && pos + u < p_end;
+        const f32x4_t v = *reinterpret_cast<const f32x4_t*>(p.dy + (ok ? (int64_t)(pos + u) * p.ldd + dn : 0));
+        rv[u] = ok ? v : z4;
+      }
+      return;
     }
-    const int pos = s0 + 8 * xpo;
+    const bool aff = kkv && p.isc != nullptr;
+    const f32x4_t isc = *reinterpret_cast<const f32x4_t*>(aff ? p.isc + xc : p.x);   // (always a global address)
+    const f32x4_t ish = *reinterpret_cast<const f32x4_t*>(aff ? p.ish + xc : p.x);
     int mm = pos < p_end ? pos : 0;
     int qw = mm % p.Qw;
     mm /= p.Qw;
@@ -280,58 +362,39 @@ __global__ __launch_bounds__(256) void wgrad32_kernel(const Wgrad32 p) {
     int qt = mm % p.Qt, nb = mm / p.Qt;
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      rx[u] = z4;
-      if (kkv && pos + u < p_end) {
-        const int ti = qt * p.st + tp.x, hi = qh * p.sh + tp.y, wi = qw * p.sw + tp.z;
-        if ((unsigned)ti < (unsigned)p.Ti && (unsigned)hi < (unsigned)p.Hi && (unsigned)wi < (unsigned)p.Wi) {
-          rx[u] = *reinterpret_cast<const float4*>(
-              p.x + ((int64_t)nb * p.Ti * HWi + (int64_t)ti * HWi + hi * p.Wi + wi) * p.ldx + xc);
-          if (p.isc != nullptr) rx[u] = affine4(rx[u], isc, ish, p.irelu);
+      {
+        const int ti = qt * p.st + tdt, hi = qh * p.sh + tdh, wi = qw * p.sw + tdw;
+        const bool ok = kkv && pos + u < p_end && (unsigned)ti < (unsigned)p.Ti && (unsigned)hi < (unsigned)p.Hi &&
+                        (unsigned)wi < (unsigned)p.Wi;
+        f32x4_t v = *reinterpret_cast<const f32x4_t*>(
+            p.x + (ok ? ((int64_t)nb * p.Ti * HWi + (int64_t)ti * HWi + hi * p.Wi + wi) * p.ldx + xc : 0));
+        if (aff) {
+          v = v * isc + ish;
+          if (p.irelu) v = __builtin_elementwise_max(v, z4);
         }
+        rv[u] = ok ? v : z4;
       }
-      if (++qw == p.Qw) {
-        qw = 0;
-        if (++qh == p.Qh) {
-          qh = 0;
-          if (++qt == p.Qt) {
-            qt = 0;
-            ++nb;
-          }
-        }
-      }
+      // next position: branch-free carry (keeps the loop unrolled and rv[] in registers)
+      ++qw;
+      const bool c1 = qw == p.Qw;
+      qw = c1 ? 0 : qw;
+      qh += c1;
+      const bool c2 = qh == p.Qh;
+      qh = c2 ? 0 : qh;
+      qt += c2;
+      const bool c3 = qt == p.Qt;
+      qt = c3 ? 0 : qt;
+      nb += c3;
     }
   };
   auto store = [&]() {
-    if (xr) {
-      uint8_t* base = smem[xpo >> 2];
-      const int cc = xpo & 3;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float f[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) f[u] = e == 0 ? rx[u].x : e == 1 ? rx[u].y : e == 2 ? rx[u].z : rx[u].w;
-        uint4 h, l;
-        split8(f, h, l);
-        const int r = 4 * xq + e;
-        *reinterpret_cast<uint4*>(base + chunk_off(r, cc)) = h;
-        *reinterpret_cast<uint4*>(base + chunk_off(r, 4 + cc)) = l;
-      }
-    }
-    if (dr) {
-      uint8_t* base = smem[dpo >> 2] + BM * 128;
-      const int cc = dpo & 3;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float f[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) f[u] = e == 0 ? rd[u].x : e == 1 ? rd[u].y : e == 2 ? rd[u].z : rd[u].w;
-        uint4 h, l;
-        split8(f, h, l);
-        const int r = 4 * dq + e;
-        *reinterpret_cast<uint4*>(base + chunk_off(r, cc)) = h;
-        *reinterpret_cast<uint4*>(base + chunk_off(r, 4 + cc)) = l;
-      }
-    }
+    if (!xr && !dr) return;
+    uint8_t* base = xr ? smem : smem + NP * BM * 64;
+    const int rows = xr ? BM : BN;
+    store_comp<NP, 0>(rv, base, rows, 4 * q + 0, po);
+    store_comp<NP, 1>(rv, base, rows, 4 * q + 1, po);
+    store_comp<NP, 2>(rv, base, rows, 4 * q + 2, po);
+    store_comp<NP, 3>(rv, base, rows, 4 * q + 3, po);
   };
 
   f32x4_t acc[FM][FN];
@@ -341,13 +404,12 @@ __global__ __launch_bounds__(256) void wgrad32_kernel(const Wgrad32 p) {
     for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
   load(p_begin);
-  for (int s0 = p_begin; s0 < p_end; s0 += 64) {
-    __syncthreads();
+  for (int s0 = p_begin; s0 < p_end; s0 += 32) {
+    if (s0 != p_begin) __syncthreads();
     store();
     __syncthreads();
-    if (s0 + 64 < p_end) load(s0 + 64);
-    mma3<FM, FN>(smem[0], smem[0] + BM * 128, wm * TM, wn * TN, lane, acc);
-    mma3<FM, FN>(smem[1], smem[1] + BM * 128, wm * TM, wn * TN, lane, acc);
+    if (s0 + 32 < p_end) load(s0 + 32);
+    mma_split<NP, FM, FN>(smem, BM, smem + NP * BM * 64, BN, wm * TM, wn * TN, lane, acc);
   }
   // D[cout][k]: lane column = k (lane & 15), rows = cout 4*(lane>>4) + r
 #pragma unroll
@@ -397,28 +459,35 @@ __global__ void wunpack_kernel(const float* dwf, float* g, int Cout, int Cin, in
 }
 
 // ---------------------------------------------------------------- host launchers
-template <int BM, int BN, int WGM>
+template <int NP, int BM, int BN, int WGM>
 static void igemm_go(const Conv32& p, hipStream_t s) {
   dim3 grid((p.M + BM - 1) / BM, (p.N + BN - 1) / BN);
-  hipLaunchKernelGGL((igemm32_kernel<BM, BN, WGM>), grid, dim3(256), 0, s, p);
+  hipLaunchKernelGGL((igemm32_kernel<NP, BM, BN, WGM>), grid, dim3(256), 0, s, p);
 }
 
 int igemm32_tile(int N) { return N > 64 ? 0 : N > 32 ? 1 : N > 16 ? 2 : 3; }
+int igemm32_bm(int N) { return igemm32_tile(N) == 3 ? 256 : 128; }
 
-void igemm32_launch(const Conv32& p, hipStream_t s) {
-  if (p.M <= 0 || p.N <= 0) return;
+template <int NP>
+static void igemm_np(const Conv32& p, hipStream_t s) {
   switch (igemm32_tile(p.N)) {
-    case 0: igemm_go<128, 128, 2>(p, s); break;
-    case 1: igemm_go<128, 64, 2>(p, s); break;
-    case 2: igemm_go<128, 32, 4>(p, s); break;
-    default: igemm_go<256, 16, 4>(p, s); break;
+    case 0: igemm_go<NP, 128, 128, 2>(p, s); break;
+    case 1: igemm_go<NP, 128, 64, 2>(p, s); break;
+    case 2: igemm_go<NP, 128, 32, 4>(p, s); break;
+    default: igemm_go<NP, 256, 16, 4>(p, s); break;
   }
 }
 
-template <int BM, int BN, int WGM>
+void igemm32_launch(const Conv32& p, int np, hipStream_t s) {
+  if (p.M <= 0 || p.N <= 0) return;
+  if (np == 2) igemm_np<2>(p, s);
+  else igemm_np<3>(p, s);
+}
+
+template <int NP, int BM, int BN, int WGM>
 static void wgrad_go(const Wgrad32& p, int splits, hipStream_t s) {
   dim3 grid((p.K + BM - 1) / BM, (p.Cout + BN - 1) / BN, splits);
-  hipLaunchKernelGGL((wgrad32_kernel<BM, BN, WGM>), grid, dim3(256), 0, s, p);
+  hipLaunchKernelGGL((wgrad32_kernel<NP, BM, BN, WGM>), grid, dim3(256), 0, s, p);
 }
 
 static int tile_of(int n) { return n > 64 ? 128 : n > 32 ? 64 : n > 16 ? 32 : 16; }
@@ -433,22 +502,28 @@ void wgrad32_tile(int K, int Cout, int* bm, int* bn) {
   *bn = b;
 }
 
-void wgrad32_launch(Wgrad32 p, hipStream_t s) {
-  if (p.P <= 0 || p.K <= 0 || p.Cout <= 0) return;
-  int bm, bn;
-  wgrad32_tile(p.K, p.Cout, &bm, &bn);
-  const int tiles = ((p.K + bm - 1) / bm) * ((p.Cout + bn - 1) / bn);
-  const int stages = (p.P + 63) / 64;
-  int splits = (2048 + tiles - 1) / tiles;
-  splits = splits < 1 ? 1 : splits > stages ? stages : splits;
-  p.chunk = ((stages + splits - 1) / splits) * 64;
-  splits = (p.P + p.chunk - 1) / p.chunk;
+template <int NP>
+static void wgrad_np(const Wgrad32& p, int bm, int bn, int splits, hipStream_t s) {
 #define PVA_W32(A, B, G) \
-  if (bm == A && bn == B) return wgrad_go<A, B, G>(p, splits, s);
+  if (bm == A && bn == B) return wgrad_go<NP, A, B, G>(p, splits, s);
   PVA_W32(128, 128, 2) PVA_W32(128, 64, 2) PVA_W32(64, 128, 2) PVA_W32(64, 64, 2) PVA_W32(128, 32, 4)
   PVA_W32(32, 128, 1) PVA_W32(128, 16, 4) PVA_W32(16, 128, 1) PVA_W32(64, 32, 2) PVA_W32(32, 64, 2)
   PVA_W32(64, 16, 4) PVA_W32(16, 64, 1) PVA_W32(32, 32, 2)
 #undef PVA_W32
+}
+
+void wgrad32_launch(Wgrad32 p, int np, hipStream_t s) {
+  if (p.P <= 0 || p.K <= 0 || p.Cout <= 0) return;
+  int bm, bn;
+  wgrad32_tile(p.K, p.Cout, &bm, &bn);
+  const int tiles = ((p.K + bm - 1) / bm) * ((p.Cout + bn - 1) / bn);
+  const int stages = (p.P + 31) / 32;
+  int splits = (2048 + tiles - 1) / tiles;
+  splits = splits < 1 ? 1 : splits > stages ? stages : splits;
+  p.chunk = ((stages + splits - 1) / splits) * 32;
+  splits = (p.P + p.chunk - 1) / p.chunk;
+  if (np == 2) wgrad_np<2>(p, bm, bn, splits, s);
+  else wgrad_np<3>(p, bm, bn, splits, s);
 }
 
 void wpack32_launch(int mode, const float* src, float* dst, int Cout, int Cin, int taps, int cip, float beta,

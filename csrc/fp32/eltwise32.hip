@@ -23,6 +23,8 @@ __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast
 __device__ __forceinline__ void st4(float* p, const float4& v) { *reinterpret_cast<float4*>(p) = v; }
 
 // mode 0: s1 = sum y, s2 = sum y^2.  mode 1: g = relu ? (o > 0 ? d : 0) : d; s1 = sum g, s2 = sum g*(y - mean).
+// mode 3: column sums only, part[block][C] (second level of the conv epilogue's [tiles][2][N] statistics: C = 2N, so
+// the output is again [blocks][2][N]).
 __global__ __launch_bounds__(256) void chan_reduce32_kernel(const float* y, int ldy, const float* d, int ldd,
                                                             const float* o, int ldo, const float* mean, int mode,
                                                             int relu, int64_t M, int C, int64_t rpb, float* part) {
@@ -68,9 +70,13 @@ __global__ __launch_bounds__(256) void chan_reduce32_kernel(const float* y, int 
         s1.x += a.x; s1.y += a.y; s1.z += a.z; s1.w += a.w;
         s2.x += b.x; s2.y += b.y; s2.z += b.z; s2.w += b.w;
       }
-      float* pp = part + (int64_t)blockIdx.x * 2 * C;
-      st4(pp + c, s1);
-      st4(pp + C + c, s2);
+      if (mode == 3) {
+        st4(part + (int64_t)blockIdx.x * C + c, s1);
+      } else {
+        float* pp = part + (int64_t)blockIdx.x * 2 * C;
+        st4(pp + c, s1);
+        st4(pp + C + c, s2);
+      }
     }
     __syncthreads();
   }
@@ -86,11 +92,12 @@ __global__ __launch_bounds__(256) void bn32_finalize_kernel(const float* part, i
                                                             float* rvar, int64_t* nbt, float momentum, float eps,
                                                             float* stat, const float* fstat, float* dgamma,
                                                             float* dbeta, float* coef, float gbeta) {
-  __shared__ double red[4][64][2];
-  const int cl = threadIdx.x & 63, l = threadIdx.x >> 6, c = blockIdx.x * 64 + cl;
+  // 16 channels x 16 row lanes per block: a partial table of R <= 1024 rows is 64 loads deep per lane
+  __shared__ double red[16][16][2];
+  const int cl = threadIdx.x & 15, l = threadIdx.x >> 4, c = blockIdx.x * 16 + cl;
   double a = 0.0, b = 0.0;
   if (c < C && mode != 2)
-    for (int r = l; r < R; r += 4) {
+    for (int r = l; r < R; r += 16) {
       a += (double)part[(int64_t)r * 2 * C + c];
       b += (double)part[(int64_t)r * 2 * C + C + c];
     }
@@ -98,7 +105,7 @@ __global__ __launch_bounds__(256) void bn32_finalize_kernel(const float* part, i
   red[l][cl][1] = b;
   __syncthreads();
   if (l != 0 || c >= C) return;
-  for (int i = 1; i < 4; ++i) {
+  for (int i = 1; i < 16; ++i) {
     a += red[i][cl][0];
     b += red[i][cl][1];
   }
@@ -337,7 +344,7 @@ void bn32_finalize_launch(const float* part, int R, int C, int64_t count, int mo
                           const float* beta, float* rmean, float* rvar, int64_t* nbt, float momentum, float eps,
                           float* stat, const float* fstat, float* dgamma, float* dbeta, float* coef, float gbeta,
                           hipStream_t s) {
-  hipLaunchKernelGGL(bn32_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, s, part, R, C, count, mode, gamma, beta,
+  hipLaunchKernelGGL(bn32_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, s, part, R, C, count, mode, gamma, beta,
                      rmean, rvar, nbt, momentum, eps, stat, fstat, dgamma, dbeta, coef, gbeta);
 }
 

@@ -13,10 +13,12 @@
 //   B[n][k] = w[n*ldw + taps[j].w*Cr + c]
 //   C[m][n] -> y[nb, qt*ost + ort, qh*osh + orh, qw*osw + orw, n]  (+= the old value when accum)
 // Optional consumer-side transform of in-range A values: relu?(x*isc[c] + ish[c]).
+// Optional BatchNorm statistics of the output: stats[blockIdx.x][0 / 1][n] = sum / sum of squares over the tile's rows.
 struct Conv32 {
   const float* x;
   const float* w;
   float* y;
+  float* stats;
   const int* taps;  // int4 per tap (dt, dh, dw, weight tap index)
   const float* isc;
   const float* ish;

@@ -33,7 +33,8 @@ inline int64_t span(const at::Tensor& t) {
 }
 
 void conv32(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, const at::Tensor& taps,
-            std::vector<int64_t> g, const OptT& isc, const OptT& ish, int64_t irelu) {
+            std::vector<int64_t> g, const OptT& isc, const OptT& ish, int64_t irelu, int64_t np, const OptT& stats) {
+  TORCH_CHECK(np == 2 || np == 3, "conv32: np (bf16 pieces per fp32 operand) must be 2 or 3");
   TORCH_CHECK(g.size() == 26, "conv32 geometry has 26 entries");
   Conv32 p{};
   p.x = fp(x, "x");
@@ -59,11 +60,17 @@ void conv32(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, const
   TORCH_CHECK((p.Qt - 1) * p.ost + p.ort < p.Yt && (p.Qh - 1) * p.osh + p.orh < p.Yh &&
                   (p.Qw - 1) * p.osw + p.orw < p.Yw,
               "conv32: output grid exceeds the output tensor");
-  pva_f32::igemm32_launch(p, stream());
+  p.stats = fpo(stats, "stats", false);
+  if (p.stats != nullptr) {
+    const int64_t tiles = (p.M + pva_f32::igemm32_bm(p.N) - 1) / pva_f32::igemm32_bm(p.N);
+    TORCH_CHECK(stats->numel() >= tiles * 2 * p.N && !p.accum, "conv32: stats needs [M tiles][2][N], no accumulate");
+  }
+  pva_f32::igemm32_launch(p, (int)np, stream());
 }
 
 void wgrad32(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& dw, const at::Tensor& taps,
-             std::vector<int64_t> g, const OptT& isc, const OptT& ish, int64_t irelu) {
+             std::vector<int64_t> g, const OptT& isc, const OptT& ish, int64_t irelu, int64_t np) {
+  TORCH_CHECK(np == 2 || np == 3, "wgrad32: np (bf16 pieces per fp32 operand) must be 2 or 3");
   TORCH_CHECK(g.size() == 16, "wgrad32 geometry has 16 entries");
   Wgrad32 p{};
   p.dy = fp(dy, "dy");
@@ -85,7 +92,7 @@ void wgrad32(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& dw, co
   TORCH_CHECK(span(dy) >= ((int64_t)p.P - 1) * p.ldd + p.Cout || p.P == 0, "wgrad32: dy too small");
   TORCH_CHECK(span(x) >= ((p.P / Q) * p.Ti * p.Hi * p.Wi - 1) * p.ldx + p.Cin || p.P == 0, "wgrad32: x too small");
   TORCH_CHECK(dw.numel() >= ((int64_t)p.Cout - 1) * p.ldw + p.K, "wgrad32: dw too small");
-  pva_f32::wgrad32_launch(p, stream());
+  pva_f32::wgrad32_launch(p, (int)np, stream());
 }
 
 }  // namespace
@@ -94,9 +101,11 @@ void register_fp32(pybind11::module& m) {
   namespace py = pybind11;
   auto f = m.def_submodule("f32", "fp32 (bf16x3 MFMA) kernels of the --mixed_precision no path");
   f.def("conv32", &conv32, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("taps"), py::arg("geo"),
-        py::arg("isc") = py::none(), py::arg("ish") = py::none(), py::arg("irelu") = 0);
+        py::arg("isc") = py::none(), py::arg("ish") = py::none(), py::arg("irelu") = 0, py::arg("np") = 3,
+        py::arg("stats") = py::none());
+  f.def("igemm32_bm", [](int64_t N) { return (int64_t)pva_f32::igemm32_bm((int)N); });
   f.def("wgrad32", &wgrad32, py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("taps"), py::arg("geo"),
-        py::arg("isc") = py::none(), py::arg("ish") = py::none(), py::arg("irelu") = 0);
+        py::arg("isc") = py::none(), py::arg("ish") = py::none(), py::arg("irelu") = 0, py::arg("np") = 3);
   f.def("igemm32_tile", [](int64_t N) { return (int64_t)pva_f32::igemm32_tile((int)N); });
   f.def("wgrad32_tile", [](int64_t K, int64_t Cout) {
     int a, b;
@@ -115,7 +124,9 @@ void register_fp32(pybind11::module& m) {
   f.def("chan_reduce32", [](const at::Tensor& y, int64_t ldy, const OptT& d, int64_t ldd, const OptT& o, int64_t ldo,
                             const OptT& mean, int64_t mode, int64_t relu, int64_t M, int64_t C, const at::Tensor& part) {
     TORCH_CHECK(C % 4 == 0 && ldy % 4 == 0 && ldd % 4 == 0 && ldo % 4 == 0, "chan_reduce32: multiples of 4");
-    TORCH_CHECK(part.dim() == 3 && part.size(1) == 2 && part.size(2) == C, "part must be [blocks][2][C]");
+    TORCH_CHECK(mode == 3 ? (part.numel() >= part.size(0) * C && C % 8 == 0)
+                          : (part.dim() == 3 && part.size(1) == 2 && part.size(2) == C),
+                "part must be [blocks][2][C] ([blocks][C] column sums in mode 3)");
     TORCH_CHECK(span(y) >= (M - 1) * ldy + C || M == 0, "chan_reduce32: y too small");
     TORCH_CHECK(mode == 0 || (d.has_value() && mean.has_value() && (!relu || o.has_value())), "chan_reduce32 args");
     pva_f32::chan_reduce32_launch(fp(y, "y"), (int)ldy, fpo(d, "d"), (int)ldd, fpo(o, "o"), (int)ldo,

@@ -279,25 +279,30 @@ class _ConvBN:
                         if C.wgrad_halo_legal(gh, plan[2], aff):
                             cands.append(16 | 256 | (o << 9))
                 gscr = eng.scratch("wgrad_tune_grad", s.cout * K)
-                eng.tuner.tuned += 1
+                # configurations borrowed from another batch size's table (ConvTuner.borrow), when still legal here
+                bc = eng.tuner.borrow_lookup("wgrad", tkey, 1)
+                if bc is not None and bc in cands:
+                    cfg = bc
+                else:
+                    eng.tuner.tuned += 1
 
-                def trial(c):
-                    if c & 1024:
-                        box_run(c, gscr, 0.0)
-                    elif slab:
-                        part = eng.scratch("wgrad_tune_slab", geometry(c)[0] * s.cout * K)
-                        sp = launch(c, part, cs_scr)
-                        C.wgrad_reduce(part, gscr, sp, s.cout, s.taps, s.cin_pad, s.cin, 1.0, 0.0, 1)
-                    else:
-                        launch(c, scratch, cs_scr)
-                # two-phase timing, agreed across data-parallel ranks (ops/tune.ConvTuner.time_candidates)
-                times = eng.tuner.time_candidates(cands, trial) if cands else []
-                cfg = cands[min(range(len(cands)), key=times.__getitem__)] if cands else -1
-                if eng.tuner.log:
-                    import sys
-                    print("wtune %s%s P=%d Cout=%d K=%d: " % (self.name, ".gram" if gram else "", dy.M, s.cout, K)
-                          + " ".join("%d=%.1fus" % (c, 1e3 * t) for c, t in zip(cands, times))
-                          + " -> %d" % cfg, file=sys.stderr, flush=True)
+                    def trial(c):
+                        if c & 1024:
+                            box_run(c, gscr, 0.0)
+                        elif slab:
+                            part = eng.scratch("wgrad_tune_slab", geometry(c)[0] * s.cout * K)
+                            sp = launch(c, part, cs_scr)
+                            C.wgrad_reduce(part, gscr, sp, s.cout, s.taps, s.cin_pad, s.cin, 1.0, 0.0, 1)
+                        else:
+                            launch(c, scratch, cs_scr)
+                    # two-phase timing, agreed across data-parallel ranks (ops/tune.ConvTuner.time_candidates)
+                    times = eng.tuner.time_candidates(cands, trial) if cands else []
+                    cfg = cands[min(range(len(cands)), key=times.__getitem__)] if cands else -1
+                    if eng.tuner.log:
+                        import sys
+                        print("wtune %s%s P=%d Cout=%d K=%d: " % (self.name, ".gram" if gram else "", dy.M, s.cout, K)
+                              + " ".join("%d=%.1fus" % (c, 1e3 * t) for c, t in zip(cands, times))
+                              + " -> %d" % cfg, file=sys.stderr, flush=True)
             eng.wtune[tkey] = cfg
         # off the critical path: a weight gradient that lands in the flat buffer runs on the lane's wgrad
         # stream, concurrently with the dgrad chain (its inputs are per-unit buffers nothing rewrites before

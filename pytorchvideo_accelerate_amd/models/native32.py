@@ -8,8 +8,8 @@ writes parameter gradients straight into the flat fp32 gradient buffer (``FlatPa
 micro-step, accumulated on later ones) and reports each finished parameter to ``grad_hook`` (the bucketed gradient
 all-reduce, ``parallel/ddp.GradSync``), so communication overlaps the rest of the backward as on the bf16 path.
 
-Numerics (what PyTorch fp32 computes, to ~1e-5 relative): convolutions accumulate in fp32 with ~16-bit operand
-mantissas (hi + lo bf16 split, three MFMA products); BatchNorm statistics are fp32 partials summed in double;
+Numerics (what PyTorch fp32 computes): convolutions accumulate in fp32 with 24-bit operands (three bf16 pieces
+per fp32 value, six MFMA products per fragment pair; arm ``f32_pieces=2``: 16-bit operands, three products); BatchNorm statistics are fp32 partials summed in double;
 running statistics use the unbiased variance with momentum 0.1; the max pool picks the first maximum of each
 window; head dropout draws a Philox stream (same distribution as torch's, not its bits).
 
@@ -23,7 +23,7 @@ import torch
 import torch.nn as nn
 
 from ..ops._ext import require
-from ..ops.f32 import ConvGeom, conv_dgrad, conv_fwd, conv_wgrad
+from ..ops.f32 import ConvGeom, conv_dgrad, conv_fwd, conv_wgrad, pieces
 from . import reference as R
 from .fused import FlatParams
 
@@ -52,13 +52,16 @@ class _ConvBN:
         wf = torch.empty(C, g.ntap * g.cip, device=dev)
         F.wpack32(0, self.conv.weight, wf, C, g.cin, g.ntap, g.cip, 0.0)
         y = torch.empty(N, To, Ho, Wo, C, device=dev)
-        conv_fwd(F, g, x, wf, y, self.taps)
         M = N * To * Ho * Wo
+        tiles = -(-M // F.igemm32_bm(C))
+        # training: BatchNorm statistics from the conv epilogue (per-tile sums, no re-read of y), reduced in two levels
+        tstat = torch.empty(tiles, 2, C, device=dev) if train else None
+        conv_fwd(F, g, x, wf, y, self.taps, stats=tstat)
         stat = torch.empty(4, C, device=dev)
         bn = self.bn
         if train:
-            part = torch.empty(F.chan_reduce32_blocks(M, C), 2, C, device=dev)
-            F.chan_reduce32(y, C, None, C, None, C, None, 0, 0, M, C, part)
+            part = torch.empty(F.chan_reduce32_blocks(tiles, 2 * C), 2, C, device=dev)
+            F.chan_reduce32(tstat, 2 * C, None, 2 * C, None, 2 * C, None, 3, 0, tiles, 2 * C, part)
             F.bn32_finalize(part, C, M, 0, bn.weight, bn.bias, bn.running_mean, bn.running_var,
                             bn.num_batches_tracked, bn.momentum, bn.eps, stat, None, None, None, None, 0.0)
         else:
@@ -126,7 +129,7 @@ class _ConvBN:
                 continue
             geo = [g.cout, g.ntap * g.cout, g.cin, N * Qt * Qh * Qw, g.cin, nt * g.cout, g.cout, 1, Qt, Qh, Qw,
                    To, Ho, Wo, 1, 1, 1, T, H, W, *g.s, rt, rh, rw]
-            F.conv32(dy, wt, dx, taps, geo)
+            F.conv32(dy, wt, dx, taps, geo, np=pieces())
 
 
 class _ResUnit:

@@ -9,8 +9,9 @@ Activations are NDHWC fp32 tensors ``[N, T, H, W, C]`` (rows of C channels, C a 
   zeros (a phase with no tap writes zeros);
 * weight gradient: positions on the reduction axis (``wgrad32``), then an unpack into PyTorch's weight layout.
 
-All three run on bf16x3 MFMA (``csrc/fp32/conv32.hip``): fp32 accuracy (~16 mantissa bits per operand) at a third
-of the bf16 matrix rate.
+All three run on split-bf16 MFMA (``csrc/fp32/conv32.hip``): each fp32 operand as ``pieces`` bf16 values — 3 (the
+default, arm ``f32_pieces``): 24-bit operands and six products per fragment pair, fp32 accuracy at a sixth of the
+bf16 matrix rate; 2: ~16-bit operands, three products.
 """
 from __future__ import annotations
 
@@ -88,8 +89,15 @@ class ConvGeom:
         return out
 
 
-def conv_fwd(F, g: ConvGeom, x: torch.Tensor, wf: torch.Tensor, y: torch.Tensor, taps: torch.Tensor):
-    """y [N, To, Ho, Wo, Cout] = conv(x [N, T, H, W, cip]) with forward-packed weights wf [Cout][taps][cip]."""
+def pieces() -> int:
+    from ..utils.arms import arm
+    return int(arm("f32_pieces"))
+
+
+def conv_fwd(F, g: ConvGeom, x: torch.Tensor, wf: torch.Tensor, y: torch.Tensor, taps: torch.Tensor,
+             stats: torch.Tensor = None):
+    """y [N, To, Ho, Wo, Cout] = conv(x [N, T, H, W, cip]) with forward-packed weights wf [Cout][taps][cip];
+    ``stats``: per-tile channel sums of y and y^2 ([ceil(M / igemm32_bm(Cout))][2][Cout]) from the epilogue."""
     N, T, H, W, C = x.shape
     assert C == g.cip
     To, Ho, Wo = g.out_thw((T, H, W))
@@ -97,7 +105,7 @@ def conv_fwd(F, g: ConvGeom, x: torch.Tensor, wf: torch.Tensor, y: torch.Tensor,
     K = g.ntap * g.cip
     geo = [g.cip, K, g.cout, N * To * Ho * Wo, g.cout, K, g.cip, 0, To, Ho, Wo, T, H, W, *g.s, To, Ho, Wo,
            1, 1, 1, 0, 0, 0]
-    F.conv32(x, wf, y, taps, geo)
+    F.conv32(x, wf, y, taps, geo, np=pieces(), stats=stats)
 
 
 def conv_dgrad(F, g: ConvGeom, dy: torch.Tensor, wt: torch.Tensor, dx: torch.Tensor, phases):
@@ -111,7 +119,7 @@ def conv_dgrad(F, g: ConvGeom, dy: torch.Tensor, wt: torch.Tensor, dx: torch.Ten
             continue
         geo = [g.cout, g.ntap * g.cout, g.cin, N * Qt * Qh * Qw, g.cin, nt * g.cout, g.cout, 0, Qt, Qh, Qw,
                To, Ho, Wo, 1, 1, 1, T, H, W, *g.s, rt, rh, rw]
-        F.conv32(dy, wt, dx, taps, geo)
+        F.conv32(dy, wt, dx, taps, geo, np=pieces())
 
 
 def conv_wgrad(F, g: ConvGeom, dy: torch.Tensor, x: torch.Tensor, dwf: torch.Tensor, taps: torch.Tensor):
@@ -120,4 +128,4 @@ def conv_wgrad(F, g: ConvGeom, dy: torch.Tensor, x: torch.Tensor, dwf: torch.Ten
     To, Ho, Wo = dy.shape[1:4]
     K = g.ntap * g.cip
     geo = [g.cout, g.cip, K, g.cout, K, g.cip, N * To * Ho * Wo, To, Ho, Wo, T, H, W, *g.s]
-    F.wgrad32(dy, x, dwf, taps, geo)
+    F.wgrad32(dy, x, dwf, taps, geo, np=pieces())

@@ -102,6 +102,11 @@ class ConvTuner:
         self.tuned = 0          # geometries timed by this process (conv + weight-gradient tunings)
         self.cache: Dict[Tuple, int] = {}
         self._scratch: Dict[Tuple, torch.Tensor] = {}
+        # borrowed choices (tests/test_benchcfg_gpu.py): {"conv": table, "wgrad": table, "ratio": M_src / M_dst} —
+        # a geometry missing here takes the source table's choice for the same geometry at ``ratio`` times the rows
+        # (another batch size), when that choice is a legal candidate here; borrow_stats counts (hits, misses)
+        self.borrow: Optional[Dict] = None
+        self.borrow_stats = [0, 0]
         # multi-rank consensus: ``agree(times) -> times`` (e.g. ``DistState.agree_times``, the per-candidate
         # max over ranks) so that every data-parallel rank picks the same configuration
         self.agree: Optional[Callable[[List[float]], List[float]]] = None
@@ -175,6 +180,10 @@ class ConvTuner:
         launch needs an epilogue the direct / pointwise kernel lacks (fused residual output, bias, statistics
         without the output); ``halo=False``: an accumulating launch (the halo kernel only stores)."""
         cfg = self.cache.get(key)
+        if cfg is None and self.borrow is not None:
+            b = self.borrow_lookup("conv", key, len(key) - len(g))
+            if b is not None and (b == -1 or b in self.candidates(g, chunk, aff, epi, direct, pw, halo)):
+                cfg = self.cache[key] = b
         if cfg is None:
             self._pw_now = self.pw_kinds is None or (len(key) > 0 and key[0] in self.pw_kinds)
             cfg = self._tune(g, chunk, run, aff, epi, direct, pw, halo) if self.enabled else -1
@@ -182,6 +191,19 @@ class ConvTuner:
             self.cache[key] = cfg
         run(cfg, False)
         return cfg
+
+    def borrow_lookup(self, table: str, key: Tuple, m_index: int) -> Optional[int]:
+        """The borrowed table's choice for ``key`` with its row count (``key[m_index]``) scaled by the ratio, or None;
+        counts a hit or a miss."""
+        if self.borrow is None:
+            return None
+        r = self.borrow["ratio"]
+        m = key[m_index] * r
+        src = None
+        if abs(m - round(m)) < 1e-6:
+            src = self.borrow[table].get(key[:m_index] + (int(round(m)),) + key[m_index + 1:])
+        self.borrow_stats[0 if src is not None else 1] += 1
+        return src
 
     def time_candidates(self, cands: Sequence[int], trial: Callable[[int], None]) -> List[float]:
         """Per-candidate time (ms per launch), two-phase: every candidate once (after a warm-up launch), then the

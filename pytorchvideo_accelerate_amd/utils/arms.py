@@ -43,6 +43,9 @@ DEFAULTS: Dict[str, tuple] = {
     "narrow_bwd": (1, "r5_narrow"),
     "narrow_splits": (1024, "r5_narrow"),
     "narrow_fold": (1, "r5_narrow"),
+    # fp32 path (models/native32.py): bf16 pieces per fp32 conv operand — 3: fp32 accuracy (6 MFMA products),
+    # 2: ~16-bit operands (3 products, 2x the throughput; tests/test_native32_gpu.py measures both)
+    "f32_pieces": (3, "r6_f32"),
     # stem kernels (csrc/kernels/stem_s2d.hip reads these itself)
     "stem_pair": (1, "r4_stem"),
     "stem_perm": (1, "r5_end"),

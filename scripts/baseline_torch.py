@@ -57,8 +57,9 @@ def main():
         opt.zero_grad(set_to_none=True)
         return loss
 
-    for _ in range(a.warmup):
+    for i in range(a.warmup):
         step()
+        print(f"warmup step {i}", file=sys.stderr, flush=True)   # progress (a silent minute reads as a hang)
     torch.cuda.synchronize()
     times = []
     for _ in range(a.steps):
@@ -69,6 +70,7 @@ def main():
         e.record()
         e.synchronize()
         times.append(s.elapsed_time(e))
+        print(f"step {len(times)}: {times[-1]:.1f} ms", file=sys.stderr, flush=True)
     times.sort()
     p50 = times[len(times) // 2]
     mean = sum(times) / len(times)

@@ -107,7 +107,9 @@ t_benches() {
   IFS=';' read -ra arms <<< "$BENCHES"
   for arm in "${arms[@]}"; do
     i=$((i+1))
-    PVA_TUNE_LOG=1 timeout -k 10 500 python bench.py $arm > $out/benches$i.json 2> $out/benches$i.err || fail $out/benches$i.err
+    local envs=(PVA_TUNE_LOG=1) args=() tok
+    for tok in $arm; do if [[ $tok == PVA_*=* ]]; then envs+=("$tok"); else args+=("$tok"); fi; done
+    env "${envs[@]}" timeout -k 10 500 python bench.py "${args[@]}" > $out/benches$i.json 2> $out/benches$i.err || fail $out/benches$i.err
     echo "$arm: $(cat $out/benches$i.json)"
   done
 }

@@ -34,11 +34,12 @@ def _rel(a, b):
 def _step_vs_oracle(model, xs, labels):
     init = copy.deepcopy(model)
     oracle = copy.deepcopy(model).to(DEV).train()
-    loss_ref = F.cross_entropy(oracle([x.to(DEV) for x in xs]), labels)
+    xin = [x.to(DEV) for x in xs] if len(xs) > 1 else xs[0].to(DEV)   # Slow-R50 takes the clip itself
+    loss_ref = F.cross_entropy(oracle(xin), labels)
     loss_ref.backward()
     ac = copy.deepcopy(init).to(DEV).train()
     with torch.autocast("cuda", dtype=torch.bfloat16):
-        out_ac = ac([x.to(DEV) for x in xs])
+        out_ac = ac(xin)
     loss_ac = F.cross_entropy(out_ac.float(), labels)
     loss_ac.backward()
     eng = FusedNet(model, DEV)
@@ -83,6 +84,17 @@ def test_slowfast_r101_32x2x256_step_vs_fp32_oracle():
     xs = _clip(1, 32, 256, 4, seed=12)
     labels = torch.tensor([77], device=DEV)
     _check(*_step_vs_oracle(model, xs, labels))
+
+
+def test_slow_r50_8x8x224_step_vs_fp32_oracle():
+    """The reference's default model (run.py:338-351, is_slowfast=False: Slow-R50, 8 frames at sampling rate 8) at
+    full shape on the fused kernels, judged like the SlowFast steps above."""
+    torch.manual_seed(0)
+    model = R.create_resnet(50, 400, head_pool_kernel_size=(8, 7, 7), dropout_rate=0.0)
+    g = torch.Generator().manual_seed(13)
+    x = torch.randn(2, 3, 8, 224, 224, generator=g).to(torch.bfloat16).float()
+    labels = torch.tensor([5, 390], device=DEV)
+    _check(*_step_vs_oracle(model, [x], labels))
 
 
 def test_fixed_batch_memorisation_tracks_fp32_oracle():

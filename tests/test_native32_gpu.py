@@ -46,8 +46,12 @@ def _ndhwc(x, cp=None):
     return x.contiguous()
 
 
+@pytest.mark.parametrize("pieces", [3, 2])
 @pytest.mark.parametrize("case", CONVS)
-def test_conv32_fwd_dgrad_wgrad(case):
+def test_conv32_fwd_dgrad_wgrad(case, pieces, monkeypatch):
+    """pieces 3 (default): fp32-class error (~1e-7 relative to the fp64 oracle); pieces 2: ~1e-5."""
+    monkeypatch.setenv("PVA_ARMS", f"f32_pieces={pieces}")
+    tol = 2e-6 if pieces == 3 else 3e-5
     cin, cout, k, s, p, N, T, H, W = case
     F = require().f32
     g = torch.Generator().manual_seed(11)
@@ -64,8 +68,14 @@ def test_conv32_fwd_dgrad_wgrad(case):
     wf = torch.empty(cout, geo.ntap * geo.cip, device=DEV)
     F.wpack32(0, wd, wf, cout, cin, geo.ntap, geo.cip, 0.0)
     yd = torch.empty(N, *y.shape[2:], cout, device=DEV)
-    conv_fwd(F, geo, xd, wf, yd, geo.taps_fwd(DEV))
-    assert _rel(yd, _ndhwc(y.detach())) < 3e-5
+    M = yd.numel() // cout
+    st = torch.full((-(-M // F.igemm32_bm(cout)), 2, cout), float("nan"), device=DEV)
+    conv_fwd(F, geo, xd, wf, yd, geo.taps_fwd(DEV), stats=st)
+    assert _rel(yd, _ndhwc(y.detach())) < tol
+    # epilogue BatchNorm statistics: per-tile sums of y and y^2 (every tile row written)
+    y2 = yd.reshape(M, cout).double()
+    assert torch.isfinite(st).all()
+    assert _rel(st[:, 0].double().sum(0), y2.sum(0)) < 1e-5 and _rel(st[:, 1].double().sum(0), (y2 * y2).sum(0)) < 1e-5
     dyd = _ndhwc(dy).float().to(DEV)
     # weight gradient
     dwf = torch.empty(cout, geo.ntap * geo.cip, device=DEV)
@@ -73,11 +83,11 @@ def test_conv32_fwd_dgrad_wgrad(case):
     conv_wgrad(F, geo, dyd, xd, dwf, geo.taps_fwd(DEV))
     dw = torch.full_like(wd, 7.0)
     F.wpack32(2, dwf, dw, cout, cin, geo.ntap, geo.cip, 0.0)
-    assert _rel(dw, w.grad) < 3e-5
+    assert _rel(dw, w.grad) < tol
     # accumulate form (beta = 1)
     dw2 = dw.clone()
     F.wpack32(2, dwf, dw2, cout, cin, geo.ntap, geo.cip, 1.0)
-    assert _rel(dw2, 2 * w.grad) < 3e-5
+    assert _rel(dw2, 2 * w.grad) < tol
     if cin % 4:
         return
     wt = torch.empty(cin, geo.ntap, cout, device=DEV)
@@ -85,7 +95,7 @@ def test_conv32_fwd_dgrad_wgrad(case):
     dx = torch.full((N, T, H, W, cin), float("nan"), device=DEV)   # every position must be written
     conv_dgrad(F, geo, dyd, wt, dx, geo.phases(DEV))
     assert torch.isfinite(dx).all()
-    assert _rel(dx, _ndhwc(x.grad)) < 3e-5
+    assert _rel(dx, _ndhwc(x.grad)) < tol
 
 
 def test_dgrad_accumulate_phases():
@@ -109,7 +119,7 @@ def test_dgrad_accumulate_phases():
     cb._dgrad(dy, wt, acc, True)
     ref = torch.nn.grad.conv3d_input((2, 64, 2, 14, 14), conv.weight.detach().double(),
                                      dy.permute(0, 4, 1, 2, 3).double(), (1, 2, 2), (0, 1, 1))
-    assert _rel(acc - base, _ndhwc(ref)) < 3e-5
+    assert _rel(acc - base, _ndhwc(ref)) < 2e-6
 
 
 @pytest.mark.parametrize("C,M,relu,add", [(64, 3000, True, False), (8, 50000, True, True), (2048, 98, False, True),
@@ -227,7 +237,9 @@ def _net_case(slowfast: bool):
 def test_native32_net_matches_torch_fp32(slowfast):
     """One training step against an fp64 oracle (the same module tree in float64 on the CPU).  The stock PyTorch fp32
     GPU step (MIOpen) is measured against the same oracle as the fp32 noise floor: a 50-layer train-mode BN network at
-    B=2 amplifies per-op rounding, so agreement is judged relative to that floor."""
+    B=2 amplifies per-op rounding (stock fp32 itself lands ~1e-2 from fp64 in gradient rel-L2 here), so agreement is
+    judged relative to that floor: logits and the median / worst per-parameter gradient error within 3x of stock
+    fp32's (round 6 measured bf16x3 pieces at 7-10x: the reason the default is three pieces)."""
     import copy
     from pytorchvideo_accelerate_amd.models.native32 import NativeF32Net
     model, xs, labels = _net_case(slowfast)
@@ -258,9 +270,9 @@ def test_native32_net_matches_torch_fp32(slowfast):
           f"vs {loss64.item():.6f}; grad rel-L2 median ours {med(ours):.2e} stock {med(stock):.2e}; worst ours "
           f"{ours[worst]:.2e} ({worst}) stock {max(stock.values()):.2e}")
     assert abs(loss.item() - loss64.item()) < 1e-4 * max(1.0, abs(loss64.item()))
-    assert _prel(logits, out64) < max(1e-4, 4 * _prel(out32, out64))
-    assert med(ours) < 1e-3
-    assert ours[worst] < max(1e-2, 4 * max(stock.values())), (worst, ours[worst])
+    assert _prel(logits, out64) < max(1e-5, 3 * _prel(out32, out64))
+    assert med(ours) < max(1e-3, 3 * med(stock))
+    assert ours[worst] < max(1e-2, 3 * max(stock.values())), (worst, ours[worst])
     for (n, b), (_, b64) in zip(model.named_buffers(), ref64.named_buffers()):
         if b.dtype.is_floating_point:
             assert _prel(b, b64) < 1e-4, n
@@ -273,6 +285,57 @@ def test_native32_net_matches_torch_fp32(slowfast):
         e64 = ref64(x64)
     e = net.forward_eval(xs)
     assert _prel(e, e64) < 1e-4
+
+
+@pytest.mark.parametrize("arch", ["slowfast_r50", "slow_r50"])
+def test_native32_full_shape_vs_fp64(arch):
+    """Full-shape training step (SlowFast-R50 32x2x224; Slow-R50 8x8x224, the reference default model, run.py:338-351)
+    against an fp64 oracle of the same module tree on the GPU, with the stock PyTorch fp32 step (MIOpen) judged
+    against the same oracle as the fp32 floor.  Two correct fp32 executions of this network disagree in gradient
+    rel-L2 by ~1e-2 (BN + ReLU amplify rounding; round 6: the native fp32 executor vs stock fp32 at B=4 had median
+    2.6e-2 while the loss agreed to 3e-7), so the gates are relative to stock fp32's own error: median and worst
+    per-parameter gradient error at most 1.5x / 2x stock's, logits and loss at fp32 level."""
+    import copy
+    from pytorchvideo_accelerate_amd.models import reference as R
+    from pytorchvideo_accelerate_amd.models.native32 import NativeF32Net
+    torch.manual_seed(3)
+    g = torch.Generator().manual_seed(4)
+    B = 2
+    if arch == "slowfast_r50":
+        model = R.create_slowfast(50, 400, dropout_rate=0.0)
+        fast = torch.randn(B, 3, 32, 224, 224, generator=g)
+        xs = [fast[:, :, torch.linspace(0, 31, 8).long()].contiguous(), fast]
+    else:
+        model = R.create_resnet(50, 400, head_pool_kernel_size=(8, 7, 7), dropout_rate=0.0)
+        xs = torch.randn(B, 3, 8, 224, 224, generator=g)
+    labels = torch.randint(0, 400, (B,), generator=g)
+
+    def torch_step(dtype):
+        m = copy.deepcopy(model).to(DEV, dtype).train()
+        xin = [x.to(DEV, dtype) for x in xs] if isinstance(xs, list) else xs.to(DEV, dtype)
+        out = m(xin)
+        loss = Fnn.cross_entropy(out, labels.to(DEV))
+        loss.backward()
+        return m, out.detach(), loss.item()
+
+    m64, out64, loss64 = torch_step(torch.float64)
+    m32, out32, loss32 = torch_step(torch.float32)
+    net = NativeF32Net(model, DEV)
+    loss, logits = net.forward_backward(xs, labels, 1.0)
+    torch.cuda.synchronize()
+    g64, g32 = dict(m64.named_parameters()), dict(m32.named_parameters())
+    ours = {n: _prel(net.flat.gview(p), g64[n].grad) for n, p in model.named_parameters()}
+    stock = {n: _prel(g32[n].grad, g64[n].grad) for n in ours}
+    vs_stock = {n: _prel(net.flat.gview(p), g32[n].grad) for n, p in model.named_parameters()}
+    med = lambda d: sorted(d.values())[len(d) // 2]   # noqa: E731
+    print(f"\n{arch}: loss ours {loss.item():.7f} stock {loss32:.7f} fp64 {loss64:.7f}; logits rel ours "
+          f"{_prel(logits, out64):.2e} stock {_prel(out32, out64):.2e}; grad rel-L2 vs fp64 median ours {med(ours):.2e} "
+          f"stock {med(stock):.2e}, worst ours {max(ours.values()):.2e} stock {max(stock.values()):.2e}; ours vs "
+          f"stock median {med(vs_stock):.2e}")
+    assert abs(loss.item() - loss64) <= 2 * abs(loss32 - loss64) + 1e-6 * abs(loss64)
+    assert _prel(logits, out64) <= 2 * _prel(out32, out64) + 1e-6
+    assert med(ours) <= 1.5 * med(stock) + 1e-4
+    assert max(ours.values()) <= 2 * max(stock.values()) + 1e-4
 
 
 def test_native32_grad_accumulates_and_progress_hook():
