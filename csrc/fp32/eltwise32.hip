@@ -23,6 +23,8 @@ __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast
 __device__ __forceinline__ void st4(float* p, const float4& v) { *reinterpret_cast<float4*>(p) = v; }
 
 // mode 0: s1 = sum y, s2 = sum y^2.  mode 1: g = relu ? (o > 0 ? d : 0) : d; s1 = sum g, s2 = sum g*(y - mean).
+// Without o (an activation its consumers recompute, models/native32.py) the ReLU mask is fma(y, scale, shift) > 0 with
+// scale / shift the forward statistics rows 2 and 3 (``mean`` points at row 0 of that [4][C] table).
 // mode 3: column sums only, part[block][C] (second level of the conv epilogue's [tiles][2][N] statistics: C = 2N, so
 // the output is again [blocks][2][N]).
 __global__ __launch_bounds__(256) void chan_reduce32_kernel(const float* y, int ldy, const float* d, int ldd,
@@ -36,7 +38,7 @@ __global__ __launch_bounds__(256) void chan_reduce32_kernel(const float* y, int 
     const bool act = rm.rl < rm.RL && qq < rm.QC;
     float4 s1 = make_float4(0.f, 0.f, 0.f, 0.f), s2 = s1;
     if (act) {
-      if (mode == 0) {
+      if (mode == 0 || mode == 3) {
 #pragma unroll 4
         for (int64_t r = rb + rm.rl; r < re; r += rm.RL) {
           const float4 v = ld4(y + r * ldy + c);
@@ -46,15 +48,20 @@ __global__ __launch_bounds__(256) void chan_reduce32_kernel(const float* y, int 
         }
       } else {
         const float4 mu = ld4(mean + c);
+        const bool ymask = relu && o == nullptr;
+        const float4 sc = ld4(mean + (ymask ? 2 * C : 0) + c), sh = ld4(mean + (ymask ? 3 * C : 0) + c);
 #pragma unroll 4
         for (int64_t r = rb + rm.rl; r < re; r += rm.RL) {
           float4 g = ld4(d + r * ldd + c);
+          const float4 v = ld4(y + r * ldy + c);
           if (relu) {
-            const float4 ov = ld4(o + r * ldo + c);
+            float4 ov;
+            if (ymask) ov = make_float4(fmaf(v.x, sc.x, sh.x), fmaf(v.y, sc.y, sh.y), fmaf(v.z, sc.z, sh.z),
+                                        fmaf(v.w, sc.w, sh.w));
+            else ov = ld4(o + r * ldo + c);
             g.x = ov.x > 0.f ? g.x : 0.f; g.y = ov.y > 0.f ? g.y : 0.f;
             g.z = ov.z > 0.f ? g.z : 0.f; g.w = ov.w > 0.f ? g.w : 0.f;
           }
-          const float4 v = ld4(y + r * ldy + c);
           s1.x += g.x; s1.y += g.y; s1.z += g.z; s1.w += g.w;
           s2.x = fmaf(g.x, v.x - mu.x, s2.x); s2.y = fmaf(g.y, v.y - mu.y, s2.y);
           s2.z = fmaf(g.z, v.z - mu.z, s2.z); s2.w = fmaf(g.w, v.w - mu.w, s2.w);
@@ -167,6 +174,7 @@ __global__ __launch_bounds__(256) void bn32_apply_kernel(const float* y, int ldy
 }
 
 // g = relu ? (o > 0 ? d : 0) : d;  dy = k1*g + k2*(y - mean) + k3;  gout (optional) = g
+// (no o: the mask is fma(y, scale, shift) > 0 from the forward statistics fstat [4][C], as in chan_reduce32)
 __global__ __launch_bounds__(256) void bn32_bwd_apply_kernel(const float* d, int ldd, const float* o, int ldo,
                                                              int relu, const float* y, int ldy, const float* fstat,
                                                              const float* coef, float* dy, int lddy, float* gout,
@@ -177,14 +185,19 @@ __global__ __launch_bounds__(256) void bn32_bwd_apply_kernel(const float* d, int
     const int qq = qb + rm.q, c = 4 * qq;
     if (qq >= rm.QC) break;
     const float4 mu = ld4(fstat + c), k1 = ld4(coef + c), k2 = ld4(coef + C + c), k3 = ld4(coef + 2 * C + c);
+    const bool ymask = relu && o == nullptr;
+    const float4 sc = ld4(fstat + 2 * C + c), sh = ld4(fstat + 3 * C + c);
     for (int64_t r = (int64_t)blockIdx.x * rm.RL + rm.rl; r < M; r += (int64_t)gridDim.x * rm.RL) {
       float4 g = ld4(d + r * ldd + c);
+      const float4 v = ld4(y + r * ldy + c);
       if (relu) {
-        const float4 ov = ld4(o + r * ldo + c);
+        float4 ov;
+        if (ymask) ov = make_float4(fmaf(v.x, sc.x, sh.x), fmaf(v.y, sc.y, sh.y), fmaf(v.z, sc.z, sh.z),
+                                    fmaf(v.w, sc.w, sh.w));
+        else ov = ld4(o + r * ldo + c);
         g.x = ov.x > 0.f ? g.x : 0.f; g.y = ov.y > 0.f ? g.y : 0.f;
         g.z = ov.z > 0.f ? g.z : 0.f; g.w = ov.w > 0.f ? g.w : 0.f;
       }
-      const float4 v = ld4(y + r * ldy + c);
       const float4 r4 = make_float4(fmaf(k1.x, g.x, fmaf(k2.x, v.x - mu.x, k3.x)),
                                     fmaf(k1.y, g.y, fmaf(k2.y, v.y - mu.y, k3.y)),
                                     fmaf(k1.z, g.z, fmaf(k2.z, v.z - mu.z, k3.z)),

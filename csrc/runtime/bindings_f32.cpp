@@ -128,7 +128,9 @@ void register_fp32(pybind11::module& m) {
                           : (part.dim() == 3 && part.size(1) == 2 && part.size(2) == C),
                 "part must be [blocks][2][C] ([blocks][C] column sums in mode 3)");
     TORCH_CHECK(span(y) >= (M - 1) * ldy + C || M == 0, "chan_reduce32: y too small");
-    TORCH_CHECK(mode == 0 || (d.has_value() && mean.has_value() && (!relu || o.has_value())), "chan_reduce32 args");
+    TORCH_CHECK(mode == 0 || mode == 3 || (d.has_value() && mean.has_value()), "chan_reduce32 args");
+    // relu without o: the mask comes from the [4][C] forward statistics that mean is row 0 of
+    TORCH_CHECK(mode != 1 || !relu || o.has_value() || span(*mean) >= 4 * C, "chan_reduce32: mask needs o or stat");
     pva_f32::chan_reduce32_launch(fp(y, "y"), (int)ldy, fpo(d, "d"), (int)ldd, fpo(o, "o"), (int)ldo,
                                   fpo(mean, "mean"), (int)mode, (int)relu, M, (int)C, (int)part.size(0),
                                   fp(part, "part"), stream());
@@ -166,7 +168,7 @@ void register_fp32(pybind11::module& m) {
                              const at::Tensor& dy, int64_t lddy, const OptT& gout, int64_t ldg, int64_t M, int64_t C) {
     TORCH_CHECK(C % 4 == 0 && ldd % 4 == 0 && ldo % 4 == 0 && ldy % 4 == 0 && lddy % 4 == 0 && ldg % 4 == 0,
                 "bn32_bwd_apply: multiples of 4");
-    TORCH_CHECK(!relu || o.has_value(), "bn32_bwd_apply: relu needs the output");
+    TORCH_CHECK(fstat.numel() >= 4 * C, "bn32_bwd_apply: fstat [4][C]");   // (relu without o: mask from fstat)
     TORCH_CHECK(M == 0 || (span(d) >= (M - 1) * ldd + C && span(y) >= (M - 1) * ldy + C &&
                            span(dy) >= (M - 1) * lddy + C),
                 "bn32_bwd_apply: sizes");

@@ -33,6 +33,18 @@ def ordered_params(model: nn.Module):
     return [(n, p) for n, p in reversed(list(model.named_parameters()))]
 
 
+class Lazy:
+    """An activation its consumers recompute: relu(y * scale + shift) with scale / shift = rows 2 / 3 of the
+    BatchNorm table ``stat`` [4][C].  The next conv's operand loaders (forward and weight gradient) apply the affine and
+    the ReLU while staging, and the BatchNorm backward derives the ReLU mask from y — the normalised tensor is never
+    written (saves its write, and a read in every consumer and in the backward)."""
+
+    __slots__ = ("y", "stat", "shape")
+
+    def __init__(self, y: torch.Tensor, stat: torch.Tensor):
+        self.y, self.stat, self.shape = y, stat, y.shape
+
+
 class _ConvBN:
     """conv (bias-free) -> BatchNorm3d (training batch statistics or running statistics) -> optional ReLU."""
 
@@ -43,8 +55,9 @@ class _ConvBN:
         self.taps = self.g.taps_fwd(net.device)
         self.phases = self.g.phases(net.device) if conv.in_channels % 4 == 0 else None
 
-    def forward(self, x: torch.Tensor, train: bool, add: Optional[torch.Tensor] = None):
-        """Returns (out, saved) — saved is what backward needs (None in eval)."""
+    def forward(self, x, train: bool, add: Optional[torch.Tensor] = None, lazy: bool = False):
+        """Returns (out, saved) — saved is what backward needs (None in eval).  ``x`` may be a :class:`Lazy`
+        activation; ``lazy``: return this layer's output as one too (BN + ReLU applied by its consumers)."""
         F, g, dev = self.net.F, self.g, self.net.device
         N, T, H, W, _ = x.shape
         To, Ho, Wo = g.out_thw((T, H, W))
@@ -67,6 +80,10 @@ class _ConvBN:
         else:
             F.bn32_finalize(None, C, M, 2, bn.weight, bn.bias, bn.running_mean, bn.running_var, None,
                             bn.momentum, bn.eps, stat, None, None, None, None, 0.0)
+        if lazy:
+            assert self.relu and add is None
+            out = Lazy(y, stat)
+            return out, ((x, y, None, stat) if train else None)
         out = torch.empty_like(y)
         F.bn32_apply(y, C, stat, add, C, int(self.relu), out, C, M, C)
         return out, ((x, y, out, stat) if train else None)
@@ -83,6 +100,7 @@ class _ConvBN:
         dev = net.device
         bn = self.bn
         part = torch.empty(F.chan_reduce32_blocks(M, C), 2, C, device=dev)
+        # (a lazy output has no stored tensor: the ReLU mask is recomputed from y and the statistics)
         F.chan_reduce32(y, C, dout, C, out if self.relu else None, C, stat[0], 1, int(self.relu), M, C, part)
         coef = torch.empty(3, C, device=dev)
         gb = net.grad_beta
@@ -98,7 +116,7 @@ class _ConvBN:
         if self.conv.weight.requires_grad:
             dwf = torch.empty(C, g.ntap * g.cip, device=dev)
             F.zero32(dwf)
-            conv_wgrad(F, g, dy, x, dwf, self.taps)
+            conv_wgrad(F, g, dy, x, dwf, self.taps)   # (x may be Lazy: the loader applies its BN + ReLU)
             F.wpack32(2, dwf, net.flat.gview(self.conv.weight), C, g.cin, g.ntap, g.cip, gb)
             net.done(self.conv.weight)
         dx = None
@@ -147,8 +165,8 @@ class _ResUnit:
             s, ss = self.sc.forward(x, train)
         else:
             s, ss = x, None
-        a, sa = self.a.forward(x, train)
-        b, sb = self.b.forward(a, train)
+        a, sa = self.a.forward(x, train, lazy=True)    # conv_a / conv_b outputs: BN + ReLU applied by the consumer
+        b, sb = self.b.forward(a, train, lazy=True)
         out, sc = self.c.forward(b, train, add=s)
         return out, ((sa, sb, sc, ss) if train else None)
 

@@ -94,10 +94,18 @@ def pieces() -> int:
     return int(arm("f32_pieces"))
 
 
-def conv_fwd(F, g: ConvGeom, x: torch.Tensor, wf: torch.Tensor, y: torch.Tensor, taps: torch.Tensor,
+def _unlazy(x):
+    """(tensor, isc, ish, irelu) of a conv operand that may be a models.native32.Lazy activation."""
+    if hasattr(x, "stat") and hasattr(x, "y"):
+        return x.y, x.stat[2], x.stat[3], 1
+    return x, None, None, 0
+
+
+def conv_fwd(F, g: ConvGeom, x, wf: torch.Tensor, y: torch.Tensor, taps: torch.Tensor,
              stats: torch.Tensor = None):
     """y [N, To, Ho, Wo, Cout] = conv(x [N, T, H, W, cip]) with forward-packed weights wf [Cout][taps][cip];
     ``stats``: per-tile channel sums of y and y^2 ([ceil(M / igemm32_bm(Cout))][2][Cout]) from the epilogue."""
+    x, isc, ish, irelu = _unlazy(x)
     N, T, H, W, C = x.shape
     assert C == g.cip
     To, Ho, Wo = g.out_thw((T, H, W))
@@ -105,7 +113,7 @@ def conv_fwd(F, g: ConvGeom, x: torch.Tensor, wf: torch.Tensor, y: torch.Tensor,
     K = g.ntap * g.cip
     geo = [g.cip, K, g.cout, N * To * Ho * Wo, g.cout, K, g.cip, 0, To, Ho, Wo, T, H, W, *g.s, To, Ho, Wo,
            1, 1, 1, 0, 0, 0]
-    F.conv32(x, wf, y, taps, geo, np=pieces(), stats=stats)
+    F.conv32(x, wf, y, taps, geo, isc=isc, ish=ish, irelu=irelu, np=pieces(), stats=stats)
 
 
 def conv_dgrad(F, g: ConvGeom, dy: torch.Tensor, wt: torch.Tensor, dx: torch.Tensor, phases):
@@ -123,9 +131,10 @@ def conv_dgrad(F, g: ConvGeom, dy: torch.Tensor, wt: torch.Tensor, dx: torch.Ten
 
 
 def conv_wgrad(F, g: ConvGeom, dy: torch.Tensor, x: torch.Tensor, dwf: torch.Tensor, taps: torch.Tensor):
-    """dwf [Cout][taps*cip] += weight gradient (caller zeroes it)."""
+    """dwf [Cout][taps*cip] += weight gradient (caller zeroes it).  ``x`` may be a Lazy activation."""
+    x, isc, ish, irelu = _unlazy(x)
     N, T, H, W, C = x.shape
     To, Ho, Wo = dy.shape[1:4]
     K = g.ntap * g.cip
     geo = [g.cout, g.cip, K, g.cout, K, g.cip, N * To * Ho * Wo, To, Ho, Wo, T, H, W, *g.s]
-    F.wgrad32(dy, x, dwf, taps, geo, np=pieces())
+    F.wgrad32(dy, x, dwf, taps, geo, isc=isc, ish=ish, irelu=irelu, np=pieces())

@@ -170,6 +170,13 @@ def test_bn32_train_forward_backward(C, M, relu, add):
     gout = torch.empty(M, C, device=DEV)
     F.bn32_bwd_apply(dd, C, out if relu else None, C, int(relu), yd, C, stat, coef, dyd, C, gout, C, M, C)
     assert _rel(dyd, yr.grad) < 1e-4
+    if relu and not add:   # the lazy-activation form: no stored output, the ReLU mask recomputed from y and stat
+        part3 = torch.empty_like(part)
+        F.chan_reduce32(yd, C, dd, C, None, C, stat[0], 1, 1, M, C, part3)
+        assert torch.equal(part3, part2)
+        dy3 = torch.empty(M, C, device=DEV)
+        F.bn32_bwd_apply(dd, C, None, C, 1, yd, C, stat, coef, dy3, C, None, C, M, C)
+        assert torch.equal(dy3, dyd)
     assert _rel(dg - 100.0, gr.grad) < 1e-4
     assert _rel(db - 100.0, br.grad) < 1e-4
     if add:
