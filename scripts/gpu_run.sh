@@ -15,6 +15,7 @@
 #            R50 64x2x224 (B=112)
 #   runpy    the reference CLI (run.py) at the headline shape on a synthetic corpus
 #   kstats   rocprofv3 --stats of bench.py $KSTATS_ARGS: per-kernel totals (kernel_stats.csv + top-25 table)
+#   losstraj the bench recipe through the bf16 and fp32 executors side by side (diag_loss_trajectory.py, $LT_ARGS)
 #   benches  bench.py once per ";"-separated $BENCHES argument set
 #   stock    stock PyTorch eager baselines (scripts/baseline_torch.py) for each ";"-separated $STOCK argument set
 #   lab      tools/gemm_lab.hip: big-tile GEMM main loop at $LAB_SHAPES ("M,N,K ..."), cold and L2-hot A operand,
@@ -128,6 +129,11 @@ print(f"total kernel time {tot/1e6:.1f} ms over {sum(int(r['Calls']) for r in ro
 for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:25]:
     print(f"{float(r['TotalDurationNs'])/1e6:9.2f} ms {int(r['Calls']):6d}  {r['Name'][:110]}")
 PY
+}
+t_losstraj() {
+  # bench recipe through the fused bf16 and the native fp32 executors side by side (scripts/diag_loss_trajectory.py)
+  timeout -k 10 600 python -u scripts/diag_loss_trajectory.py ${LT_ARGS:---batch 48 --steps 8} > $out/loss_trajectory.jsonl 2> $out/loss_trajectory.err || fail $out/loss_trajectory.err
+  tail -1 $out/loss_trajectory.jsonl
 }
 t_stock() {
   # stock PyTorch-ROCm eager baselines (scripts/baseline_torch.py), one run per ";"-separated argument set
