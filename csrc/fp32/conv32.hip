@@ -56,6 +56,17 @@ __device__ __forceinline__ void split8(float (&f)[8], uint4 (&o)[NP]) {
   }
 }
 
+// n / d for 0 <= n < 2^31 with the host-computed (m, s) of magic_div
+__device__ __forceinline__ int fdiv(int n, unsigned m, int s) {
+  return (int)((__umulhi((unsigned)n, m) + (unsigned)n) >> s);
+}
+static void magic_div(int d, unsigned* m, int* s) {
+  int k = 0;
+  while ((1LL << k) < d) ++k;
+  *s = k;
+  *m = (unsigned)((((1ULL << 32) * ((1ULL << k) - (unsigned long long)d)) / (unsigned long long)d + 1) & 0xffffffffULL);
+}
+
 __device__ __forceinline__ int chunk_off(int r, int c) { return r * 64 + ((c ^ ((r >> 1) & 3)) << 4); }
 
 __device__ __forceinline__ float4 affine4(float4 v, const float4& s, const float4& h, int relu) {
@@ -110,12 +121,18 @@ __device__ __forceinline__ void mma_split(const uint8_t* sA, int rowsA, const ui
   }
 }
 
-template <int NP, int BM, int BN, int WGM>
+// A operand loads go through a buffer resource rebased to the first clip this tile's rows read (32-bit offsets, no
+// 64-bit address math): per row, the position part of the offset is fixed for the whole k loop (VGPR) and the tap +
+// channel part is wave-uniform (SGPR soffset) when the k-step lies inside one tap (UNI: Cr % 32 == 0); an
+// out-of-range tap position or a row past M gets an offset past the resource, which loads zeros in hardware.  B rows
+// are the pre-split weight planes (wpack32: piece p of row n at p * wplane + n * ldw), stored to LDS as loaded.
+template <int NP, int BM, int BN, int WGM, bool UNI>
 __global__ __launch_bounds__(256) void igemm32_kernel(const Conv32 p) {
   constexpr int WGN = 4 / WGM, TM = BM / WGM, TN = BN / WGN, FM = TM / 16, FN = TN / 16;
   constexpr int LA = (BM + 31) / 32, LB = (BN + 31) / 32;
   constexpr int NBUF = NP == 2 ? 2 : 1;   // NP = 3 images are 1.5x larger: one buffer, two barriers per step
   constexpr int IMG = NP * (BM + BN) * 64;
+  constexpr unsigned OOB = 0x80000000u;
   static_assert(FM >= 1 && FN >= 1 && TM % 16 == 0 && TN % 16 == 0, "wave tile");
   __shared__ __attribute__((aligned(16))) uint8_t smem[NBUF][IMG];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -123,62 +140,90 @@ __global__ __launch_bounds__(256) void igemm32_kernel(const Conv32 p) {
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
   const int kq = tid & 7, r0 = tid >> 3;
   const int HWi = p.Hi * p.Wi;
-  int64_t abase[LA];
+  const int Q = p.Qt * p.Qh * p.Qw;
+  const int64_t clip = (int64_t)p.Ti * HWi * p.ldx;   // elements per input clip
+  const int nbf = m0 / Q, nbl = min(m0 + BM - 1, p.M - 1) / Q;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(p.x + nbf * clip), (short)0, (int)((nbl - nbf + 1) * clip * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, 3 * p.wplane * 2,
+                                                                      0x00020000);
+  // per A row: position offset in bytes (channel quad kq included) and the tap-free input coordinates
+  unsigned aoff[LA];
   int at[LA], ahh[LA], aww[LA];
-  bool aval[LA];
 #pragma unroll
   for (int i = 0; i < LA; ++i) {
     const int r = r0 + 32 * i, m = m0 + r;
-    aval[i] = r < BM && m < p.M;
-    int mm = aval[i] ? m : 0;
+    const bool ok = r < BM && m < p.M;
+    int mm = ok ? m : 0;
     const int qw = mm % p.Qw;
     mm /= p.Qw;
     const int qh = mm % p.Qh;
     mm /= p.Qh;
     const int qt = mm % p.Qt, nb = mm / p.Qt;
-    abase[i] = (int64_t)nb * p.Ti * HWi;
-    at[i] = qt * p.st;
+    at[i] = ok ? qt * p.st : -(1 << 20);   // a row past M fails every bounds test
     ahh[i] = qh * p.sh;
     aww[i] = qw * p.sw;
+    aoff[i] = (unsigned)((((int64_t)(nb - nbf) * p.Ti * HWi + (int64_t)at[i] * HWi + ahh[i] * p.Wi + aww[i]) * p.ldx +
+                          4 * kq) * 4);
   }
-  float4 ra[LA], rb[LB];
+  unsigned boff[LB];
+#pragma unroll
+  for (int i = 0; i < LB; ++i) {
+    const int r = r0 + 32 * i, n = n0 + r;
+    boff[i] = (r < BN && n < p.N) ? (unsigned)((n * p.ldw + 4 * kq) * 2) : OOB;
+  }
+  f32x4_t ra[LA];
+  uint2 rb[LB][NP];
   const int nk = (p.K + 31) / 32;
-  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  const f32x4_t z4 = {0.f, 0.f, 0.f, 0.f};
+  int tj = 0, tc = 0;   // UNI: tap index and channel base of the next k-step to load (wave-uniform)
 
   auto load = [&](int kt) {
-    const int k = kt * 32 + 4 * kq;
-    const bool kv = k < p.K;
-    int c = 0;
-    int4 tp = make_int4(0, 0, 0, 0);
-    if (kv) {
-      const int j = k / p.Cr;
-      c = k - j * p.Cr;
-      tp = reinterpret_cast<const int4*>(p.taps)[j];
+    int dt, dh, dw, widx, c;   // c: this lane's first channel (UNI: + 4 kq is inside aoff)
+    bool kv = true;
+    if constexpr (UNI) {
+      const int4 tp = reinterpret_cast<const int4*>(p.taps)[tj];
+      dt = tp.x; dh = tp.y; dw = tp.z; widx = tp.w;
+      c = tc;
+      tc += 32;
+      if (tc == p.Cr) { tc = 0; ++tj; }
+    } else {
+      const int k = kt * 32 + 4 * kq;
+      kv = k < p.K;
+      const int j = kv ? k / p.Cr : 0;
+      c = k - j * p.Cr - 4 * kq;
+      const int4 tp = reinterpret_cast<const int4*>(p.taps)[j];
+      dt = tp.x; dh = tp.y; dw = tp.z; widx = tp.w;
     }
-    float4 sc = z4, sh = z4;
-    if (p.isc != nullptr && kv) {
-      sc = *reinterpret_cast<const float4*>(p.isc + c);
-      sh = *reinterpret_cast<const float4*>(p.ish + c);
+    const int toff = ((dt * p.Hi + dh) * p.Wi + dw) * p.ldx + c;   // elements
+    f32x4_t sc = z4, sh = z4;
+    const bool aff = p.isc != nullptr;
+    if (aff) {
+      sc = *reinterpret_cast<const f32x4_t*>(p.isc + c + 4 * kq);
+      sh = *reinterpret_cast<const f32x4_t*>(p.ish + c + 4 * kq);
     }
 #pragma unroll
     for (int i = 0; i < LA; ++i) {
-      ra[i] = z4;
-      if (kv && aval[i]) {
-        const int ti = at[i] + tp.x, hi = ahh[i] + tp.y, wi = aww[i] + tp.z;
-        if ((unsigned)ti < (unsigned)p.Ti && (unsigned)hi < (unsigned)p.Hi && (unsigned)wi < (unsigned)p.Wi) {
-          const float* src = p.x + (abase[i] + (int64_t)ti * HWi + hi * p.Wi + wi) * p.ldx + c;
-          ra[i] = *reinterpret_cast<const float4*>(src);
-          if (p.isc != nullptr) ra[i] = affine4(ra[i], sc, sh, p.irelu);
-        }
+      const bool ok = kv && (unsigned)(at[i] + dt) < (unsigned)p.Ti && (unsigned)(ahh[i] + dh) < (unsigned)p.Hi &&
+                      (unsigned)(aww[i] + dw) < (unsigned)p.Wi;
+      // (the whole offset in the VGPR: the hardware range check does not cover a negative tap offset in soffset)
+      f32x4_t v = __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(
+                                                  xr, ok ? aoff[i] + (unsigned)(toff * 4) : OOB, 0, 0));
+      if (aff) {
+        v = v * sc + sh;
+        if (p.irelu) v = __builtin_elementwise_max(v, z4);
+        v = ok ? v : z4;   // padding stays zero after the transform
       }
+      ra[i] = v;
     }
+    const int wk = (widx * p.Cr + c) * 2;   // bytes
 #pragma unroll
-    for (int i = 0; i < LB; ++i) {
-      rb[i] = z4;
-      const int r = r0 + 32 * i, n = n0 + r;
-      if (kv && r < BN && n < p.N)
-        rb[i] = *reinterpret_cast<const float4*>(p.w + (int64_t)n * p.ldw + tp.w * p.Cr + c);
-    }
+    for (int i = 0; i < LB; ++i)
+#pragma unroll
+      for (int q = 0; q < NP; ++q) {
+        const unsigned o = UNI ? boff[i] : (kv ? boff[i] + wk : OOB);
+        rb[i][q] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(wr, o, (UNI ? wk : 0) + q * p.wplane * 2, 0));
+      }
   };
   auto store = [&](uint8_t* img) {
     const int hc = kq >> 1, ho = (kq & 1) << 3;
@@ -187,7 +232,7 @@ __global__ __launch_bounds__(256) void igemm32_kernel(const Conv32 p) {
       const int r = r0 + 32 * i;
       if (r < BM) {
         uint2 o[NP];
-        split4<NP>(ra[i], o);
+        split4<NP>(float4{ra[i][0], ra[i][1], ra[i][2], ra[i][3]}, o);
         const int off = chunk_off(r, hc) + ho;
 #pragma unroll
         for (int q = 0; q < NP; ++q) *reinterpret_cast<uint2*>(img + q * BM * 64 + off) = o[q];
@@ -198,11 +243,9 @@ __global__ __launch_bounds__(256) void igemm32_kernel(const Conv32 p) {
     for (int i = 0; i < LB; ++i) {
       const int r = r0 + 32 * i;
       if (r < BN) {
-        uint2 o[NP];
-        split4<NP>(rb[i], o);
         const int off = chunk_off(r, hc) + ho;
 #pragma unroll
-        for (int q = 0; q < NP; ++q) *reinterpret_cast<uint2*>(imgB + q * BN * 64 + off) = o[q];
+        for (int q = 0; q < NP; ++q) *reinterpret_cast<uint2*>(imgB + q * BN * 64 + off) = rb[i][q];
       }
     }
   };
@@ -354,12 +397,10 @@ __global__ __launch_bounds__(256) void wgrad32_kernel(const Wgrad32 p) {
     const bool aff = kkv && p.isc != nullptr;
     const f32x4_t isc = *reinterpret_cast<const f32x4_t*>(aff ? p.isc + xc : p.x);   // (always a global address)
     const f32x4_t ish = *reinterpret_cast<const f32x4_t*>(aff ? p.ish + xc : p.x);
-    int mm = pos < p_end ? pos : 0;
-    int qw = mm % p.Qw;
-    mm /= p.Qw;
-    int qh = mm % p.Qh;
-    mm /= p.Qh;
-    int qt = mm % p.Qt, nb = mm / p.Qt;
+    const int m0p = pos < p_end ? pos : 0;
+    const int m1 = fdiv(m0p, p.mqw, p.sqw), m2 = fdiv(m1, p.mqh, p.sqh);
+    int qw = m0p - m1 * p.Qw, qh = m1 - m2 * p.Qh;
+    int nb = fdiv(m2, p.mqt, p.sqt), qt = m2 - nb * p.Qt;
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       {
@@ -427,24 +468,34 @@ __global__ __launch_bounds__(256) void wgrad32_kernel(const Wgrad32 p) {
 }
 
 // ---------------------------------------------------------------- weight layouts
-// torch w[co][ci][tap] -> forward B rows wf[co][tap][cip] (zero channels ci >= Cin)
-__global__ void wpack_fwd_kernel(const float* w, float* wf, int Cout, int Cin, int taps, int cip) {
+// the three bf16 pieces of an fp32 weight (the same split as split4<3>), one per plane
+__device__ __forceinline__ void put_split3(uint16_t* dst, int64_t i, int64_t plane, float v) {
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const uint32_t b = cvt_pk_e16(v, 0.f);
+    dst[q * plane + i] = (uint16_t)(b & 0xffffu);
+    v -= lo2f(b);
+  }
+}
+
+// torch w[co][ci][tap] -> forward B rows wf[piece][co][tap][cip] (zero channels ci >= Cin)
+__global__ void wpack_fwd_kernel(const float* w, uint16_t* wf, int Cout, int Cin, int taps, int cip) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, n = (int64_t)Cout * taps * cip;
   if (i >= n) return;
   const int c = i % cip;
   const int64_t t = i / cip;
   const int tap = t % taps, co = t / taps;
-  wf[i] = c < Cin ? w[((int64_t)co * Cin + c) * taps + tap] : 0.f;
+  put_split3(wf, i, n, c < Cin ? w[((int64_t)co * Cin + c) * taps + tap] : 0.f);
 }
 
-// torch w[co][ci][tap] -> input-gradient B rows wt[ci][tap][co]
-__global__ void wpack_dgrad_kernel(const float* w, float* wt, int Cout, int Cin, int taps) {
+// torch w[co][ci][tap] -> input-gradient B rows wt[piece][ci][tap][co]
+__global__ void wpack_dgrad_kernel(const float* w, uint16_t* wt, int Cout, int Cin, int taps) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, n = (int64_t)Cout * taps * Cin;
   if (i >= n) return;
   const int co = i % Cout;
   const int64_t t = i / Cout;
   const int tap = t % taps, ci = t / taps;
-  wt[i] = w[((int64_t)co * Cin + ci) * taps + tap];
+  put_split3(wt, i, n, w[((int64_t)co * Cin + ci) * taps + tap]);
 }
 
 // wgrad layout dwf[co][tap][cip] -> torch g[co][ci][tap] (= beta*g + value)
@@ -462,7 +513,8 @@ __global__ void wunpack_kernel(const float* dwf, float* g, int Cout, int Cin, in
 template <int NP, int BM, int BN, int WGM>
 static void igemm_go(const Conv32& p, hipStream_t s) {
   dim3 grid((p.M + BM - 1) / BM, (p.N + BN - 1) / BN);
-  hipLaunchKernelGGL((igemm32_kernel<NP, BM, BN, WGM>), grid, dim3(256), 0, s, p);
+  if (p.Cr % 32 == 0) hipLaunchKernelGGL((igemm32_kernel<NP, BM, BN, WGM, true>), grid, dim3(256), 0, s, p);
+  else hipLaunchKernelGGL((igemm32_kernel<NP, BM, BN, WGM, false>), grid, dim3(256), 0, s, p);
 }
 
 int igemm32_tile(int N) { return N > 64 ? 0 : N > 32 ? 1 : N > 16 ? 2 : 3; }
@@ -522,22 +574,25 @@ void wgrad32_launch(Wgrad32 p, int np, hipStream_t s) {
   splits = splits < 1 ? 1 : splits > stages ? stages : splits;
   p.chunk = ((stages + splits - 1) / splits) * 32;
   splits = (p.P + p.chunk - 1) / p.chunk;
+  magic_div(p.Qw, &p.mqw, &p.sqw);
+  magic_div(p.Qh, &p.mqh, &p.sqh);
+  magic_div(p.Qt, &p.mqt, &p.sqt);
   if (np == 2) wgrad_np<2>(p, bm, bn, splits, s);
   else wgrad_np<3>(p, bm, bn, splits, s);
 }
 
-void wpack32_launch(int mode, const float* src, float* dst, int Cout, int Cin, int taps, int cip, float beta,
+void wpack32_launch(int mode, const float* src, void* dst, int Cout, int Cin, int taps, int cip, float beta,
                     hipStream_t s) {
   const int64_t n = mode == 1 ? (int64_t)Cout * taps * Cin : mode == 0 ? (int64_t)Cout * taps * cip
                                                                        : (int64_t)Cout * Cin * taps;
   if (n == 0) return;
   const int blocks = (int)((n + 255) / 256);
   if (mode == 0)
-    hipLaunchKernelGGL(wpack_fwd_kernel, dim3(blocks), dim3(256), 0, s, src, dst, Cout, Cin, taps, cip);
+    hipLaunchKernelGGL(wpack_fwd_kernel, dim3(blocks), dim3(256), 0, s, src, (uint16_t*)dst, Cout, Cin, taps, cip);
   else if (mode == 1)
-    hipLaunchKernelGGL(wpack_dgrad_kernel, dim3(blocks), dim3(256), 0, s, src, dst, Cout, Cin, taps);
+    hipLaunchKernelGGL(wpack_dgrad_kernel, dim3(blocks), dim3(256), 0, s, src, (uint16_t*)dst, Cout, Cin, taps);
   else
-    hipLaunchKernelGGL(wunpack_kernel, dim3(blocks), dim3(256), 0, s, src, dst, Cout, Cin, taps, cip, beta);
+    hipLaunchKernelGGL(wunpack_kernel, dim3(blocks), dim3(256), 0, s, src, (float*)dst, Cout, Cin, taps, cip, beta);
 }
 
 }  // namespace pva_f32

@@ -10,7 +10,7 @@ int igemm32_bm(int N);   // output-position rows per workgroup (= rows per stati
 void igemm32_launch(const Conv32& p, int np, hipStream_t s);   // np: bf16 pieces per fp32 operand (2 or 3)
 void wgrad32_tile(int K, int Cout, int* bm, int* bn);
 void wgrad32_launch(Wgrad32 p, int np, hipStream_t s);
-void wpack32_launch(int mode, const float* src, float* dst, int Cout, int Cin, int taps, int cip, float beta,
+void wpack32_launch(int mode, const float* src, void* dst, int Cout, int Cin, int taps, int cip, float beta,
                     hipStream_t s);
 int chan_reduce32_blocks(int64_t M, int C);
 void chan_reduce32_launch(const float* y, int ldy, const float* d, int ldd, const float* o, int ldo, const float* mean,

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include "../fp32/launchers32.h"
+#include <algorithm>
 #include <cstddef>
 
 static_assert(offsetof(Conv32, orw) - offsetof(Conv32, ldx) == 25 * sizeof(int), "Conv32 integer block contiguous");
@@ -38,7 +39,12 @@ void conv32(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, const
   TORCH_CHECK(g.size() == 26, "conv32 geometry has 26 entries");
   Conv32 p{};
   p.x = fp(x, "x");
-  p.w = fp(w, "w");
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.is_contiguous() && w.numel() % 3 == 0,
+              "conv32: w must be the three bf16 weight planes of wpack32 (mode 0 / 1)");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0, "w must be 16-B aligned");
+  p.w = reinterpret_cast<const uint16_t*>(w.data_ptr());
+  TORCH_CHECK(w.numel() / 3 * 6 < (int64_t(1) << 31), "conv32: weight planes exceed 2 GB");
+  p.wplane = (int)(w.numel() / 3);
   p.y = fp(y, "y");
   TORCH_CHECK(taps.is_cuda() && taps.scalar_type() == at::kInt, "taps must be int32 GPU");
   p.taps = taps.data_ptr<int>();
@@ -56,7 +62,12 @@ void conv32(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, const
   const int64_t nb = p.M / Q;
   TORCH_CHECK(span(x) >= (nb * p.Ti * p.Hi * p.Wi - 1) * p.ldx + p.Cr || p.M == 0, "conv32: x too small");
   TORCH_CHECK(span(y) >= (nb * p.Yt * p.Yh * p.Yw - 1) * p.ldy + p.N || p.M == 0, "conv32: y too small");
-  TORCH_CHECK(span(w) >= ((int64_t)p.N - 1) * p.ldw + p.K || p.N == 0, "conv32: w too small");
+  TORCH_CHECK((int64_t)p.wplane >= ((int64_t)p.N - 1) * p.ldw + p.K || p.N == 0, "conv32: w too small");
+  {  // the A loads address the clips one tile's rows read through a buffer resource with a 32-bit byte range
+    const int64_t bm = pva_f32::igemm32_bm(p.N), clips = std::min<int64_t>(nb, bm / Q + 2);
+    TORCH_CHECK(clips * p.Ti * p.Hi * p.Wi * (int64_t)p.ldx * 4 < (int64_t(1) << 31),
+                "conv32: one tile's input clips exceed the 2 GB buffer range");
+  }
   TORCH_CHECK((p.Qt - 1) * p.ost + p.ort < p.Yt && (p.Qh - 1) * p.osh + p.orh < p.Yh &&
                   (p.Qw - 1) * p.osw + p.orw < p.Yw,
               "conv32: output grid exceeds the output tensor");
@@ -116,9 +127,18 @@ void register_fp32(pybind11::module& m) {
                       int64_t taps, int64_t cip, double beta) {
     const int64_t n = mode == 1 ? Cout * taps * Cin : mode == 0 ? Cout * taps * cip : Cout * Cin * taps;
     const int64_t ns = mode == 2 ? Cout * taps * cip : Cout * Cin * taps;
-    TORCH_CHECK(dst.numel() >= n && src.numel() >= ns && cip >= Cin, "wpack32: sizes");
-    pva_f32::wpack32_launch((int)mode, fp(src, "src", false), fp(dst, "dst", false), (int)Cout, (int)Cin, (int)taps,
-                            (int)cip, (float)beta, stream());
+    void* d;
+    if (mode == 2) {   // gradient unpack: fp32 torch layout
+      TORCH_CHECK(dst.numel() >= n, "wpack32: sizes");
+      d = fp(dst, "dst", false);
+    } else {           // forward / input-gradient B rows: three bf16 planes of n elements
+      TORCH_CHECK(dst.is_cuda() && dst.scalar_type() == at::kBFloat16 && dst.is_contiguous() && dst.numel() == 3 * n,
+                  "wpack32: mode 0 / 1 write three bf16 planes of the packed rows");
+      d = dst.data_ptr();
+    }
+    TORCH_CHECK(src.numel() >= ns && cip >= Cin, "wpack32: sizes");
+    pva_f32::wpack32_launch((int)mode, fp(src, "src", false), d, (int)Cout, (int)Cin, (int)taps, (int)cip,
+                            (float)beta, stream());
   });
   f.def("chan_reduce32_blocks", [](int64_t M, int64_t C) { return (int64_t)pva_f32::chan_reduce32_blocks(M, (int)C); });
   f.def("chan_reduce32", [](const at::Tensor& y, int64_t ldy, const OptT& d, int64_t ldd, const OptT& o, int64_t ldo,

@@ -23,7 +23,7 @@ import torch
 import torch.nn as nn
 
 from ..ops._ext import require
-from ..ops.f32 import ConvGeom, conv_dgrad, conv_fwd, conv_wgrad, pieces
+from ..ops.f32 import ConvGeom, conv_dgrad, conv_fwd, conv_wgrad, pack_weight, pieces
 from . import reference as R
 from .fused import FlatParams
 
@@ -62,8 +62,7 @@ class _ConvBN:
         N, T, H, W, _ = x.shape
         To, Ho, Wo = g.out_thw((T, H, W))
         C = g.cout
-        wf = torch.empty(C, g.ntap * g.cip, device=dev)
-        F.wpack32(0, self.conv.weight, wf, C, g.cin, g.ntap, g.cip, 0.0)
+        wf = pack_weight(F, g, self.conv.weight, 0)
         y = torch.empty(N, To, Ho, Wo, C, device=dev)
         M = N * To * Ho * Wo
         tiles = -(-M // F.igemm32_bm(C))
@@ -122,8 +121,7 @@ class _ConvBN:
         dx = None
         if need_dx:
             assert self.phases is not None, "input gradient of a padded-channel conv"
-            wt = torch.empty(g.cin, g.ntap, C, device=dev)
-            F.wpack32(1, self.conv.weight, wt, C, g.cin, g.ntap, g.cip, 0.0)
+            wt = pack_weight(F, g, self.conv.weight, 1)
             if dx_acc is not None:
                 dx = dx_acc
                 geo_acc = True

@@ -94,6 +94,16 @@ def pieces() -> int:
     return int(arm("f32_pieces"))
 
 
+def pack_weight(F, g: ConvGeom, w: torch.Tensor, mode: int) -> torch.Tensor:
+    """The implicit GEMM's B rows of a torch weight ``[Cout, Cin, kt, kh, kw]`` (fp32), pre-split into the three bf16
+    pieces the kernels multiply (``[3][rows][K]``): mode 0 forward rows ``[Cout][taps][cip]``, mode 1 input-gradient
+    rows ``[Cin][taps][Cout]``.  Split once per step here instead of once per output tile in every launch."""
+    rows, K = (g.cout, g.ntap * g.cip) if mode == 0 else (g.cin, g.ntap * g.cout)
+    out = torch.empty(3, rows, K, device=w.device, dtype=torch.bfloat16)
+    F.wpack32(mode, w, out, g.cout, g.cin, g.ntap, g.cip, 0.0)
+    return out
+
+
 def _unlazy(x):
     """(tensor, isc, ish, irelu) of a conv operand that may be a models.native32.Lazy activation."""
     if hasattr(x, "stat") and hasattr(x, "y"):
@@ -103,7 +113,7 @@ def _unlazy(x):
 
 def conv_fwd(F, g: ConvGeom, x, wf: torch.Tensor, y: torch.Tensor, taps: torch.Tensor,
              stats: torch.Tensor = None):
-    """y [N, To, Ho, Wo, Cout] = conv(x [N, T, H, W, cip]) with forward-packed weights wf [Cout][taps][cip];
+    """y [N, To, Ho, Wo, Cout] = conv(x [N, T, H, W, cip]) with forward-packed weights wf (pack_weight mode 0);
     ``stats``: per-tile channel sums of y and y^2 ([ceil(M / igemm32_bm(Cout))][2][Cout]) from the epilogue."""
     x, isc, ish, irelu = _unlazy(x)
     N, T, H, W, C = x.shape
@@ -117,7 +127,7 @@ def conv_fwd(F, g: ConvGeom, x, wf: torch.Tensor, y: torch.Tensor, taps: torch.T
 
 
 def conv_dgrad(F, g: ConvGeom, dy: torch.Tensor, wt: torch.Tensor, dx: torch.Tensor, phases):
-    """dx [N, T, H, W, cin] = input gradient of dy [N, To, Ho, Wo, Cout] (wt = [cin][taps][Cout])."""
+    """dx [N, T, H, W, cin] = input gradient of dy [N, To, Ho, Wo, Cout] (wt = pack_weight mode 1)."""
     N, T, H, W, C = dx.shape
     assert C == g.cin and C % 4 == 0
     To, Ho, Wo = dy.shape[1:4]

@@ -11,6 +11,7 @@
 #   layers   serialised per-op profile at B=$BATCH (default 160) + roofline table
 #   trace    rocprofv3 kernel trace of 3 steps -> steady-state kernel table
 #   pmc      rocprofv3 PMC passes (one run each) over a bench step at B=$BATCH -> per-kernel summary
+#            ($PMC_ARGS replaces "--batch $BATCH", $PMC_TAG the summary's suffix, e.g. the fp32 path)
 #   cfg      non-headline configs: bench + serialised per-op profile + roofline for R101 32x2x256 (B=160) and
 #            R50 64x2x224 (B=112)
 #   runpy    the reference CLI (run.py) at the headline shape on a synthetic corpus
@@ -66,13 +67,13 @@ t_trace() {
 }
 t_pmc() {
   local P1="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE"
-  local i=0
+  local i=0 tag=${PMC_TAG:-b$B}
   for P in "$P1" "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
     i=$((i+1))
-    timeout -k 10 420 rocprofv3 --pmc $P --kernel-trace --output-format csv -d $out/pmc/p$i -o p -- python3 bench.py --steps 2 --warmup 1 --batch $B > $out/pmc_p$i.log 2>&1 || fail $out/pmc_p$i.log 5
+    timeout -k 10 420 rocprofv3 --pmc $P --kernel-trace --output-format csv -d $out/pmc/p$i -o p -- python3 bench.py --steps 2 --warmup 1 ${PMC_ARGS:---batch $B} > $out/pmc_${tag}_p$i.log 2>&1 || fail $out/pmc_${tag}_p$i.log 5
   done
   # raw per-dispatch CSVs are large (gpurun copies back at most 64 MiB): keep the summary only
-  python3 scripts/pmc_step_summary.py $out/pmc > $out/pmc_summary_b$B.txt && rm -rf $out/pmc && head -30 $out/pmc_summary_b$B.txt
+  python3 scripts/pmc_step_summary.py $out/pmc > $out/pmc_summary_$tag.txt && rm -rf $out/pmc && head -30 $out/pmc_summary_$tag.txt
 }
 t_cfg() {
   local spec tag args

@@ -13,7 +13,7 @@ import torch
 import torch.nn.functional as Fnn
 
 from pytorchvideo_accelerate_amd.ops._ext import require
-from pytorchvideo_accelerate_amd.ops.f32 import ConvGeom, conv_dgrad, conv_fwd, conv_wgrad
+from pytorchvideo_accelerate_amd.ops.f32 import ConvGeom, conv_dgrad, conv_fwd, conv_wgrad, pack_weight
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -65,8 +65,7 @@ def test_conv32_fwd_dgrad_wgrad(case, pieces, monkeypatch):
     geo = ConvGeom(cin, cout, k, s, p, cip=(cin + 3) // 4 * 4)
     xd = _ndhwc(x.detach(), geo.cip).float().to(DEV)
     wd = w.detach().float().to(DEV).contiguous()
-    wf = torch.empty(cout, geo.ntap * geo.cip, device=DEV)
-    F.wpack32(0, wd, wf, cout, cin, geo.ntap, geo.cip, 0.0)
+    wf = pack_weight(F, geo, wd, 0)
     yd = torch.empty(N, *y.shape[2:], cout, device=DEV)
     M = yd.numel() // cout
     st = torch.full((-(-M // F.igemm32_bm(cout)), 2, cout), float("nan"), device=DEV)
@@ -90,12 +89,31 @@ def test_conv32_fwd_dgrad_wgrad(case, pieces, monkeypatch):
     assert _rel(dw2, 2 * w.grad) < tol
     if cin % 4:
         return
-    wt = torch.empty(cin, geo.ntap, cout, device=DEV)
-    F.wpack32(1, wd, wt, cout, cin, geo.ntap, geo.cip, 0.0)
+    wt = pack_weight(F, geo, wd, 1)
     dx = torch.full((N, T, H, W, cin), float("nan"), device=DEV)   # every position must be written
     conv_dgrad(F, geo, dyd, wt, dx, geo.phases(DEV))
     assert torch.isfinite(dx).all()
     assert _rel(dx, _ndhwc(x.grad)) < tol
+
+
+def test_pack_weight_planes():
+    """wpack32 modes 0 / 1: three bf16 pieces whose sum is the fp32 weight (24 significant bits) in the forward
+    ([Cout][taps][cip], padded channels zero) and input-gradient ([Cin][taps][Cout]) row layouts."""
+    F = require().f32
+    g = ConvGeom(3, 8, (3, 3, 3), (1, 1, 1), (1, 1, 1), cip=4)
+    w = torch.randn(8, 3, 3, 3, 3, device=DEV) * 1e-2
+    wf = pack_weight(F, g, w, 0)
+    assert wf.shape == (3, 8, 27 * 4) and wf.dtype == torch.bfloat16
+    ref = torch.zeros(8, 27, 4, device=DEV, dtype=torch.float64)
+    ref[:, :, :3] = w.double().reshape(8, 3, 27).permute(0, 2, 1)
+    got = wf.double().sum(0).reshape(8, 27, 4)
+    assert (got - ref).abs().max() <= 2 ** -24 * ref.abs().max()
+    g2 = ConvGeom(4, 8, (1, 3, 3), (1, 1, 1), (0, 1, 1))
+    w2 = torch.randn(8, 4, 1, 3, 3, device=DEV)
+    wt = pack_weight(F, g2, w2, 1)
+    ref2 = w2.double().reshape(8, 4, 9).permute(1, 2, 0)
+    assert wt.shape == (3, 4, 9 * 8)
+    assert (wt.double().sum(0).reshape(4, 9, 8) - ref2).abs().max() <= 2 ** -24 * ref2.abs().max()
 
 
 def test_dgrad_accumulate_phases():
@@ -112,8 +130,7 @@ def test_dgrad_accumulate_phases():
     n.F = F
     cb = _ConvBN(n, conv, bn, True)
     dy = torch.randn(2, 2, 7, 7, 128, device=DEV)
-    wt = torch.empty(64, 9, 128, device=DEV)
-    F.wpack32(1, conv.weight.detach(), wt, 128, 64, 9, 64, 0.0)
+    wt = pack_weight(F, cb.g, conv.weight.detach(), 1)
     base = torch.randn(2, 2, 14, 14, 64, device=DEV)
     acc = base.clone()
     cb._dgrad(dy, wt, acc, True)
