@@ -620,6 +620,283 @@ void launch_halo64p(const ConvParams& p, int cfg, hipStream_t st) {
 
 
 // ------------------------------------------------------------------------------------------------------------------
+// Double-buffered 64 -> 64 channel variant (launch-word bits 1 + 3; slow res2 conv_b at 56x56).  The persistent
+// kernel above runs each tile as three serialised phases — halo store (VALU + ds_write, no MFMA), 18 k-steps of MFMA
+// at 0.75 LDS reads per MFMA with two waves per SIMD, epilogue — at 28-31 % MFMA busy (profiles/r6_pmc).  Here:
+//   * tiles are 8 rows x 28 columns (P = 224 as before; the halo is 10 x 30 = 300 positions, 1.34x the outputs
+//     instead of 1.55x), so TWO halo images fit next to the 72 KB of LDS-resident weights: tile t+1's halo is written
+//     (BN+ReLU applied) one chunk per k-step behind tile t's MFMAs, and each tile has one barrier;
+//   * 8 waves (two per SIMD, so one wave's staging and epilogue overlap the other's MFMAs) = 4 position groups x 2
+//     channel halves, each 4 position blocks x 32 channels, the fragments of step s+1 read during step s;
+//   * a staging register is refilled with tile t+2's chunk as soon as it is written, so every global load has a
+//     whole tile of latency to hide.
+// Epilogues as conv_halo64p_kernel (EPI 0 raw output + BN partial sums per tile, EPI 1 dgrad with the BN_a ReLU mask
+// from y0 and the BN_a backward partials).
+constexpr int HD_THREADS = 512, HD_R = 8, HD_CW = 28;
+constexpr int HD_PW = HD_CW + 2, HD_NPOS = (HD_R + 2) * HD_PW, HD_NPOSP = (HD_NPOS + 15) & ~15;
+constexpr int HD_STG = (HD_NPOSP * 8 + HD_THREADS - 1) / HD_THREADS;   // 16-B halo chunks per thread (10)
+constexpr int HD_HALO = 8 * HD_NPOSP * 16;                             // bytes of one halo image
+constexpr int HD_WI = 18 * 4 * 64 * 16;                                // weight image
+constexpr size_t HD_LDS = HD_WI + 2 * HD_HALO + (2 * 4 * 2 + 4 + 2) * 64 * 4;
+static_assert(HD_LDS <= 160 * 1024, "double-buffered halo tile exceeds LDS");
+
+template <int EPI, int AFF, int DIR>
+__global__ __launch_bounds__(HD_THREADS, 1) void conv_halo64d_kernel(const ConvParams p, const int ntiles) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int C = 64, W = 56, P = HD_R * HD_CW;
+  char* WI = smem;                                                // [18][4][64][16 B] weights
+  char* HI = smem + HD_WI;                                        // [2][8][NPOSP][16 B] halo images
+  float* red = reinterpret_cast<float*>(HI + 2 * HD_HALO);        // [2][4 waves][2][64]
+  float* bnp = red + 2 * 4 * 2 * C;                               // EPI 1: [4][64] mean0 rstd0 msc msh
+  float* aff = bnp + 4 * C;                                       // [2][64] consumer-side affine
+  const int H = p.Rh;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int wn = wid & 1, wm = wid >> 1;
+  const int t_begin = (int)((long long)blockIdx.x * ntiles / gridDim.x);
+  const int t_end = (int)((long long)(blockIdx.x + 1) * ntiles / gridDim.x);
+  const int tpf = (H / HD_R) * 2;   // tiles per frame: row bands x two column halves
+
+  // ---- weights -> LDS (as conv_halo64p_kernel): chunk q = (k-step s, channel group g, output channel n)
+  int wtap[9];
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) {
+    const int jh = tap / 3, jw = tap - jh * 3;
+    wtap[tap] = (p.bt0 * p.kh + p.bh0 + jh * p.bhs) * p.kw + p.bw0 + jw * p.bws;
+  }
+  for (int q = tid; q < 18 * 4 * 64; q += HD_THREADS) {
+    const int s = q >> 8, g = (q >> 6) & 3, n = q & 63;
+    const int tap = s >> 1, half = s & 1;
+    int wt = 0;
+#pragma unroll
+    for (int u = 0; u < 9; ++u) wt = (u == tap) ? wtap[u] : wt;
+    *reinterpret_cast<uint4*>(WI + q * 16) =
+        *reinterpret_cast<const uint4*>(p.w + (size_t)n * p.Kfull + wt * C + half * 32 + g * 8);
+  }
+  if constexpr (EPI == 1) {
+    for (int i = tid; i < C; i += HD_THREADS) {
+      bnp[i] = p.emean0[i]; bnp[C + i] = p.erstd0[i]; bnp[2 * C + i] = p.emsc[i]; bnp[3 * C + i] = p.emsh[i];
+    }
+  }
+  // ---- staging roles: channel group cg = lane >> 3, halo position u*64 + wid*8 + (lane & 7) of chunk u
+  const int cg = lane >> 3;
+  float sc[8], sh[8];
+  if constexpr (AFF != 0) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { sc[e] = p.in_scale[cg * 8 + e]; sh[e] = p.in_shift[cg * 8 + e]; }
+  }
+  // halo row (bits 8-15) and column (bits 0-7) of each chunk, bit 16: a real halo position
+  int hcode[HD_STG];
+#pragma unroll
+  for (int u = 0; u < HD_STG; ++u) {
+    const int pos = u * 64 + wid * 8 + (lane & 7);
+    const int h = pos / HD_PW, w = pos - h * HD_PW;
+    hcode[u] = pos < HD_NPOS ? ((1 << 16) | (h << 8) | w) : 0;
+  }
+  // image row of chunk u in tile t (clamped into the image) and whether it lies inside the image
+  auto chunk_at = [&](int t, int u, size_t& row, bool& ok) {
+    const int frame = t / tpf, rem = t - frame * tpf;
+    const int r = (rem >> 1) * HD_R - 1 + ((hcode[u] >> 8) & 255);
+    const int c = (rem & 1) * HD_CW - 1 + (hcode[u] & 255);
+    ok = (hcode[u] >> 16) && (unsigned)r < (unsigned)H && (unsigned)c < (unsigned)W;
+    row = (size_t)frame * H * W + (size_t)(ok ? r : 0) * W + (ok ? c : 0);
+  };
+  // staging registers as native vectors and unconditional loads from clamped addresses: no branch around a load, so
+  // the wait before each chunk's LDS write counts only the loads issued after it (a predicated load made the
+  // compiler wait for every outstanding load — the chunk just requested for tile t+2 included)
+  typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+  u32x4_t stg[HD_STG];
+  unsigned okm = 0;   // bit u: chunk u of the staged tile lies inside the image
+  auto load_chunk = [&](int t, int u) {
+    size_t row;
+    bool ok;
+    chunk_at(t, u, row, ok);
+    stg[u] = *reinterpret_cast<const u32x4_t*>(p.x + row * p.ldx + cg * 8);
+    okm = ok ? (okm | (1u << u)) : (okm & ~(1u << u));
+  };
+  auto store_chunk = [&](int u, char* img) {
+    if (!(hcode[u] >> 16)) return;
+    const bool ok = (okm >> u) & 1u;
+    uint4 o = __builtin_bit_cast(uint4, stg[u]);
+    if constexpr (AFF != 0) {
+      float f[8];
+      unpack8(o, f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] = __builtin_fmaf(f[e], sc[e], sh[e]);
+      o = pack8_fast(f);
+      if constexpr (AFF == 2) o = relu_e16x8(o);
+    }
+    const u32x4_t z = {0u, 0u, 0u, 0u};
+    const u32x4_t ov = ok ? __builtin_bit_cast(u32x4_t, o) : z;   // padding stays zero
+    const int pos = u * 64 + wid * 8 + (lane & 7);
+    *reinterpret_cast<u32x4_t*>(img + (cg * HD_NPOSP + pos) * 16) = ov;
+  };
+
+  // ---- this wave's position blocks: 14 blocks of 16 as 4 + 4 + 3 + 3 (a 3-block wave's 4th block re-reads block
+  // 13 and is not stored).  A fragment's 16 positions must sit on 16 distinct 16-B LDS units, unit(h, w) =
+  // (h * 30 + w + 31) mod 16: blocks 0-7 are the first 16 columns of rows 0-7; the 12-column row remnants are paired
+  // into blocks 8-13 from rows h, h+2, h+4, h+6 (whose units start 4 lower per two rows), e.g. row h columns 16-27 +
+  // row h+2 columns 16-19 — no block straddles a row end the way consecutive positions would
+  const int b0 = wm < 2 ? wm * 4 : 8 + (wm - 2) * 3;
+  const int nb = wm < 2 ? 4 : 3;
+  int abase[4], ph[4], pw[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int b = min(b0 + i, 13);
+    int h, w;
+    if (b < 8) {
+      h = b;
+      w = fr;
+    } else {
+      const int k = b - 8, hb = k / 3, sub = k - hb * 3;
+      const int cut = 12 - 4 * sub;   // lanes [0, cut) from row hb + 2 sub, columns 16 + 4 sub ...
+      h = hb + 2 * sub + (fr < cut ? 0 : 2);
+      w = fr < cut ? 16 + 4 * sub + fr : 16 + fr - cut;
+    }
+    ph[i] = h;
+    pw[i] = w;
+    abase[i] = (fg * HD_NPOSP + (h + 1) * HD_PW + (w + 1)) * 16;
+  }
+  const int wbase = fg * 1024 + (32 * wn + fr) * 16;   // + s * 4096 + j * 256
+
+  // prologue: first tile's halo into image 0, the second tile's chunks into the staging registers
+  if (t_begin < t_end) {
+#pragma unroll
+    for (int u = 0; u < HD_STG; ++u) load_chunk(t_begin, u);
+#pragma unroll
+    for (int u = 0; u < HD_STG; ++u) store_chunk(u, HI);
+#pragma unroll
+    for (int u = 0; u < HD_STG; ++u) load_chunk(t_begin + 1 < t_end ? t_begin + 1 : t_begin, u);
+  }
+  __syncthreads();
+
+  for (int t = t_begin; t < t_end; ++t) {
+    const int cur = (t - t_begin) & 1;
+    const char* img = HI + cur * HD_HALO;
+    char* nxt = HI + (cur ^ 1) * HD_HALO;
+    const bool has1 = t + 1 < t_end, has2 = t + 2 < t_end;
+    const int frame = t / tpf, rem = t - frame * tpf;
+    const int r0 = (rem >> 1) * HD_R, c0 = (rem & 1) * HD_CW;
+    const size_t fbase = (size_t)frame * H * W;
+    uint2 y0v[4][2];
+    if constexpr (EPI == 1) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const size_t row = fbase + (size_t)(r0 + ph[i]) * W + c0 + pw[i];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          y0v[i][j] = *reinterpret_cast<const uint2*>(p.ey0 + row * C + 32 * wn + 16 * j + 4 * fg);
+      }
+    }
+    f32x4_t acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    ev8_t wa[2][2], xb[2][4];
+    auto frag = [&](int s, int c) {
+      const int jh = (s >> 1) / 3, jw = (s >> 1) % 3;
+      const int ao = ((-DIR + DIR * jh) * HD_PW + (-DIR + DIR * jw)) * 16 + (s & 1) * 4 * HD_NPOSP * 16;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) wa[c][j] = *reinterpret_cast<const ev8_t*>(WI + s * 4096 + j * 256 + wbase);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) xb[c][i] = *reinterpret_cast<const ev8_t*>(img + abase[i] + ao);
+    };
+    frag(0, 0);
+#pragma unroll
+    for (int s = 0; s < 18; ++s) {
+      const int c = s & 1;
+      if (s + 1 < 18) {
+        frag(s + 1, c ^ 1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = PVA_MFMA16(wa[c][j], xb[c][i], acc[i][j], 0, 0, 0);
+      // next tile's halo chunk s-2 -> the other image, then its register takes tile t+2's chunk
+      if (s >= 2 && s - 2 < HD_STG) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (has1) store_chunk(s - 2, nxt);
+        load_chunk(has2 ? t + 2 : t, s - 2);   // (past the range: a harmless reload of this tile)
+      }
+    }
+
+    // ---- epilogue: lane holds channels 32 wn + 16 j + 4 fg + r of position (b0 + i) * 16 + fr
+    float s1[2][4], s2[2][4];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { s1[j][r] = 0.f; s2[j][r] = 0.f; }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (i >= nb) continue;
+      const size_t row = fbase + (size_t)(r0 + ph[i]) * W + c0 + pw[i];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int n = 32 * wn + 16 * j + 4 * fg;
+        float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        float a[4];
+        if constexpr (EPI == 1) {
+          unpack4(y0v[i][j], a);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = (a[r] * bnp[2 * C + n + r] + bnp[3 * C + n + r] > 0.f) ? v[r] : 0.f;
+        }
+        const uint2 pk = pack4(v);
+        *reinterpret_cast<uint2*>(p.y + row * p.ldy + n) = pk;
+        float q[4];
+        unpack4(pk, q);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          s1[j][r] += q[r];
+          if constexpr (EPI == 1) s2[j][r] += q[r] * a[r];
+          else s2[j][r] += q[r] * q[r];
+        }
+      }
+    }
+    float* rb = red + cur * (4 * 2 * C);
+    const bool want = !(EPI == 0 && p.stats == nullptr);
+    if (want) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float a = sum16(s1[j][r]), b = sum16(s2[j][r]);
+          if (fr == 0) {
+            const int n = 32 * wn + 16 * j + 4 * fg + r;
+            rb[(wm * 2) * C + n] = a;
+            rb[(wm * 2 + 1) * C + n] = b;
+          }
+        }
+    }
+    __syncthreads();   // next image written, this image read by every wave, partials complete
+    if (want && tid < C) {
+      const int n = tid;
+      float a = 0.f, b = 0.f;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) { a += rb[(m * 2) * C + n]; b += rb[(m * 2 + 1) * C + n]; }
+      if constexpr (EPI == 0) {
+        p.stats[((size_t)t * 2) * C + n] = a;
+        p.stats[((size_t)t * 2 + 1) * C + n] = b;
+      } else {
+        p.epart[((size_t)t * 3) * C + n] = a;
+        p.epart[((size_t)t * 3 + 1) * C + n] = (b - bnp[n] * a) * bnp[C + n];
+        p.epart[((size_t)t * 3 + 2) * C + n] = 0.f;
+      }
+    }
+  }
+}
+
+template <int EPI, int AFF, int DIR>
+void launch_halo64d(const ConvParams& p, int cfg, hipStream_t st) {
+  const int ntiles = p.M / (HD_R * HD_CW);
+  const int cap = (cfg & 4) ? 1024 : 256;   // one workgroup per CU (LDS-bound); 4x that for load balance
+  const int grid = ntiles < cap ? ntiles : cap;
+  hipLaunchKernelGGL((conv_halo64d_kernel<EPI, AFF, DIR>), dim3(grid), dim3(HD_THREADS), HD_LDS, st, p, ntiles);
+}
+
+
+// ------------------------------------------------------------------------------------------------------------------
 // Narrow variant (fast pathway: 8 / 16 / 32 channels in and out, P = R*W <= 1024 positions per tile).  At these
 // widths the conv is a pure streaming problem (K = 9*C <= 288): the halo [(R+2) x (W+2)][C] is staged once
 // (position-major, 16/32/64 B per position), the weights of every k-step live in registers for the whole kernel,
@@ -843,13 +1120,15 @@ int conv_halo_legal(const ConvParams& p, int chunk) {
   return R * p.Rw;
 }
 
-// 1 when the persistent 64-channel variant (launch-word bit 1) can run this geometry (conv_halo_legal > 0 too)
+// 1 when the persistent 64-channel variant (launch-word bit 1) can run this geometry (conv_halo_legal > 0 too), 2 when
+// the double-buffered variant (bits 1 + 3: 56-wide images, 8-row bands, the same 224-position tiles) can as well
 int conv_halo64p_legal(const ConvParams& p, int chunk) {
   if (p.Cg != 64 || p.Ngemm != 64 || p.Kfull < 9 * 64 || conv_halo_legal(p, chunk) <= 0) return 0;
   if (!((p.dir == 1 && p.aoh == -1 && p.aow == -1) || (p.dir == -1 && p.aoh == 1 && p.aow == 1))) return 0;
   const int R = halo_rows(p.Rh, p.Rw);   // instantiated image widths: 56 (224 crop) and 64 (R101's 256 crop)
   if (p.epart && p.dir != -1) return 0;
-  return ((p.Rw == 56 && R == 4) || (p.Rw == 64 && R == 2)) ? 1 : 0;
+  if (p.Rw == 56 && R == 4) return p.Rh % HD_R == 0 ? 2 : 1;
+  return (p.Rw == 64 && R == 2) ? 1 : 0;
 }
 
 int conv_halo_epi_ok(const ConvParams& p) {
@@ -877,6 +1156,14 @@ void conv_halo_launch(const ConvParams& p, int cfg, hipStream_t st) {
   }
   const int R = halo_rows(p.Rh, p.Rw);
   const bool epi = p.epart != nullptr;
+  if ((cfg & 2) && (cfg & 8)) {   // double-buffered 64-channel variant (legality: conv_halo64p_legal == 2)
+    if (epi) launch_halo64d<1, 0, -1>(p, cfg, st);
+    else if (p.dir < 0) launch_halo64d<0, 0, -1>(p, cfg, st);
+    else if (p.affine == 0) launch_halo64d<0, 0, 1>(p, cfg, st);
+    else if (p.affine == 1) launch_halo64d<0, 1, 1>(p, cfg, st);
+    else launch_halo64d<0, 2, 1>(p, cfg, st);
+    return;
+  }
   if (cfg & 2) {   // persistent 64-channel variant (legality checked by the bindings: conv_halo64p_legal)
     if (epi) launch_halo64p<1, 0, -1>(p, cfg, st);
     else if (p.dir < 0) launch_halo64p<0, 0, -1>(p, cfg, st);

@@ -99,7 +99,7 @@ static void check_pw(const ConvParams& p, int64_t chunk, int64_t cfg) {
     const int P = pva_bf16::conv_halo_legal(p, (int)chunk);
     TORCH_CHECK(P > 0 && P == (int)(cfg >> 12), "halo conv kernel selected for an unsupported geometry");
     TORCH_CHECK(pva_bf16::conv_halo_epi_ok(p), "halo conv kernel selected for an unsupported epilogue");
-    TORCH_CHECK(!(cfg & 2) || pva_bf16::conv_halo64p_legal(p, (int)chunk),
+    TORCH_CHECK(!(cfg & 2) || pva_bf16::conv_halo64p_legal(p, (int)chunk) >= ((cfg & 8) ? 2 : 1),
                 "persistent 64-channel halo conv kernel selected for an unsupported geometry");
     return;
   }

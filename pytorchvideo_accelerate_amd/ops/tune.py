@@ -46,8 +46,9 @@ PW_SOLO = 4                     # bit 2 one workgroup per CU
 PW_W4 = 8                       # bit 3 4-wave workgroups (three per CU at <= 168 VGPRs)
 HALO = 2048           # halo-staged (1,3,3) stride-1 kernel (csrc/kernels/conv_halo.hip): bit 0 = 64-channel
                       # n-tiles (else 128), bits 12+ = positions per tile; bit 1 = persistent 64-channel variant
-HALO_P = 2            #   (weights resident in LDS; bit 2: 4 workgroups per CU-slot instead of 1)
-HALO_P4 = 4
+HALO_P = 2            #   (weights resident in LDS; bit 2: 4 workgroups per CU-slot instead of 1;
+HALO_P4 = 4           #   bit 3: the double-buffered 8x28-tile variant, halo writes behind the MFMAs)
+HALO_D = 8
 TILE_BN = (128, 64, 32, 16)   # variants 0..3
 TILE_BM = (128, 128, 256, 256)
 
@@ -58,7 +59,7 @@ def describe(cfg: int) -> str:
         return "heuristic"
     if cfg & HALO:
         if cfg & HALO_P:
-            return "halo%d/p%d" % (cfg >> 12, 1024 if cfg & HALO_P4 else 256)
+            return "halo%d/%s%d" % (cfg >> 12, "d" if cfg & HALO_D else "p", 1024 if cfg & HALO_P4 else 256)
         return "halo%d/n%d" % (cfg >> 12, 64 if cfg & 1 else 128)
     if cfg & PW:
         return "pw%d%s%s" % (PW_ROWS[cfg & 3], "s" if cfg & PW_SOLO else "", "/w4" if cfg & PW_W4 else "")
@@ -86,6 +87,7 @@ class ConvTuner:
         self.dma = on("conv_dma")
         self.pw = on("conv_pw")
         self.halo = on("conv_halo")
+        self.halo_d = on("conv_halo_d")
         self.big_half = on("conv_big_half")
         self.pf = on("conv_pf")
         self.pw_w4 = on("conv_pw_w4")
@@ -149,8 +151,11 @@ class ConvTuner:
             P = int(self.C.conv_halo_legal(list(g), chunk))
             if P > 0:
                 out += [EXPLICIT | HALO | (P << 12) | v for v in ((0, 1) if N % 128 == 0 else (1,))]
-                if self.C.conv_halo64p_legal(list(g), chunk):
+                lg = int(self.C.conv_halo64p_legal(list(g), chunk))
+                if lg:
                     out += [EXPLICIT | HALO | (P << 12) | 1 | HALO_P | g4 for g4 in (0, HALO_P4)]
+                if lg == 2 and self.halo_d:
+                    out += [EXPLICIT | HALO | (P << 12) | 1 | HALO_P | HALO_D | g4 for g4 in (0, HALO_P4)]
         if pw and self.pw and self._pw_now and self.C.conv_pw_legal(list(g), chunk):
             self._pw_seen += 1
             if self.pw_only is None or self.pw_only == self._pw_seen - 1:

@@ -24,6 +24,7 @@ DEFAULTS: Dict[str, tuple] = {
     "conv_dma": (1, "r3_knobs"),
     "conv_pw": (1, "r2_final"),
     "conv_halo": (1, "r3_halo"),
+    "conv_halo_d": (1, "r6_halo: double-buffered 64-channel halo conv as a tuner candidate"),
     "conv_big_half": (1, "r4_big_half"),
     "conv_pf": (1, "r5_lab"),
     "conv_pw_w4": (1, "r5_lateral"),

@@ -44,8 +44,11 @@ def _cfgs(g, C):
     assert P > 0, "halo kernel must accept this geometry"
     base = EXPLICIT | HALO | (P << 12)
     cfgs = [base, base | 1] if C % 128 == 0 else [base | 1]
-    if require().conv_halo64p_legal(list(g), 8):   # persistent 64-channel variant, 256 / 1024 workgroups
+    lg = require().conv_halo64p_legal(list(g), 8)
+    if lg:   # persistent 64-channel variant, 256 / 1024 workgroups
         cfgs += [base | 1 | 2, base | 1 | 2 | 4]
+    if lg == 2:   # double-buffered 8x28-tile variant
+        cfgs += [base | 1 | 2 | 8, base | 1 | 2 | 8 | 4]
     return P, cfgs
 
 
@@ -124,7 +127,8 @@ def test_halo_legality():
     assert Cm.conv_halo_legal(fwd_geometry(ConvSpec(512, 512, (1, 3, 3), (1, 1, 1), (0, 1, 1)), 2, 4, 7, 7, 512, 512), 8) == 0
     assert Cm.conv_halo_legal(fwd_geometry(ConvSpec(24, 24, (1, 3, 3), (1, 1, 1), (0, 1, 1)), 2, 4, 56, 56, 24, 24), 8) == 0
     assert Cm.conv_halo_legal(fwd_geometry(ConvSpec(16, 16, (1, 3, 3), (1, 1, 1), (0, 1, 1)), 2, 4, 56, 56, 16, 16), 8) == 784
-    assert Cm.conv_halo64p_legal(ok, 8) == 1
+    assert Cm.conv_halo64p_legal(ok, 8) == 2   # persistent and double-buffered variants
+    assert Cm.conv_halo64p_legal(fwd_geometry(ConvSpec(64, 64, (1, 3, 3), (1, 1, 1), (0, 1, 1)), 1, 1, 64, 64, 64, 64), 8) == 1
     assert Cm.conv_halo64p_legal(fwd_geometry(ConvSpec(128, 128, (1, 3, 3), (1, 1, 1), (0, 1, 1)), 2, 4, 28, 28, 128, 128), 8) == 0
 
 
