@@ -114,12 +114,32 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
-// Sum across the 16 lanes that share (lane >> 4).
+// v of the lane selected by DPP control CTRL (within each 16-lane row)
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
+}
+
+// Sum across the 16 lanes that share (lane >> 4), every lane getting the sum: four DPP-modified adds (quad_perm
+// [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror, row_mirror) instead of __shfl_xor, which compiles to
+// ds_bpermute_b32 — an LDS round trip and an lgkmcnt wait per step, 64 of them in a 16-value epilogue.
 __device__ __forceinline__ float sum16(float v) {
-  v += __shfl_xor(v, 1, 64);
-  v += __shfl_xor(v, 2, 64);
-  v += __shfl_xor(v, 4, 64);
-  v += __shfl_xor(v, 8, 64);
+  v += dpp_f<0xB1>(v);
+  v += dpp_f<0x4E>(v);
+  v += dpp_f<0x141>(v);
+  v += dpp_f<0x140>(v);
+  return v;
+}
+
+// Sum across aligned groups of G adjacent lanes (G = 1, 2, 4, 8, 16), every lane getting its group's sum (DPP, as
+// sum16: after the quad steps every lane of a quad holds the same value, so the mirrors pair whole quads / halves)
+template <int G>
+__device__ __forceinline__ float sum_lanes(float v) {
+  static_assert(G == 1 || G == 2 || G == 4 || G == 8 || G == 16, "DPP lane groups stay inside a 16-lane row");
+  if constexpr (G >= 2) v += dpp_f<0xB1>(v);
+  if constexpr (G >= 4) v += dpp_f<0x4E>(v);
+  if constexpr (G >= 8) v += dpp_f<0x141>(v);
+  if constexpr (G >= 16) v += dpp_f<0x140>(v);
   return v;
 }
 

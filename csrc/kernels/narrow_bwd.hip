@@ -14,7 +14,7 @@
 //
 // Layout: LPR = CO / 8 lanes per row, each owning 8 output channels c (16-B loads of g / yc / dz); every lane keeps
 // the 8 x CI partial weight gradient of its channels in registers over the workgroup's row range, and the 8 x CI
-// slice of Wc.  The per-row dgrad partials are summed over the row's lanes with xor shuffles; lane q then finishes
+// slice of Wc.  The per-row dgrad partials are summed over the row's lanes with DPP adds; lane q then finishes
 // input channels k = q*CI/LPR .. (q+1)*CI/LPR - 1 (mask, round, store, partial sums).  Workgroup w owns rows
 // [w*rps, (w+1)*rps): its weight-gradient slab and BN partial sums are written once, summed in a fixed order by the
 // slab reduction / BN finalize (bitwise reproducible).
@@ -181,11 +181,9 @@ __global__ __launch_bounds__(256) void narrow_c_bwd_kernel(const NarrowBwdParams
         acc[e][k] = __builtin_fmaf(dy[e], ab[k], acc[e][k]);
         pd[k] = __builtin_fmaf(dy[e], W[e][k], pd[k]);
       }
-    // sum the row's LPR lanes (adjacent lanes): every lane ends with the row's full dgrad
+    // sum the row's LPR lanes (adjacent lanes, DPP): every lane ends with the row's full dgrad
 #pragma unroll
-    for (int o = 1; o < LPR; o <<= 1)
-#pragma unroll
-      for (int k = 0; k < CI; ++k) pd[k] += __shfl_xor(pd[k], o, 64);
+    for (int k = 0; k < CI; ++k) pd[k] = sum_lanes<LPR>(pd[k]);
     // lane q: input channels k = q*KPL + j — BN_b ReLU mask (affine of yb > 0), round, store, partial sums
     uint16_t* dst = p.dab + r * p.ldo + q * KPL;
     float old[KPL];
