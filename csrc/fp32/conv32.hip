@@ -281,11 +281,8 @@ __global__ __launch_bounds__(256) void igemm32_kernel(const Conv32 p) {
             s1 += v;
             s2 = fmaf(v, v, s2);
           }
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-          s1 += __shfl_xor(s1, o, 64);
-          s2 += __shfl_xor(s2, o, 64);
-        }
+        s1 = sum16(s1);
+        s2 = sum16(s2);
         if ((lane & 15) == 0) {
           const int nl = wn * TN + 16 * j + 4 * (lane >> 4) + r;
           red[(wm * 2) * BN + nl] = s1;

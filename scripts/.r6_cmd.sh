@@ -1,2 +1,2 @@
-export OUT=r6_dpp
+export OUT=r6_dpp4
 bash scripts/gpu_run.sh smoke tests bench
