@@ -214,10 +214,10 @@ void conv_igemm_kernel(const ConvParams p) {
       const bool rv = idx < A_CHUNKS && m < p.M;
       int at = 0, ah = 0, aw = 0, off = 0;
       if (rv) {
-        const int b = m / RTHW;
+        const int b = pva_fdiv(m, p.mg_thw, p.sh_thw);
         int r = m - b * RTHW;
-        const int qt = r / RHW; r -= qt * RHW;
-        const int qh = r / p.Rw; const int qw = r - qh * p.Rw;
+        const int qt = pva_fdiv(r, p.mg_hw, p.sh_hw); r -= qt * RHW;
+        const int qh = pva_fdiv(r, p.mg_w, p.sh_w); const int qw = r - qh * p.Rw;
         at = qt * p.ast + p.aot; ah = qh * p.ash + p.aoh; aw = qw * p.asw + p.aow;
         // LDS-DMA staging: the lane's LDS slot is `col`, so it loads the logical chunk that the XOR swizzle
         // places there (lds_off: physical slot = logical ^ swz(row), an involution)
@@ -265,10 +265,10 @@ void conv_igemm_kernel(const ConvParams p) {
       t_on = lane < TRPW && m < p.M;
       int at = 0, ah = 0, aw = 0, off = 0;
       if (t_on) {
-        const int b = m / RTHW;
+        const int b = pva_fdiv(m, p.mg_thw, p.sh_thw);
         int r = m - b * RTHW;
-        const int qt = r / RHW; r -= qt * RHW;
-        const int qh = r / p.Rw; const int qw = r - qh * p.Rw;
+        const int qt = pva_fdiv(r, p.mg_hw, p.sh_hw); r -= qt * RHW;
+        const int qh = pva_fdiv(r, p.mg_w, p.sh_w); const int qw = r - qh * p.Rw;
         at = qt * p.ast + p.aot; ah = qh * p.ash + p.aoh; aw = qw * p.asw + p.aow;
         off = (b * GTHW + (at * p.Gh + ah) * p.Gw + aw) * p.ldx;
         if (check) {
@@ -588,10 +588,10 @@ void conv_igemm_kernel(const ConvParams p) {
       const int m = m0 + row;
       a_off[s] = 0; a_t[s] = 0; a_h[s] = 0; a_w[s] = 0;
       if (idx < A_CHUNKS && m < p.M) {
-        const int b = m / RTHW;
+        const int b = pva_fdiv(m, p.mg_thw, p.sh_thw);
         int r = m - b * RTHW;
-        const int qt = r / RHW; r -= qt * RHW;
-        const int qh = r / p.Rw; const int qw = r - qh * p.Rw;
+        const int qt = pva_fdiv(r, p.mg_hw, p.sh_hw); r -= qt * RHW;
+        const int qh = pva_fdiv(r, p.mg_w, p.sh_w); const int qw = r - qh * p.Rw;
         a_t[s] = qt * p.ast + p.aot; a_h[s] = qh * p.ash + p.aoh; a_w[s] = qw * p.asw + p.aow;
         a_off[s] = (b * GTHW + (a_t[s] * p.Gh + a_h[s]) * p.Gw + a_w[s]) * p.ldx;
         rowok |= 1u << s;
@@ -738,10 +738,10 @@ void conv_igemm_kernel(const ConvParams p) {
     const int m = m0 + wm * WM + i * 16 + frow;
     int pos = m;
     if (!dense_rows && m < p.M) {
-      const int b = m / RTHW;
+      const int b = pva_fdiv(m, p.mg_thw, p.sh_thw);
       int r = m - b * RTHW;
-      const int qt = r / RHW; r -= qt * RHW;
-      const int qh = r / p.Rw; const int qw = r - qh * p.Rw;
+      const int qt = pva_fdiv(r, p.mg_hw, p.sh_hw); r -= qt * RHW;
+      const int qh = pva_fdiv(r, p.mg_w, p.sh_w); const int qw = r - qh * p.Rw;
       pos = ((b * p.Ot + qt * p.ost + p.ort) * p.Oh + qh * p.osh + p.orh) * p.Ow + qw * p.osw + p.orw;
     }
     if constexpr (EPI == 0) {
@@ -854,10 +854,10 @@ void conv_igemm_kernel(const ConvParams p) {
         ok[u] = rr < r_lo + SR && m < p.M;
         int ps = m;
         if (!dense_rows && ok[u]) {
-          const int b = m / RTHW;
+          const int b = pva_fdiv(m, p.mg_thw, p.sh_thw);
           int r = m - b * RTHW;
-          const int qt = r / RHW; r -= qt * RHW;
-          const int qh = r / p.Rw; const int qw = r - qh * p.Rw;
+          const int qt = pva_fdiv(r, p.mg_hw, p.sh_hw); r -= qt * RHW;
+          const int qh = pva_fdiv(r, p.mg_w, p.sh_w); const int qw = r - qh * p.Rw;
           ps = ((b * p.Ot + qt * p.ost + p.ort) * p.Oh + qh * p.osh + p.orh) * p.Ow + qw * p.osw + p.orw;
         }
         pos[u] = ps;
@@ -1181,8 +1181,12 @@ void conv_igemm_set_bk(int bk) { g_bk_override = bk; }
 // 1 when the uniform-tap loader may run this launch with that BK
 int conv_igemm_ut_legal(const ConvParams& p, int chunk, int bk) { return conv_ut_legal(p, chunk, bk) ? 1 : 0; }
 
-void conv_igemm_launch(const ConvParams& p, int chunk, hipStream_t stream, int cfg) {
-  if ((p.eres || p.emask || p.epart || p.fres) && chunk != 8) return;  // host binding rejects this combination
+void conv_igemm_launch(const ConvParams& p0, int chunk, hipStream_t stream, int cfg) {
+  if ((p0.eres || p0.emask || p0.epart || p0.fres) && chunk != 8) return;  // host binding rejects this combination
+  ConvParams p = p0;
+  pva_magic_div(p.Rt * p.Rh * p.Rw, &p.mg_thw, &p.sh_thw);
+  pva_magic_div(p.Rh * p.Rw, &p.mg_hw, &p.sh_hw);
+  pva_magic_div(p.Rw, &p.mg_w, &p.sh_w);
   int v, bk, ut_force;
   bool dma = false, pf = false;
   if (cfg >= 0 && (cfg & 16) && (cfg & 2048)) {  // halo-staged 3x3 kernel (legality checked by the bindings)

@@ -66,7 +66,22 @@ struct ConvParams {
   // 1: statistics-only forward (EPI 0 with stats): the per-tile BN partial sums of the bf16-rounded output are
   // produced, the output itself is never stored (exact BN statistics of a folded conv, models/fused.py)
   int nostore;
+  // row-lattice decode by magic numbers (m / (Rt*Rh*Rw), r / (Rh*Rw), r / Rw as (umulhi(n, mg) + n) >> sh; exact for
+  // 0 <= n < 2^31), filled by conv_igemm_launch: the kernels' integer divisions cost ~35 VALU each, three per row
+  unsigned mg_thw, mg_hw, mg_w;
+  int sh_thw, sh_hw, sh_w;
 };
+
+// Magic-number division helpers (host fills, device divides)
+static inline void pva_magic_div(int d, unsigned* m, int* s) {
+  int k = 0;
+  while ((1LL << k) < d) ++k;
+  *s = k;
+  *m = (unsigned)((((1ULL << 32) * ((1ULL << k) - (unsigned long long)d)) / (unsigned long long)d + 1) & 0xffffffffULL);
+}
+__device__ __forceinline__ int pva_fdiv(int n, unsigned m, int s) {
+  return (int)((__umulhi((unsigned)n, m) + (unsigned)n) >> s);
+}
 
 // Weight gradient: dW[n = cout][k = (tap, cin)] = sum_p dY[p][cout] * im2col(X)[p][k]
 // Split over p in `splits` slices whose fp32 results are atomically added into one zero-initialised

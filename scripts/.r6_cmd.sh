@@ -1,2 +1,2 @@
-export OUT=r6_dpp4
+export OUT=r6_magic
 bash scripts/gpu_run.sh smoke tests bench
