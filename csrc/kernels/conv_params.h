@@ -107,4 +107,8 @@ struct WgradParams {
   // k-tile-0 blocks of each split
   int dy_affine;
   float* colsum;
+  // magic-number decode of a dY position (q / (To*Ho*Wo), q / (Ho*Wo), q / Wo; pva_fdiv), filled by the narrow
+  // weight-gradient launcher
+  unsigned mg_othw, mg_ohw, mg_wo;
+  int sh_othw, sh_ohw, sh_wo;
 };

@@ -449,6 +449,18 @@ __global__ __launch_bounds__(256) void wgrad_narrow_kernel(const WgradParams p) 
   const int tr_row = 8 * g + (li >> 2);
   const int tr_colb = (li & 3) * 8;
   uint4 ra[MC], rb[KC];
+  // the im2col chunk kc = (tap, 8 channels) is the same for every position: decode it once (dt | dh << 4 | dw << 8 |
+  // c0 << 12, and its element offset from the position's base) instead of three divisions per chunk and position
+  int kcode[KC], ktoff[KC];
+#pragma unroll
+  for (int kc = 0; kc < KC; ++kc) {
+    const int k = kc * 8;
+    const int tap = k / p.Cin, c0 = k - tap * p.Cin;
+    const int dt = tap / (p.kh * p.kw), r = tap - dt * p.kh * p.kw;
+    const int dh = r / p.kw, dw = r - dh * p.kw;
+    kcode[kc] = dt | (dh << 4) | (dw << 8) | (c0 << 12);
+    ktoff[kc] = ((dt * p.Hi + dh) * p.Wi + dw) * p.ldx + c0;
+  }
   auto act8 = [&](uint4 v, const float* sc, const float* sh) {
     float f[8];
     unpack8(v, f);
@@ -471,26 +483,25 @@ __global__ __launch_bounds__(256) void wgrad_narrow_kernel(const WgradParams p) 
     for (int mc = 0; mc < MC; ++mc)
       if (mc < mchunks) ra[mc] = *reinterpret_cast<const uint4*>(dyr + mc * 8);
     int q = pp;
-    const int b = q / OTHW; q -= b * OTHW;
-    const int t = q / OHW; q -= t * OHW;
-    const int h = q / p.Wo, w = q - (q / p.Wo) * p.Wo;
+    const int b = pva_fdiv(q, p.mg_othw, p.sh_othw); q -= b * OTHW;
+    const int t = pva_fdiv(q, p.mg_ohw, p.sh_ohw); q -= t * OHW;
+    const int h = pva_fdiv(q, p.mg_wo, p.sh_wo), w = q - h * p.Wo;
     const int bt = t * p.st - p.pt, bh = h * p.sh - p.ph, bw = w * p.sw - p.pw;
-    const int64_t base = (((int64_t)b * p.Ti + bt) * p.Hi + bh) * p.Wi + bw;
+    const uint16_t* xb = p.x + ((((int64_t)b * p.Ti + bt) * p.Hi + bh) * p.Wi + bw) * p.ldx;
 #pragma unroll
     for (int kc = 0; kc < KC; ++kc) {
       if (kc < kchunks) {
-        const int k = kc * 8;
-        const int tap = k / p.Cin, c0 = k - tap * p.Cin;
-        const int dt = tap / (p.kh * p.kw), r = tap - dt * p.kh * p.kw;
-        const int dh = r / p.kw, dw = r - (r / p.kw) * p.kw;
+        const int dt = kcode[kc] & 15, dh = (kcode[kc] >> 4) & 15, dw = (kcode[kc] >> 8) & 15;
         bool v = true;
         if (check)
           v = (unsigned)(bt + dt) < (unsigned)p.Ti && (unsigned)(bh + dh) < (unsigned)p.Hi &&
               (unsigned)(bw + dw) < (unsigned)p.Wi;
         if (v) {
-          const int64_t off = (base + ((int64_t)dt * p.Hi + dh) * p.Wi + dw) * p.ldx + c0;
-          rb[kc] = *reinterpret_cast<const uint4*>(p.x + off);
-          if (affine) rb[kc] = act8(rb[kc], p.in_scale + c0, p.in_shift + c0);   // padding stays zero
+          rb[kc] = *reinterpret_cast<const uint4*>(xb + ktoff[kc]);
+          if (affine) {   // padding stays zero
+            const int c0 = kcode[kc] >> 12;
+            rb[kc] = act8(rb[kc], p.in_scale + c0, p.in_shift + c0);
+          }
         }
       }
     }
@@ -566,7 +577,11 @@ __global__ __launch_bounds__(256) void wgrad_narrow_kernel(const WgradParams p) 
 }
 
 template <int MT, int NTN>
-void launch_narrow(const WgradParams& p, hipStream_t stream) {
+void launch_narrow(const WgradParams& p0, hipStream_t stream) {
+  WgradParams p = p0;
+  pva_magic_div(p.To * p.Ho * p.Wo, &p.mg_othw, &p.sh_othw);
+  pva_magic_div(p.Ho * p.Wo, &p.mg_ohw, &p.sh_ohw);
+  pva_magic_div(p.Wo, &p.mg_wo, &p.sh_wo);
   const int blocks = (p.splits + 3) / 4;
   const size_t lds = 4 * (64 * 16 * MT * 2 + 64 * 16 * NTN * 2);
   hipLaunchKernelGGL((wgrad_narrow_kernel<MT, NTN>), dim3(blocks), dim3(256), lds, stream, p);
