@@ -108,11 +108,6 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / PVA_NXCD;
 }
 
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
 
 // v of the lane selected by DPP control CTRL (within each 16-lane row)
 template <int CTRL>
@@ -143,11 +138,61 @@ __device__ __forceinline__ float sum_lanes(float v) {
   return v;
 }
 
+// v[l] + v[l ^ 16] and v[l] + v[l ^ 32] for every lane: gfx950's row / half-wave swaps (v_permlane16_swap_b32 with
+// vdst = src = v leaves rows (r0, r0, r2, r2) in one result and (r1, r1, r3, r3) in the other; likewise for halves;
+// tools/probe/permlane_probe.hip).  fetch-inactive set: like ds_bpermute, a lane's partner is read even when the
+// partner is outside EXEC.  The results are copied to scalars first (a bit_cast of the vector element r[1] reads
+// element 0).
+__device__ __forceinline__ float swap_sum16(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), true, false);
+  const unsigned a = r[0], b = r[1];
+  return __uint_as_float(a) + __uint_as_float(b);
+}
+__device__ __forceinline__ float swap_sum32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), true, false);
+  const unsigned a = r[0], b = r[1];
+  return __uint_as_float(a) + __uint_as_float(b);
+}
+
+// Sum over the lanes sharing (lane % S), S a compile-time power of two <= 64, every lane getting its group's sum:
+// row_ror:4 / row_ror:8 DPP adds inside 16-lane rows, permlane swaps across rows (no ds_bpermute round trips).
+// (quad_perm xor steps for strides 1 and 2).  Full-EXEC callers only: DPP does not read lanes outside EXEC.
+template <int S>
+__device__ __forceinline__ float wave_sum_stride_c(float v) {
+  static_assert(S >= 1 && S <= 64 && (S & (S - 1)) == 0, "stride");
+  if constexpr (S <= 1) v += dpp_f<0xB1>(v);
+  if constexpr (S <= 2) v += dpp_f<0x4E>(v);
+  if constexpr (S <= 4) v += dpp_f<0x124>(v);
+  if constexpr (S <= 8) v += dpp_f<0x128>(v);
+  if constexpr (S <= 16) v = swap_sum16(v);
+  if constexpr (S <= 32) v = swap_sum32(v);
+  return v;
+}
+
+// Sum over the whole wave (full EXEC), every lane getting it
+__device__ __forceinline__ float wave_sum(float v) { return swap_sum32(swap_sum16(sum16(v))); }
+
+// v of lane l ^ 16 (fetch-inactive, as ds_bpermute)
+__device__ __forceinline__ unsigned swap_partner16(unsigned v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(v, v, true, false);
+  const unsigned a = r[0], b = r[1];
+  return a ^ b ^ v;
+}
+
 // Sum over the lanes of a wave that share (lane % S), S a power of two <= 64 (uniform).  Every lane
 // gets its group's sum.  Used before LDS atomics: same-address ds_add_f32 lanes serialise badly.
 __device__ __forceinline__ float wave_sum_stride(float v, int S) {
-  for (int off = S; off < 64; off <<= 1) v += __shfl_xor(v, off, 64);
-  return v;
+  switch (S) {   // (wave-uniform; full-EXEC callers)
+    case 1: return wave_sum_stride_c<1>(v);
+    case 2: return wave_sum_stride_c<2>(v);
+    case 4: return wave_sum_stride_c<4>(v);
+    case 8: return wave_sum_stride_c<8>(v);
+    case 16: return wave_sum_stride_c<16>(v);
+    case 32: return wave_sum_stride_c<32>(v);
+    default:
+      for (int off = S; off < 64; off <<= 1) v += __shfl_xor(v, off, 64);
+      return v;
+  }
 }
 
 // Sum across lanes l, l^16, l^32, l^48 (same lane & 15).

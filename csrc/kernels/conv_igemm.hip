@@ -776,7 +776,7 @@ void conv_igemm_kernel(const ConvParams p) {
             }
           }
           // channels 8k..8k+7 of a row live in lanes l (fslot even) and l ^ 16: one mask byte per pair
-          const unsigned other = __shfl_xor(bits, 16, 64);
+          const unsigned other = swap_partner16(bits);
           if (ok && !(fslot & 1)) p.emask_out[pos * (p.Ngemm >> 3) + (n >> 3)] = (uint8_t)(bits | (other << 4));
           continue;
         }

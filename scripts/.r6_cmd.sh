@@ -1,2 +1,2 @@
-export OUT=r6_cfg2
-bash scripts/gpu_run.sh cfg
+export OUT=r6_epi2
+bash scripts/gpu_run.sh smoke tests bench
