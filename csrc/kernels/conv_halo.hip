@@ -637,18 +637,17 @@ constexpr int HD_PW = HD_CW + 2, HD_NPOS = (HD_R + 2) * HD_PW, HD_NPOSP = (HD_NP
 constexpr int HD_STG = (HD_NPOSP * 8 + HD_THREADS - 1) / HD_THREADS;   // 16-B halo chunks per thread (10)
 constexpr int HD_HALO = 8 * HD_NPOSP * 16;                             // bytes of one halo image
 constexpr int HD_WI = 18 * 4 * 64 * 16;                                // weight image
-constexpr size_t HD_LDS = HD_WI + 2 * HD_HALO + (2 * 4 * 2 + 4 + 2) * 64 * 4;
+constexpr size_t HD_LDS = HD_WI + 2 * HD_HALO + (2 * 4 * 2 + 4) * 64 * 4;
 static_assert(HD_LDS <= 160 * 1024, "double-buffered halo tile exceeds LDS");
 
 template <int EPI, int AFF, int DIR>
 __global__ __launch_bounds__(HD_THREADS, 1) void conv_halo64d_kernel(const ConvParams p, const int ntiles) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int C = 64, W = 56, P = HD_R * HD_CW;
+  constexpr int C = 64, W = 56;
   char* WI = smem;                                                // [18][4][64][16 B] weights
   char* HI = smem + HD_WI;                                        // [2][8][NPOSP][16 B] halo images
-  float* red = reinterpret_cast<float*>(HI + 2 * HD_HALO);        // [2][4 waves][2][64]
+  float* red = reinterpret_cast<float*>(HI + 2 * HD_HALO);        // [2][4 position groups][2][64]
   float* bnp = red + 2 * 4 * 2 * C;                               // EPI 1: [4][64] mean0 rstd0 msc msh
-  float* aff = bnp + 4 * C;                                       // [2][64] consumer-side affine
   const int H = p.Rh;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int fr = lane & 15, fg = lane >> 4;
