@@ -667,6 +667,12 @@ void conv_igemm_kernel(const ConvParams p) {
     auto store_lds = [&](int buf) {
       char* A = smem + buf * TILE_BYTES;
       char* B = A + BM * BK * 2;
+      // every A slot of this thread stages the same channels (ra_c): read their affine once, not once per slot
+      float asc[CH], ash[CH];
+      if (affine) {
+  #pragma unroll
+        for (int e = 0; e < CH; ++e) { asc[e] = aff[ra_c + e]; ash[e] = aff[p.Cg + ra_c + e]; }
+      }
   #pragma unroll
       for (int s = 0; s < A_SLOTS; ++s) {
         if constexpr (A_CHUNKS % NT != 0) if (tid + s * NT >= A_CHUNKS) break;
@@ -676,7 +682,7 @@ void conv_igemm_kernel(const ConvParams p) {
           if constexpr (CH == 8) unpack8(v, f); else unpack4(v, f);
   #pragma unroll
           for (int e = 0; e < CH; ++e) {
-            float z = f[e] * aff[ra_c + e] + aff[p.Cg + ra_c + e];
+            float z = f[e] * asc[e] + ash[e];
             f[e] = (affine == 2) ? fmaxf(z, 0.f) : z;
           }
           if constexpr (CH == 8) v = pack8(f); else v = pack4(f);
