@@ -110,7 +110,7 @@ void wgrad32(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& dw, co
 
 void register_fp32(pybind11::module& m) {
   namespace py = pybind11;
-  auto f = m.def_submodule("f32", "fp32 (bf16x3 MFMA) kernels of the --mixed_precision no path");
+  auto f = m.def_submodule("f32", "fp32 (split-bf16 MFMA) kernels of the --mixed_precision no path");
   f.def("conv32", &conv32, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("taps"), py::arg("geo"),
         py::arg("isc") = py::none(), py::arg("ish") = py::none(), py::arg("irelu") = 0, py::arg("np") = 3,
         py::arg("stats") = py::none());

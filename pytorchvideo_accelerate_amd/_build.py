@@ -172,7 +172,7 @@ def _build_locked(jobs, force, verbose, csrc, build_dir, out) -> str:
         return out
     hdr = _headers_digest(csrc)
     kernels = sorted(glob.glob(os.path.join(csrc, "kernels", "*.hip")))
-    kernels32 = sorted(glob.glob(os.path.join(csrc, "fp32", "*.hip")))   # fp32 path: one build (bf16x3 MFMA)
+    kernels32 = sorted(glob.glob(os.path.join(csrc, "fp32", "*.hip")))   # fp32 path: one build (split-bf16 MFMA)
     runtime = sorted(glob.glob(os.path.join(csrc, "runtime", "*.cpp")))
     id_src = os.path.join(build_dir, f"build_id.{bid}.cpp")
     if not os.path.exists(id_src):

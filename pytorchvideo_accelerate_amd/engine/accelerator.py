@@ -65,7 +65,7 @@ class Accelerator:
         #    activations, fp32 accumulation, statistics, master weights and optimizer); fp16 also runs the dynamic
         #    loss-scale state machine of the reference recipe (run_slowfast_r50.sh, GradScaler semantics);
         #  * "no" (the reference default, fp32 math) on a GPU -> the native fp32 kernels (kernels="fp32":
-        #    fp32 activations, bf16x3-MFMA convolutions with fp32 accumulation, fp32 BatchNorm / pooling / head);
+        #    fp32 activations, split-bf16 MFMA convolutions (three pieces, six products: fp32 accuracy) with fp32 accumulation, fp32 BatchNorm / pooling / head);
         #  * CPU, or kernels="torch" -> the PyTorch module path (fp32, or autocast for bf16 / fp16).
         if kernels == "auto":
             if self.device.type == "cuda":

@@ -3,7 +3,7 @@
 * :class:`FusedBackend` — the MI355X path: ``models/fused.FusedNet`` (gfx950 kernels, bf16 or fp16) with the
   bucketed RCCL gradient all-reduce of ``parallel/ddp.GradSync`` overlapped with the backward pass.
 * :class:`NativeF32Backend` — the reference default precision (``--mixed_precision no``) on the gfx950 fp32 kernels
-  (``models/native32.NativeF32Net``: bf16x3-MFMA convolutions, fp32 BatchNorm/pool/head), same bucketed all-reduce.
+  (``models/native32.NativeF32Net``: split-bf16 (bf16x6) MFMA convolutions, fp32 BatchNorm/pool/head), same bucketed all-reduce.
 * :class:`TorchBackend` — the reference PyTorch modules with autograd: CPU runs (``--cpu``, gloo DDP), or
   autocast fp16/bf16 / fp32 modules on GPU when asked for (``--kernels torch``); its bucketed all-reduce overlaps backward through
   per-parameter gradient hooks, as DDP's reducer does.  Gradients land in the same flat buffer

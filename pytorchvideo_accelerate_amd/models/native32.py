@@ -1,5 +1,5 @@
 """Native fp32 executor: the reference's default precision (``--mixed_precision no``, reference run.py:330) on the
-gfx950 fp32 kernels (``csrc/fp32``: bf16x3-MFMA convolutions, fp32 BatchNorm / pooling, the fp32 head kernels).
+gfx950 fp32 kernels (``csrc/fp32``: split-bf16 MFMA convolutions (three pieces per operand), fp32 BatchNorm / pooling, the fp32 head kernels).
 
 ``NativeF32Net`` runs the pytorchvideo-keyed module tree of ``models/reference.py`` — SlowFast-R50/R101 and
 Slow-R50 (reference run.py:105-118, the default ``is_slowfast=False`` model at run.py:338-351) — with its own tape

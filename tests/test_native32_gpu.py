@@ -2,11 +2,16 @@
 
 * every convolution geometry family of SlowFast / Slow-R50 (stems with RGB padded to 4 channels, temporal conv_a,
   strided and stride-1 conv_b, strided 1x1 branch1, lateral (7,1,1)/(4,1,1), fast stem (5,7,7)): forward, stride-phase
-  input gradient (plain and accumulating) and weight gradient vs an fp64 CPU oracle — bf16x3 must give ~1e-5;
+  input gradient (plain and accumulating) and weight gradient vs an fp64 CPU oracle — three pieces (bf16x6, the
+  default) < 2e-6 relative L2, two pieces (bf16x3) ~1e-5;
+* the pre-split weight planes (three bf16 pieces summing to the fp32 weight);
 * BatchNorm train forward (statistics, running-stat update) + backward, max pool and stride-1 average pool;
-* whole networks (SlowFast-R50 and Slow-R50 at small shapes): one training step (loss, logits, every parameter
-  gradient, BN running statistics) and an eval forward vs the PyTorch fp32 module path — median per-parameter
-  relative L2 <= 1e-3 (verdict round 5, item 3) and every parameter <= 1e-2.
+* whole networks (SlowFast-R50 and Slow-R50): one training step at small shapes against the PyTorch fp32 module path
+  (median per-parameter gradient error within 3x of stock fp32's own distance to an fp64 run, or 1e-3), and at the
+  full shapes against an fp64 oracle next to stock fp32 (median within 1.5x, worst within 2x of stock fp32's error):
+  two correct fp32 executions of these random-init BN networks differ by ~2e-2 per parameter, so a fixed 1e-3 gate
+  between them is not attainable (profiles/r6_f32/README.md);
+* gradient accumulation into the flat buffer and the per-parameter progress hook.
 """
 import pytest
 import torch
