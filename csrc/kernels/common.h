@@ -90,6 +90,13 @@ __device__ __forceinline__ uint4 relu_e16x8(const uint4& v) {
   return make_uint4(relu_e16x2(v.x), relu_e16x2(v.y), relu_e16x2(v.z), relu_e16x2(v.w));
 }
 
+// The same max against a run-time floor pair: floor 0 is the ReLU, floor 0x80008000 (int16 minimum in both lanes)
+// keeps every value — a wave-uniform switch between BN and BN+ReLU without a select per element.
+__device__ __forceinline__ uint32_t max_e16x2(uint32_t w, uint32_t floor) {
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(s16x2_t, w),
+                                                                __builtin_bit_cast(s16x2_t, floor)));
+}
+
 __device__ __forceinline__ void unpack4(const uint2& v, float* f) {
   f[0] = lo2f(v.x); f[1] = hi2f(v.x);
   f[2] = lo2f(v.y); f[3] = hi2f(v.y);

@@ -646,12 +646,9 @@ void conv_igemm_kernel(const ConvParams p) {
         if (check)
           v = v && (unsigned)(a_t[s] + dgt) < (unsigned)p.Gt && (unsigned)(a_h[s] + dgh) < (unsigned)p.Gh &&
               (unsigned)(a_w[s] + dgw) < (unsigned)p.Gw;
-        if (v) {
-          ra[s] = *reinterpret_cast<const VT*>(p.x + (a_off[s] + tap_lin + kc));
-          ra_valid |= 1u << s;
-        } else {
-          ra[s] = VT{};
-        }
+        // branch-free: an invalid slot loads from the tensor's first chunk and store_lds masks it to zero
+        ra[s] = *reinterpret_cast<const VT*>(p.x + (v ? a_off[s] + tap_lin + kc : 0));
+        ra_valid |= (unsigned)v << s;
       }
       const int boff = tap_w + kc;
   #pragma unroll
@@ -673,19 +670,30 @@ void conv_igemm_kernel(const ConvParams p) {
   #pragma unroll
         for (int e = 0; e < CH; ++e) { asc[e] = aff[ra_c + e]; ash[e] = aff[p.Cg + ra_c + e]; }
       }
+      // branch-free packed BN(+ReLU), as in the uniform-tap loader: FMAs, cvt_pk, then one v_pk_max_i16 per pair
+      // against a wave-uniform floor (0 = ReLU, int16 min = none) and a mask that zeroes padding slots
+      const uint32_t rfloor = affine == 2 ? 0u : 0x80008000u;
   #pragma unroll
       for (int s = 0; s < A_SLOTS; ++s) {
         if constexpr (A_CHUNKS % NT != 0) if (tid + s * NT >= A_CHUNKS) break;
         VT v = ra[s];
-        if (affine && (ra_valid >> s & 1)) {
+        const uint32_t keep = 0u - ((ra_valid >> s) & 1u);
+        if (!affine) {
+          if constexpr (CH == 8) v = make_uint4(v.x & keep, v.y & keep, v.z & keep, v.w & keep);
+          else v = make_uint2(v.x & keep, v.y & keep);
+        } else {
           float f[CH];
           if constexpr (CH == 8) unpack8(v, f); else unpack4(v, f);
   #pragma unroll
-          for (int e = 0; e < CH; ++e) {
-            float z = f[e] * asc[e] + ash[e];
-            f[e] = (affine == 2) ? fmaxf(z, 0.f) : z;
+          for (int e = 0; e < CH; ++e) f[e] = __builtin_fmaf(f[e], asc[e], ash[e]);
+          if constexpr (CH == 8) {
+            v = pack8_fast(f);
+            v = make_uint4(max_e16x2(v.x, rfloor) & keep, max_e16x2(v.y, rfloor) & keep,
+                           max_e16x2(v.z, rfloor) & keep, max_e16x2(v.w, rfloor) & keep);
+          } else {
+            v = make_uint2(max_e16x2(cvt_pk_e16(f[0], f[1]), rfloor) & keep,
+                           max_e16x2(cvt_pk_e16(f[2], f[3]), rfloor) & keep);
           }
-          if constexpr (CH == 8) v = pack8(f); else v = pack4(f);
         }
         *reinterpret_cast<VT*>(A + sa[s]) = v;
       }
