@@ -1,2 +1,2 @@
-export OUT=r6_gen2
-bash scripts/gpu_run.sh layers bench
+export OUT=r6_gen3
+bash scripts/gpu_run.sh pmc fp16 host
