@@ -91,6 +91,7 @@ void conv_wgrad_kernel(const WgradParams p) {
   const bool a_col_ok = a_n < p.Cout;
   // Gram mode: dY is the same BN-ReLU input as x (affine on both operands) + column sums
   const bool dy_aff = p.dy_affine != 0;
+  const uint32_t rfloor = affine == 2 ? 0u : 0x80008000u;   // packed ReLU floor (int16 min = no ReLU)
   float dsc[8], dsh[8], csum[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
@@ -245,17 +246,15 @@ void conv_wgrad_kernel(const WgradParams p) {
     for (int s = 0; s < A_SLOTS; ++s) {
       if constexpr (A_CHUNKS % NT != 0) if (tid + s * NT >= A_CHUNKS) break;
       uint4 v = ra[s];
-      if (dy_aff) {
+      if (dy_aff) {   // packed: FMAs, cvt_pk, v_pk_max_i16 against the uniform floor, row mask
         float f[8];
         unpack8(v, f);
-        const bool ok = (ra_valid >> s) & 1u;
+        const uint32_t keep = 0u - ((ra_valid >> s) & 1u);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          float z = __builtin_fmaf(f[e], dsc[e], dsh[e]);
-          z = affine == 2 ? fmaxf(z, 0.f) : z;
-          f[e] = ok ? z : 0.f;
-        }
+        for (int e = 0; e < 8; ++e) f[e] = __builtin_fmaf(f[e], dsc[e], dsh[e]);
         v = pack8_fast(f);
+        v = make_uint4(max_e16x2(v.x, rfloor) & keep, max_e16x2(v.y, rfloor) & keep,
+                       max_e16x2(v.z, rfloor) & keep, max_e16x2(v.w, rfloor) & keep);
         if (do_csum) {   // sum of the bf16 operand values actually multiplied
           float q[8];
           unpack8(v, q);
@@ -269,21 +268,20 @@ void conv_wgrad_kernel(const WgradParams p) {
     for (int s = 0; s < B_SLOTS; ++s) {
       if constexpr (B_CHUNKS % NT != 0) if (tid + s * NT >= B_CHUNKS) break;
       VT v = rb[s];
+      const uint32_t keep = 0u - ((rb_valid >> s) & 1u);   // padding stays zero (all ones on the dense path)
       if (affine) {
-        // recompute the producer's BN(+ReLU) on the fly: packed cvt + v_pk_max_i16 ReLU
+        // recompute the producer's BN(+ReLU) on the fly: packed cvt + v_pk_max_i16 against the uniform floor
         float f[CH];
         if constexpr (CH == 8) unpack8(v, f); else unpack4(v, f);
 #pragma unroll
         for (int e = 0; e < CH; ++e) f[e] = __builtin_fmaf(f[e], asc[e], ash[e]);
         if constexpr (CH == 8) {
           v = pack8_fast(f);
-          if (affine == 2) v = relu_e16x8(v);
-          if ((!DENSE || dy_aff) && !((rb_valid >> s) & 1u)) v = uint4{0, 0, 0, 0};   // padding stays zero
+          v = make_uint4(max_e16x2(v.x, rfloor) & keep, max_e16x2(v.y, rfloor) & keep,
+                         max_e16x2(v.z, rfloor) & keep, max_e16x2(v.w, rfloor) & keep);
         } else {
-          if (affine == 2)
-            for (int e = 0; e < CH; ++e) f[e] = fmaxf(f[e], 0.f);
-          v = pack4(f);
-          if (!((rb_valid >> s) & 1u)) v = VT{};
+          v = make_uint2(max_e16x2(cvt_pk_e16(f[0], f[1]), rfloor) & keep,
+                         max_e16x2(cvt_pk_e16(f[2], f[3]), rfloor) & keep);
         }
       }
       *reinterpret_cast<VT*>(B + sb[s]) = v;

@@ -1,2 +1,2 @@
-export OUT=r6_gen3
-bash scripts/gpu_run.sh pmc fp16 host
+export OUT=r6_wgp
+bash scripts/gpu_run.sh smoke tests bench
