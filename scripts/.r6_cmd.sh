@@ -1,2 +1,2 @@
-export OUT=r6_wgp
+export OUT=r6_pwp
 bash scripts/gpu_run.sh smoke tests bench
