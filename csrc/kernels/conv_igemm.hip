@@ -642,10 +642,11 @@ void conv_igemm_kernel(const ConvParams p) {
       const int dgt = p.dir * kdt, dgh = p.dir * kdh, dgw = p.dir * kdw;
   #pragma unroll
       for (int s = 0; s < A_SLOTS; ++s) {
-        bool v = tap_ok && (rowok >> s & 1);
+        // non-short-circuit '&': three compares and ANDs instead of a branch per term
+        bool v = tap_ok & ((rowok >> s & 1) != 0);
         if (check)
-          v = v && (unsigned)(a_t[s] + dgt) < (unsigned)p.Gt && (unsigned)(a_h[s] + dgh) < (unsigned)p.Gh &&
-              (unsigned)(a_w[s] + dgw) < (unsigned)p.Gw;
+          v = v & ((unsigned)(a_t[s] + dgt) < (unsigned)p.Gt) & ((unsigned)(a_h[s] + dgh) < (unsigned)p.Gh) &
+              ((unsigned)(a_w[s] + dgw) < (unsigned)p.Gw);
         // branch-free: an invalid slot loads from the tensor's first chunk and store_lds masks it to zero
         ra[s] = *reinterpret_cast<const VT*>(p.x + (v ? a_off[s] + tap_lin + kc : 0));
         ra_valid |= (unsigned)v << s;

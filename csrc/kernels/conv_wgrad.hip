@@ -224,10 +224,10 @@ void conv_wgrad_kernel(const WgradParams p) {
     }
 #pragma unroll
     for (int s = 0; s < B_SLOTS; ++s) {
-      bool v = tid + s * NT < B_CHUNKS && b_col_ok && pcur + b_row[s] < p_end;
+      bool v = (tid + s * NT < B_CHUNKS) & b_col_ok & (pcur + b_row[s] < p_end);   // '&': no branch per term
       if (check)
-        v = v && (unsigned)(bt[s] + b_dt) < (unsigned)p.Ti && (unsigned)(bh[s] + b_dh) < (unsigned)p.Hi &&
-            (unsigned)(bw[s] + b_dw) < (unsigned)p.Wi;
+        v = v & ((unsigned)(bt[s] + b_dt) < (unsigned)p.Ti) & ((unsigned)(bh[s] + b_dh) < (unsigned)p.Hi) &
+            ((unsigned)(bw[s] + b_dw) < (unsigned)p.Wi);
       if (v) {
         rb[s] = *reinterpret_cast<const VT*>(p.x + (bio[s] + tapoff));
         rb_valid |= 1u << s;
