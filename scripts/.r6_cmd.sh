@@ -1,2 +1,1 @@
-export OUT=r6_nsc
-bash scripts/gpu_run.sh smoke tests bench
+timeout -k 10 700 python -u scripts/.r6_detchk.py
