@@ -1,1 +1,2 @@
-timeout -k 10 700 python -u scripts/.r6_detchk.py
+export OUT=r6_final2
+bash scripts/gpu_run.sh smoke tests bench
