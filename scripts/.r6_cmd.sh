@@ -1,2 +1,1 @@
-export OUT=r6_final2
-bash scripts/gpu_run.sh smoke tests bench
+timeout -k 10 600 python -u scripts/dp_det_check.py --reps 5 --load

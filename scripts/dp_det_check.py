@@ -1,10 +1,16 @@
-# DP (2 ranks, gloo, one GPU) deterministic gradient vs the mean of single-rank gradients: default buckets vs one
-# bucket launched at the end of backward; three repetitions each (numeric check, no fault involved).
-import json, os, subprocess, sys, torch
+"""DP (2 gloo ranks sharing one GPU) deterministic gradient vs the mean of single-rank gradients, repeated, optionally
+under a concurrent GPU load (``--load``): prints the relative error and, when non-zero, where in the flat gradient
+the differences sit (a race on an all-reduce bucket stays inside that bucket's range; a perturbed computation spreads
+over every parameter whose gradient is computed after it).  Numeric check only — no fault is involved."""
+import argparse, os, subprocess, sys, torch
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(REPO, "gpurun_out", "dp_det_check")
 os.makedirs(OUT, exist_ok=True)
-BASE = ["--batch", "4", "--steps", "3", "--warmup", "1", "--deterministic"]
+ap = argparse.ArgumentParser()
+ap.add_argument("--reps", type=int, default=3)
+ap.add_argument("--load", action="store_true")
+a = ap.parse_args()
+BASE = ["--batch", "4", "--steps", "3", "--warmup", "1", "--deterministic", "--bucket-mb", "8", "--first-bucket-mb", "1"]
 env = dict(os.environ, OMP_NUM_THREADS="2", PVA_DIST_BACKEND="gloo")
 for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
     env.pop(k, None)
@@ -13,10 +19,25 @@ def run(args, name):
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py")] + BASE + args + ["--dump", dump],
                        stdout=subprocess.DEVNULL, stderr=open(os.path.join(OUT, name + ".err"), "w"), env=env, timeout=300)
     assert r.returncode == 0, name
-    return torch.load(dump, weights_only=True)["grad"]
-s = [run(["--gpus", "1", "--data-rank", str(r), "--bucket-mb", "8", "--first-bucket-mb", "1"], f"single{r}") for r in range(2)]
+    g = torch.load(dump, weights_only=True)["grad"]
+    os.remove(dump)
+    return g
+s = [run(["--gpus", "1", "--data-rank", str(r)], f"single{r}") for r in range(2)]
 ref = (s[0] + s[1]) / 2
-for tag, bk in (("default", ["--bucket-mb", "8", "--first-bucket-mb", "1"]), ("onebucket", ["--bucket-mb", "100000", "--first-bucket-mb", "100000"])):
-    for i in range(3):
-        g = run(["--gpus", "2"] + bk, f"dp_{tag}{i}")
-        print(tag, i, "err %.3e" % float((g - ref).norm() / ref.norm()), flush=True)
+load = None
+if a.load:
+    load = subprocess.Popen(["timeout", "-k", "10", "400", sys.executable, os.path.join(REPO, "bench.py"), "--batch", "32",
+                             "--steps", "2000", "--warmup", "1"], stdout=subprocess.DEVNULL,
+                            stderr=open(os.path.join(OUT, "load.err"), "w"))
+try:
+    for i in range(a.reps):
+        g = run(["--gpus", "2"], f"dp{i}")
+        d = (g - ref).abs()
+        nz = (d > 0).nonzero().flatten()
+        msg = "err %.3e" % float((g - ref).norm() / ref.norm())
+        if nz.numel():
+            msg += " differing %d of %d, flat index %d..%d (numel %d)" % (nz.numel(), d.numel(), int(nz[0]), int(nz[-1]), d.numel())
+        print("rep", i, msg, flush=True)
+finally:
+    if load is not None:
+        load.kill(); load.wait()
