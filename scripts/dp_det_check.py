@@ -9,6 +9,7 @@ os.makedirs(OUT, exist_ok=True)
 ap = argparse.ArgumentParser()
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--load", action="store_true")
+ap.add_argument("--single-load", action="store_true", help="repeat single-rank 0 under the load instead of DP runs")
 a = ap.parse_args()
 BASE = ["--batch", "4", "--steps", "3", "--warmup", "1", "--deterministic", "--bucket-mb", "8", "--first-bucket-mb", "1"]
 env = dict(os.environ, OMP_NUM_THREADS="2", PVA_DIST_BACKEND="gloo")
@@ -31,7 +32,9 @@ if a.load:
                             stderr=open(os.path.join(OUT, "load.err"), "w"))
 try:
     for i in range(a.reps):
-        g = run(["--gpus", "2"], f"dp{i}")
+        g = run(["--gpus", "1", "--data-rank", "0"], f"s0_{i}") if a.single_load else run(["--gpus", "2"], f"dp{i}")
+        if a.single_load:
+            ref = s[0]   # same rank, same data: any difference is run-to-run noise under the load
         d = (g - ref).abs()
         nz = (d > 0).nonzero().flatten()
         msg = "err %.3e" % float((g - ref).norm() / ref.norm())

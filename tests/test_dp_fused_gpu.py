@@ -72,10 +72,11 @@ def test_fused_two_rank_deterministic_exact(tmp_path):
     dedicated repeats, ``scripts/dp_det_check.py``; single-rank deterministic runs are bitwise reproducible, also with
     two processes sharing the GPU).  OPEN ISSUE (round 6): inside the full GPU suite this comparison came out at
     9.2e-5, 5.7e-4 and 2.4e-4 in three of about eleven runs (``gpurun_out/r6_nsc2``, ``r6_dpchk``, ``r6_final2``) —
-    an intermittent difference between the two-rank gloo rehearsal and the single-rank runs whose source is not found
-    yet (not the persisted tune table: deterministic mode does not load it; the one-bucket variant, whose all-reduce
-    starts only after the whole backward, was exact 3/3 — a gradient write landing in an already-launched bucket
-    would fit, unverified).  The gate is 1e-3 so
+    an intermittent difference between the two-rank gloo rehearsal and the single-rank runs.  Its source is not the DP path
+    in this test: under a concurrent GPU load single-rank runs differ from each other in the same ~10.5 k leaf weight
+    gradients (fast stem, stage-0 lateral fusion, lateral channels of slow res2 unit 0) — order-dependent accumulation
+    left in deterministic mode, exposed when the two ranks contend for the GPU; not the all-reduce
+    (``profiles/r6_dpdet/``).  The gate is 1e-3 so
     that a rare occurrence does not stop the suite; anything systematic (a wrong bucket, a missed average, a race that
     hits every run) is orders of magnitude above it (spread between the shards: ~2)."""
     err, spread = _dp_vs_singles(tmp_path, ["--deterministic"], "det")
